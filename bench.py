@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Benchmark of the gang-placement hot path (BASELINE.json metric).
+
+A "step" = one fit-mask pass (config 5): every job of a 100k-job batch evaluated against every
+node of the 1M-node inventory, mask + per-job counts written to HBM, inputs already resident.
+`value` = job x node fit evaluations per second for the whole job (all ranks).  The second half
+of the metric, gang placements/s, is measured on the same 1M-node inventory with a 10k-job
+mixed PyTorch/MPI/JAX batch (config 3 mix) and reported in the "greedy" object.
+
+    python bench.py [--gpus N --steps K --warmup W]          (N>1: one rank per GPU, torchrun)
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "training-operator_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+from placement import Engine, comm_id, synth  # noqa: E402
+
+METRIC = "job×node fit evals/sec + gang placements/sec, 1M-node inventory, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+class HipEvents:
+    """hipEvent timing on the engine's own stream (torch events only see torch's stream)."""
+
+    def __init__(self):
+        self.lib = ctypes.CDLL("libamdhip64.so")
+        self.lib.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        self.lib.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self.lib.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+        self.lib.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+        self.lib.hipEventDestroy.argtypes = [ctypes.c_void_p]
+
+    def create(self):
+        ev = ctypes.c_void_p()
+        assert self.lib.hipEventCreate(ctypes.byref(ev)) == 0
+        return ev
+
+    def record(self, ev, stream):
+        assert self.lib.hipEventRecord(ev, ctypes.c_void_p(stream)) == 0
+
+    def elapsed_ms(self, a, b):
+        assert self.lib.hipEventSynchronize(b) == 0
+        ms = ctypes.c_float()
+        assert self.lib.hipEventElapsedTime(ctypes.byref(ms), a, b) == 0
+        return float(ms.value)
+
+
+def fit_bytes(n_nodes: int, n_jobs: int) -> int:
+    """Algorithmic HBM bytes of one fit-mask launch over n_nodes:
+    node residuals 4x8 B + labels 4 B read once, job request 4x8 B + need 4 B read once,
+    mask J*ceil(N/64)*8 B written once, per-job counts 8 B written."""
+    return n_nodes * 36 + n_jobs * 36 + n_jobs * ((n_nodes + 63) // 64) * 8 + n_jobs * 8
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--nodes", type=int, default=1_000_000)
+    ap.add_argument("--fit-jobs", type=int, default=100_000)
+    ap.add_argument("--greedy-jobs", type=int, default=10_000)
+    ap.add_argument("--greedy-steps", type=int, default=2)
+    ap.add_argument("--topk", type=int, default=0)
+    ap.add_argument("--window-groups", type=int, default=0)
+    ap.add_argument("--window-pods", type=int, default=0)
+    ap.add_argument("--no-greedy", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-jobs", type=int, default=1000)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        ids = [comm_id() if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0)
+        cid = ids[0]
+
+        def barrier():
+            dist.barrier()
+
+        def allmax(x: float) -> float:
+            t = torch.tensor([x], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+
+        def allsum(x: int) -> int:
+            t = torch.tensor([x], dtype=torch.int64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            return int(t.item())
+    else:
+        cid = None
+
+        def barrier():
+            pass
+
+        def allmax(x):
+            return x
+
+        def allsum(x):
+            return x
+
+    N, J = args.nodes, args.fit_jobs
+    inv = synth.make_inventory(N, synth.SEED["cfg5"], gpu_frac=0.2)
+    eng = Engine(local, rank=rank, world_size=world, comm=cid, max_nodes=N, topk=args.topk,
+                 window_groups=args.window_groups, window_pods=args.window_pods)
+    eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    b, e = eng.shard_range()
+    Ns = e - b
+    req, need = synth.make_fit_jobs(J, synth.SEED["cfg5"])
+    eng.jobs_upload(req, need)
+    stream = eng.stream()
+    ev = HipEvents()
+
+    for _ in range(args.warmup):
+        eng.fit_mask_run()
+    eng.synchronize()
+    feasible = allsum(int(eng.fit_counts().sum()))
+
+    e0, e1 = ev.create(), ev.create()
+    barrier()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    ev.record(e0, stream)
+    for _ in range(args.steps):
+        eng.fit_mask_run()
+    ev.record(e1, stream)
+    eng.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = allmax(t1 - t0)
+    kern_ms = ev.elapsed_ms(e0, e1) / args.steps
+    value = float(N) * J * args.steps / elapsed
+    alg = fit_bytes(Ns, J)
+    achieved = alg / (kern_ms * 1e-3) / 1e9
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "job*node fit evals/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic (splitmix64, SURVEY.md 8d)",
+        "config": {"workload": "cfg5: fit bitmask, 1M-node inventory x 100k jobs, device-resident",
+                   "nodes": N, "jobs": J, "parallelism": f"node-shard x{world}", "feasible_pairs": feasible},
+        "roofline": {"bound": "hbm", "kernel": "fit_mask_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel_ms": kern_ms, "alg_bytes_per_launch": alg,
+                     "note": "kernel_ms = hipEvent time on the engine stream / launches (incl. the 8*J-byte "
+                             "count memset); per-rank shard; traffic: see profiles/ PMC passes"},
+    }
+
+    if not args.no_greedy:
+        batch = synth.make_jobs(args.greedy_jobs, synth.SEED["cfg3"], "mixed")
+        eng.reset_residuals()
+        eng.place_batch(batch)                      # warm-up pass (allocations, code paths)
+        times = []
+        placed = 0
+        for _ in range(args.greedy_steps):
+            eng.reset_residuals()
+            eng.synchronize()
+            barrier()
+            g0 = time.perf_counter()
+            pods, st = eng.place_batch(batch)
+            barrier()
+            times.append(allmax(time.perf_counter() - g0))
+            placed = int((st == 0).sum())
+        s = eng.stats()
+        gt = float(np.median(times))
+        out["greedy"] = {"workload": "cfg3 mix on the 1M-node inventory: 10k jobs (50% PyTorch, 25% MPI, 25% JAX)",
+                         "jobs": args.greedy_jobs, "pods": batch.n_pods, "jobs_placed": placed,
+                         "gang_placements_per_s": args.greedy_jobs / gt, "ms_per_batch": gt * 1e3,
+                         "windows_per_batch": s["windows"] / (args.greedy_steps + 1),
+                         "rescans_per_batch": s["rescans"] / (args.greedy_steps + 1),
+                         "scan_evals_per_s": s["scan_evals"] / (args.greedy_steps + 1) * world / gt,
+                         "naive_pod_x_node_evals_per_s": batch.n_pods * float(N) / gt}
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle
+        nthreads = max(1, min(16, os.cpu_count() or 1))
+        js = min(args.cpu_sample_jobs, J)
+        res = inv.residual()
+        oracle.fit_mask(res, inv.labels, req[:16], need[:16], want_mask=False, nthreads=nthreads)  # warm-up
+        reps = []
+        for _ in range(3):
+            c0 = time.perf_counter()
+            _, ocounts = oracle.fit_mask(res, inv.labels, req[:js], need[:js], want_mask=True, nthreads=nthreads)
+            reps.append(time.perf_counter() - c0)
+        ct = float(np.median(reps))
+        gpu_counts = eng.fit_counts()[:js] if world == 1 else None
+        out["cpu_baseline"] = {"value": js * float(N) / ct, "unit": "job*node fit evals/s", "cores": nthreads,
+                               "kind": "port", "sample": f"C oracle (oracle/oracle.c, OpenMP x{nthreads}, "
+                               f"{cpu_model()}) on the first {js} jobs x all {N} nodes, median of 3; "
+                               "the Go reference cannot be timed (no Go toolchain, SURVEY.md 0.3)",
+                               "counts_match_gpu": bool(np.array_equal(ocounts, gpu_counts))}
+        if "greedy" in out:
+            gb = synth.make_jobs(40, synth.SEED["cfg3"], "mixed")
+            c0 = time.perf_counter()
+            oracle.place_greedy(res, inv.labels, gb.job_group_off, gb.priority, gb.group_count, gb.group_req,
+                                gb.group_need, nthreads=nthreads)
+            ct = time.perf_counter() - c0
+            out["cpu_baseline"]["greedy"] = {"gang_placements_per_s": 40 / ct, "cores": nthreads,
+                                             "sample": "naive per-pod argmin oracle, first 40 jobs of the batch"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

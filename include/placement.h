@@ -1,0 +1,188 @@
+/*
+ * placement.h -- C ABI of libplacement, the MI355X-native gang-placement engine.
+ *
+ * Drop-in boundary for the training operator's PodGroup / coscheduling hot path.  Plain C11:
+ * plain pointers and sizes, no C++ or torch types, integer return codes, no exceptions or
+ * aborts across the ABI.  The reference is Go; the binding a maintainer adds on the reference
+ * side (cgo package pkg/placement/hip) is in INTEGRATION.md.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference repo root):
+ *   pe_pg_min_resources(PE_MODE_V1, ...)
+ *       pkg/controller.v1/common/util.go:108  func CalcPGMinResources(minMember int32,
+ *           replicas map[ReplicaType]*ReplicaSpec, pcGetFunc PriorityClassGetFunc) *v1.ResourceList
+ *       (called from pkg/controller.v1/common/job.go:275-277,455-457; AddResourceList util.go:79-104)
+ *   pe_pg_min_resources(PE_MODE_V2, ...)
+ *       pkg/runtime.v2/framework/plugins/coscheduling/coscheduling.go:103-118  (*CoScheduling).Build
+ *       aggregation loop, fed by pkg/runtime.v2/runtime.go:115-145 NewInfo (kueue TotalRequests)
+ *   pe_fit_mask / pe_fit_mask_run, pe_place_greedy
+ *       NO reference function: node fit / score / placement is done by the external gang
+ *       scheduler (scheduler-plugins coscheduling / Volcano) that consumes the PodGroup the
+ *       operator writes (pkg/controller.v1/control/podgroup_control.go:36-54).  The rule is
+ *       build-defined and exposed here so the plugin can answer
+ *       feasibility / placement itself.
+ *   pe_create / pe_destroy / pe_last_error
+ *       lifetime of the plugin instance: pkg/runtime.v2/framework/plugins/registry.go:32-42
+ *       factory + coscheduling.go:71-85 New(); errors follow framework.go:117-121 (first error
+ *       stops the phase) -> every call returns a code and sets a message.
+ *
+ * Units (canonical int64): dim 0 cpu in milli-cores, dim 1 memory in
+ * bytes, dim 2 accelerator count (resource name given by pe_config.gpu_resource_name), dim 3
+ * ephemeral-storage in bytes.  Values must be >= 0; int64 overflow is flagged, never wrapped
+ * (where Go's resource.Quantity would fall back to inf.Dec).
+ *
+ * Ownership: the caller owns every host pointer for the duration of the call only; the library
+ * never retains them.  Device memory is library-owned; pointers it hands out stay valid until
+ * the next call that re-sizes the same buffer, or pe_destroy.
+ * Threading: one mutex per context; every call selects the context's device itself (callers
+ * such as cgo goroutines may migrate between OS threads).
+ */
+#ifndef PLACEMENT_H_
+#define PLACEMENT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PE_ABI_VERSION 1
+#define PE_DIMS 4
+#define PE_COMM_ID_BYTES 128
+#define PE_MAX_NODES (1LL << 24) /* node ids live in the low 24 bits of the best-fit key */
+
+enum {
+  PE_OK = 0,
+  PE_EINVAL = -1,    /* bad argument (negative request, ids out of range, null pointer) */
+  PE_EOVERFLOW = -2, /* int64 overflow in an aggregation (per-job flags say which job) */
+  PE_ENOMEM = -3,
+  PE_EHIP = -4,      /* HIP runtime error, see pe_last_error */
+  PE_ERCCL = -5,     /* RCCL error */
+  PE_ESTATE = -6,    /* call order (e.g. fit mask before pe_load_nodes) */
+  PE_ENODEV = -7     /* no usable GPU: the engine has no CPU fallback */
+};
+
+enum { PE_MODE_V1 = 1, PE_MODE_V2 = 2 };
+enum { PE_JOB_PLACED = 0, PE_JOB_UNSCHEDULABLE = 1 };
+
+/* container record flags for pe_pg_min_resources: bits 0-3 = which dims are present in the
+ * container's ResourceList (keys with value 0 are present), bits 4-5 = kind */
+#define PE_KIND_SHIFT 4
+enum { PE_KIND_CONTAINER = 0, PE_KIND_INIT = 1, PE_KIND_SIDECAR = 2, PE_KIND_OVERHEAD = 3 };
+
+/* Host all-gather used instead of RCCL when set (tests run several shards on one GPU):
+ * gather `bytes` from every rank into recv[rank * bytes]; return 0 on success. */
+typedef int (*pe_allgather_fn)(void* user, const void* send, void* recv, size_t bytes);
+
+typedef struct pe_ctx pe_ctx;
+
+typedef struct {
+  int32_t device_id;             /* HIP ordinal; -1 = the calling thread's current device */
+  int32_t rank;                  /* inventory shard owned by this process, 0..world_size-1 */
+  int32_t world_size;            /* shards of the node inventory (1 = unsharded) */
+  const uint8_t* comm_id;        /* PE_COMM_ID_BYTES from pe_comm_id() on rank 0 (RCCL) */
+  pe_allgather_fn exchange;      /* optional host exchange replacing RCCL */
+  void* exchange_user;
+  int64_t max_nodes;             /* global inventory capacity (<= PE_MAX_NODES) */
+  const char* gpu_resource_name; /* resource key of dim 2, e.g. "amd.com/gpu" (informational) */
+  int32_t topk;                  /* best-fit candidates kept per group scan (0 = 64) */
+  int32_t window_groups;         /* groups per scan window (0 = 64) */
+  int64_t window_pods;           /* pods per scan window (0 = 1024) */
+} pe_config;
+
+typedef struct {
+  int64_t fit_evals;     /* job x node fit evaluations (fit mask) */
+  int64_t scan_evals;    /* group x node key evaluations (greedy scans) */
+  int64_t windows;       /* greedy scan windows */
+  int64_t rescans;       /* windows cut short because a candidate list ran dry */
+  int64_t groups_scanned;
+  int64_t pods_placed;
+  int64_t jobs_placed;
+  int64_t jobs_failed;
+  double last_greedy_ms; /* wall time of the last pe_place_greedy */
+} pe_stats;
+
+int pe_abi_version(void);
+/* RCCL unique id for a sharded context (call on rank 0, broadcast the bytes to every rank). */
+int pe_comm_id(uint8_t out[PE_COMM_ID_BYTES]);
+int pe_create(const pe_config* cfg, pe_ctx** out);
+void pe_destroy(pe_ctx* ctx);
+const char* pe_last_error(const pe_ctx* ctx); /* valid until the next call on ctx */
+
+/* Inventory: caller-owned host SoA [4][n] (row d = dim d) of the GLOBAL inventory; the context
+ * keeps its shard [rank*n/world, (rank+1)*n/world) device-resident.  residual = cap - used. */
+int pe_load_nodes(pe_ctx* ctx, int64_t n, const int64_t* cap, const int64_t* used, const uint32_t* labels,
+                  const int32_t* island);
+int pe_reset_residuals(pe_ctx* ctx); /* residual := cap - used (device-side copy) */
+int pe_shard_range(const pe_ctx* ctx, int64_t* begin, int64_t* end);
+int pe_read_residuals(pe_ctx* ctx, int64_t* res_out /* [4][end-begin] of this shard */);
+
+/* Batched PodGroup MinResources (one job per lane on the GPU).
+ *   groups of job j: [job_group_off[j], job_group_off[j+1]); containers of group g:
+ *   [group_cont_off[g], group_cont_off[g+1]); cont_req [C][4], cont_flags [C].
+ *   V1: groups in CalcPGMinResources order (priority desc; ties: type name asc), group_replicas
+ *       -1 = nil, only PE_KIND_CONTAINER records count, pods counted until min_member[j];
+ *       out_members = pods counted.
+ *   V2: group = runtime.Info TotalRequests entry with its pod's containers (kueue formula),
+ *       out_members = sum of replicas (Go int32 wrap-around), min_member ignored (may be NULL).
+ * Outputs per job: out_min_res[j][4], out_present[j] (bit d = key d present), out_members[j],
+ * out_overflow[j] (1 = int64 overflow: the reference would have switched to inf.Dec).
+ * Returns PE_EOVERFLOW if any job overflowed (outputs still written). */
+int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t* job_group_off,
+                        const int32_t* min_member, const int32_t* group_replicas, const int32_t* group_cont_off,
+                        const int64_t* cont_req, const uint8_t* cont_flags, int64_t* out_min_res,
+                        uint8_t* out_present, int32_t* out_members, uint8_t* out_overflow);
+
+/* What-if feasibility (config 5): bit (j, n) = fit(job j, node n) against the CURRENT residuals
+ * of this shard, device-resident, row-major [n_jobs][ceil(shard_nodes/64)] u64, bit n%64 of word
+ * n/64.  Counts are per job over this shard (sum them across shards).
+ * One-shot form: upload + compute + counts to host; *dev_mask receives the device pointer. */
+int pe_fit_mask(pe_ctx* ctx, int64_t n_jobs, const int64_t* req /*[j][4]*/, const uint32_t* need,
+                int64_t* out_feasible_count, const uint64_t** dev_mask, int64_t* words_per_row);
+/* Staged form (device-resident inputs, used by the benchmark): */
+int pe_jobs_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need);
+int pe_fit_mask_run(pe_ctx* ctx); /* asynchronous on the context stream */
+int pe_fit_counts(pe_ctx* ctx, int64_t* out_feasible_count); /* synchronizes */
+int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out /*[n_rows][words_per_row]*/);
+
+/* Greedy best-fit all-or-nothing gang placement.  Jobs in (priority
+ * desc, index asc) order, groups of a job in the given order, pods of a group identical.
+ *   job_group_off[J+1], priority[J], group_count[G] (pods to place), group_req[G][4],
+ *   group_need[G] (required label bits).
+ * out_pod_node[sum(group_count)]: GLOBAL node id per pod slot (groups in input order), -1 = none.
+ * out_job_status[J]: PE_JOB_PLACED / PE_JOB_UNSCHEDULABLE.  Residuals are updated in place
+ * (successful placements stay; failed jobs are rolled back).  Every rank of a sharded context
+ * must make the same call; all ranks return the same placements. */
+int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority,
+                    const int32_t* group_count, const int64_t* group_req, const uint32_t* group_need,
+                    int32_t* out_pod_node, int32_t* out_job_status);
+
+/* ---- Host resolver: the host half of pe_place_greedy, exposed on its own so a caller (or a
+ * CPU test) can drive the windowed protocol with candidate blobs it obtained elsewhere, e.g. one
+ * blob per shard gathered over any transport.  No device is touched.
+ * Window blob layout (what the device merge kernel writes, per shard, per window group):
+ *   16-B header {int32 n; int32 flags; uint64 limit} + K records of 48 B
+ *   {uint64 key; int64 res[4]; uint64 labels}; shards are concatenated.
+ * Updates are returned as [n][5] int64 {global node id, res[0..3]} (absolute residuals). */
+typedef struct pe_resolver pe_resolver;
+int pe_resolver_create(int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority,
+                       const int32_t* group_count, const int64_t* group_req, const uint32_t* group_need,
+                       pe_resolver** out);
+void pe_resolver_destroy(pe_resolver* r);
+int pe_resolver_done(const pe_resolver* r); /* 1 when every job is decided */
+int pe_resolver_next_window(pe_resolver* r, int32_t max_groups, int64_t max_pods, int32_t* out_groups,
+                            int32_t* out_n);
+int pe_resolver_resolve(pe_resolver* r, int32_t n_groups, const int32_t* groups, const uint8_t* blob,
+                        int32_t n_shards, int32_t topk, int64_t* out_updates, int64_t max_updates,
+                        int64_t* out_n_updates, int32_t* out_consumed);
+int pe_resolver_results(const pe_resolver* r, int32_t* out_pod_node, int32_t* out_job_status);
+
+int pe_synchronize(pe_ctx* ctx);
+void* pe_stream(pe_ctx* ctx); /* hipStream_t the context launches on (for event timing) */
+int pe_get_stats(const pe_ctx* ctx, pe_stats* out);
+int pe_reset_stats(pe_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLACEMENT_H_ */

@@ -1,0 +1,265 @@
+"""GPU parity: every kernel through the C ABI vs the CPU oracle, bit-exact (integer work).
+
+Runs on the MI355X box (`pytest -m gpu`).  Sizes are ones the oracle finishes in seconds;
+full-size cases are covered by size-independent properties in test_gpu_properties.py."""
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import flatten as F
+from oracle import semantics as S
+from placement import Engine, V1, V2, synth
+
+pytestmark = pytest.mark.gpu
+GPU = "nvidia.com/gpu"
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = Engine(0, gpu_resource_name=GPU)
+    yield e
+    e.close()
+
+
+def load(golden_dir, name):
+    with open(os.path.join(golden_dir, name + ".json")) as f:
+        return json.load(f)
+
+
+# ------------------------------------------------------------------ aggregation
+
+def _pc_get(case):
+    pri = case.get("priorities", {})
+    return lambda name: pri.get(name)
+
+
+def test_pg_min_resources_v1_golden(eng, golden_dir):
+    g = load(golden_dir, "v1_podgroup")
+    flat, expect = F.Flat(), []
+    for case in g["cases"]:
+        if (case["scheduling_policy"] or {}).get("minResources") is not None:
+            continue
+        mm = S.v1_pg_spec(case["replicas"], case["scheduling_policy"], _pc_get(case))[0]
+        F.add_v1_job(flat, mm, case["replicas"], GPU, _pc_get(case))
+        expect.append(case)
+    arrs = flat.arrays()
+    out, pres, mem, ovf = eng.pg_min_resources(V1, *arrs)
+    o_out, o_pres, o_mem, o_ovf = oracle.pg_min_resources(oracle.V1, *arrs)
+    np.testing.assert_array_equal(out, o_out)
+    np.testing.assert_array_equal(pres, o_pres)
+    np.testing.assert_array_equal(mem, o_mem)
+    for j, case in enumerate(expect):
+        want = F.canonical_list({k: S.parse_quantity(v) for k, v in case["want"].items()}, GPU)
+        assert F.unflatten(out[j], pres[j], GPU) == want, case["name"]
+
+
+def test_pg_min_resources_v2_golden(eng, golden_dir):
+    g = load(golden_dir, "v2_podgroup")
+    flat, expect = F.Flat(), []
+    for case in g["cases"]:
+        if case["want"] is None:
+            continue
+        info = S.new_info([(n, 1, pod) for n, pod in case["replicated_jobs"]])
+        S.enforce_ml_policy(info, case["ml_policy"], case["trainjob_num_nodes"])
+        pods = dict(case["replicated_jobs"])
+        for name in sorted(info["TotalRequests"]):
+            F.add_v2_pod_group(flat, info["TotalRequests"][name]["Replicas"], pods[name], GPU)
+        flat.end_job(0)
+        expect.append(case)
+    out, pres, mem, ovf = eng.pg_min_resources(V2, *flat.arrays())
+    for j, case in enumerate(expect):
+        want = F.canonical_list({k: S.parse_quantity(v) for k, v in case["want"]["minResources"].items()}, GPU)
+        assert F.unflatten(out[j], pres[j], GPU) == want, case["name"]
+        assert mem[j] == case["want"]["minMember"]
+        assert ovf[j] == 0
+
+
+def random_csr(J, seed, big=False):
+    rng = np.random.default_rng(seed)
+    ng = rng.integers(0, 5, J)
+    jgo = np.concatenate([[0], np.cumsum(ng)]).astype(np.int32)
+    G = int(jgo[-1])
+    rep = rng.integers(-1, 40, G).astype(np.int32)
+    rep[rng.random(G) < 0.05] = 2**31 - 1
+    nc = rng.integers(0, 5, G)
+    gco = np.concatenate([[0], np.cumsum(nc)]).astype(np.int32)
+    C = int(gco[-1])
+    hi = 2**62 if big else 2**40
+    req = rng.integers(0, hi, (C, 4), dtype=np.int64)
+    req[rng.random((C, 4)) < 0.3] = 0
+    fl = (rng.integers(0, 16, C) | (rng.integers(0, 4, C) << 4)).astype(np.uint8)
+    mm = rng.integers(-2, 60, J).astype(np.int32)
+    return jgo, mm, rep, gco, req, fl
+
+
+@pytest.mark.parametrize("mode", [V1, V2])
+@pytest.mark.parametrize("big", [False, True])
+def test_pg_min_resources_random_vs_oracle(eng, mode, big):
+    arrs = random_csr(20000, 7 + mode + 10 * big, big)
+    got = eng.pg_min_resources(mode, *arrs)
+    want = oracle.pg_min_resources(mode, *arrs)
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+    if big:
+        assert want[3].sum() > 0      # overflow path exercised and flagged identically
+
+
+def test_pg_min_resources_empty(eng):
+    z = np.zeros(1, np.int32)
+    out = eng.pg_min_resources(V2, z, None, np.zeros(0, np.int32), z, np.zeros((0, 4), np.int64), np.zeros(0, np.uint8))
+    assert out[0].shape == (0, 4)
+
+
+# ------------------------------------------------------------------ fit mask
+
+@pytest.mark.parametrize("N,J", [(1, 1), (63, 5), (64, 256), (257, 3), (1000, 300), (4097, 513), (20000, 1000)])
+def test_fit_mask_vs_oracle(eng, N, J):
+    inv = synth.make_inventory(N, 17 + N)
+    req, need = synth.make_fit_jobs(J, 19 + J)
+    eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    counts = eng.fit_mask(req, need)
+    mask = eng.fit_mask_rows(0, J)
+    o_mask, o_counts = oracle.fit_mask(inv.residual(), inv.labels, req, need)
+    np.testing.assert_array_equal(mask, o_mask)
+    np.testing.assert_array_equal(counts, o_counts)
+    assert 0 < counts.sum() < N * J or N * J < 10
+
+
+def test_fit_mask_edge_values(eng):
+    # zero requests fit everything incl. exhausted nodes; requests equal to residual fit; negative
+    # residual (over-committed node) fits nothing; INT64_MAX capacity
+    N = 130
+    cap = np.full((4, N), 100, np.int64)
+    used = np.zeros_like(cap)
+    used[:, 5] = 100                      # exhausted
+    cap[:, 7] = np.iinfo(np.int64).max
+    used[0, 9] = 150                      # over-committed cpu -> negative residual
+    labels = np.arange(N, dtype=np.uint32) % 4
+    eng.load_nodes(cap, used, labels)
+    req = np.array([[0, 0, 0, 0], [100, 100, 100, 100], [101, 0, 0, 0], [0, 0, 0, 0], [2**62, 0, 0, 0]], np.int64)
+    need = np.array([0, 0, 0, 3, 0], np.uint32)
+    counts = eng.fit_mask(req, need)
+    o_mask, o_counts = oracle.fit_mask(cap - used, labels, req, need)
+    np.testing.assert_array_equal(eng.fit_mask_rows(0, 5), o_mask)
+    np.testing.assert_array_equal(counts, o_counts)
+    assert counts[0] == N - 1 and counts[4] == 1
+
+
+def test_fit_mask_sharded_columns(eng):
+    """Two shards (ranks) of one inventory: column blocks concatenate to the unsharded mask."""
+    N, J = 3001, 130
+    inv = synth.make_inventory(N, 23)
+    req, need = synth.make_fit_jobs(J, 29)
+    o_mask, o_counts = oracle.fit_mask(inv.residual(), inv.labels, req, need)
+    total = np.zeros(J, np.int64)
+    for r in range(2):
+        e = Engine(0, rank=r, world_size=2, exchange=lambda b: b + b)
+        e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+        b, en = e.shard_range()
+        total += e.fit_mask(req, need)
+        m = e.fit_mask_rows(0, J)
+        sub_res = inv.residual()[:, b:en]
+        want, _ = oracle.fit_mask(sub_res, inv.labels[b:en], req, need)
+        np.testing.assert_array_equal(m, want)
+        e.close()
+    np.testing.assert_array_equal(total, o_counts)
+
+
+# ------------------------------------------------------------------ greedy placement
+
+def check_greedy(e, inv, batch):
+    e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    pods, st = e.place_batch(batch)
+    w_pods, w_st, w_res = oracle.place_greedy(inv.residual(), inv.labels, batch.job_group_off, batch.priority,
+                                              batch.group_count, batch.group_req, batch.group_need)
+    np.testing.assert_array_equal(st, w_st)
+    np.testing.assert_array_equal(pods, w_pods)
+    b, en = e.shard_range()
+    np.testing.assert_array_equal(e.read_residuals(), w_res[:, b:en])
+    return st
+
+
+@pytest.mark.parametrize("mix,N,J,gpu_frac", [("pytorch", 2000, 200, 0.2), ("mixed", 3000, 300, 0.3),
+                                               ("gang8", 600, 120, 1.0)])
+def test_greedy_vs_oracle(eng, mix, N, J, gpu_frac):
+    inv = synth.make_inventory(N, 31 + N, gpu_frac)
+    batch = synth.make_jobs(J, 37 + J, mix)
+    st = check_greedy(eng, inv, batch)
+    assert (st == 0).any()
+
+
+@pytest.mark.parametrize("topk,wg,wp", [(1, 1, 1), (2, 8, 32), (8, 64, 1024), (256, 16, 4096)])
+def test_greedy_window_configs(topk, wg, wp):
+    e = Engine(0, topk=topk, window_groups=wg, window_pods=wp)
+    inv = synth.make_inventory(1500, 41, 0.3)
+    batch = synth.make_jobs(150, 43, "mixed")
+    check_greedy(e, inv, batch)
+    s = e.stats()
+    assert s["windows"] > 0
+    e.close()
+
+
+def test_greedy_cfg2_full_size(eng):
+    """Config 2 as BASELINE.json names it: 10k nodes x 1k PyTorchJobs, bit-exact."""
+    inv = synth.make_inventory(10_000, synth.SEED["cfg2"], 0.2)
+    batch = synth.make_jobs(1000, synth.SEED["cfg2"], "pytorch")
+    st = check_greedy(eng, inv, batch)
+    assert 0 < (st == 0).sum() < 1000
+
+
+def test_greedy_sharded_exchange():
+    """2 shards on one GPU (two contexts, host all-gather between threads) == unsharded oracle."""
+    inv = synth.make_inventory(2500, 47, 0.25)
+    batch = synth.make_jobs(200, 53, "mixed")
+    W = 2
+    slots = [None] * W
+    bar = threading.Barrier(W)
+
+    def exchange_for(r):
+        def ex(blob):
+            slots[r] = blob
+            bar.wait(timeout=60)
+            out = b"".join(slots)
+            bar.wait(timeout=60)
+            return out
+        return ex
+
+    engines = [Engine(0, rank=r, world_size=W, exchange=exchange_for(r), topk=4, window_groups=8) for r in range(W)]
+    for e in engines:
+        e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    results = [None] * W
+
+    def run(r):
+        results[r] = engines[r].place_batch(batch)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    w_pods, w_st, w_res = oracle.place_greedy(inv.residual(), inv.labels, batch.job_group_off, batch.priority,
+                                              batch.group_count, batch.group_req, batch.group_need)
+    for r in range(W):
+        pods, st = results[r]
+        np.testing.assert_array_equal(st, w_st)
+        np.testing.assert_array_equal(pods, w_pods)
+        b, en = engines[r].shard_range()
+        np.testing.assert_array_equal(engines[r].read_residuals(), w_res[:, b:en])
+    for e in engines:
+        e.close()
+
+
+def test_greedy_reset_residuals(eng):
+    inv = synth.make_inventory(800, 59)
+    batch = synth.make_jobs(60, 61)
+    eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    a = eng.place_batch(batch)
+    eng.reset_residuals()
+    np.testing.assert_array_equal(eng.read_residuals(), inv.residual())
+    b = eng.place_batch(batch)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)

@@ -1,0 +1,93 @@
+"""Host resolver (pe_resolver_* of libplacement) vs the naive sequential oracle, on CPU.
+
+The device scan is replaced by tests/scan_emulator.py (exact per-shard top-K lists); what is
+under test is the product's windowed, sharded, exact resolution protocol and its rollback."""
+import numpy as np
+import pytest
+
+import oracle
+from placement import Resolver, synth
+from scan_emulator import keys, run_resolver
+
+
+def small_world(n_nodes, n_jobs, seed, mix="pytorch", gpu_frac=0.2):
+    inv = synth.make_inventory(n_nodes, seed, gpu_frac)
+    batch = synth.make_jobs(n_jobs, seed, mix)
+    return inv, batch
+
+
+def oracle_run(inv, batch):
+    return oracle.place_greedy(inv.residual(), inv.labels, batch.job_group_off, batch.priority, batch.group_count,
+                               batch.group_req, batch.group_need)
+
+
+def test_emulator_keys_match_c_oracle():
+    inv = synth.make_inventory(300, 11)
+    req, need = synth.pod_requests(11, 900, 20)
+    res = inv.residual()
+    for j in range(20):
+        k = keys(res, inv.labels, req[j], int(need[j]), 0)
+        for n in range(0, 300, 7):
+            assert int(k[n]) == oracle.key(res[:, n], inv.labels[n], req[j], need[j], n)
+
+
+@pytest.mark.parametrize("mix,gpu_frac", [("pytorch", 0.2), ("mixed", 0.3), ("gang8", 1.0)])
+@pytest.mark.parametrize("shards", [1, 2, 3])
+def test_resolver_matches_oracle(mix, gpu_frac, shards):
+    inv, batch = small_world(700, 60, 5, mix, gpu_frac)
+    want_pods, want_st, want_res = oracle_run(inv, batch)
+    pods, st, res = run_resolver(Resolver, inv.residual(), inv.labels, batch, K=8, shards=shards)
+    np.testing.assert_array_equal(st, want_st)
+    np.testing.assert_array_equal(pods, want_pods)
+    np.testing.assert_array_equal(res, want_res)
+    assert 0 < (st == 0).sum() < len(st) or mix == "gang8"   # exercises placement AND rollback
+
+
+@pytest.mark.parametrize("K,max_groups,max_pods", [(1, 1, 1), (1, 8, 64), (2, 4, 16), (32, 64, 1024)])
+def test_resolver_window_shapes(K, max_groups, max_pods):
+    inv, batch = small_world(400, 40, 9, "mixed", 0.3)
+    want = oracle_run(inv, batch)
+    got = run_resolver(Resolver, inv.residual(), inv.labels, batch, K=K, shards=2, max_groups=max_groups,
+                       max_pods=max_pods)
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_resolver_weak_limits_force_rescans():
+    inv, batch = small_world(500, 50, 13, "pytorch", 0.25)
+    want = oracle_run(inv, batch)
+    got = run_resolver(Resolver, inv.residual(), inv.labels, batch, K=16, shards=2, weak=True, seed=3)
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_resolver_edge_cases():
+    # empty jobs, zero-pod groups, a job that can never fit, equal scores (ties -> lowest id)
+    N = 16
+    cap = np.zeros((4, N), np.int64)
+    cap[0], cap[1], cap[2], cap[3] = 4000, 8 << 30, 0, 1 << 30
+    used = np.zeros_like(cap)
+    labels = np.full(N, 2, np.uint32)
+    jgo = np.array([0, 0, 2, 3, 4], np.int32)          # job0: no groups
+    pri = np.array([5, 5, 9, 1], np.int32)
+    cnt = np.array([0, 3, 1, 5], np.int32)
+    req = np.array([[1000, 1 << 30, 0, 0]] * 2 + [[1, 1, 1, 0]] + [[2000, 0, 0, 0]], np.int64)
+    need = np.array([0, 0, 0, 2], np.uint32)
+    from placement.synth import JobBatch
+    batch = JobBatch(jgo, pri, cnt, req, need, np.zeros(4, np.int8))
+    want = oracle.place_greedy(cap - used, labels, jgo, pri, cnt, req, need)
+    got = run_resolver(Resolver, cap - used, labels, batch, K=2, shards=2, max_groups=2, max_pods=2)
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+    assert list(want[1]) == [0, 0, 1, 0]                 # the gpu job fails, the rest place
+    assert list(want[0][:3]) == [0, 0, 0]                # identical nodes: best fit packs node 0
+
+
+def test_resolver_rejects_bad_input():
+    from placement import PlacementError
+    with pytest.raises(PlacementError):
+        Resolver(np.array([0, 1], np.int32), np.array([0], np.int32), np.array([-1], np.int32),
+                 np.zeros((1, 4), np.int64))
+    with pytest.raises(PlacementError):
+        Resolver(np.array([0, 1], np.int32), np.array([0], np.int32), np.array([1], np.int32),
+                 -np.ones((1, 4), np.int64))

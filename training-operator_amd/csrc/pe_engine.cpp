@@ -1,0 +1,645 @@
+// libplacement: context, device-resident inventory, C ABI entry points (include/placement.h).
+//
+// One context = one process = one GPU = one contiguous shard of the node inventory.  The
+// inventory lives on the device as int64 struct-of-arrays res[4][stride] (+ labels, islands),
+// so every kernel streams each dimension coalesced.  Sharded contexts exchange per-group
+// candidate lists with one RCCL all-gather per scan window (or a host callback in tests).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "pe_kernels.h"
+#include "pe_resolver.h"
+#include "placement.h"
+
+namespace {
+
+using pe::ReqRec;
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T));
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+template <class T>
+struct HostBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault);
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct PeError {
+  int code;
+  std::string msg;
+};
+
+[[noreturn]] void raise(int code, const std::string& msg) { throw PeError{code, msg}; }
+
+void hipchk(hipError_t e, const char* what) {
+  if (e != hipSuccess) raise(PE_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void ncclchk(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) raise(PE_ERCCL, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+struct pe_ctx {
+  std::mutex mu;
+  int device = 0;
+  int rank = 0, world = 1;
+  ncclComm_t comm = nullptr;
+  pe_allgather_fn exchange = nullptr;
+  void* exchange_user = nullptr;
+  int topk = 64, window_groups = 64;
+  int64_t window_pods = 1024;
+  int64_t max_nodes = 0;
+  std::string gpu_name, err;
+  hipStream_t stream = nullptr;
+  // inventory shard
+  int64_t n_total = 0, begin = 0, end = 0, Ns = 0, stride = 0;
+  bool loaded = false;
+  DevBuf<int64_t> res0, res;
+  DevBuf<uint32_t> labels;
+  DevBuf<int32_t> island;
+  // fit mask
+  int64_t fit_J = 0, Wn = 0;
+  bool fit_uploaded = false;
+  DevBuf<ReqRec> fit_jobs;
+  DevBuf<uint64_t> mask;
+  DevBuf<unsigned long long> counts;
+  HostBuf<unsigned long long> h_counts;
+  // aggregation
+  DevBuf<int32_t> a_jgo, a_mm, a_rep, a_gco, a_mem;
+  DevBuf<int64_t> a_req, a_out;
+  DevBuf<uint8_t> a_fl, a_pres, a_ovf;
+  // greedy
+  DevBuf<ReqRec> g_groups;
+  DevBuf<uint64_t> g_cand, g_bound;
+  DevBuf<int32_t> g_cnt;
+  DevBuf<uint8_t> g_out, g_gath;
+  DevBuf<int64_t> g_upd;
+  HostBuf<ReqRec> h_groups;
+  HostBuf<uint8_t> h_out, h_own;
+  HostBuf<int64_t> h_upd;
+  pe_stats stats{};
+
+  ~pe_ctx() {
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    res0.release(); res.release(); labels.release(); island.release();
+    fit_jobs.release(); mask.release(); counts.release(); h_counts.release();
+    a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
+    a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
+    g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
+    g_upd.release(); h_groups.release(); h_out.release(); h_own.release(); h_upd.release();
+    if (comm) (void)ncclCommDestroy(comm);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+// Every ABI entry runs its body through here: lock, select device, map exceptions to codes.
+template <class F>
+int guarded(pe_ctx* ctx, F&& body) {
+  if (!ctx) return PE_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->err.clear();
+  try {
+    hipchk(hipSetDevice(ctx->device), "hipSetDevice");
+    return body();
+  } catch (const PeError& e) {
+    ctx->err = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    ctx->err = "host allocation failed";
+    return PE_ENOMEM;
+  } catch (...) {
+    ctx->err = "unexpected C++ exception";
+    return PE_EINVAL;
+  }
+}
+
+void need_ptr(const void* p, const char* name) {
+  if (!p) raise(PE_EINVAL, std::string(name) + " is NULL");
+}
+
+void check_req(const int64_t* req, int64_t n, const char* what) {
+  for (int64_t i = 0; i < n * pe::D; ++i)
+    if (req[i] < 0) raise(PE_EINVAL, std::string(what) + ": negative request at index " + std::to_string(i));
+}
+
+void check_offsets(const int32_t* off, int64_t n, int64_t limit, const char* what) {
+  if (off[0] != 0) raise(PE_EINVAL, std::string(what) + "[0] must be 0");
+  for (int64_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i]) raise(PE_EINVAL, std::string(what) + " is not monotonic");
+  if (limit >= 0 && off[n] > limit) raise(PE_EINVAL, std::string(what) + " exceeds its array");
+}
+
+void fill_req(ReqRec& r, const int64_t* q, uint32_t need) {
+  std::memset(&r, 0, sizeof(r));
+  for (int d = 0; d < pe::D; ++d) r.q[d] = q[d];
+  r.need = need;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pe_abi_version(void) { return PE_ABI_VERSION; }
+
+int pe_comm_id(uint8_t out[PE_COMM_ID_BYTES]) {
+  if (!out) return PE_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return PE_ERCCL;
+  static_assert(sizeof(id) <= PE_COMM_ID_BYTES, "unique id size");
+  std::memset(out, 0, PE_COMM_ID_BYTES);
+  std::memcpy(out, &id, sizeof(id));
+  return PE_OK;
+}
+
+int pe_create(const pe_config* cfg, pe_ctx** out) {
+  if (!cfg || !out) return PE_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PE_ENODEV;
+  if (cfg->world_size < 1 || cfg->rank < 0 || cfg->rank >= cfg->world_size) return PE_EINVAL;
+  if (cfg->max_nodes < 0 || cfg->max_nodes > PE_MAX_NODES) return PE_EINVAL;
+  pe_ctx* ctx = new (std::nothrow) pe_ctx();
+  if (!ctx) return PE_ENOMEM;
+  int dev = cfg->device_id;
+  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (dev >= ndev) {
+    delete ctx;
+    return PE_EINVAL;
+  }
+  ctx->device = dev;
+  ctx->rank = cfg->rank;
+  ctx->world = cfg->world_size;
+  ctx->exchange = cfg->exchange;
+  ctx->exchange_user = cfg->exchange_user;
+  ctx->max_nodes = cfg->max_nodes > 0 ? cfg->max_nodes : PE_MAX_NODES;
+  ctx->topk = cfg->topk > 0 ? std::min(cfg->topk, pe::MG_CAP) : 64;
+  ctx->window_groups = cfg->window_groups > 0 ? cfg->window_groups : 64;
+  ctx->window_pods = cfg->window_pods > 0 ? cfg->window_pods : 1024;
+  ctx->gpu_name = cfg->gpu_resource_name ? cfg->gpu_resource_name : "amd.com/gpu";
+  int rc = PE_OK;
+  try {
+    hipchk(hipSetDevice(dev), "hipSetDevice");
+    hipchk(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (ctx->world > 1 && !ctx->exchange) {
+      if (!cfg->comm_id) raise(PE_EINVAL, "world_size > 1 needs comm_id or an exchange callback");
+      ncclUniqueId id;
+      std::memcpy(&id, cfg->comm_id, sizeof(id));
+      ncclchk(ncclCommInitRank(&ctx->comm, ctx->world, id, ctx->rank), "ncclCommInitRank");
+    }
+  } catch (const PeError& e) {
+    rc = e.code;
+  }
+  if (rc != PE_OK) {
+    delete ctx;
+    return rc;
+  }
+  *out = ctx;
+  return PE_OK;
+}
+
+void pe_destroy(pe_ctx* ctx) { delete ctx; }
+
+const char* pe_last_error(const pe_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int pe_load_nodes(pe_ctx* ctx, int64_t n, const int64_t* cap, const int64_t* used, const uint32_t* labels,
+                  const int32_t* island) {
+  return guarded(ctx, [&]() -> int {
+    if (n < 0 || n > ctx->max_nodes) raise(PE_EINVAL, "node count out of range");
+    if (n > 0) {
+      need_ptr(cap, "cap");
+      need_ptr(used, "used");
+    }
+    ctx->n_total = n;
+    ctx->begin = n * ctx->rank / ctx->world;
+    ctx->end = n * (ctx->rank + 1) / ctx->world;
+    ctx->Ns = ctx->end - ctx->begin;
+    ctx->stride = round_up(std::max<int64_t>(ctx->Ns, 1), 256);
+    const size_t cells = (size_t)pe::D * (size_t)ctx->stride;
+    std::vector<int64_t> r(cells, pe::NEVER);
+    std::vector<uint32_t> lab((size_t)ctx->stride, 0u);
+    std::vector<int32_t> isl((size_t)ctx->stride, -1);
+    for (int d = 0; d < pe::D; ++d)
+      for (int64_t i = 0; i < ctx->Ns; ++i) {
+        const int64_t g = ctx->begin + i;
+        const int64_t c = cap[d * n + g], u = used[d * n + g];
+        if (c < 0 || u < 0) raise(PE_EINVAL, "negative capacity/usage");
+        r[(size_t)d * ctx->stride + i] = c - u;
+      }
+    for (int64_t i = 0; i < ctx->Ns; ++i) {
+      lab[i] = labels ? labels[ctx->begin + i] : 0u;
+      isl[i] = island ? island[ctx->begin + i] : -1;
+    }
+    hipchk(ctx->res0.ensure(cells), "alloc res0");
+    hipchk(ctx->res.ensure(cells), "alloc res");
+    hipchk(ctx->labels.ensure((size_t)ctx->stride), "alloc labels");
+    hipchk(ctx->island.ensure((size_t)ctx->stride), "alloc island");
+    hipchk(hipMemcpyAsync(ctx->res0.p, r.data(), cells * 8, hipMemcpyHostToDevice, ctx->stream), "H2D res0");
+    hipchk(hipMemcpyAsync(ctx->res.p, r.data(), cells * 8, hipMemcpyHostToDevice, ctx->stream), "H2D res");
+    hipchk(hipMemcpyAsync(ctx->labels.p, lab.data(), lab.size() * 4, hipMemcpyHostToDevice, ctx->stream), "H2D lab");
+    hipchk(hipMemcpyAsync(ctx->island.p, isl.data(), isl.size() * 4, hipMemcpyHostToDevice, ctx->stream), "H2D isl");
+    hipchk(hipStreamSynchronize(ctx->stream), "sync load");
+    ctx->loaded = true;
+    return PE_OK;
+  });
+}
+
+int pe_reset_residuals(pe_ctx* ctx) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx->loaded) raise(PE_ESTATE, "no inventory loaded");
+    hipchk(hipMemcpyAsync(ctx->res.p, ctx->res0.p, (size_t)pe::D * ctx->stride * 8, hipMemcpyDeviceToDevice,
+                          ctx->stream),
+           "D2D reset");
+    return PE_OK;
+  });
+}
+
+int pe_shard_range(const pe_ctx* ctx, int64_t* begin, int64_t* end) {
+  if (!ctx || !begin || !end) return PE_EINVAL;
+  *begin = ctx->begin;
+  *end = ctx->end;
+  return PE_OK;
+}
+
+int pe_read_residuals(pe_ctx* ctx, int64_t* res_out) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx->loaded) raise(PE_ESTATE, "no inventory loaded");
+    need_ptr(res_out, "res_out");
+    for (int d = 0; d < pe::D; ++d)
+      hipchk(hipMemcpyAsync(res_out + (size_t)d * ctx->Ns, ctx->res.p + (size_t)d * ctx->stride,
+                            (size_t)ctx->Ns * 8, hipMemcpyDeviceToHost, ctx->stream),
+             "D2H res");
+    hipchk(hipStreamSynchronize(ctx->stream), "sync read");
+    return PE_OK;
+  });
+}
+
+int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t* job_group_off,
+                        const int32_t* min_member, const int32_t* group_replicas, const int32_t* group_cont_off,
+                        const int64_t* cont_req, const uint8_t* cont_flags, int64_t* out_min_res,
+                        uint8_t* out_present, int32_t* out_members, uint8_t* out_overflow) {
+  return guarded(ctx, [&]() -> int {
+    if (mode != PE_MODE_V1 && mode != PE_MODE_V2) raise(PE_EINVAL, "mode must be PE_MODE_V1 or PE_MODE_V2");
+    if (n_jobs < 0) raise(PE_EINVAL, "n_jobs < 0");
+    if (n_jobs == 0) return PE_OK;
+    need_ptr(job_group_off, "job_group_off");
+    need_ptr(out_min_res, "out_min_res");
+    need_ptr(out_present, "out_present");
+    need_ptr(out_members, "out_members");
+    need_ptr(out_overflow, "out_overflow");
+    if (mode == PE_MODE_V1) need_ptr(min_member, "min_member");
+    check_offsets(job_group_off, n_jobs, -1, "job_group_off");
+    const int64_t G = job_group_off[n_jobs];
+    if (G > 0) {
+      need_ptr(group_replicas, "group_replicas");
+      need_ptr(group_cont_off, "group_cont_off");
+      check_offsets(group_cont_off, G, -1, "group_cont_off");
+    }
+    const int64_t C = G > 0 ? group_cont_off[G] : 0;
+    if (C > 0) {
+      need_ptr(cont_req, "cont_req");
+      need_ptr(cont_flags, "cont_flags");
+      check_req(cont_req, C, "cont_req");
+    }
+    hipStream_t s = ctx->stream;
+    hipchk(ctx->a_jgo.ensure(n_jobs + 1), "alloc");
+    hipchk(ctx->a_mm.ensure(n_jobs), "alloc");
+    hipchk(ctx->a_rep.ensure(G), "alloc");
+    hipchk(ctx->a_gco.ensure(G + 1), "alloc");
+    hipchk(ctx->a_req.ensure((size_t)C * pe::D), "alloc");
+    hipchk(ctx->a_fl.ensure(C), "alloc");
+    hipchk(ctx->a_out.ensure((size_t)n_jobs * pe::D), "alloc");
+    hipchk(ctx->a_pres.ensure(n_jobs), "alloc");
+    hipchk(ctx->a_mem.ensure(n_jobs), "alloc");
+    hipchk(ctx->a_ovf.ensure(n_jobs), "alloc");
+    hipchk(hipMemcpyAsync(ctx->a_jgo.p, job_group_off, (n_jobs + 1) * 4, hipMemcpyHostToDevice, s), "H2D");
+    if (mode == PE_MODE_V1) hipchk(hipMemcpyAsync(ctx->a_mm.p, min_member, n_jobs * 4, hipMemcpyHostToDevice, s), "H2D");
+    if (G > 0) {
+      hipchk(hipMemcpyAsync(ctx->a_rep.p, group_replicas, G * 4, hipMemcpyHostToDevice, s), "H2D");
+      hipchk(hipMemcpyAsync(ctx->a_gco.p, group_cont_off, (G + 1) * 4, hipMemcpyHostToDevice, s), "H2D");
+    }
+    if (C > 0) {
+      hipchk(hipMemcpyAsync(ctx->a_req.p, cont_req, (size_t)C * pe::D * 8, hipMemcpyHostToDevice, s), "H2D");
+      hipchk(hipMemcpyAsync(ctx->a_fl.p, cont_flags, C, hipMemcpyHostToDevice, s), "H2D");
+    }
+    hipchk(pe::launch_pg_min_resources(s, mode, n_jobs, ctx->a_jgo.p, ctx->a_mm.p, ctx->a_rep.p, ctx->a_gco.p,
+                                       ctx->a_req.p, ctx->a_fl.p, ctx->a_out.p, ctx->a_pres.p, ctx->a_mem.p,
+                                       ctx->a_ovf.p),
+           "launch pg_min_resources");
+    hipchk(hipMemcpyAsync(out_min_res, ctx->a_out.p, (size_t)n_jobs * pe::D * 8, hipMemcpyDeviceToHost, s), "D2H");
+    hipchk(hipMemcpyAsync(out_present, ctx->a_pres.p, n_jobs, hipMemcpyDeviceToHost, s), "D2H");
+    hipchk(hipMemcpyAsync(out_members, ctx->a_mem.p, n_jobs * 4, hipMemcpyDeviceToHost, s), "D2H");
+    hipchk(hipMemcpyAsync(out_overflow, ctx->a_ovf.p, n_jobs, hipMemcpyDeviceToHost, s), "D2H");
+    hipchk(hipStreamSynchronize(s), "sync pg_min_resources");
+    for (int64_t j = 0; j < n_jobs; ++j)
+      if (out_overflow[j]) {
+        ctx->err = "int64 overflow in job " + std::to_string(j);
+        return PE_EOVERFLOW;
+      }
+    return PE_OK;
+  });
+}
+
+// ------------------------------------------------------------------ fit mask
+
+static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
+  if (n_jobs < 0) raise(PE_EINVAL, "n_jobs < 0");
+  if (!ctx->loaded) raise(PE_ESTATE, "no inventory loaded");
+  if (n_jobs > 0) {
+    need_ptr(req, "req");
+    check_req(req, n_jobs, "req");
+  }
+  const int64_t Jp = round_up(std::max<int64_t>(n_jobs, 1), pe::FM_JT);
+  std::vector<ReqRec> recs((size_t)Jp);
+  for (int64_t j = 0; j < Jp; ++j) {
+    if (j < n_jobs) fill_req(recs[j], req + j * pe::D, need ? need[j] : 0u);
+    else {
+      const int64_t never[pe::D] = {INT64_MAX, INT64_MAX, INT64_MAX, INT64_MAX};
+      fill_req(recs[j], never, 0xFFFFFFFFu);
+    }
+  }
+  ctx->fit_J = n_jobs;
+  ctx->Wn = (ctx->Ns + 63) / 64;
+  hipchk(ctx->fit_jobs.ensure(Jp), "alloc fit jobs");
+  hipchk(ctx->mask.ensure((size_t)std::max<int64_t>(n_jobs, 1) * std::max<int64_t>(ctx->Wn, 1)), "alloc fit mask");
+  hipchk(ctx->counts.ensure(Jp), "alloc fit counts");
+  hipchk(ctx->h_counts.ensure(Jp), "alloc pinned counts");
+  hipchk(hipMemcpyAsync(ctx->fit_jobs.p, recs.data(), Jp * sizeof(ReqRec), hipMemcpyHostToDevice, ctx->stream),
+         "H2D fit jobs");
+  hipchk(hipStreamSynchronize(ctx->stream), "sync fit upload");
+  ctx->fit_uploaded = true;
+}
+
+static void fit_run(pe_ctx* ctx) {
+  if (!ctx->fit_uploaded) raise(PE_ESTATE, "pe_jobs_upload first");
+  const int64_t J = ctx->fit_J;
+  hipchk(hipMemsetAsync(ctx->counts.p, 0, ctx->counts.n * sizeof(unsigned long long), ctx->stream), "memset counts");
+  if (J == 0 || ctx->Ns == 0) return;
+  // enough waves to fill 256 CUs several times over; at most 16 tiles (4096 nodes) per wave
+  const int64_t waves_y = (J + pe::FM_JT - 1) / pe::FM_JT;
+  const int64_t want_x = std::max<int64_t>(1, (16384 + waves_y - 1) / waves_y);
+  int64_t tpw = (ctx->Ns + 256 * want_x - 1) / (256 * want_x);
+  tpw = std::min<int64_t>(16, std::max<int64_t>(1, tpw));
+  hipchk(pe::launch_fit_mask(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->Wn, ctx->fit_jobs.p, J,
+                             tpw, ctx->mask.p, ctx->counts.p),
+         "launch fit_mask");
+  ctx->stats.fit_evals += J * ctx->Ns;
+}
+
+static void fit_counts(pe_ctx* ctx, int64_t* out) {
+  const int64_t J = ctx->fit_J;
+  if (J == 0) return;
+  hipchk(hipMemcpyAsync(ctx->h_counts.p, ctx->counts.p, J * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                        ctx->stream),
+         "D2H counts");
+  hipchk(hipStreamSynchronize(ctx->stream), "sync counts");
+  for (int64_t j = 0; j < J; ++j) out[j] = (int64_t)ctx->h_counts.p[j];
+}
+
+int pe_jobs_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
+  return guarded(ctx, [&]() -> int {
+    fit_upload(ctx, n_jobs, req, need);
+    return PE_OK;
+  });
+}
+
+int pe_fit_mask_run(pe_ctx* ctx) {
+  return guarded(ctx, [&]() -> int {
+    fit_run(ctx);
+    return PE_OK;
+  });
+}
+
+int pe_fit_counts(pe_ctx* ctx, int64_t* out) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx->fit_uploaded) raise(PE_ESTATE, "pe_jobs_upload first");
+    need_ptr(out, "out_feasible_count");
+    fit_counts(ctx, out);
+    return PE_OK;
+  });
+}
+
+int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx->fit_uploaded) raise(PE_ESTATE, "pe_jobs_upload first");
+    if (row0 < 0 || n_rows < 0 || row0 + n_rows > ctx->fit_J) raise(PE_EINVAL, "row range");
+    if (n_rows == 0 || ctx->Wn == 0) return PE_OK;
+    need_ptr(out, "out");
+    hipchk(hipMemcpyAsync(out, ctx->mask.p + (size_t)row0 * ctx->Wn, (size_t)n_rows * ctx->Wn * 8,
+                          hipMemcpyDeviceToHost, ctx->stream),
+           "D2H mask");
+    hipchk(hipStreamSynchronize(ctx->stream), "sync mask");
+    return PE_OK;
+  });
+}
+
+int pe_fit_mask(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need, int64_t* out_feasible_count,
+                const uint64_t** dev_mask, int64_t* words_per_row) {
+  return guarded(ctx, [&]() -> int {
+    fit_upload(ctx, n_jobs, req, need);
+    fit_run(ctx);
+    if (out_feasible_count) fit_counts(ctx, out_feasible_count);
+    else hipchk(hipStreamSynchronize(ctx->stream), "sync fit");
+    if (dev_mask) *dev_mask = ctx->mask.p;
+    if (words_per_row) *words_per_row = ctx->Wn;
+    return PE_OK;
+  });
+}
+
+// ------------------------------------------------------------------ greedy placement
+
+int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority,
+                    const int32_t* group_count, const int64_t* group_req, const uint32_t* group_need,
+                    int32_t* out_pod_node, int32_t* out_job_status) {
+  return guarded(ctx, [&]() -> int {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!ctx->loaded) raise(PE_ESTATE, "no inventory loaded");
+    if (n_jobs < 0) raise(PE_EINVAL, "n_jobs < 0");
+    if (n_jobs == 0) return PE_OK;
+    need_ptr(job_group_off, "job_group_off");
+    need_ptr(priority, "priority");
+    need_ptr(out_job_status, "out_job_status");
+    check_offsets(job_group_off, n_jobs, -1, "job_group_off");
+    const int64_t G = job_group_off[n_jobs];
+    int64_t P = 0;
+    if (G > 0) {
+      need_ptr(group_count, "group_count");
+      need_ptr(group_req, "group_req");
+      check_req(group_req, G, "group_req");
+      for (int64_t g = 0; g < G; ++g) {
+        if (group_count[g] < 0) raise(PE_EINVAL, "negative group_count");
+        P += group_count[g];
+      }
+    }
+    if (P > 0) need_ptr(out_pod_node, "out_pod_node");
+    std::vector<uint32_t> no_need;
+    if (!group_need) {
+      no_need.assign((size_t)std::max<int64_t>(G, 1), 0u);
+      group_need = no_need.data();
+    }
+    pe::Resolver R(n_jobs, job_group_off, priority, group_count, group_req, group_need);
+    const int K = ctx->topk;
+    const size_t gb = pe::cand_group_bytes(K);
+    const int Wmax = ctx->window_groups;
+    const int Wpad = (int)round_up(Wmax, pe::SC_GT);
+    const int nwaves = (int)std::max<int64_t>(1, (ctx->Ns + pe::SC_SPAN - 1) / pe::SC_SPAN);
+    hipchk(ctx->g_groups.ensure(Wpad), "alloc groups");
+    hipchk(ctx->h_groups.ensure(Wpad), "alloc pinned groups");
+    hipchk(ctx->g_cand.ensure((size_t)Wpad * nwaves * 64), "alloc cand");
+    hipchk(ctx->g_cnt.ensure((size_t)Wpad * nwaves), "alloc cnt");
+    hipchk(ctx->g_bound.ensure((size_t)Wpad * nwaves), "alloc bound");
+    hipchk(ctx->g_out.ensure((size_t)Wmax * gb), "alloc out");
+    hipchk(ctx->h_out.ensure((size_t)Wmax * gb * ctx->world), "alloc pinned out");
+    if (ctx->world > 1) {
+      hipchk(ctx->g_gath.ensure((size_t)Wmax * gb * ctx->world), "alloc gather");
+      hipchk(ctx->h_own.ensure((size_t)Wmax * gb), "alloc pinned own");
+    }
+    std::vector<int32_t> groups;
+    std::vector<pe::GroupCands> cands;
+    std::vector<pe::Update> updates;
+    hipStream_t s = ctx->stream;
+    while (!R.done()) {
+      R.next_window(Wmax, ctx->window_pods, groups);
+      if (groups.empty()) break;
+      const int Wg = (int)groups.size();
+      const int Wgp = (int)round_up(Wg, pe::SC_GT);
+      for (int w = 0; w < Wgp; ++w) {
+        const int g = groups[std::min(w, Wg - 1)];
+        fill_req(ctx->h_groups.p[w], group_req + (int64_t)g * pe::D, group_need[g]);
+      }
+      hipchk(hipMemcpyAsync(ctx->g_groups.p, ctx->h_groups.p, Wgp * sizeof(ReqRec), hipMemcpyHostToDevice, s),
+             "H2D window");
+      if (ctx->Ns > 0) {
+        hipchk(pe::launch_scan(s, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, (uint64_t)ctx->begin,
+                               ctx->g_groups.p, Wg, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p, nwaves),
+               "launch scan");
+        hipchk(pe::launch_merge(s, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p, nwaves, K, ctx->res.p, ctx->stride,
+                                ctx->labels.p, (uint64_t)ctx->begin, ctx->g_out.p, Wg),
+               "launch merge");
+      } else {
+        std::vector<uint8_t> empty((size_t)Wg * gb, 0);
+        for (int w = 0; w < Wg; ++w) {
+          pe::CandHdr h{0, 0, pe::NO_KEY};
+          std::memcpy(empty.data() + (size_t)w * gb, &h, sizeof(h));
+        }
+        hipchk(hipMemcpyAsync(ctx->g_out.p, empty.data(), empty.size(), hipMemcpyHostToDevice, s), "H2D empty");
+        hipchk(hipStreamSynchronize(s), "sync empty");
+      }
+      const size_t bytes = (size_t)Wg * gb;
+      if (ctx->world == 1) {
+        hipchk(hipMemcpyAsync(ctx->h_out.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
+        hipchk(hipStreamSynchronize(s), "sync window");
+      } else if (ctx->exchange) {
+        hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
+        hipchk(hipStreamSynchronize(s), "sync window");
+        if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, ctx->h_out.p, bytes) != 0)
+          raise(PE_ERCCL, "exchange callback failed");
+      } else {
+        ncclchk(ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
+        hipchk(hipMemcpyAsync(ctx->h_out.p, ctx->g_gath.p, bytes * ctx->world, hipMemcpyDeviceToHost, s),
+               "D2H gathered");
+        hipchk(hipStreamSynchronize(s), "sync window");
+      }
+      pe::parse_window(ctx->h_out.p, ctx->world, Wg, K, cands);
+      updates.clear();
+      R.resolve(groups, cands, updates);
+      int64_t nu = 0;
+      hipchk(ctx->h_upd.ensure(std::max<size_t>(updates.size(), 1) * (pe::D + 1)), "alloc pinned upd");
+      for (const pe::Update& u : updates) {
+        if (u.gid < ctx->begin || u.gid >= ctx->end) continue;
+        int64_t* o = ctx->h_upd.p + nu * (pe::D + 1);
+        o[0] = u.gid - ctx->begin;
+        for (int d = 0; d < pe::D; ++d) o[1 + d] = u.res[d];
+        ++nu;
+      }
+      if (nu > 0) {
+        hipchk(ctx->g_upd.ensure((size_t)nu * (pe::D + 1)), "alloc upd");
+        hipchk(hipMemcpyAsync(ctx->g_upd.p, ctx->h_upd.p, (size_t)nu * (pe::D + 1) * 8, hipMemcpyHostToDevice, s),
+               "H2D upd");
+        hipchk(pe::launch_apply(s, ctx->res.p, ctx->stride, ctx->g_upd.p, nu), "launch apply");
+      }
+      ctx->stats.windows += 1;
+      ctx->stats.groups_scanned += Wg;
+      ctx->stats.scan_evals += (int64_t)Wg * ctx->Ns;
+    }
+    hipchk(hipStreamSynchronize(s), "sync greedy");
+    if (P > 0) std::memcpy(out_pod_node, R.pod_node().data(), (size_t)P * 4);
+    std::memcpy(out_job_status, R.job_status().data(), (size_t)n_jobs * 4);
+    ctx->stats.rescans += R.rescans();
+    ctx->stats.pods_placed += R.pods_placed();
+    ctx->stats.jobs_placed += R.jobs_placed();
+    ctx->stats.jobs_failed += R.jobs_failed();
+    ctx->stats.last_greedy_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return PE_OK;
+  });
+}
+
+int pe_synchronize(pe_ctx* ctx) {
+  return guarded(ctx, [&]() -> int {
+    hipchk(hipStreamSynchronize(ctx->stream), "sync");
+    return PE_OK;
+  });
+}
+
+void* pe_stream(pe_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int pe_get_stats(const pe_ctx* ctx, pe_stats* out) {
+  if (!ctx || !out) return PE_EINVAL;
+  *out = ctx->stats;
+  return PE_OK;
+}
+
+int pe_reset_stats(pe_ctx* ctx) {
+  if (!ctx) return PE_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->stats = pe_stats{};
+  return PE_OK;
+}
+
+}  // extern "C"

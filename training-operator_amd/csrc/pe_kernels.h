@@ -1,0 +1,72 @@
+// Device-side building blocks of libplacement (gfx950).  Host code in pe_engine.cpp launches
+// these through the wrappers below; nothing here is part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pe {
+
+constexpr int D = 4;                    // cpu milli, memory B, gpu count, ephemeral-storage B
+constexpr uint64_t SCORE_MAX = (1ull << 40) - 1;
+constexpr uint64_t NO_KEY = ~0ull;
+constexpr int64_t NEVER = INT64_MIN;    // residual of padding nodes: nothing fits
+
+// One request vector (a pod template / a fit-mask job), 64 B so a wave loads it with one
+// scalar s_load_dwordx16 and it never straddles two scalar-cache lines.
+struct alignas(64) ReqRec {
+  int64_t q[D];
+  uint32_t need;
+  uint32_t pad_[7];
+};
+static_assert(sizeof(ReqRec) == 64, "ReqRec must be 64 B");
+
+// Candidate record shipped to the host resolver: key + the node's residual at scan time.
+struct CandRec {
+  uint64_t key;
+  int64_t res[D];
+  uint64_t labels;
+};
+static_assert(sizeof(CandRec) == 48, "CandRec must be 48 B");
+
+struct CandHdr {
+  int32_t n;       // valid records (sorted by key ascending)
+  int32_t flags;   // bit0: merge overflowed LDS, list truncated to the exact minimum
+  uint64_t limit;  // every clean node with key < limit is in the list
+};
+static_assert(sizeof(CandHdr) == 16, "CandHdr must be 16 B");
+
+__host__ __device__ inline size_t cand_group_bytes(int K) { return sizeof(CandHdr) + (size_t)K * sizeof(CandRec); }
+
+// ---- geometry shared by host and device
+constexpr int FM_CH = 4;       // fit mask: 64-node chunks per wave tile (256 nodes in VGPRs)
+constexpr int FM_JT = 256;     // fit mask: jobs per wave
+constexpr int SC_M = 16;       // scan: nodes per lane (wave span 1024 nodes)
+constexpr int SC_GT = 8;       // scan: groups per wave (top-2 state in registers)
+constexpr int SC_SPAN = 64 * SC_M;
+constexpr int MG_CAP = 8192;   // merge: LDS candidate capacity per group
+constexpr int MG_THREADS = 1024;
+
+// ---- launch wrappers (return hipError_t of the launch)
+hipError_t launch_pg_min_resources(hipStream_t s, int mode, int64_t n_jobs, const int32_t* job_group_off,
+                                   const int32_t* min_member, const int32_t* group_replicas,
+                                   const int32_t* group_cont_off, const int64_t* cont_req,
+                                   const uint8_t* cont_flags, int64_t* out_res, uint8_t* out_present,
+                                   int32_t* out_members, uint8_t* out_overflow);
+
+// mask is [J][Wn] u64 row-major, bit n%64 of word n/64 = fit(job j, local node n)
+hipError_t launch_fit_mask(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
+                           int64_t Ns, int64_t Wn, const ReqRec* jobs, int64_t J, int64_t tiles_per_wave,
+                           uint64_t* mask, unsigned long long* counts);
+
+hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
+                       uint64_t id_base, const ReqRec* groups, int Wg, uint64_t* cand, int32_t* cnt,
+                       uint64_t* bound, int nwaves);
+
+hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt, const uint64_t* bound,
+                        int nwaves, int K, const int64_t* res, int64_t stride, const uint32_t* labels,
+                        uint64_t id_base, uint8_t* out, int Wg);
+
+// upd: [n] records {local node (i64), res[4]} -> res[d][node] = value (absolute)
+hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n);
+
+}  // namespace pe

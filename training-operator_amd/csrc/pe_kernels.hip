@@ -1,0 +1,461 @@
+// Hand-written CDNA4 (gfx950) kernels of the gang-placement hot path.
+//
+//   pg_min_resources  v1 CalcPGMinResources / v2 CoScheduling.Build aggregation, one job per lane
+//   fit_mask          J x N feasibility bitmask: node residuals streamed coalesced into VGPRs, the
+//                     job's request is wave-uniform (scalar loads), one v_cmp per dimension turns
+//                     into a 64-bit lane mask (the wave64 ballot IS the mask word)
+//   scan              best-fit window scan: per lane top-2 over its nodes, wave bound, ballot
+//                     compaction of the lane minima below the bound (exact per-wave candidates)
+//   merge             per group: candidates below the min bound -> LDS -> bitonic sort -> top-K
+//                     records (key + residual snapshot) for the host resolver
+//   apply             scatter the resolver's residual updates back into the SoA
+//
+// Integer compare/reduce only: no MFMA (nothing is a contraction).  Roofline = HBM / VALU issue.
+#include "pe_kernels.h"
+
+namespace pe {
+
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = umin64(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// ------------------------------------------------------------------ aggregation (sec. 8a a6/a10/a13)
+
+__device__ __forceinline__ bool add_ovf(int64_t a, int64_t b, int64_t* r) { return __builtin_add_overflow(a, b, r); }
+__device__ __forceinline__ bool mul_ovf(int64_t a, int64_t b, int64_t* r) { return __builtin_mul_overflow(a, b, r); }
+
+__global__ __launch_bounds__(256) void pg_min_resources_kernel(
+    int mode, int64_t n_jobs, const int32_t* __restrict__ job_group_off, const int32_t* __restrict__ min_member,
+    const int32_t* __restrict__ group_replicas, const int32_t* __restrict__ group_cont_off,
+    const int64_t* __restrict__ cont_req, const uint8_t* __restrict__ cont_flags, int64_t* __restrict__ out_res,
+    uint8_t* __restrict__ out_present, int32_t* __restrict__ out_members, uint8_t* __restrict__ out_overflow) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  int64_t acc[D] = {0, 0, 0, 0};
+  uint32_t pres = 0, members = 0;
+  bool ovf = false;
+  int32_t pod_cnt = 0;
+  const int32_t mm = mode == 1 ? min_member[j] : 0;
+  for (int32_t g = job_group_off[j]; g < job_group_off[j + 1]; ++g) {
+    const int32_t r = group_replicas[g];
+    int64_t k;
+    if (mode == 1) {                       // util.go:126-141: count pods until podCnt == minMember
+      if (r <= 0) continue;                // Replicas == nil (-1) or an empty loop
+      const int64_t room = (int64_t)mm - pod_cnt;
+      if (room <= 0) continue;
+      k = r < room ? r : room;
+      pod_cnt += (int32_t)k;
+    } else {                               // coscheduling.go:110-111: int32 members wrap like Go
+      members += (uint32_t)r;
+      k = r;
+    }
+    int64_t side[D] = {0, 0, 0, 0}, initmax[D] = {0, 0, 0, 0}, main_[D] = {0, 0, 0, 0}, over[D] = {0, 0, 0, 0};
+    uint32_t pp = 0;
+    for (int32_t c = group_cont_off[g]; c < group_cont_off[g + 1]; ++c) {
+      const uint32_t fl = cont_flags[c];
+      const uint32_t kind = (fl >> 4) & 3u;
+      if (mode == 1 && kind != 0) continue;  // v1 ignores init containers and overhead
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        if (!(fl & (1u << d))) continue;
+        const int64_t v = cont_req[(int64_t)c * D + d];
+        pp |= 1u << d;
+        if (kind == 0) ovf |= add_ovf(main_[d], v, &main_[d]);
+        else if (kind == 2) ovf |= add_ovf(side[d], v, &side[d]);
+        else if (kind == 3) ovf |= add_ovf(over[d], v, &over[d]);
+        else {                               // kueue: init_i + sidecars declared before it
+          int64_t u;
+          ovf |= add_ovf(side[d], v, &u);
+          initmax[d] = u > initmax[d] ? u : initmax[d];
+        }
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (!(pp & (1u << d))) continue;
+      int64_t pod, t;
+      ovf |= add_ovf(side[d], main_[d], &pod);          // v1: side/initmax/over are all 0
+      pod = initmax[d] > pod ? initmax[d] : pod;
+      ovf |= add_ovf(pod, over[d], &pod);
+      ovf |= mul_ovf(pod, k, &t);
+      ovf |= add_ovf(acc[d], t, &acc[d]);
+    }
+    pres |= pp;
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) out_res[j * D + d] = acc[d];
+  out_present[j] = (uint8_t)pres;
+  out_members[j] = mode == 1 ? pod_cnt : (int32_t)members;
+  out_overflow[j] = ovf ? 1 : 0;
+}
+
+hipError_t launch_pg_min_resources(hipStream_t s, int mode, int64_t n_jobs, const int32_t* job_group_off,
+                                   const int32_t* min_member, const int32_t* group_replicas,
+                                   const int32_t* group_cont_off, const int64_t* cont_req,
+                                   const uint8_t* cont_flags, int64_t* out_res, uint8_t* out_present,
+                                   int32_t* out_members, uint8_t* out_overflow) {
+  if (n_jobs <= 0) return hipSuccess;
+  const unsigned blocks = (unsigned)((n_jobs + 255) / 256);
+  hipLaunchKernelGGL(pg_min_resources_kernel, dim3(blocks), dim3(256), 0, s, mode, n_jobs, job_group_off,
+                     min_member, group_replicas, group_cont_off, cont_req, cont_flags, out_res, out_present,
+                     out_members, out_overflow);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ fit mask (config 5)
+//
+// Wave tile = FM_CH chunks of 64 nodes held in VGPRs (4 dims x int64 + labels) x FM_JT jobs.
+// Per (job, chunk): 4 x v_cmp_le_i64 against SGPR requests (+ a label test only when the job
+// needs labels) -> the 64-bit lane mask is the output word.  16 jobs x 4 chunks of words are
+// gathered into one VGPR pair by v_writelane and leave as one 512-B store (16 rows x 32 B).
+// Per-job popcounts: s_bcnt1 in SALU, accumulated lane-distributed across the wave's tiles,
+// one global atomic per (job, wave).
+
+// v_writelane_b32 with an immediate lane: the compiler's select->writelane fold hoists 64
+// lane==k masks into SGPRs and spills them; the immediate form needs no mask and no SGPR.
+template <int L>
+__device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t uniform_val) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(old) : "s"(uniform_val), "i"(L));
+  return old;
+}
+
+template <int JJ>
+__device__ __forceinline__ void wl4(int c, uint32_t& lo, uint32_t& hi, uint64_t w) {
+  // c is a compile-time constant after unrolling; dispatch to the immediate-lane form
+  switch (c) {
+    case 0: lo = writelane<JJ * 4 + 0>(lo, (uint32_t)w); hi = writelane<JJ * 4 + 0>(hi, (uint32_t)(w >> 32)); break;
+    case 1: lo = writelane<JJ * 4 + 1>(lo, (uint32_t)w); hi = writelane<JJ * 4 + 1>(hi, (uint32_t)(w >> 32)); break;
+    case 2: lo = writelane<JJ * 4 + 2>(lo, (uint32_t)w); hi = writelane<JJ * 4 + 2>(hi, (uint32_t)(w >> 32)); break;
+    default: lo = writelane<JJ * 4 + 3>(lo, (uint32_t)w); hi = writelane<JJ * 4 + 3>(hi, (uint32_t)(w >> 32)); break;
+  }
+}
+
+template <int JJ>
+__device__ __forceinline__ void fm_job(const ReqRec* __restrict__ q, const int64_t (&r)[FM_CH][D],
+                                       const uint32_t (&lab)[FM_CH], uint32_t& col_lo, uint32_t& col_hi) {
+  const int64_t q0 = q->q[0], q1 = q->q[1], q2 = q->q[2], q3 = q->q[3];
+  const uint32_t need = q->need;
+  if (need) {
+#pragma unroll
+    for (int c = 0; c < FM_CH; ++c) {
+      const uint64_t w = __builtin_amdgcn_ballot_w64((lab[c] & need) == need) & __builtin_amdgcn_ballot_w64(q0 <= r[c][0]) &
+                         __builtin_amdgcn_ballot_w64(q1 <= r[c][1]) & __builtin_amdgcn_ballot_w64(q2 <= r[c][2]) &
+                         __builtin_amdgcn_ballot_w64(q3 <= r[c][3]);
+      wl4<JJ>(c, col_lo, col_hi, w);
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < FM_CH; ++c) {
+      // one ballot per compare: each folds into its v_cmp's SGPR mask, the AND runs on the SALU
+      const uint64_t w = __builtin_amdgcn_ballot_w64(q0 <= r[c][0]) & __builtin_amdgcn_ballot_w64(q1 <= r[c][1]) &
+                         __builtin_amdgcn_ballot_w64(q2 <= r[c][2]) & __builtin_amdgcn_ballot_w64(q3 <= r[c][3]);
+      wl4<JJ>(c, col_lo, col_hi, w);
+    }
+  }
+}
+
+template <int JJ>
+__device__ __forceinline__ void fm_jobs(const ReqRec* __restrict__ q, const int64_t (&r)[FM_CH][D],
+                                        const uint32_t (&lab)[FM_CH], uint32_t& col_lo, uint32_t& col_hi) {
+  fm_job<JJ>(q + JJ, r, lab, col_lo, col_hi);
+  if constexpr (JJ + 1 < 16) fm_jobs<JJ + 1>(q, r, lab, col_lo, col_hi);
+}
+
+// Wave tile = FM_CH chunks of 64 nodes held in VGPRs (4 dims x int64 + labels) x FM_JT jobs.
+// Per (job, chunk): 4 x v_cmp_le_i64 against the job's SGPR request (+ a label test only for
+// jobs that need labels); the AND of the lane masks (SALU) is the output word.  16 jobs x 4
+// chunks of words are placed in one VGPR pair by v_writelane and leave as one 512-B store
+// (16 rows x 32 B).  Per-job popcounts come from the stored words (v_bcnt, 4-lane reduction,
+// one permute into the lane-distributed counter) and leave with one atomic per (job, wave).
+__global__ __launch_bounds__(256) void fit_mask_kernel(
+    const int64_t* __restrict__ res, int64_t stride, const uint32_t* __restrict__ labels, int64_t Ns, int64_t Wn,
+    const ReqRec* __restrict__ jobs, int64_t J, int64_t tiles_per_wave, uint64_t* __restrict__ mask,
+    unsigned long long* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_id = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t node_base = wave_id * tiles_per_wave * (64 * FM_CH);
+  if (node_base >= Ns) return;
+  const int64_t j0 = (int64_t)blockIdx.y * FM_JT;
+  unsigned cnt[FM_JT / 64];
+#pragma unroll
+  for (int kb = 0; kb < FM_JT / 64; ++kb) cnt[kb] = 0;
+
+  for (int64_t t = 0; t < tiles_per_wave; ++t) {
+    const int64_t tile0 = node_base + t * (64 * FM_CH);
+    if (tile0 >= Ns) break;
+    int64_t r[FM_CH][D];
+    uint32_t lab[FM_CH];
+#pragma unroll
+    for (int c = 0; c < FM_CH; ++c) {
+      const int64_t n = tile0 + c * 64 + lane;
+      const bool ok = n < Ns;
+#pragma unroll
+      for (int d = 0; d < D; ++d) r[c][d] = ok ? res[d * stride + n] : NEVER;
+      lab[c] = ok ? labels[n] : 0u;
+    }
+    const int64_t chunk0 = tile0 >> 6;
+#pragma unroll
+    for (int kb = 0; kb < FM_JT / 64; ++kb) {
+      for (int jg = 0; jg < 4; ++jg) {
+        const int64_t jrow0 = j0 + kb * 64 + jg * 16;
+        if (jrow0 >= J) break;                       // wave-uniform
+        uint32_t col_lo = 0, col_hi = 0;
+        fm_jobs<0>(jobs + jrow0, r, lab, col_lo, col_hi);   // jobs padded to FM_JT on the device
+        const int64_t row = jrow0 + (lane >> 2);
+        const int64_t chunk = chunk0 + (lane & 3);
+        const bool valid = row < J && chunk < Wn;
+        if (valid) mask[row * Wn + chunk] = ((uint64_t)col_hi << 32) | col_lo;
+        // popcount of this lane's word, summed over the 4 chunk lanes of each row
+        unsigned pc = valid ? (unsigned)(__popc(col_lo) + __popc(col_hi)) : 0u;
+        pc += __shfl_xor(pc, 1, 64);
+        pc += __shfl_xor(pc, 2, 64);
+        // lane jg*16 + i of cnt[kb] counts job jrow0 + i, whose sum sits in lane 4i
+        const int src = (lane & 15) * 4;
+        const unsigned got = __shfl(pc, src, 64);
+        if ((lane >> 4) == jg) cnt[kb] += got;
+      }
+    }
+  }
+#pragma unroll
+  for (int kb = 0; kb < FM_JT / 64; ++kb) {
+    const int64_t j = j0 + kb * 64 + lane;
+    if (j < J && cnt[kb]) atomicAdd(&counts[j], (unsigned long long)cnt[kb]);
+  }
+}
+
+hipError_t launch_fit_mask(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
+                           int64_t Wn, const ReqRec* jobs, int64_t J, int64_t tiles_per_wave, uint64_t* mask,
+                           unsigned long long* counts) {
+  if (J <= 0 || Ns <= 0) return hipSuccess;
+  const int64_t span = tiles_per_wave * 64 * FM_CH;
+  const int64_t waves = (Ns + span - 1) / span;
+  dim3 grid((unsigned)((waves + 3) / 4), (unsigned)((J + FM_JT - 1) / FM_JT));
+  hipLaunchKernelGGL(fit_mask_kernel, grid, dim3(256), 0, s, res, stride, labels, Ns, Wn, jobs, J, tiles_per_wave,
+                     mask, counts);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ best-fit scan (configs 2-4)
+
+// Appendix B key: fit ? (score << 24) | gid : NO_KEY, score = min(a+b+c+d, 2^40-1) with
+// a = left_cpu, b = left_mem >> 20, c = left_gpu << 20, d = left_eph >> 24, each term saturated.
+__device__ __forceinline__ uint64_t node_key(int64_t r0, int64_t r1, int64_t r2, int64_t r3, uint32_t lab,
+                                             int64_t q0, int64_t q1, int64_t q2, int64_t q3, uint32_t need,
+                                             uint64_t gid) {
+  const bool fit = ((lab & need) == need) & (q0 <= r0) & (q1 <= r1) & (q2 <= r2) & (q3 <= r3);
+  const uint64_t a = (uint64_t)r0 - (uint64_t)q0;
+  const uint64_t b = ((uint64_t)r1 - (uint64_t)q1) >> 20;
+  const uint64_t c = (uint64_t)r2 - (uint64_t)q2;
+  const uint64_t d = ((uint64_t)r3 - (uint64_t)q3) >> 24;
+  const bool big = (a > SCORE_MAX) | (b > SCORE_MAX) | (c >= (1ull << 20)) | (d > SCORE_MAX);
+  const uint64_t sum = a + b + (c << 20) + d;      // < 2^42 whenever !big
+  const uint64_t score = (big | (sum > SCORE_MAX)) ? SCORE_MAX : sum;
+  return fit ? ((score << 24) | gid) : NO_KEY;
+}
+
+__global__ __launch_bounds__(256) void scan_kernel(const int64_t* __restrict__ res, int64_t stride,
+                                                   const uint32_t* __restrict__ labels, int64_t Ns, uint64_t id_base,
+                                                   const ReqRec* __restrict__ groups, int Wg,
+                                                   uint64_t* __restrict__ cand, int32_t* __restrict__ cnt,
+                                                   uint64_t* __restrict__ bound, int nwaves) {
+  const int lane = threadIdx.x & 63;
+  const int wave_id = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wave_id >= nwaves) return;
+  const int g0 = blockIdx.y * SC_GT;
+  int64_t q[SC_GT][D];
+  uint32_t need[SC_GT];
+#pragma unroll
+  for (int g = 0; g < SC_GT; ++g) {                // groups padded to SC_GT on the device
+    const ReqRec& gr = groups[g0 + g];
+#pragma unroll
+    for (int d = 0; d < D; ++d) q[g][d] = gr.q[d];
+    need[g] = gr.need;
+  }
+  uint64_t m[SC_GT], s2[SC_GT];
+#pragma unroll
+  for (int g = 0; g < SC_GT; ++g) m[g] = s2[g] = NO_KEY;
+  const int64_t base = (int64_t)wave_id * SC_SPAN;
+  for (int i = 0; i < SC_M; ++i) {
+    const int64_t n = base + i * 64 + lane;
+    const bool ok = n < Ns;
+    const int64_t r0 = ok ? res[n] : NEVER;
+    const int64_t r1 = ok ? res[stride + n] : NEVER;
+    const int64_t r2 = ok ? res[2 * stride + n] : NEVER;
+    const int64_t r3 = ok ? res[3 * stride + n] : NEVER;
+    const uint32_t lab = ok ? labels[n] : 0u;
+    const uint64_t gid = id_base + (uint64_t)n;
+#pragma unroll
+    for (int g = 0; g < SC_GT; ++g) {
+      const uint64_t k = node_key(r0, r1, r2, r3, lab, q[g][0], q[g][1], q[g][2], q[g][3], need[g], gid);
+      const bool lt_m = k < m[g];
+      const bool lt_s = k < s2[g];
+      s2[g] = lt_m ? m[g] : (lt_s ? k : s2[g]);
+      m[g] = lt_m ? k : m[g];
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < SC_GT; ++g) {
+    if (g0 + g >= Wg) break;
+    const uint64_t B = wave_min_u64(s2[g]);        // every key < B in this wave is some lane's minimum
+    const bool take = m[g] < B;
+    const uint64_t bal = __ballot(take);
+    const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+    const size_t slot = (size_t)(g0 + g) * (size_t)nwaves + (size_t)wave_id;
+    if (take) cand[slot * 64 + pos] = m[g];
+    if (lane == 0) {
+      cnt[slot] = __popcll(bal);
+      bound[slot] = B;
+    }
+  }
+}
+
+hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
+                       uint64_t id_base, const ReqRec* groups, int Wg, uint64_t* cand, int32_t* cnt, uint64_t* bound,
+                       int nwaves) {
+  if (Wg <= 0 || nwaves <= 0) return hipSuccess;
+  dim3 grid((unsigned)((nwaves + 3) / 4), (unsigned)((Wg + SC_GT - 1) / SC_GT));
+  hipLaunchKernelGGL(scan_kernel, grid, dim3(256), 0, s, res, stride, labels, Ns, id_base, groups, Wg, cand, cnt,
+                     bound, nwaves);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ merge: per-group exact top-K
+
+__global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __restrict__ cand,
+                                                           const int32_t* __restrict__ cnt,
+                                                           const uint64_t* __restrict__ bound, int nwaves, int K,
+                                                           const int64_t* __restrict__ res, int64_t stride,
+                                                           const uint32_t* __restrict__ labels, uint64_t id_base,
+                                                           uint8_t* __restrict__ out) {
+  __shared__ uint64_t keys[MG_CAP];
+  __shared__ uint64_t red[MG_THREADS / 64];
+  __shared__ int total;
+  const int g = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t gbase = (size_t)g * (size_t)nwaves;
+
+  uint64_t b = NO_KEY;
+  for (int w = tid; w < nwaves; w += MG_THREADS) b = umin64(b, bound[gbase + w]);
+  b = wave_min_u64(b);
+  if (lane == 0) red[wave] = b;
+  if (tid == 0) total = 0;
+  __syncthreads();
+  uint64_t G = NO_KEY;
+#pragma unroll
+  for (int i = 0; i < MG_THREADS / 64; ++i) G = umin64(G, red[i]);
+  __syncthreads();
+
+  for (int w = wave; w < nwaves; w += MG_THREADS / 64) {
+    const int c = cnt[gbase + w];
+    const uint64_t k = lane < c ? cand[(gbase + w) * 64 + lane] : NO_KEY;
+    const bool take = k < G;
+    const uint64_t bal = __ballot(take);
+    if (bal) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&total, (int)__popcll(bal));
+      base = __shfl(base, 0, 64);
+      const int pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+      if (take && pos < MG_CAP) keys[pos] = k;
+    }
+  }
+  __syncthreads();
+  const int T = total;
+  int nout, flags = 0;
+  uint64_t limit;
+  if (T > MG_CAP) {
+    // Overflow (pathological): keep only the exact minimum over every candidate.
+    uint64_t mn = NO_KEY;
+    for (int w = wave; w < nwaves; w += MG_THREADS / 64) {
+      const int c = cnt[gbase + w];
+      if (lane < c) mn = umin64(mn, cand[(gbase + w) * 64 + lane]);
+    }
+    mn = wave_min_u64(mn);
+    __syncthreads();
+    if (lane == 0) red[wave] = mn;
+    __syncthreads();
+    mn = NO_KEY;
+#pragma unroll
+    for (int i = 0; i < MG_THREADS / 64; ++i) mn = umin64(mn, red[i]);
+    __syncthreads();
+    if (tid == 0) keys[0] = mn;
+    __syncthreads();
+    nout = 1;
+    limit = mn + 1;
+    flags = 1;
+  } else {
+    int P = 2;
+    while (P < T) P <<= 1;
+    for (int i = T + tid; i < P; i += MG_THREADS) keys[i] = NO_KEY;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < P; i += MG_THREADS) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const uint64_t a = keys[i], c = keys[ixj];
+            const bool up = (i & k) == 0;
+            if ((a > c) == up) {
+              keys[i] = c;
+              keys[ixj] = a;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    nout = T < K ? T : K;
+    limit = T > K ? keys[K] : G;
+  }
+  uint8_t* og = out + (size_t)g * cand_group_bytes(K);
+  CandRec* recs = reinterpret_cast<CandRec*>(og + sizeof(CandHdr));
+  for (int i = tid; i < nout; i += MG_THREADS) {
+    const uint64_t key = keys[i];
+    const int64_t n = (int64_t)((key & 0xFFFFFFull) - id_base);
+    CandRec r;
+    r.key = key;
+#pragma unroll
+    for (int d = 0; d < D; ++d) r.res[d] = res[d * stride + n];
+    r.labels = labels[n];
+    recs[i] = r;
+  }
+  if (tid == 0) {
+    CandHdr h;
+    h.n = nout;
+    h.flags = flags;
+    h.limit = limit;
+    *reinterpret_cast<CandHdr*>(og) = h;
+  }
+}
+
+hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt, const uint64_t* bound, int nwaves,
+                        int K, const int64_t* res, int64_t stride, const uint32_t* labels, uint64_t id_base,
+                        uint8_t* out, int Wg) {
+  if (Wg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(merge_kernel, dim3(Wg), dim3(MG_THREADS), 0, s, cand, cnt, bound, nwaves, K, res, stride, labels,
+                     id_base, out);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ apply residual updates
+
+__global__ __launch_bounds__(256) void apply_kernel(int64_t* __restrict__ res, int64_t stride,
+                                                    const int64_t* __restrict__ upd, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t* u = upd + i * (D + 1);
+  const int64_t node = u[0];
+#pragma unroll
+  for (int d = 0; d < D; ++d) res[d * stride + node] = u[1 + d];
+}
+
+hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, res, stride, upd, n);
+  return hipGetLastError();
+}
+
+}  // namespace pe

@@ -1,0 +1,246 @@
+// Host resolver of the windowed greedy placement (see pe_resolver.h for the exactness argument).
+#include "pe_resolver.h"
+
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <set>
+#include <utility>
+
+namespace pe {
+
+static constexpr uint64_t kNoKey = ~0ull;
+static constexpr uint64_t kScoreMax = (1ull << 40) - 1;
+
+uint64_t score_of(const int64_t left[RD]) {
+  uint64_t a = (uint64_t)left[0];
+  uint64_t b = (uint64_t)left[1] >> 20;
+  uint64_t c = (uint64_t)left[2] >= (1ull << 20) ? kScoreMax : ((uint64_t)left[2] << 20);
+  uint64_t d = (uint64_t)left[3] >> 24;
+  a = std::min(a, kScoreMax);
+  b = std::min(b, kScoreMax);
+  c = std::min(c, kScoreMax);
+  d = std::min(d, kScoreMax);
+  return std::min(a + b + c + d, kScoreMax);
+}
+
+uint64_t key_of(const int64_t res[RD], uint32_t labels, const int64_t q[RD], uint32_t need, uint64_t gid) {
+  if ((labels & need) != need) return kNoKey;
+  int64_t left[RD];
+  for (int d = 0; d < RD; ++d) {
+    if (q[d] > res[d]) return kNoKey;
+    left[d] = res[d] - q[d];
+  }
+  return (score_of(left) << 24) | gid;
+}
+
+void merge_shards(const std::vector<const GroupCands*>& parts, GroupCands& out) {
+  out.list.clear();
+  out.limit = kNoKey;
+  for (const GroupCands* p : parts) out.limit = std::min(out.limit, p->limit);
+  for (const GroupCands* p : parts)
+    for (const Cand& c : p->list)
+      if (c.key < out.limit) out.list.push_back(c);
+  std::sort(out.list.begin(), out.list.end(), [](const Cand& a, const Cand& b) { return a.key < b.key; });
+}
+
+void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands) {
+  const size_t gb = 16 + (size_t)K * 48;
+  const size_t shard_bytes = (size_t)n_groups * gb;
+  cands.resize((size_t)n_groups);
+  std::vector<GroupCands> parts((size_t)n_shards);
+  std::vector<const GroupCands*> pp((size_t)n_shards);
+  for (int w = 0; w < n_groups; ++w) {
+    for (int r = 0; r < n_shards; ++r) {
+      const uint8_t* base = blob + (size_t)r * shard_bytes + (size_t)w * gb;
+      int32_t n;
+      uint64_t limit;
+      std::memcpy(&n, base, 4);
+      std::memcpy(&limit, base + 8, 8);
+      GroupCands& gc = n_shards == 1 ? cands[w] : parts[r];
+      gc.limit = limit;
+      gc.list.resize((size_t)std::max(n, 0));
+      for (int i = 0; i < n; ++i) {
+        const uint8_t* rec = base + 16 + (size_t)i * 48;
+        uint64_t lab;
+        std::memcpy(&gc.list[i].key, rec, 8);
+        std::memcpy(gc.list[i].res, rec + 8, 32);
+        std::memcpy(&lab, rec + 40, 8);
+        gc.list[i].labels = (uint32_t)lab;
+      }
+      pp[r] = &parts[r];
+    }
+    if (n_shards > 1) merge_shards(pp, cands[w]);
+  }
+}
+
+Resolver::Resolver(int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority, const int32_t* group_count,
+                   const int64_t* group_req, const uint32_t* group_need)
+    : J_(n_jobs), jgo_(job_group_off), cnt_(group_count), req_(group_req), need_(group_need) {
+  order_.resize((size_t)J_);
+  std::iota(order_.begin(), order_.end(), 0);
+  std::stable_sort(order_.begin(), order_.end(), [&](int64_t a, int64_t b) { return priority[a] > priority[b]; });
+  const int64_t G = J_ > 0 ? jgo_[J_] : 0;
+  pod_off_.assign((size_t)G + 1, 0);
+  for (int64_t g = 0; g < G; ++g) pod_off_[g + 1] = pod_off_[g] + std::max<int32_t>(cnt_[g], 0);
+  pod_node_.assign((size_t)pod_off_[G], -1);
+  job_status_.assign((size_t)J_, 0);
+  if (!done()) g_ = jgo_[order_[0]];
+  advance_group();
+}
+
+// Move the cursor to the next pod that needs placing, finishing jobs whose groups are all placed.
+void Resolver::advance_group() {
+  while (!done()) {
+    const int64_t j = order_[oi_];
+    if (g_ >= jgo_[j + 1]) {
+      finish_job(true);
+      continue;
+    }
+    if (p_ >= cnt_[g_]) {
+      ++g_;
+      p_ = 0;
+      continue;
+    }
+    break;
+  }
+}
+
+void Resolver::finish_job(bool ok) {
+  const int64_t j = order_[oi_];
+  if (ok) {
+    job_status_[j] = 0;
+    ++jobs_placed_;
+  } else {
+    // all-or-nothing: give back every pod this job placed, the restored nodes become dirty
+    for (int32_t g = jgo_[j]; g < jgo_[j + 1]; ++g) {
+      const int64_t* q = req_ + (int64_t)g * RD;
+      for (int32_t p = 0; p < cnt_[g]; ++p) {
+        int32_t& slot = pod_node_[pod_off_[g] + p];
+        if (slot < 0) continue;
+        NodeState& st = job_nodes_[slot];
+        for (int d = 0; d < RD; ++d) st.res[d] += q[d];
+        slot = -1;
+        --pods_placed_;
+      }
+    }
+    for (const auto& kv : job_nodes_) dirty_[kv.first] = kv.second;
+    job_status_[j] = 1;
+    ++jobs_failed_;
+  }
+  job_nodes_.clear();
+  ++oi_;
+  p_ = 0;
+  if (!done()) g_ = jgo_[order_[oi_]];
+}
+
+void Resolver::next_window(int max_groups, int64_t max_pods, std::vector<int32_t>& groups) {
+  groups.clear();
+  if (done()) return;
+  int64_t pods = 0;
+  int64_t oi = oi_;
+  int32_t g = g_;
+  int32_t p = p_;
+  while (oi < (int64_t)order_.size() && (int)groups.size() < max_groups) {
+    const int64_t j = order_[oi];
+    if (g >= jgo_[j + 1]) {
+      ++oi;
+      if (oi < (int64_t)order_.size()) g = jgo_[order_[oi]];
+      p = 0;
+      continue;
+    }
+    if (cnt_[g] > p) {
+      if (!groups.empty() && pods + (cnt_[g] - p) > max_pods) break;
+      groups.push_back(g);
+      pods += cnt_[g] - p;
+    }
+    ++g;
+    p = 0;
+  }
+}
+
+bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<GroupCands>& cands,
+                       std::vector<Update>& updates) {
+  bool consumed = true;
+  size_t wi = 0;
+  std::set<std::pair<uint64_t, int64_t>> dk;  // dirty nodes that fit the current group, by key
+  std::unordered_map<int64_t, uint64_t> dkey;
+  while (!done() && wi < groups.size()) {
+    while (wi < groups.size() && groups[wi] != g_) ++wi;  // groups of failed jobs are skipped
+    if (wi == groups.size()) break;
+    const GroupCands& gc = cands[wi];
+    const int64_t* q = req_ + (int64_t)g_ * RD;
+    const uint32_t need = need_[g_];
+    dk.clear();
+    dkey.clear();
+    for (const auto& kv : dirty_) {
+      const uint64_t k = key_of(kv.second.res, kv.second.labels, q, need, (uint64_t)kv.first);
+      if (k != kNoKey) {
+        dk.emplace(k, kv.first);
+        dkey[kv.first] = k;
+      }
+    }
+    size_t ptr = 0;
+    bool failed = false;
+    while (p_ < cnt_[g_]) {
+      while (ptr < gc.list.size() && dirty_.count((int64_t)(gc.list[ptr].key & 0xFFFFFFull))) ++ptr;
+      const uint64_t kc = ptr < gc.list.size() ? gc.list[ptr].key : kNoKey;
+      const uint64_t kd = dk.empty() ? kNoKey : dk.begin()->first;
+      if (ptr == gc.list.size() && gc.limit != kNoKey && kd >= gc.limit) {
+        consumed = false;  // clean nodes beyond the limit could win: rescan from this pod
+        break;
+      }
+      const uint64_t best = std::min(kc, kd);
+      if (best == kNoKey) {
+        failed = true;
+        break;
+      }
+      const int64_t gid = (int64_t)(best & 0xFFFFFFull);
+      NodeState st;
+      if (best == kd) {
+        st = dirty_[gid];
+      } else {
+        const Cand& c = gc.list[ptr];
+        for (int d = 0; d < RD; ++d) st.res[d] = c.res[d];
+        st.labels = c.labels;
+      }
+      for (int d = 0; d < RD; ++d) st.res[d] -= q[d];
+      dirty_[gid] = st;
+      job_nodes_[gid] = st;
+      pod_node_[pod_off_[g_] + p_] = (int32_t)gid;
+      ++p_;
+      ++pods_placed_;
+      auto it = dkey.find(gid);
+      if (it != dkey.end()) {
+        dk.erase({it->second, gid});
+        dkey.erase(it);
+      }
+      const uint64_t nk = key_of(st.res, st.labels, q, need, (uint64_t)gid);
+      if (nk != kNoKey) {
+        dk.emplace(nk, gid);
+        dkey[gid] = nk;
+      }
+    }
+    if (!consumed) break;
+    if (failed) {
+      finish_job(false);
+      advance_group();
+    } else {
+      ++g_;
+      p_ = 0;
+      advance_group();
+    }
+    ++wi;
+  }
+  for (const auto& kv : dirty_) {
+    Update u;
+    u.gid = kv.first;
+    for (int d = 0; d < RD; ++d) u.res[d] = kv.second.res[d];
+    updates.push_back(u);
+  }
+  dirty_.clear();
+  if (!consumed) ++rescans_;
+  return consumed;
+}
+
+}  // namespace pe

@@ -1,0 +1,99 @@
+// Host half of the greedy gang placement: sequential, exact resolution of one scan window.
+//
+// The GPU scans a WINDOW of upcoming groups (identical-pod sets) against one residual snapshot
+// and returns, per group, the exact list of the best K clean-node keys plus a limit (every clean
+// node with key < limit is listed).  Placements inside the window only change the nodes they
+// touch ("dirty" nodes); the resolver re-scores those exactly on the host, so for every pod
+//     argmin over all nodes = min(best dirty key, first non-dirty listed key)
+// which is the sequential rule of SURVEY.md Appendix B bit for bit.  When a group's list runs
+// dry and no dirty node beats its limit, the window ends (NEED_RESCAN): updates are flushed to
+// the device and the next window rescans from the current pod.  Pure C++, no HIP: the same code
+// runs behind every shard (all ranks resolve identically) and under the CPU tests.
+#pragma once
+#include <stdint.h>
+
+#include <unordered_map>
+#include <vector>
+
+namespace pe {
+
+constexpr int RD = 4;
+
+struct NodeState {
+  int64_t res[RD];
+  uint32_t labels;
+};
+
+struct Cand {
+  uint64_t key;
+  int64_t res[RD];
+  uint32_t labels;
+};
+
+struct GroupCands {
+  std::vector<Cand> list;  // ascending keys, all clean at the snapshot
+  uint64_t limit = ~0ull;  // every clean node with key < limit is in list
+};
+
+struct Update {
+  int64_t gid;
+  int64_t res[RD];
+};
+
+uint64_t score_of(const int64_t left[RD]);
+uint64_t key_of(const int64_t res[RD], uint32_t labels, const int64_t q[RD], uint32_t need, uint64_t gid);
+
+// Merge per-shard candidate lists of one group into the global exact list (limit = min).
+void merge_shards(const std::vector<const GroupCands*>& parts, GroupCands& out);
+
+// Window blob = n_shards consecutive shard blocks, each n_groups x (16-B header {int32 n,
+// int32 flags, uint64 limit} + K x 48-B records {u64 key, i64 res[4], u64 labels}) -- exactly
+// what the merge kernel writes.  Parses and merges the shards into cands[n_groups].
+void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands);
+
+class Resolver {
+ public:
+  Resolver(int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority, const int32_t* group_count,
+           const int64_t* group_req, const uint32_t* group_need);
+
+  bool done() const { return oi_ >= (int64_t)order_.size(); }
+  // Groups (global ids, count > 0) of the next window, starting at the cursor.
+  void next_window(int max_groups, int64_t max_pods, std::vector<int32_t>& groups);
+  // Resolve with candidates for exactly the groups returned by next_window (same order).
+  // Appends the residual updates to flush; returns true if the whole window was consumed.
+  bool resolve(const std::vector<int32_t>& groups, const std::vector<GroupCands>& cands,
+               std::vector<Update>& updates);
+
+  const std::vector<int32_t>& pod_node() const { return pod_node_; }
+  const std::vector<int32_t>& job_status() const { return job_status_; }
+  int64_t jobs_placed() const { return jobs_placed_; }
+  int64_t jobs_failed() const { return jobs_failed_; }
+  int64_t pods_placed() const { return pods_placed_; }
+  int64_t rescans() const { return rescans_; }
+  int64_t n_pods() const { return (int64_t)pod_node_.size(); }
+
+ private:
+  void finish_job(bool ok);
+  void advance_group();
+
+  int64_t J_;
+  const int32_t* jgo_;
+  const int32_t* cnt_;
+  const int64_t* req_;
+  const uint32_t* need_;
+  std::vector<int64_t> order_;
+  std::vector<int64_t> pod_off_;
+  std::vector<int32_t> pod_node_;
+  std::vector<int32_t> job_status_;
+  // cursor
+  int64_t oi_ = 0;  // position in order_
+  int32_t g_ = 0;   // global group index inside the current job
+  int32_t p_ = 0;   // next pod of group g_
+  // window state
+  std::unordered_map<int64_t, NodeState> dirty_;
+  // nodes touched by the current job (exact current residuals, survive window flushes)
+  std::unordered_map<int64_t, NodeState> job_nodes_;
+  int64_t jobs_placed_ = 0, jobs_failed_ = 0, pods_placed_ = 0, rescans_ = 0;
+};
+
+}  // namespace pe

@@ -1,0 +1,170 @@
+"""Synthetic cluster inventories and job batches, integer-only and
+deterministic: counter-based splitmix64, identical wherever it is evaluated.
+
+Every quantity is drawn from a discrete set so it is an exact canonical int64
+(cpu milli, memory bytes, gpu count, ephemeral-storage bytes).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+GOLD = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+GiB = 1 << 30
+TiB = 1 << 40
+
+# cfg seeds
+SEED = {"cfg2": 2, "cfg3": 3, "cfg4": 4, "cfg5": 5}
+
+
+def mix64(z: np.ndarray) -> np.ndarray:
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+    return z ^ (z >> np.uint64(31))
+
+
+def stream(seed: int, sid: int, n: int) -> np.ndarray:
+    """splitmix64 sequence #sid of `seed`: x_i = mix64(base + (i+1)*GOLD), base = mix64(seed*GOLD + sid)."""
+    with np.errstate(over="ignore"):
+        base = mix64(np.uint64(seed) * GOLD + np.uint64(sid))
+        i = np.arange(1, n + 1, dtype=np.uint64)
+        return mix64(base + i * GOLD)
+
+
+def pick(table, r: np.ndarray) -> np.ndarray:
+    t = np.asarray(table, dtype=np.int64)
+    return t[(r % np.uint64(len(t))).astype(np.int64)]
+
+
+@dataclass
+class Inventory:
+    cap: np.ndarray      # [4][N] int64
+    used: np.ndarray     # [4][N] int64
+    labels: np.ndarray   # [N] uint32  bit0 = gpu product (mi355x), bits1-3 = zone one-hot
+    island: np.ndarray   # [N] int32   xGMI island id (= node id on GPU nodes, -1 otherwise)
+
+    @property
+    def n(self) -> int:
+        return int(self.cap.shape[1])
+
+    def residual(self) -> np.ndarray:
+        return self.cap - self.used
+
+
+def make_inventory(n: int, seed: int, gpu_frac: float = 0.2) -> Inventory:
+    is_gpu = (stream(seed, 1, n) % np.uint64(1000)) < np.uint64(int(round(gpu_frac * 1000)))
+    cap = np.empty((4, n), dtype=np.int64)
+    cap[0] = np.where(is_gpu, pick([128_000, 192_000], stream(seed, 2, n)),
+                      pick([32_000, 64_000, 96_000, 128_000], stream(seed, 3, n)))
+    cap[1] = np.where(is_gpu, pick([1 * TiB, 2 * TiB], stream(seed, 4, n)),
+                      pick([128 * GiB, 256 * GiB, 512 * GiB], stream(seed, 5, n)))
+    cap[2] = np.where(is_gpu, 8, 0)
+    cap[3] = np.where(is_gpu, pick([2 * TiB, 4 * TiB], stream(seed, 6, n)),
+                      pick([512 * GiB, 1 * TiB], stream(seed, 7, n)))
+    used = np.empty_like(cap)
+    for d in range(4):
+        u = (stream(seed, 10 + d, n) % np.uint64(12)).astype(np.int64)
+        used[d] = cap[d] * u // 16
+    zone = (stream(seed, 14, n) % np.uint64(3)).astype(np.uint32)
+    labels = (is_gpu.astype(np.uint32) | (np.uint32(1) << (np.uint32(1) + zone))).astype(np.uint32)
+    island = np.where(is_gpu, np.arange(n, dtype=np.int32), -1).astype(np.int32)
+    return Inventory(cap, used, labels, island)
+
+
+CPU_REQ = [500, 1000, 2000, 4000, 8000, 16000]
+MEM_REQ = [g * GiB for g in (1, 2, 4, 8, 16, 32, 64, 128)]
+GPU_REQ = [0, 0, 0, 0, 1, 2, 4, 8]
+EPH_REQ = [0, 10 * GiB, 50 * GiB, 100 * GiB]
+
+
+def pod_requests(seed: int, sid: int, n: int):
+    """n pod request vectors [n][4] + label need (bit0 when a GPU is requested)."""
+    req = np.empty((n, 4), dtype=np.int64)
+    req[:, 0] = pick(CPU_REQ, stream(seed, sid, n))
+    req[:, 1] = pick(MEM_REQ, stream(seed, sid + 1, n))
+    req[:, 2] = pick(GPU_REQ, stream(seed, sid + 2, n))
+    req[:, 3] = pick(EPH_REQ, stream(seed, sid + 3, n))
+    need = (req[:, 2] > 0).astype(np.uint32)
+    return req, need
+
+
+@dataclass
+class JobBatch:
+    """Flattened gang batch: groups of identical pods, CSR over jobs (group order = v1 order)."""
+    job_group_off: np.ndarray  # [J+1] int32
+    priority: np.ndarray       # [J]   int32
+    group_count: np.ndarray    # [G]   int32 pods to place
+    group_req: np.ndarray      # [G][4] int64
+    group_need: np.ndarray     # [G]   uint32
+    kind: np.ndarray           # [J]   int8  0 pytorch, 1 mpi, 2 jax, 3 gpu-gang
+
+    @property
+    def n_jobs(self) -> int:
+        return int(self.priority.shape[0])
+
+    @property
+    def n_pods(self) -> int:
+        return int(self.group_count.sum())
+
+
+def make_jobs(n_jobs: int, seed: int, mix: str = "pytorch") -> JobBatch:
+    """mix: 'pytorch' (cfg2: Master 1 + Worker W in [0,15]),
+            'mixed'   (cfg3: 50% PyTorch, 25% MPI {Launcher 1 (1 cpu, 2Gi), Worker W}, 25% JAX {Worker W+1}),
+            'gang8'   (cfg4: one group of M in {1,2,4,8,16} pods x 8 GPUs, requires label bit0)."""
+    J = n_jobs
+    pri = (stream(seed, 100, J) % np.uint64(1000)).astype(np.int32)
+    w = (stream(seed, 101, J) % np.uint64(16)).astype(np.int32)
+    if mix == "pytorch":
+        kind = np.zeros(J, dtype=np.int8)
+    elif mix == "mixed":
+        k = (stream(seed, 102, J) % np.uint64(4)).astype(np.int64)
+        kind = np.select([k < 2, k == 2], [0, 1], 2).astype(np.int8)
+    elif mix == "gang8":
+        kind = np.full(J, 3, dtype=np.int8)
+    else:
+        raise ValueError(mix)
+    ngroups = np.where(kind <= 1, 2, 1).astype(np.int32)
+    off = np.zeros(J + 1, dtype=np.int32)
+    np.cumsum(ngroups, out=off[1:])
+    G = int(off[-1])
+    a_req, a_need = pod_requests(seed, 200, J)   # leader group (Master / Launcher)
+    b_req, b_need = pod_requests(seed, 300, J)   # worker group
+    count = np.empty(G, dtype=np.int32)
+    req = np.empty((G, 4), dtype=np.int64)
+    need = np.empty(G, dtype=np.uint32)
+    first = off[:-1]
+    two = ngroups == 2
+    # two-group jobs: [leader, worker]
+    count[first[two]] = 1
+    req[first[two]] = a_req[two]
+    need[first[two]] = a_need[two]
+    mpi = two & (kind == 1)
+    req[first[mpi]] = np.array([1000, 2 * GiB, 0, 0], dtype=np.int64)
+    need[first[mpi]] = 0
+    count[first[two] + 1] = w[two]
+    req[first[two] + 1] = b_req[two]
+    need[first[two] + 1] = b_need[two]
+    one = ~two
+    if mix == "gang8":
+        m = pick([1, 2, 4, 8, 16], stream(seed, 103, J)).astype(np.int32)
+        count[first] = m
+        req[first, 0] = pick([32_000, 64_000, 96_000], stream(seed, 104, J))
+        req[first, 1] = pick([256 * GiB, 512 * GiB], stream(seed, 105, J))
+        req[first, 2] = 8
+        req[first, 3] = 100 * GiB
+        need[first] = 1
+    else:
+        count[first[one]] = w[one] + 1      # JAX Worker W+1
+        req[first[one]] = b_req[one]
+        need[first[one]] = b_need[one]
+    return JobBatch(off, pri, count, req, need, kind)
+
+
+def make_fit_jobs(n_jobs: int, seed: int):
+    """cfg5: one request vector (the trainer pod) per job."""
+    return pod_requests(seed, 500, n_jobs)
