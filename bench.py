@@ -199,6 +199,8 @@ def main():
                          "windows_per_batch": s["windows"] / (args.greedy_steps + 1),
                          "rescans_per_batch": s["rescans"] / (args.greedy_steps + 1),
                          "scan_evals_per_s": s["scan_evals"] / (args.greedy_steps + 1) * world / gt,
+                         "device_wait_ms_per_batch": s["greedy_wait_ms"] / (args.greedy_steps + 1),
+                         "host_resolve_ms_per_batch": s["greedy_host_ms"] / (args.greedy_steps + 1),
                          "naive_pod_x_node_evals_per_s": batch.n_pods * float(N) / gt}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -100,6 +100,8 @@ typedef struct {
   int64_t jobs_placed;
   int64_t jobs_failed;
   double last_greedy_ms; /* wall time of the last pe_place_greedy */
+  double greedy_wait_ms; /* host time blocked on window scans + transfers (cumulative) */
+  double greedy_host_ms; /* host time parsing + resolving windows (cumulative) */
 } pe_stats;
 
 int pe_abi_version(void);
@@ -126,7 +128,8 @@ int pe_read_residuals(pe_ctx* ctx, int64_t* res_out /* [4][end-begin] of this sh
  *   V2: group = runtime.Info TotalRequests entry with its pod's containers (kueue formula),
  *       out_members = sum of replicas (Go int32 wrap-around), min_member ignored (may be NULL).
  * Outputs per job: out_min_res[j][4], out_present[j] (bit d = key d present), out_members[j],
- * out_overflow[j] (1 = int64 overflow: the reference would have switched to inf.Dec).
+ * out_overflow[j] (1 = int64 overflow: the reference would have switched to inf.Dec; that job's
+ * out_min_res values are then defined as 0, its presence bits and members are still exact).
  * Returns PE_EOVERFLOW if any job overflowed (outputs still written). */
 int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t* job_group_off,
                         const int32_t* min_member, const int32_t* group_replicas, const int32_t* group_cont_off,
@@ -134,8 +137,11 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
                         uint8_t* out_present, int32_t* out_members, uint8_t* out_overflow);
 
 /* What-if feasibility (config 5): bit (j, n) = fit(job j, node n) against the CURRENT residuals
- * of this shard, device-resident, row-major [n_jobs][ceil(shard_nodes/64)] u64, bit n%64 of word
- * n/64.  Counts are per job over this shard (sum them across shards).
+ * of this shard, device-resident.  Word (j, c) holds nodes 64c..64c+63 (bit n%64) and lives at
+ *   ((j / 16) * Wt + c / 4) * 64 + (j % 16) * 4 + c % 4,   Wt = ceil(words_per_row / 4)
+ * (tile-major: 16 jobs x 256 nodes per 512-B tile, so the kernel writes whole cache lines);
+ * pe_fit_mask_rows hands rows back row-major [n_rows][words_per_row].  Counts are per job over
+ * this shard (sum them across shards).
  * One-shot form: upload + compute + counts to host; *dev_mask receives the device pointer. */
 int pe_fit_mask(pe_ctx* ctx, int64_t n_jobs, const int64_t* req /*[j][4]*/, const uint32_t* need,
                 int64_t* out_feasible_count, const uint64_t** dev_mask, int64_t* words_per_row);

@@ -142,7 +142,8 @@ int orc_pg_min_resources(int32_t mode, int64_t n_jobs, const int32_t* job_group_
         }
       pres |= pp;
     }
-    for (int d = 0; d < ORC_D; ++d) out_res[j * ORC_D + d] = acc[d];
+    /* an overflowed job has no int64 answer (Go holds it in inf.Dec): values are defined as 0 */
+    for (int d = 0; d < ORC_D; ++d) out_res[j * ORC_D + d] = ovf ? 0 : acc[d];
     out_present[j] = pres;
     out_members[j] = mode == ORC_V1 ? pod_cnt : (int32_t)members;
     out_overflow[j] = ovf ? 1 : 0;

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Profiles the bench workload on the GPU box (run via gpurun from the repo root).
+#   1) kernel trace + stats of the full bench (fit mask + greedy)        -> gpurun_out/prof_<tag>
+#   2) separate PMC passes (never combined with sys/runtime traces):
+#      FETCH_SIZE, WRITE_SIZE (HBM traffic; gfx950 FETCH_SIZE reads 1/2 of wide streaming reads),
+#      SQ instruction mix of the fit-mask kernel
+# Usage: profiles/run_profile.sh <tag> [bench args...]
+set -euo pipefail
+TAG=${1:-r1}; shift || true
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_${TAG}
+mkdir -p $OUT
+BENCH_SMALL="--steps 2 --warmup 1 --no-greedy --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- \
+  python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > $OUT/bench_trace.json 2> $OUT/trace.err
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- \
+  python3 bench.py $BENCH_SMALL "$@" > $OUT/bench_fetch.json 2> $OUT/fetch.err
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- \
+  python3 bench.py $BENCH_SMALL "$@" > $OUT/bench_write.json 2> $OUT/write.err
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+  -d $OUT/sq -o sq --output-format csv -- python3 bench.py $BENCH_SMALL "$@" > $OUT/bench_sq.json 2> $OUT/sq.err
+echo "profile $TAG done"

@@ -101,7 +101,7 @@ struct pe_ctx {
   DevBuf<uint32_t> labels;
   DevBuf<int32_t> island;
   // fit mask
-  int64_t fit_J = 0, Wn = 0;
+  int64_t fit_J = 0, fit_Jp = 0, Wn = 0, Wt = 0;
   bool fit_uploaded = false;
   DevBuf<ReqRec> fit_jobs;
   DevBuf<uint64_t> mask;
@@ -404,9 +404,11 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
     }
   }
   ctx->fit_J = n_jobs;
+  ctx->fit_Jp = Jp;
   ctx->Wn = (ctx->Ns + 63) / 64;
+  ctx->Wt = (ctx->Wn + 3) / 4;
   hipchk(ctx->fit_jobs.ensure(Jp), "alloc fit jobs");
-  hipchk(ctx->mask.ensure((size_t)std::max<int64_t>(n_jobs, 1) * std::max<int64_t>(ctx->Wn, 1)), "alloc fit mask");
+  hipchk(ctx->mask.ensure((size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4), "alloc fit mask");
   hipchk(ctx->counts.ensure(Jp), "alloc fit counts");
   hipchk(ctx->h_counts.ensure(Jp), "alloc pinned counts");
   hipchk(hipMemcpyAsync(ctx->fit_jobs.p, recs.data(), Jp * sizeof(ReqRec), hipMemcpyHostToDevice, ctx->stream),
@@ -425,7 +427,7 @@ static void fit_run(pe_ctx* ctx) {
   const int64_t want_x = std::max<int64_t>(1, (16384 + waves_y - 1) / waves_y);
   int64_t tpw = (ctx->Ns + 256 * want_x - 1) / (256 * want_x);
   tpw = std::min<int64_t>(16, std::max<int64_t>(1, tpw));
-  hipchk(pe::launch_fit_mask(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->Wn, ctx->fit_jobs.p, J,
+  hipchk(pe::launch_fit_mask(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->Wt, ctx->fit_jobs.p, J,
                              tpw, ctx->mask.p, ctx->counts.p),
          "launch fit_mask");
   ctx->stats.fit_evals += J * ctx->Ns;
@@ -470,10 +472,17 @@ int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out) {
     if (row0 < 0 || n_rows < 0 || row0 + n_rows > ctx->fit_J) raise(PE_EINVAL, "row range");
     if (n_rows == 0 || ctx->Wn == 0) return PE_OK;
     need_ptr(out, "out");
-    hipchk(hipMemcpyAsync(out, ctx->mask.p + (size_t)row0 * ctx->Wn, (size_t)n_rows * ctx->Wn * 8,
-                          hipMemcpyDeviceToHost, ctx->stream),
+    // copy the 16-row tile bands covering the rows, then untile into row-major
+    const int64_t t0 = row0 / 16, t1 = (row0 + n_rows - 1) / 16;
+    const size_t band = (size_t)ctx->Wt * 64;
+    std::vector<uint64_t> tiles((size_t)(t1 - t0 + 1) * band);
+    hipchk(hipMemcpyAsync(tiles.data(), ctx->mask.p + (size_t)t0 * band, tiles.size() * 8, hipMemcpyDeviceToHost,
+                          ctx->stream),
            "D2H mask");
     hipchk(hipStreamSynchronize(ctx->stream), "sync mask");
+    for (int64_t r = 0; r < n_rows; ++r)
+      for (int64_t c = 0; c < ctx->Wn; ++c)
+        out[(size_t)r * ctx->Wn + c] = tiles[(size_t)(pe::fm_word_index(row0 + r, c, ctx->Wt) - t0 * (int64_t)band)];
     return PE_OK;
   });
 }
@@ -571,6 +580,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         hipchk(hipStreamSynchronize(s), "sync empty");
       }
       const size_t bytes = (size_t)Wg * gb;
+      const auto tw = std::chrono::steady_clock::now();
       if (ctx->world == 1) {
         hipchk(hipMemcpyAsync(ctx->h_out.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
         hipchk(hipStreamSynchronize(s), "sync window");
@@ -585,6 +595,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
                "D2H gathered");
         hipchk(hipStreamSynchronize(s), "sync window");
       }
+      const auto th = std::chrono::steady_clock::now();
+      ctx->stats.greedy_wait_ms += std::chrono::duration<double, std::milli>(th - tw).count();
       pe::parse_window(ctx->h_out.p, ctx->world, Wg, K, cands);
       updates.clear();
       R.resolve(groups, cands, updates);
@@ -597,6 +609,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         for (int d = 0; d < pe::D; ++d) o[1 + d] = u.res[d];
         ++nu;
       }
+      ctx->stats.greedy_host_ms +=
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
       if (nu > 0) {
         hipchk(ctx->g_upd.ensure((size_t)nu * (pe::D + 1)), "alloc upd");
         hipchk(hipMemcpyAsync(ctx->g_upd.p, ctx->h_upd.p, (size_t)nu * (pe::D + 1) * 8, hipMemcpyHostToDevice, s),

@@ -53,9 +53,15 @@ hipError_t launch_pg_min_resources(hipStream_t s, int mode, int64_t n_jobs, cons
                                    const uint8_t* cont_flags, int64_t* out_res, uint8_t* out_present,
                                    int32_t* out_members, uint8_t* out_overflow);
 
-// mask is [J][Wn] u64 row-major, bit n%64 of word n/64 = fit(job j, local node n)
+// Device mask layout (tile-major, so every store writes whole 128-B lines): tiles of 16 jobs x 4
+// words (256 nodes); word (j, c) -- bit n%64 of chunk c = n/64 = fit(job j, local node n) -- sits at
+//   ((j / 16) * Wt + c / 4) * 64 + (j % 16) * 4 + c % 4,      Wt = ceil(ceil(Ns/64) / 4).
+// Rows are padded to FM_JT, chunks to a multiple of 4; pe_fit_mask_rows returns row-major.
+__host__ __device__ inline int64_t fm_word_index(int64_t j, int64_t c, int64_t Wt) {
+  return ((j >> 4) * Wt + (c >> 2)) * 64 + (j & 15) * 4 + (c & 3);
+}
 hipError_t launch_fit_mask(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
-                           int64_t Ns, int64_t Wn, const ReqRec* jobs, int64_t J, int64_t tiles_per_wave,
+                           int64_t Ns, int64_t Wt, const ReqRec* jobs, int64_t J, int64_t tiles_per_wave,
                            uint64_t* mask, unsigned long long* counts);
 
 hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,

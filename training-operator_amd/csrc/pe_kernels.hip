@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void pg_min_resources_kernel(
     pres |= pp;
   }
 #pragma unroll
-  for (int d = 0; d < D; ++d) out_res[j * D + d] = acc[d];
+  for (int d = 0; d < D; ++d) out_res[j * D + d] = ovf ? 0 : acc[d];   // no int64 answer: defined as 0
   out_present[j] = (uint8_t)pres;
   out_members[j] = mode == 1 ? pod_cnt : (int32_t)members;
   out_overflow[j] = ovf ? 1 : 0;
@@ -168,11 +168,11 @@ __device__ __forceinline__ void fm_jobs(const ReqRec* __restrict__ q, const int6
 // Wave tile = FM_CH chunks of 64 nodes held in VGPRs (4 dims x int64 + labels) x FM_JT jobs.
 // Per (job, chunk): 4 x v_cmp_le_i64 against the job's SGPR request (+ a label test only for
 // jobs that need labels); the AND of the lane masks (SALU) is the output word.  16 jobs x 4
-// chunks of words are placed in one VGPR pair by v_writelane and leave as one 512-B store
-// (16 rows x 32 B).  Per-job popcounts come from the stored words (v_bcnt, 4-lane reduction,
+// chunks of words are placed in one VGPR pair by v_writelane and leave as one 512-B store of
+// whole 128-B lines (tile-major mask layout, pe_kernels.h).  Per-job popcounts come from the stored words (v_bcnt, 4-lane reduction,
 // one permute into the lane-distributed counter) and leave with one atomic per (job, wave).
 __global__ __launch_bounds__(256) void fit_mask_kernel(
-    const int64_t* __restrict__ res, int64_t stride, const uint32_t* __restrict__ labels, int64_t Ns, int64_t Wn,
+    const int64_t* __restrict__ res, int64_t stride, const uint32_t* __restrict__ labels, int64_t Ns, int64_t Wt,
     const ReqRec* __restrict__ jobs, int64_t J, int64_t tiles_per_wave, uint64_t* __restrict__ mask,
     unsigned long long* __restrict__ counts) {
   const int lane = threadIdx.x & 63;
@@ -205,12 +205,10 @@ __global__ __launch_bounds__(256) void fit_mask_kernel(
         if (jrow0 >= J) break;                       // wave-uniform
         uint32_t col_lo = 0, col_hi = 0;
         fm_jobs<0>(jobs + jrow0, r, lab, col_lo, col_hi);   // jobs padded to FM_JT on the device
-        const int64_t row = jrow0 + (lane >> 2);
-        const int64_t chunk = chunk0 + (lane & 3);
-        const bool valid = row < J && chunk < Wn;
-        if (valid) mask[row * Wn + chunk] = ((uint64_t)col_hi << 32) | col_lo;
-        // popcount of this lane's word, summed over the 4 chunk lanes of each row
-        unsigned pc = valid ? (unsigned)(__popc(col_lo) + __popc(col_hi)) : 0u;
+        // tile-major layout: the 16 rows x 4 chunks of this collector are 512 contiguous bytes
+        mask[((jrow0 >> 4) * Wt + (chunk0 >> 2)) * 64 + lane] = ((uint64_t)col_hi << 32) | col_lo;
+        // popcount of this lane's word, summed over the 4 chunk lanes of each row (padding is 0)
+        unsigned pc = (unsigned)(__popc(col_lo) + __popc(col_hi));
         pc += __shfl_xor(pc, 1, 64);
         pc += __shfl_xor(pc, 2, 64);
         // lane jg*16 + i of cnt[kb] counts job jrow0 + i, whose sum sits in lane 4i
@@ -228,13 +226,13 @@ __global__ __launch_bounds__(256) void fit_mask_kernel(
 }
 
 hipError_t launch_fit_mask(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
-                           int64_t Wn, const ReqRec* jobs, int64_t J, int64_t tiles_per_wave, uint64_t* mask,
+                           int64_t Wt, const ReqRec* jobs, int64_t J, int64_t tiles_per_wave, uint64_t* mask,
                            unsigned long long* counts) {
   if (J <= 0 || Ns <= 0) return hipSuccess;
   const int64_t span = tiles_per_wave * 64 * FM_CH;
   const int64_t waves = (Ns + span - 1) / span;
   dim3 grid((unsigned)((waves + 3) / 4), (unsigned)((J + FM_JT - 1) / FM_JT));
-  hipLaunchKernelGGL(fit_mask_kernel, grid, dim3(256), 0, s, res, stride, labels, Ns, Wn, jobs, J, tiles_per_wave,
+  hipLaunchKernelGGL(fit_mask_kernel, grid, dim3(256), 0, s, res, stride, labels, Ns, Wt, jobs, J, tiles_per_wave,
                      mask, counts);
   return hipGetLastError();
 }
@@ -338,6 +336,7 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t gbase = (size_t)g * (size_t)nwaves;
 
+  // phase A: min bound over the wave lists (one list per thread, coalesced)
   uint64_t b = NO_KEY;
   for (int w = tid; w < nwaves; w += MG_THREADS) b = umin64(b, bound[gbase + w]);
   b = wave_min_u64(b);
@@ -349,17 +348,21 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
   for (int i = 0; i < MG_THREADS / 64; ++i) G = umin64(G, red[i]);
   __syncthreads();
 
-  for (int w = wave; w < nwaves; w += MG_THREADS / 64) {
+  // phase B: every thread walks one list with independent loads (latency overlapped across the
+  // block instead of one dependent list per wave); keys below G are appended to LDS.
+  for (int w = tid; w < nwaves; w += MG_THREADS) {
     const int c = cnt[gbase + w];
-    const uint64_t k = lane < c ? cand[(gbase + w) * 64 + lane] : NO_KEY;
-    const bool take = k < G;
-    const uint64_t bal = __ballot(take);
-    if (bal) {
-      int base = 0;
-      if (lane == 0) base = atomicAdd(&total, (int)__popcll(bal));
-      base = __shfl(base, 0, 64);
-      const int pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-      if (take && pos < MG_CAP) keys[pos] = k;
+    const uint64_t* lst = cand + (gbase + w) * 64;
+    for (int i0 = 0; i0 < c; i0 += 8) {
+      uint64_t k[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) k[u] = i0 + u < c ? lst[i0 + u] : NO_KEY;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k[u] < G) {
+          const int pos = atomicAdd(&total, 1);
+          if (pos < MG_CAP) keys[pos] = k[u];
+        }
     }
   }
   __syncthreads();
@@ -369,9 +372,9 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
   if (T > MG_CAP) {
     // Overflow (pathological): keep only the exact minimum over every candidate.
     uint64_t mn = NO_KEY;
-    for (int w = wave; w < nwaves; w += MG_THREADS / 64) {
+    for (int w = tid; w < nwaves; w += MG_THREADS) {
       const int c = cnt[gbase + w];
-      if (lane < c) mn = umin64(mn, cand[(gbase + w) * 64 + lane]);
+      for (int i = 0; i < c; ++i) mn = umin64(mn, cand[(gbase + w) * 64 + i]);
     }
     mn = wave_min_u64(mn);
     __syncthreads();
