@@ -102,6 +102,8 @@ typedef struct {
   double last_greedy_ms; /* wall time of the last pe_place_greedy */
   double greedy_wait_ms; /* host time blocked on window scans + transfers (cumulative) */
   double greedy_host_ms; /* host time parsing + resolving windows (cumulative) */
+  int64_t fit_runs_i32;  /* fit-mask launches on the exact 32-bit path (scaled requests) */
+  int64_t fit_runs_i64;  /* fit-mask launches on the general 64-bit path */
 } pe_stats;
 
 int pe_abi_version(void);

@@ -17,6 +17,8 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-for
   python3 bench.py $BENCH_SMALL "$@" > $OUT/bench_fetch.json 2> $OUT/fetch.err
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- \
   python3 bench.py $BENCH_SMALL "$@" > $OUT/bench_write.json 2> $OUT/write.err
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES \
   -d $OUT/sq -o sq --output-format csv -- python3 bench.py $BENCH_SMALL "$@" > $OUT/bench_sq.json 2> $OUT/sq.err
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INST_CYCLES_SALU SQ_INSTS_SMEM SQ_BUSY_CU_CYCLES SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_INT32 \
+  -d $OUT/sq2 -o sq2 --output-format csv -- python3 bench.py $BENCH_SMALL "$@" > $OUT/bench_sq2.json 2> $OUT/sq2.err
 echo "profile $TAG done"

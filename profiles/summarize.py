@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 profile directory (profiles/run_profile.sh output) into one JSON:
+per-kernel average duration (kernel trace --stats) and per-launch PMC values, with the gfx950
+HBM correction of MI355X_MICROARCH.md sec. HBM: FETCH_SIZE reports 1/2 of wide streaming reads
+(doubled here), WRITE_SIZE is exact for 16-B/lane streaming stores.  Units: FETCH/WRITE_SIZE KB."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main(d):
+    out = {"kernels": {}, "pmc": collections.defaultdict(dict)}
+    for f in glob.glob(os.path.join(d, "trace", "*kernel_stats.csv")):
+        for r in csv.DictReader(open(f)):
+            out["kernels"][r["Name"].split("(")[0]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                                       "total_ns": float(r["TotalDurationNs"])}
+    for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
+        acc = collections.defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            acc[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append(float(r["Counter_Value"]))
+        for (k, c), v in acc.items():
+            out["pmc"][k][c] = sum(v) / len(v)
+    for k, p in out["pmc"].items():
+        if "FETCH_SIZE" in p:
+            p["hbm_read_bytes_corrected"] = p["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in p:
+            p["hbm_write_bytes"] = p["WRITE_SIZE"] * 1024
+        if "FETCH_SIZE" in p and "WRITE_SIZE" in p:
+            p["hbm_traffic_bytes"] = p["hbm_read_bytes_corrected"] + p["hbm_write_bytes"]
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

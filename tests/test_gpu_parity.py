@@ -149,6 +149,27 @@ def test_fit_mask_edge_values(eng):
     assert counts[0] == N - 1 and counts[4] == 1
 
 
+@pytest.mark.parametrize("path", ["i32", "i64"])
+def test_fit_mask_paths(path):
+    """Same inventory, requests that do / do not admit the exact 32-bit form; residuals span the
+    int32 saturation point after scaling (nodes with TiB of memory)."""
+    e = Engine(0)
+    N, J = 5000, 300
+    inv = synth.make_inventory(N, 71, 0.5)
+    inv.cap[1, ::7] = 1 << 50                   # huge memory: saturates in the 32-bit form
+    req, need = synth.make_fit_jobs(J, 73)
+    if path == "i64":
+        req[5, 1] += 1                           # one odd byte count: no common power of two
+    e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    counts = e.fit_mask(req, need)
+    o_mask, o_counts = oracle.fit_mask(inv.residual(), inv.labels, req, need)
+    np.testing.assert_array_equal(e.fit_mask_rows(0, J), o_mask)
+    np.testing.assert_array_equal(counts, o_counts)
+    s = e.stats()
+    assert (s["fit_runs_i32"], s["fit_runs_i64"]) == ((1, 0) if path == "i32" else (0, 1))
+    e.close()
+
+
 def test_fit_mask_sharded_columns(eng):
     """Two shards (ranks) of one inventory: column blocks concatenate to the unsharded mask."""
     N, J = 3001, 130

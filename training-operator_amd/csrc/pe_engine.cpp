@@ -104,6 +104,10 @@ struct pe_ctx {
   int64_t fit_J = 0, fit_Jp = 0, Wn = 0, Wt = 0;
   bool fit_uploaded = false;
   DevBuf<ReqRec> fit_jobs;
+  DevBuf<pe::ReqRec32> fit_jobs32;
+  DevBuf<int32_t> res32;
+  bool fit32 = false;      // batch is exactly representable in 32 bits (see ReqRec32)
+  int fit_shift[pe::D] = {0, 0, 0, 0};
   DevBuf<uint64_t> mask;
   DevBuf<unsigned long long> counts;
   HostBuf<unsigned long long> h_counts;
@@ -126,7 +130,7 @@ struct pe_ctx {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
     res0.release(); res.release(); labels.release(); island.release();
-    fit_jobs.release(); mask.release(); counts.release(); h_counts.release();
+    fit_jobs.release(); fit_jobs32.release(); res32.release(); mask.release(); counts.release(); h_counts.release();
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
@@ -403,6 +407,35 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
       fill_req(recs[j], never, 0xFFFFFFFFu);
     }
   }
+  // exact 32-bit form: per dim the shift that brings the largest request below 2^31, valid only
+  // if 2^shift divides every request of the batch in that dim
+  bool use32 = true;
+  for (int d = 0; d < pe::D && use32; ++d) {
+    int64_t mx = 0, orv = 0;
+    for (int64_t j = 0; j < n_jobs; ++j) {
+      mx = std::max(mx, req[j * pe::D + d]);
+      orv |= req[j * pe::D + d];
+    }
+    int sh = 0;
+    while (sh < 62 && (mx >> sh) > (int64_t)INT32_MAX) ++sh;
+    if (orv & ((int64_t(1) << sh) - 1)) use32 = false;
+    ctx->fit_shift[d] = sh;
+  }
+  ctx->fit32 = use32;
+  if (use32) {
+    std::vector<pe::ReqRec32> r32((size_t)Jp);
+    for (int64_t j = 0; j < Jp; ++j) {
+      std::memset(&r32[j], 0, sizeof(pe::ReqRec32));
+      for (int d = 0; d < pe::D; ++d)
+        r32[j].q[d] = j < n_jobs ? (int32_t)(req[j * pe::D + d] >> ctx->fit_shift[d]) : INT32_MAX;
+      r32[j].need = j < n_jobs ? (need ? need[j] : 0u) : 0xFFFFFFFFu;
+    }
+    hipchk(ctx->fit_jobs32.ensure(Jp), "alloc fit jobs32");
+    hipchk(ctx->res32.ensure((size_t)pe::D * ctx->stride), "alloc res32");
+    hipchk(hipMemcpyAsync(ctx->fit_jobs32.p, r32.data(), Jp * sizeof(pe::ReqRec32), hipMemcpyHostToDevice,
+                          ctx->stream),
+           "H2D fit jobs32");
+  }
   ctx->fit_J = n_jobs;
   ctx->fit_Jp = Jp;
   ctx->Wn = (ctx->Ns + 63) / 64;
@@ -427,9 +460,19 @@ static void fit_run(pe_ctx* ctx) {
   const int64_t want_x = std::max<int64_t>(1, (16384 + waves_y - 1) / waves_y);
   int64_t tpw = (ctx->Ns + 256 * want_x - 1) / (256 * want_x);
   tpw = std::min<int64_t>(16, std::max<int64_t>(1, tpw));
-  hipchk(pe::launch_fit_mask(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->Wt, ctx->fit_jobs.p, J,
-                             tpw, ctx->mask.p, ctx->counts.p),
-         "launch fit_mask");
+  if (ctx->fit32) {
+    hipchk(pe::launch_compress_res(ctx->stream, ctx->res.p, ctx->res32.p, ctx->stride, ctx->Ns, ctx->fit_shift),
+           "launch compress_res");
+    hipchk(pe::launch_fit_mask32(ctx->stream, ctx->res32.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->Wt,
+                                 ctx->fit_jobs32.p, J, tpw, ctx->mask.p, ctx->counts.p),
+           "launch fit_mask32");
+    ctx->stats.fit_runs_i32 += 1;
+  } else {
+    hipchk(pe::launch_fit_mask(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->Wt,
+                               ctx->fit_jobs.p, J, tpw, ctx->mask.p, ctx->counts.p),
+           "launch fit_mask");
+    ctx->stats.fit_runs_i64 += 1;
+  }
   ctx->stats.fit_evals += J * ctx->Ns;
 }
 

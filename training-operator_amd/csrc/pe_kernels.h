@@ -20,6 +20,16 @@ struct alignas(64) ReqRec {
 };
 static_assert(sizeof(ReqRec) == 64, "ReqRec must be 64 B");
 
+// Exact 32-bit form of a request batch: q32[d] = q[d] >> shift[d] where 2^shift[d] divides every
+// request of the batch in dim d, so  q <= r  <=>  q32 <= sat32(floor(r / 2^shift))  (r's floor
+// loses nothing because q is a multiple of 2^shift; r >= 2^31 saturates, r < 0 becomes -1).
+struct alignas(32) ReqRec32 {
+  int32_t q[D];
+  uint32_t need;
+  uint32_t pad_[3];
+};
+static_assert(sizeof(ReqRec32) == 32, "ReqRec32 must be 32 B");
+
 // Candidate record shipped to the host resolver: key + the node's residual at scan time.
 struct CandRec {
   uint64_t key;
@@ -63,6 +73,14 @@ __host__ __device__ inline int64_t fm_word_index(int64_t j, int64_t c, int64_t W
 hipError_t launch_fit_mask(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
                            int64_t Ns, int64_t Wt, const ReqRec* jobs, int64_t J, int64_t tiles_per_wave,
                            uint64_t* mask, unsigned long long* counts);
+
+// 32-bit path: residuals compressed per fit run (res32 = sat32(res >> shift)), then the same kernel
+// with v_cmp_le_i32 instead of the (quarter-rate) v_cmp_le_i64.
+hipError_t launch_compress_res(hipStream_t s, const int64_t* res, int32_t* res32, int64_t stride, int64_t Ns,
+                               const int* shift);
+hipError_t launch_fit_mask32(hipStream_t s, const int32_t* res32, int64_t stride, const uint32_t* labels,
+                             int64_t Ns, int64_t Wt, const ReqRec32* jobs, int64_t J, int64_t tiles_per_wave,
+                             uint64_t* mask, unsigned long long* counts);
 
 hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
                        uint64_t id_base, const ReqRec* groups, int Wg, uint64_t* cand, int32_t* cnt,

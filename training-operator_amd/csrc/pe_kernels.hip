@@ -134,10 +134,14 @@ __device__ __forceinline__ void wl4(int c, uint32_t& lo, uint32_t& hi, uint64_t 
   }
 }
 
-template <int JJ>
-__device__ __forceinline__ void fm_job(const ReqRec* __restrict__ q, const int64_t (&r)[FM_CH][D],
+template <class T> __device__ __forceinline__ T never_res();
+template <> __device__ __forceinline__ int64_t never_res<int64_t>() { return NEVER; }
+template <> __device__ __forceinline__ int32_t never_res<int32_t>() { return INT32_MIN; }
+
+template <int JJ, class T, class JR>
+__device__ __forceinline__ void fm_job(const JR* __restrict__ q, const T (&r)[FM_CH][D],
                                        const uint32_t (&lab)[FM_CH], uint32_t& col_lo, uint32_t& col_hi) {
-  const int64_t q0 = q->q[0], q1 = q->q[1], q2 = q->q[2], q3 = q->q[3];
+  const T q0 = q->q[0], q1 = q->q[1], q2 = q->q[2], q3 = q->q[3];
   const uint32_t need = q->need;
   if (need) {
 #pragma unroll
@@ -158,11 +162,11 @@ __device__ __forceinline__ void fm_job(const ReqRec* __restrict__ q, const int64
   }
 }
 
-template <int JJ>
-__device__ __forceinline__ void fm_jobs(const ReqRec* __restrict__ q, const int64_t (&r)[FM_CH][D],
+template <int JJ, class T, class JR>
+__device__ __forceinline__ void fm_jobs(const JR* __restrict__ q, const T (&r)[FM_CH][D],
                                         const uint32_t (&lab)[FM_CH], uint32_t& col_lo, uint32_t& col_hi) {
-  fm_job<JJ>(q + JJ, r, lab, col_lo, col_hi);
-  if constexpr (JJ + 1 < 16) fm_jobs<JJ + 1>(q, r, lab, col_lo, col_hi);
+  fm_job<JJ, T, JR>(q + JJ, r, lab, col_lo, col_hi);
+  if constexpr (JJ + 1 < 16) fm_jobs<JJ + 1, T, JR>(q, r, lab, col_lo, col_hi);
 }
 
 // Wave tile = FM_CH chunks of 64 nodes held in VGPRs (4 dims x int64 + labels) x FM_JT jobs.
@@ -171,9 +175,10 @@ __device__ __forceinline__ void fm_jobs(const ReqRec* __restrict__ q, const int6
 // chunks of words are placed in one VGPR pair by v_writelane and leave as one 512-B store of
 // whole 128-B lines (tile-major mask layout, pe_kernels.h).  Per-job popcounts come from the stored words (v_bcnt, 4-lane reduction,
 // one permute into the lane-distributed counter) and leave with one atomic per (job, wave).
+template <class T, class JR>
 __global__ __launch_bounds__(256) void fit_mask_kernel(
-    const int64_t* __restrict__ res, int64_t stride, const uint32_t* __restrict__ labels, int64_t Ns, int64_t Wt,
-    const ReqRec* __restrict__ jobs, int64_t J, int64_t tiles_per_wave, uint64_t* __restrict__ mask,
+    const T* __restrict__ res, int64_t stride, const uint32_t* __restrict__ labels, int64_t Ns, int64_t Wt,
+    const JR* __restrict__ jobs, int64_t J, int64_t tiles_per_wave, uint64_t* __restrict__ mask,
     unsigned long long* __restrict__ counts) {
   const int lane = threadIdx.x & 63;
   const int64_t wave_id = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -187,14 +192,14 @@ __global__ __launch_bounds__(256) void fit_mask_kernel(
   for (int64_t t = 0; t < tiles_per_wave; ++t) {
     const int64_t tile0 = node_base + t * (64 * FM_CH);
     if (tile0 >= Ns) break;
-    int64_t r[FM_CH][D];
+    T r[FM_CH][D];
     uint32_t lab[FM_CH];
 #pragma unroll
     for (int c = 0; c < FM_CH; ++c) {
       const int64_t n = tile0 + c * 64 + lane;
       const bool ok = n < Ns;
 #pragma unroll
-      for (int d = 0; d < D; ++d) r[c][d] = ok ? res[d * stride + n] : NEVER;
+      for (int d = 0; d < D; ++d) r[c][d] = ok ? res[d * stride + n] : never_res<T>();
       lab[c] = ok ? labels[n] : 0u;
     }
     const int64_t chunk0 = tile0 >> 6;
@@ -204,7 +209,7 @@ __global__ __launch_bounds__(256) void fit_mask_kernel(
         const int64_t jrow0 = j0 + kb * 64 + jg * 16;
         if (jrow0 >= J) break;                       // wave-uniform
         uint32_t col_lo = 0, col_hi = 0;
-        fm_jobs<0>(jobs + jrow0, r, lab, col_lo, col_hi);   // jobs padded to FM_JT on the device
+        fm_jobs<0, T, JR>(jobs + jrow0, r, lab, col_lo, col_hi);   // jobs padded to FM_JT on the device
         // tile-major layout: the 16 rows x 4 chunks of this collector are 512 contiguous bytes
         mask[((jrow0 >> 4) * Wt + (chunk0 >> 2)) * 64 + lane] = ((uint64_t)col_hi << 32) | col_lo;
         // popcount of this lane's word, summed over the 4 chunk lanes of each row (padding is 0)
@@ -232,8 +237,45 @@ hipError_t launch_fit_mask(hipStream_t s, const int64_t* res, int64_t stride, co
   const int64_t span = tiles_per_wave * 64 * FM_CH;
   const int64_t waves = (Ns + span - 1) / span;
   dim3 grid((unsigned)((waves + 3) / 4), (unsigned)((J + FM_JT - 1) / FM_JT));
-  hipLaunchKernelGGL(fit_mask_kernel, grid, dim3(256), 0, s, res, stride, labels, Ns, Wt, jobs, J, tiles_per_wave,
-                     mask, counts);
+  hipLaunchKernelGGL((fit_mask_kernel<int64_t, ReqRec>), grid, dim3(256), 0, s, res, stride, labels, Ns, Wt, jobs, J,
+                     tiles_per_wave, mask, counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_fit_mask32(hipStream_t s, const int32_t* res32, int64_t stride, const uint32_t* labels, int64_t Ns,
+                             int64_t Wt, const ReqRec32* jobs, int64_t J, int64_t tiles_per_wave, uint64_t* mask,
+                             unsigned long long* counts) {
+  if (J <= 0 || Ns <= 0) return hipSuccess;
+  const int64_t span = tiles_per_wave * 64 * FM_CH;
+  const int64_t waves = (Ns + span - 1) / span;
+  dim3 grid((unsigned)((waves + 3) / 4), (unsigned)((J + FM_JT - 1) / FM_JT));
+  hipLaunchKernelGGL((fit_mask_kernel<int32_t, ReqRec32>), grid, dim3(256), 0, s, res32, stride, labels, Ns, Wt, jobs,
+                     J, tiles_per_wave, mask, counts);
+  return hipGetLastError();
+}
+
+struct Shift4 {
+  int s[D];
+};
+
+__global__ __launch_bounds__(256) void compress_res_kernel(const int64_t* __restrict__ res, int32_t* __restrict__ res32,
+                                                           int64_t stride, int64_t Ns, Shift4 sh) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= Ns) return;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const int64_t v = res[d * stride + n] >> sh.s[d];          // arithmetic: floor(r / 2^s)
+    res32[d * stride + n] = v < 0 ? -1 : (v > INT32_MAX ? INT32_MAX : (int32_t)v);
+  }
+}
+
+hipError_t launch_compress_res(hipStream_t s, const int64_t* res, int32_t* res32, int64_t stride, int64_t Ns,
+                               const int* shift) {
+  if (Ns <= 0) return hipSuccess;
+  Shift4 sh;
+  for (int d = 0; d < D; ++d) sh.s[d] = shift[d];
+  hipLaunchKernelGGL(compress_res_kernel, dim3((unsigned)((Ns + 255) / 256)), dim3(256), 0, s, res, res32, stride, Ns,
+                     sh);
   return hipGetLastError();
 }
 
