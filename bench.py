@@ -96,30 +96,43 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    cid, exchange, device = None, None, local
+    host_exchange = os.environ.get("PE_BENCH_EXCHANGE", "rccl") == "host"
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        ids = [comm_id() if rank == 0 else None]
-        dist.broadcast_object_list(ids, src=0)
-        cid = ids[0]
+        if host_exchange:
+            # rehearsal mode for a 1-GPU box: every rank on one device, candidate blobs exchanged
+            # over gloo instead of RCCL (the driver's multi-GPU runs use the RCCL default)
+            dist.init_process_group("gloo")
+            device = int(os.environ.get("PE_BENCH_DEVICE", "0"))
+            tdev = "cpu"
+
+            def exchange(blob: bytes) -> bytes:
+                parts = [None] * world
+                dist.all_gather_object(parts, blob)
+                return b"".join(parts)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            tdev = "cuda"
+            ids = [comm_id() if rank == 0 else None]
+            dist.broadcast_object_list(ids, src=0)
+            cid = ids[0]
 
         def barrier():
             dist.barrier()
 
         def allmax(x: float) -> float:
-            t = torch.tensor([x], dtype=torch.float64, device="cuda")
+            t = torch.tensor([x], dtype=torch.float64, device=tdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return float(t.item())
 
         def allsum(x: int) -> int:
-            t = torch.tensor([x], dtype=torch.int64, device="cuda")
+            t = torch.tensor([x], dtype=torch.int64, device=tdev)
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
             return int(t.item())
     else:
-        cid = None
-
         def barrier():
             pass
 
@@ -131,7 +144,7 @@ def main():
 
     N, J = args.nodes, args.fit_jobs
     inv = synth.make_inventory(N, synth.SEED["cfg5"], gpu_frac=0.2)
-    eng = Engine(local, rank=rank, world_size=world, comm=cid, max_nodes=N, topk=args.topk,
+    eng = Engine(device, rank=rank, world_size=world, comm=cid, exchange=exchange, max_nodes=N, topk=args.topk,
                  window_groups=args.window_groups, window_pods=args.window_pods)
     eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     b, e = eng.shard_range()
@@ -168,7 +181,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic (splitmix64, SURVEY.md 8d)",
         "config": {"workload": "cfg5: fit bitmask, 1M-node inventory x 100k jobs, device-resident",
-                   "nodes": N, "jobs": J, "parallelism": f"node-shard x{world}", "feasible_pairs": feasible},
+                   "nodes": N, "jobs": J, "parallelism": f"node-shard x{world}" + (" (host exchange rehearsal)" if host_exchange and world > 1 else ""), "feasible_pairs": feasible},
         "roofline": {"bound": "hbm", "kernel": "fit_mask_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg,

@@ -80,7 +80,8 @@ typedef struct {
   int32_t device_id;             /* HIP ordinal; -1 = the calling thread's current device */
   int32_t rank;                  /* inventory shard owned by this process, 0..world_size-1 */
   int32_t world_size;            /* shards of the node inventory (1 = unsharded) */
-  const uint8_t* comm_id;        /* PE_COMM_ID_BYTES from pe_comm_id() on rank 0 (RCCL) */
+  const uint8_t* comm_id;        /* PE_COMM_ID_BYTES from pe_comm_id() on rank 0 (RCCL); at
+                                    world_size 1 it builds a 1-rank communicator */
   pe_allgather_fn exchange;      /* optional host exchange replacing RCCL */
   void* exchange_user;
   int64_t max_nodes;             /* global inventory capacity (<= PE_MAX_NODES) */

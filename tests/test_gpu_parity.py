@@ -274,6 +274,16 @@ def test_greedy_sharded_exchange():
         e.close()
 
 
+def test_greedy_rccl_single_rank():
+    """The RCCL window path (ncclAllGather of the candidate blobs) on a 1-rank communicator."""
+    from placement import comm_id
+    e = Engine(0, world_size=1, comm=comm_id(), topk=8, window_groups=16)
+    inv = synth.make_inventory(3000, 83, 0.25)
+    batch = synth.make_jobs(250, 89, "mixed")
+    check_greedy(e, inv, batch)
+    e.close()
+
+
 def test_greedy_reset_residuals(eng):
     inv = synth.make_inventory(800, 59)
     batch = synth.make_jobs(60, 61)

@@ -230,7 +230,9 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   try {
     hipchk(hipSetDevice(dev), "hipSetDevice");
     hipchk(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "hipStreamCreate");
-    if (ctx->world > 1 && !ctx->exchange) {
+    // RCCL whenever shards exchange without a host callback; a comm_id at world_size 1 also
+    // builds a 1-rank communicator (exercises the RCCL window path on a single GPU)
+    if (!ctx->exchange && (ctx->world > 1 || cfg->comm_id)) {
       if (!cfg->comm_id) raise(PE_EINVAL, "world_size > 1 needs comm_id or an exchange callback");
       ncclUniqueId id;
       std::memcpy(&id, cfg->comm_id, sizeof(id));
@@ -587,7 +589,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     hipchk(ctx->g_bound.ensure((size_t)Wpad * nwaves), "alloc bound");
     hipchk(ctx->g_out.ensure((size_t)Wmax * gb), "alloc out");
     hipchk(ctx->h_out.ensure((size_t)Wmax * gb * ctx->world), "alloc pinned out");
-    if (ctx->world > 1) {
+    if (ctx->world > 1 || ctx->comm) {
       hipchk(ctx->g_gath.ensure((size_t)Wmax * gb * ctx->world), "alloc gather");
       hipchk(ctx->h_own.ensure((size_t)Wmax * gb), "alloc pinned own");
     }
@@ -624,7 +626,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       const size_t bytes = (size_t)Wg * gb;
       const auto tw = std::chrono::steady_clock::now();
-      if (ctx->world == 1) {
+      if (ctx->world == 1 && !ctx->comm) {
         hipchk(hipMemcpyAsync(ctx->h_out.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
         hipchk(hipStreamSynchronize(s), "sync window");
       } else if (ctx->exchange) {
