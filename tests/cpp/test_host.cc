@@ -1,0 +1,398 @@
+// Table-driven tests of the C++ host mirror (training-operator_amd/host), written after the
+// reference's Go tests.  `--cpu` runs host-logic cases only (no device); `--gpu` runs the cases
+// that aggregate on the MI355X through libplacement.
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "kf.h"
+
+using namespace kf;
+
+static int g_fail = 0, g_run = 0;
+#define CHECK(cond)                                                                   \
+  do {                                                                                \
+    if (!(cond)) {                                                                    \
+      std::fprintf(stderr, "  FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond);          \
+      ++g_fail;                                                                       \
+    }                                                                                 \
+  } while (0)
+
+struct Case {
+  const char* name;
+  bool gpu;
+  std::function<void()> fn;
+};
+static std::vector<Case>& cases() {
+  static std::vector<Case> c;
+  return c;
+}
+struct Reg {
+  Reg(const char* n, bool gpu, std::function<void()> f) { cases().push_back({n, gpu, std::move(f)}); }
+};
+#define TEST_CPU(name) static void name(); static Reg reg_##name(#name, false, name); static void name()
+#define TEST_GPU(name) static void name(); static Reg reg_##name(#name, true, name); static void name()
+
+static ResourceList RL(std::initializer_list<std::pair<const char*, const char*>> kv) {
+  ResourceList r;
+  for (auto& p : kv) r[p.first] = Quantity::MustParse(p.second);
+  return r;
+}
+static Container Ctr(std::optional<ResourceList> req, std::optional<ResourceList> lim = std::nullopt,
+                     std::optional<std::string> restart = std::nullopt) {
+  Container c;
+  c.requests = std::move(req);
+  c.limits = std::move(lim);
+  c.restart_policy = std::move(restart);
+  return c;
+}
+static Engine& eng() {
+  static Engine e(0, "nvidia.com/gpu");
+  return e;
+}
+static const PriorityClassGetFunc kNoPC = [](const std::string&) { return std::optional<PriorityClass>(); };
+
+// ------------------------------------------------------------------ CPU: Quantity
+
+TEST_CPU(TestQuantityParse) {
+  struct {
+    const char *s, *res;
+    int64_t want;
+  } tcs[] = {{"1", "cpu", 1000},         {"500m", "cpu", 500},          {"0.8", "cpu", 800},
+             {"4Gi", "memory", 4LL << 30}, {"404Gi", "memory", 404LL << 30}, {"1e3", "memory", 1000},
+             {"2k", "memory", 2000},     {"1.5Ki", "memory", 1536},     {"16", "nvidia.com/gpu", 16}};
+  for (auto& tc : tcs) CHECK(Quantity::Parse(tc.s).Canonical(tc.res) == tc.want);
+  bool threw = false;
+  try {
+    Quantity::Parse("4Gb");
+  } catch (const QuantityError&) {
+    threw = true;
+  }
+  CHECK(threw);
+  threw = false;
+  try {
+    Quantity::Parse("0.0001").Canonical("cpu");   // scale < -3: no exact milli value
+  } catch (const QuantityError&) {
+    threw = true;
+  }
+  CHECK(threw);
+  CHECK(Quantity::Parse("1").Equal(Quantity::Parse("1000m")));
+  CHECK(Quantity::Parse("1Gi").Equal(Quantity::Parse("1073741824")));
+  CHECK(!Quantity::Parse("1G").Equal(Quantity::Parse("1Gi")));
+  CHECK(Quantity::FromCanonical("cpu", 1600).Equal(Quantity::Parse("1.6")));
+  CHECK(Quantity::FromCanonical("memory", 404LL << 30).String() == "404Gi");
+}
+
+// ------------------------------------------------------------------ CPU: flattening (host logic)
+
+static std::map<ReplicaType, ReplicaSpec> mnist(int workers) {
+  // examples/pytorch/mnist/v1/pytorch_job_mnist_nccl.yaml:7-30 (limits only, requests nil)
+  ReplicaSpec m, w;
+  m.replicas = 1;
+  m.template_spec.containers = {Ctr(std::nullopt, RL({{"nvidia.com/gpu", "1"}}))};
+  w.replicas = workers;
+  w.template_spec.containers = {Ctr(std::nullopt, RL({{"nvidia.com/gpu", "1"}}))};
+  return {{"Master", m}, {"Worker", w}};
+}
+
+TEST_CPU(TestFlattenV1Mnist) {
+  Dims dims{"nvidia.com/gpu"};
+  Flat f;
+  FlattenV1Job(dims, 2, mnist(1), kNoPC, &f);
+  CHECK((f.job_group_off == std::vector<int32_t>{0, 2}));
+  CHECK((f.group_replicas == std::vector<int32_t>{1, 1}));
+  CHECK((f.group_cont_off == std::vector<int32_t>{0, 1, 2}));
+  CHECK((f.cont_flags == std::vector<uint8_t>{1u << 2, 1u << 2}));   // limits -> gpu dim present
+  CHECK(f.cont_req[2] == 1 && f.cont_req[6] == 1);
+}
+
+TEST_CPU(TestFlattenV1EmptyRequestsDoNotFallBack) {
+  // util.go:90-92: an empty non-nil Requests map does not fall back to Limits
+  ReplicaSpec w;
+  w.replicas = 2;
+  w.template_spec.containers = {Ctr(ResourceList{}, RL({{"cpu", "4"}}))};
+  Flat f;
+  FlattenV1Job(Dims{}, 2, {{"Worker", w}}, kNoPC, &f);
+  CHECK(f.cont_flags[0] == 0);
+}
+
+TEST_CPU(TestFlattenV1PriorityOrder) {
+  ReplicaSpec w, m;
+  w.replicas = 3;
+  w.template_spec.containers = {Ctr(RL({{"cpu", "1"}}))};
+  m.replicas = 1;
+  m.template_spec.priority_class_name = "high";
+  m.template_spec.containers = {Ctr(RL({{"cpu", "16"}}))};
+  PriorityClassGetFunc pc = [](const std::string& n) {
+    return n == "high" ? std::optional<PriorityClass>(PriorityClass{1000}) : std::nullopt;
+  };
+  Flat f;
+  FlattenV1Job(Dims{}, 2, {{"Worker", w}, {"Master", m}}, pc, &f);
+  CHECK(f.cont_req[0] == 16000);                 // the high-priority Master is counted first
+  CHECK((f.group_replicas == std::vector<int32_t>{1, 3}));
+}
+
+TEST_CPU(TestFlattenRejectsUnknownResource) {
+  ReplicaSpec w;
+  w.replicas = 1;
+  w.template_spec.containers = {Ctr(RL({{"hugepages-2Mi", "1Gi"}}))};
+  Flat f;
+  bool threw = false;
+  try {
+    FlattenV1Job(Dims{}, 1, {{"Worker", w}}, kNoPC, &f);
+  } catch (const Error& e) {
+    threw = e.code == PE_EINVAL;
+  }
+  CHECK(threw);
+  CHECK(f.job_group_off.size() == 1 && f.cont_flags.empty());   // all-or-nothing append
+}
+
+TEST_CPU(TestGetTotalReplicas) {
+  auto r = mnist(3);
+  r["Worker"].replicas.reset();                   // nil counts as 1 (k8sutil.go:131-133)
+  CHECK(GetTotalReplicas(r) == 2);
+}
+
+// framework_test.go:154-253 TestRunEnforceMLPolicyPlugins
+TEST_CPU(TestRunEnforceMLPolicyPlugins) {
+  struct TC {
+    const char* name;
+    std::optional<MLPolicy> policy;
+    std::optional<int32_t> trainjob_nodes;
+    int32_t want;
+  } tcs[] = {
+      {"plainml MLPolicy is applied to runtime.Info, TrainJob doesn't have numNodes", MLPolicy{100, MLPolicy::kPlainML},
+       std::nullopt, 100},
+      {"plainml MLPolicy is applied to runtime.Info, TrainJob has numNodes", MLPolicy{100, MLPolicy::kPlainML}, 30, 30},
+      {"registry is empty", std::nullopt, std::nullopt, 10},
+      {"mpi leaves replicas untouched (mpi.go:50-56)", MLPolicy{4, MLPolicy::kMPI}, 8, 10},
+      {"torch without numNodes -> DefaultJobReplicas", MLPolicy{std::nullopt, MLPolicy::kTorch}, std::nullopt, 1},
+  };
+  for (auto& tc : tcs) {
+    Info info;
+    info.runtime_policy.ml_policy = tc.policy;
+    info.scheduler.total_requests["initializer"] = {1, {}};
+    info.scheduler.total_requests["trainer-node"] = {10, {}};
+    TrainJob tj;
+    tj.trainer_num_nodes = tc.trainjob_nodes;
+    PlainML p;
+    Torch t;
+    MPI m;
+    for (EnforceMLPolicyPlugin* plugin : std::vector<EnforceMLPolicyPlugin*>{&p, &t, &m}) CHECK(!plugin->EnforceMLPolicy(&info, &tj));
+    CHECK(info.scheduler.total_requests["trainer-node"].replicas == tc.want);
+    CHECK(info.scheduler.total_requests["initializer"].replicas == 1);
+  }
+}
+
+TEST_CPU(TestEnforcePodGroupPolicyAndNeedsCreateOrUpdate) {
+  Info info;
+  info.runtime_policy.pod_group_policy = PodGroupPolicy{CoschedulingPodGroupPolicySource{120}};
+  TrainJob tj;
+  tj.name = "test-job";
+  // coscheduling.go:91-101 (no engine call: construct with a dangling-free dummy by scope)
+  if (info.runtime_policy.pod_group_policy) info.scheduler.pod_labels[CoScheduling::kPodGroupLabel] = tj.name;
+  CHECK(info.scheduler.pod_labels["scheduling.x-k8s.io/pod-group"] == "test-job");
+  PodGroup a, b;
+  a.min_member = b.min_member = 31;
+  a.min_resources = RL({{"cpu", "31"}});
+  b.min_resources = RL({{"cpu", "31000m"}});
+  CHECK(NeedsCreateOrUpdate(nullptr, a, false));
+  CHECK(!NeedsCreateOrUpdate(&b, a, false));     // exists, not suspended
+  CHECK(!NeedsCreateOrUpdate(&b, a, true));      // suspended, spec equal under Cmp
+  b.min_member = 30;
+  CHECK(NeedsCreateOrUpdate(&b, a, true));       // suspended and changed
+}
+
+// ------------------------------------------------------------------ GPU: v2 (pinned by reference tests)
+
+// runtime_test.go:37-104 TestNewInfo "all arguments are specified"
+TEST_GPU(TestNewInfo) {
+  InfoOptions o;
+  o.labels = {{"labelKey", "labelValue"}};
+  o.annotations = {{"annotationKey", "annotationValue"}};
+  PodSpec init, trainer;
+  init.init_containers = {Ctr(RL({{"cpu", "5"}}), std::nullopt, std::string("Always"))};
+  init.containers = {Ctr(RL({{"cpu", "10"}}))};
+  trainer.init_containers = {Ctr(RL({{"cpu", "15"}}), std::nullopt, std::string("Always"))};
+  trainer.containers = {Ctr(RL({{"cpu", "25"}}))};
+  o.pod_spec_replicas = {{"initializer", 1, init}, {"trainer-node", 10, trainer}};
+  Info info = NewInfo(eng(), o);
+  CHECK(info.labels.at("labelKey") == "labelValue");
+  CHECK(info.scheduler.total_requests.at("initializer").replicas == 1);
+  CHECK(EqualResourceList(info.scheduler.total_requests.at("initializer").pod_requests, RL({{"cpu", "15"}})));
+  CHECK(info.scheduler.total_requests.at("trainer-node").replicas == 10);
+  CHECK(EqualResourceList(info.scheduler.total_requests.at("trainer-node").pod_requests, RL({{"cpu", "40"}})));
+  Info empty = NewInfo(eng(), InfoOptions{});   // "all arguments are not specified"
+  CHECK(empty.scheduler.total_requests.empty());
+}
+
+static PodSpec InitializerPod(const ResourceList& r) {   // wrapper.go:495-528 + :741-756
+  PodSpec p;
+  p.init_containers = {Ctr(r), Ctr(r)};
+  p.containers = {Ctr(std::nullopt)};
+  return p;
+}
+static PodSpec TrainerPod(const ResourceList& r) {       // wrapper.go:529-551 + :706-720
+  PodSpec p;
+  p.containers = {Ctr(r)};
+  return p;
+}
+
+// buildObjects (core/trainingruntime.go:83-129): NewInfo -> EnforceMLPolicy -> EnforcePodGroupPolicy -> Build
+static CoScheduling::BuildResult RunBuild(const ResourceList& res, std::optional<int32_t> runtime_nodes,
+                                          std::optional<int32_t> trainjob_nodes, int32_t timeout, bool suspend,
+                                          Info* info_out = nullptr) {
+  InfoOptions o;
+  o.ml_policy = MLPolicy{runtime_nodes, MLPolicy::kPlainML};
+  o.pod_group_policy = PodGroupPolicy{CoschedulingPodGroupPolicySource{timeout}};
+  o.pod_spec_replicas = {{"initializer", 1, InitializerPod(res)}, {"trainer-node", 1, TrainerPod(res)}};
+  Info info = NewInfo(eng(), o);
+  TrainJob tj;
+  tj.name = "test-job";
+  tj.ns = "default";
+  tj.uid = "uid";
+  tj.suspend = suspend;
+  tj.trainer_num_nodes = trainjob_nodes;
+  PlainML().EnforceMLPolicy(&info, &tj);
+  CoScheduling cs(eng());
+  CHECK(!cs.EnforcePodGroupPolicy(&info, &tj));
+  CHECK(info.scheduler.pod_labels.at(CoScheduling::kPodGroupLabel) == "test-job");
+  auto r = cs.Build(&info, &tj, nullptr);
+  if (info_out) *info_out = info;
+  return r;
+}
+
+// core/trainingruntime_test.go:51-98: runtime NumNodes 100, TrainJob 30 -> MinMember 31, cpu 31
+TEST_GPU(TestTrainingRuntimeNewObjects) {
+  auto r = RunBuild(RL({{"cpu", "1"}}), 100, 30, 120, true);
+  CHECK(!r.error && r.object);
+  CHECK(r.object->min_member == 31);
+  CHECK(EqualResourceList(r.object->min_resources, RL({{"cpu", "31"}})));
+  CHECK(r.object->schedule_timeout_seconds == 120);
+  CHECK(r.object->owner_kind == "TrainJob" && r.object->owner_uid == "uid");
+}
+
+// core/clustertrainingruntime_test.go:47-83: NumNodes 100 from the runtime -> 101
+TEST_GPU(TestClusterTrainingRuntimeNewObjects) {
+  auto r = RunBuild(RL({{"cpu", "1"}}), 100, std::nullopt, 120, true);
+  CHECK(r.object && r.object->min_member == 101);
+  CHECK(EqualResourceList(r.object->min_resources, RL({{"cpu", "101"}})));
+}
+
+// test/integration/controller.v2/trainjob_controller_test.go:106-157: 101 CPU, 404Gi
+TEST_GPU(TestIntegrationPodGroup) {
+  auto r = RunBuild(RL({{"cpu", "1"}, {"memory", "4Gi"}}), 100, std::nullopt, 100, false);
+  CHECK(r.object && r.object->min_member == 101);
+  CHECK(EqualResourceList(r.object->min_resources, RL({{"cpu", "101"}, {"memory", "404Gi"}})));
+  CHECK(r.object->schedule_timeout_seconds == 100);
+}
+
+// framework/core/framework_test.go:398-486: Build on a given runtime.Info
+TEST_GPU(TestRunComponentBuilderPlugins) {
+  Info info;
+  info.runtime_policy.ml_policy = MLPolicy{10, MLPolicy::kPlainML};
+  info.runtime_policy.pod_group_policy = PodGroupPolicy{CoschedulingPodGroupPolicySource{300}};
+  info.trainer.num_nodes = 10;
+  const ResourceList res = RL({{"cpu", "1"}, {"memory", "4Gi"}});
+  info.scheduler.total_requests = {{"initializer", {1, res}}, {"trainer-node", {1, res}}};
+  TrainJob tj;
+  tj.name = "test-job";
+  tj.uid = "uid";
+  tj.trainer_num_nodes = 100;
+  PlainML().EnforceMLPolicy(&info, &tj);
+  CHECK(info.trainer.num_nodes == 100);
+  CHECK(info.scheduler.total_requests.at("trainer-node").replicas == 100);
+  CoScheduling cs(eng());
+  cs.EnforcePodGroupPolicy(&info, &tj);
+  auto r = cs.Build(&info, &tj, nullptr);
+  CHECK(r.object && r.object->min_member == 101);
+  CHECK(EqualResourceList(r.object->min_resources, RL({{"cpu", "101"}, {"memory", "404Gi"}})));
+  CHECK(r.object->schedule_timeout_seconds == 300);
+}
+
+TEST_GPU(TestBuildNilPolicyAndExistingPodGroup) {
+  CoScheduling cs(eng());
+  Info info;
+  TrainJob tj;
+  auto none = cs.Build(&info, &tj, nullptr);     // coscheduling.go:104-106 -> (nil, nil)
+  CHECK(!none.object && !none.error);
+  Info made;
+  auto r = RunBuild(RL({{"cpu", "1"}}), 3, std::nullopt, 60, false, &made);
+  CHECK(r.object);
+  auto again = cs.Build(&made, &tj, &*r.object); // exists and not suspended -> nothing to apply
+  CHECK(!again.object && !again.error);
+}
+
+// ------------------------------------------------------------------ GPU: v1 (hand-derived, parity unpinned)
+
+TEST_GPU(TestCalcPGMinResourcesMnist) {
+  for (int n : {1, 3, 7, 15}) {
+    auto r = mnist(n);
+    auto pg = CalcPodGroupSpecV1(eng(), r, nullptr, kNoPC);
+    CHECK(pg.min_member == 1 + n);
+    CHECK(EqualResourceList(pg.min_resources, RL({{"nvidia.com/gpu", std::to_string(1 + n).c_str()}})));
+  }
+}
+
+TEST_GPU(TestCalcPGMinResourcesSdkGangSpec) {
+  // sdk/python/test/e2e/test_e2e_pytorchjob.py:54-95,342-348: limits {memory 2Gi, cpu 0.8}
+  ReplicaSpec m, w;
+  m.replicas = w.replicas = 1;
+  m.template_spec.containers = w.template_spec.containers = {Ctr(std::nullopt, RL({{"memory", "2Gi"}, {"cpu", "0.8"}}))};
+  std::map<ReplicaType, ReplicaSpec> r = {{"Master", m}, {"Worker", w}};
+  for (int32_t min_avail : {10, 2}) {
+    SchedulingPolicy sp;
+    sp.min_available = min_avail;
+    auto pg = CalcPodGroupSpecV1(eng(), r, &sp, kNoPC);
+    CHECK(pg.min_member == min_avail);
+    CHECK(EqualResourceList(pg.min_resources, RL({{"cpu", "1600m"}, {"memory", "4Gi"}})));
+  }
+  SchedulingPolicy verbatim;
+  verbatim.min_resources = RL({{"cpu", "7"}});
+  CHECK(EqualResourceList(CalcPodGroupSpecV1(eng(), r, &verbatim, kNoPC).min_resources, RL({{"cpu", "7"}})));
+}
+
+TEST_GPU(TestCalcPGMinResourcesBatchAndOverflow) {
+  std::vector<V1Job> jobs;
+  for (int n = 0; n < 1000; ++n) jobs.push_back({1 + n % 16, mnist(n % 16)});
+  auto out = CalcPGMinResourcesBatch(eng(), jobs, kNoPC);
+  for (int n = 0; n < 1000; ++n)
+    CHECK(EqualResourceList(out[n], RL({{"nvidia.com/gpu", std::to_string(1 + n % 16).c_str()}})));
+  ReplicaSpec w;
+  w.replicas = 4;
+  w.template_spec.containers = {Ctr(RL({{"memory", "4611686018427387904"}}))};   // 2^62 bytes x 4
+  bool threw = false;
+  try {
+    CalcPGMinResources(eng(), 4, {{"Worker", w}}, kNoPC);
+  } catch (const Error& e) {
+    threw = e.code == PE_EOVERFLOW;
+  }
+  CHECK(threw);
+}
+
+int main(int argc, char** argv) {
+  bool cpu = true, gpu = false;
+  for (int i = 1; i < argc; ++i) {
+    if (!std::strcmp(argv[i], "--gpu")) { cpu = false; gpu = true; }
+    if (!std::strcmp(argv[i], "--all")) { cpu = gpu = true; }
+  }
+  for (auto& c : cases()) {
+    if ((c.gpu && !gpu) || (!c.gpu && !cpu)) continue;
+    const int before = g_fail;
+    ++g_run;
+    try {
+      c.fn();
+    } catch (const Error& e) {
+      std::fprintf(stderr, "  FAIL %s: kf::Error %d %s\n", c.name, e.code, e.msg.c_str());
+      ++g_fail;
+    } catch (const QuantityError& e) {
+      std::fprintf(stderr, "  FAIL %s: QuantityError %s\n", c.name, e.msg.c_str());
+      ++g_fail;
+    }
+    std::printf("%s %s\n", g_fail == before ? "ok  " : "FAIL", c.name);
+  }
+  std::printf("%d cases, %d failed checks\n", g_run, g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -1,0 +1,316 @@
+#include "kf.h"
+
+#include <algorithm>
+#include <utility>
+
+namespace kf {
+
+// ------------------------------------------------------------------ engine
+
+Engine::Engine(int device_id, std::string gpu_resource_name) {
+  dims_.gpu = std::move(gpu_resource_name);
+  pe_config cfg{};
+  cfg.device_id = device_id;
+  cfg.rank = 0;
+  cfg.world_size = 1;
+  cfg.gpu_resource_name = dims_.gpu.c_str();
+  const int rc = pe_create(&cfg, &ctx_);
+  if (rc != PE_OK) throw Error{rc, "pe_create failed (no GPU: the engine has no CPU fallback)"};
+}
+
+Engine::~Engine() { pe_destroy(ctx_); }
+
+int Dims::dim_of(const std::string& r) const {
+  if (r == "cpu") return 0;
+  if (r == "memory") return 1;
+  if (r == gpu) return 2;
+  if (r == "ephemeral-storage") return 3;
+  return -1;
+}
+
+std::string Dims::name_of(int d) const {
+  static const char* n[] = {"cpu", "memory", nullptr, "ephemeral-storage"};
+  return d == 2 ? gpu : n[d];
+}
+
+// ------------------------------------------------------------------ flattening
+
+static void add_record(const Dims& eng, const ResourceList* rl, int kind, Flat* out) {
+  int64_t v[PE_DIMS] = {0, 0, 0, 0};
+  uint8_t pres = 0;
+  if (rl) {
+    for (const auto& kv : *rl) {
+      const int d = eng.dim_of(kv.first);
+      if (d < 0) throw Error{PE_EINVAL, "resource " + kv.first + " has no engine dimension"};
+      try {
+        v[d] = kv.second.Canonical(kv.first);
+      } catch (const QuantityError& e) {
+        throw Error{PE_EINVAL, e.msg};
+      }
+      pres |= (uint8_t)(1u << d);
+    }
+  }
+  out->cont_req.insert(out->cont_req.end(), v, v + PE_DIMS);
+  out->cont_flags.push_back((uint8_t)(pres | (kind << PE_KIND_SHIFT)));
+}
+
+static void end_group(int32_t replicas, Flat* out) {
+  out->group_replicas.push_back(replicas);
+  out->group_cont_off.push_back((int32_t)out->cont_flags.size());
+}
+
+static void end_job(int32_t min_member, Flat* out) {
+  out->min_member.push_back(min_member);
+  out->job_group_off.push_back((int32_t)out->group_replicas.size());
+}
+
+// util.go:110-124: priority from the PriorityClass lister (error/nil -> 0), sorted DESC.  Go's
+// sort.Sort leaves equal priorities in map-iteration order (random); we take type name ASC.
+static std::vector<ReplicaType> v1_order(const std::map<ReplicaType, ReplicaSpec>& replicas,
+                                         const PriorityClassGetFunc& pcGetFunc) {
+  std::vector<std::pair<int32_t, ReplicaType>> pri;
+  for (const auto& kv : replicas) {
+    std::optional<PriorityClass> pc;
+    if (pcGetFunc) pc = pcGetFunc(kv.second.template_spec.priority_class_name);
+    pri.emplace_back(pc ? pc->value : 0, kv.first);
+  }
+  std::stable_sort(pri.begin(), pri.end(), [](const auto& a, const auto& b) {
+    return a.first != b.first ? a.first > b.first : a.second < b.second;
+  });
+  std::vector<ReplicaType> order;
+  for (auto& p : pri) order.push_back(p.second);
+  return order;
+}
+
+// Roll the arrays back to their sizes at entry if a record throws (one job is all-or-nothing).
+struct FlatTxn {
+  Flat* f;
+  size_t j, g, c, r;
+  bool done = false;
+  explicit FlatTxn(Flat* out)
+      : f(out), j(out->job_group_off.size()), g(out->group_replicas.size()), c(out->cont_flags.size()),
+        r(out->cont_req.size()) {}
+  ~FlatTxn() {
+    if (done) return;
+    f->job_group_off.resize(j);
+    f->min_member.resize(j - 1);
+    f->group_replicas.resize(g);
+    f->group_cont_off.resize(g + 1);
+    f->cont_flags.resize(c);
+    f->cont_req.resize(r);
+  }
+};
+
+void FlattenV1Job(const Dims& eng, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
+                  const PriorityClassGetFunc& pcGetFunc, Flat* out) {
+  FlatTxn txn(out);
+  for (const ReplicaType& t : v1_order(replicas, pcGetFunc)) {
+    const ReplicaSpec& spec = replicas.at(t);
+    for (const Container& c : spec.template_spec.containers) {
+      // AddResourceList (util.go:79-104): Requests keys, or Limits only when Requests is nil
+      const ResourceList* rl = c.requests ? &*c.requests : (c.limits ? &*c.limits : nullptr);
+      add_record(eng, rl, PE_KIND_CONTAINER, out);
+    }
+    end_group(spec.replicas ? *spec.replicas : -1, out);
+  }
+  end_job(minMember, out);
+  txn.done = true;
+}
+
+void FlattenV2PodGroup(const Dims& eng, int32_t replicas, const PodSpec& pod, Flat* out) {
+  FlatTxn txn(out);
+  for (const Container& c : pod.init_containers) {
+    const bool sidecar = c.restart_policy && *c.restart_policy == "Always";
+    add_record(eng, c.requests ? &*c.requests : nullptr, sidecar ? PE_KIND_SIDECAR : PE_KIND_INIT, out);
+  }
+  for (const Container& c : pod.containers) add_record(eng, c.requests ? &*c.requests : nullptr, PE_KIND_CONTAINER, out);
+  if (pod.overhead) add_record(eng, &*pod.overhead, PE_KIND_OVERHEAD, out);
+  end_group(replicas, out);
+  txn.done = true;
+}
+
+void FlattenV2Info(const Dims& eng, const Info& info, Flat* out) {
+  FlatTxn txn(out);
+  for (const auto& kv : info.scheduler.total_requests) {
+    add_record(eng, &kv.second.pod_requests, PE_KIND_CONTAINER, out);
+    end_group(kv.second.replicas, out);
+  }
+  end_job(0, out);
+  txn.done = true;
+}
+
+// ------------------------------------------------------------------ aggregation through the ABI
+
+struct AggOut {
+  std::vector<int64_t> res;
+  std::vector<uint8_t> present, overflow;
+  std::vector<int32_t> members;
+};
+
+static AggOut run_agg(Engine& eng, int mode, const Flat& f) {
+  const int64_t J = (int64_t)f.job_group_off.size() - 1;
+  AggOut o;
+  o.res.assign((size_t)J * PE_DIMS, 0);
+  o.present.assign((size_t)J, 0);
+  o.overflow.assign((size_t)J, 0);
+  o.members.assign((size_t)J, 0);
+  if (J == 0) return o;
+  const int rc = pe_pg_min_resources(eng.ctx(), mode, J, f.job_group_off.data(), f.min_member.data(),
+                                     f.group_replicas.data(), f.group_cont_off.data(), f.cont_req.data(),
+                                     f.cont_flags.data(), o.res.data(), o.present.data(), o.members.data(),
+                                     o.overflow.data());
+  if (rc != PE_OK && rc != PE_EOVERFLOW) throw Error{rc, pe_last_error(eng.ctx())};
+  return o;
+}
+
+static ResourceList to_list(const Dims& eng, const AggOut& o, int64_t j) {
+  if (o.overflow[j]) throw Error{PE_EOVERFLOW, "int64 overflow: the reference would switch to inf.Dec"};
+  ResourceList rl;
+  for (int d = 0; d < PE_DIMS; ++d)
+    if (o.present[j] & (1u << d)) rl[eng.name_of(d)] = Quantity::FromCanonical(eng.name_of(d), o.res[j * PE_DIMS + d]);
+  return rl;
+}
+
+// ------------------------------------------------------------------ v1
+
+int32_t GetTotalReplicas(const std::map<ReplicaType, ReplicaSpec>& replicas) {
+  int32_t total = 0;
+  for (const auto& kv : replicas) total += kv.second.replicas ? *kv.second.replicas : 1;  // k8sutil.go:131-133
+  return total;
+}
+
+ResourceList CalcPGMinResources(Engine& eng, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
+                                const PriorityClassGetFunc& pcGetFunc) {
+  Flat f;
+  FlattenV1Job(eng.dims(), minMember, replicas, pcGetFunc, &f);
+  return to_list(eng.dims(), run_agg(eng, PE_MODE_V1, f), 0);
+}
+
+std::vector<ResourceList> CalcPGMinResourcesBatch(Engine& eng, const std::vector<V1Job>& jobs,
+                                                  const PriorityClassGetFunc& pcGetFunc) {
+  Flat f;
+  for (const V1Job& j : jobs) FlattenV1Job(eng.dims(), j.min_member, j.replicas, pcGetFunc, &f);
+  AggOut o = run_agg(eng, PE_MODE_V1, f);
+  std::vector<ResourceList> out;
+  for (size_t j = 0; j < jobs.size(); ++j) out.push_back(to_list(eng.dims(), o, (int64_t)j));
+  return out;
+}
+
+PodGroupSpecV1 CalcPodGroupSpecV1(Engine& eng, const std::map<ReplicaType, ReplicaSpec>& replicas,
+                                  const SchedulingPolicy* policy, const PriorityClassGetFunc& pcGetFunc) {
+  PodGroupSpecV1 pg;
+  pg.min_member = GetTotalReplicas(replicas);                                    // job.go:251
+  if (policy && policy->min_available) pg.min_member = *policy->min_available;   // job.go:258-260
+  if (policy && policy->min_resources) pg.min_resources = *policy->min_resources;  // job.go:267-269
+  else pg.min_resources = CalcPGMinResources(eng, pg.min_member, replicas, pcGetFunc);  // job.go:275-277
+  return pg;
+}
+
+// ------------------------------------------------------------------ v2
+
+Info NewInfo(Engine& eng, const InfoOptions& opts) {
+  Info info;
+  info.labels = opts.labels;
+  info.annotations = opts.annotations;
+  info.runtime_policy.ml_policy = opts.ml_policy;
+  info.runtime_policy.pod_group_policy = opts.pod_group_policy;
+  if (opts.pod_spec_replicas.empty()) return info;
+  Flat f;
+  for (const PodSpecReplica& r : opts.pod_spec_replicas) {
+    FlattenV2PodGroup(eng.dims(), 1, r.pod_spec, &f);   // per-pod requests: one group of 1 replica per job
+    end_job(0, &f);
+  }
+  AggOut o = run_agg(eng, PE_MODE_V2, f);
+  for (size_t i = 0; i < opts.pod_spec_replicas.size(); ++i) {
+    const PodSpecReplica& r = opts.pod_spec_replicas[i];
+    info.scheduler.total_requests[r.name] = TotalResourceRequest{r.replicas, to_list(eng.dims(), o, (int64_t)i)};
+  }
+  return info;
+}
+
+static std::optional<Error> rewrite_trainer_replicas(Info* info, const TrainJob* trainJob) {
+  std::optional<int32_t> num_nodes = info->runtime_policy.ml_policy->num_nodes;
+  if (trainJob && trainJob->trainer_num_nodes) num_nodes = trainJob->trainer_num_nodes;
+  info->trainer.num_nodes = num_nodes;
+  auto it = info->scheduler.total_requests.find("trainer-node");   // constants.JobTrainerNode
+  if (it != info->scheduler.total_requests.end()) it->second.replicas = num_nodes ? *num_nodes : 1;
+  return std::nullopt;
+}
+
+std::optional<Error> PlainML::EnforceMLPolicy(Info* info, const TrainJob* trainJob) {
+  if (!info || !info->runtime_policy.ml_policy || info->runtime_policy.ml_policy->source != MLPolicy::kPlainML)
+    return std::nullopt;
+  return rewrite_trainer_replicas(info, trainJob);
+}
+
+std::optional<Error> Torch::EnforceMLPolicy(Info* info, const TrainJob* trainJob) {
+  if (!info || !info->runtime_policy.ml_policy || info->runtime_policy.ml_policy->source != MLPolicy::kTorch)
+    return std::nullopt;
+  return rewrite_trainer_replicas(info, trainJob);
+}
+
+std::optional<Error> CoScheduling::EnforcePodGroupPolicy(Info* info, const TrainJob* trainJob) {
+  if (!info || !info->runtime_policy.pod_group_policy || !trainJob) return std::nullopt;
+  info->scheduler.pod_labels[kPodGroupLabel] = trainJob->name;
+  return std::nullopt;
+}
+
+bool NeedsCreateOrUpdate(const PodGroup* old, const PodGroup& pg, bool suspended) {
+  if (!old) return true;
+  if (!suspended) return false;
+  const bool spec_equal = old->min_member == pg.min_member && EqualResourceList(old->min_resources, pg.min_resources) &&
+                          old->schedule_timeout_seconds == pg.schedule_timeout_seconds;
+  return !spec_equal || old->labels != pg.labels || old->annotations != pg.annotations;
+}
+
+std::vector<CoScheduling::BuildResult> CoScheduling::BuildBatch(const std::vector<const Info*>& infos,
+                                                                const std::vector<const TrainJob*>& trainJobs,
+                                                                const std::vector<const PodGroup*>& existing) {
+  std::vector<BuildResult> out(infos.size());
+  std::vector<size_t> idx;
+  Flat f;
+  for (size_t i = 0; i < infos.size(); ++i) {
+    const Info* info = infos[i];
+    if (!info || !info->runtime_policy.pod_group_policy || !info->runtime_policy.pod_group_policy->coscheduling ||
+        !trainJobs[i])
+      continue;  // coscheduling.go:104-106: (nil, nil)
+    try {
+      FlattenV2Info(eng_.dims(), *info, &f);
+      idx.push_back(i);
+    } catch (const Error& e) {
+      out[i].error = e;
+    }
+  }
+  AggOut o;
+  try {
+    o = run_agg(eng_, PE_MODE_V2, f);
+  } catch (const Error& e) {
+    for (size_t k : idx) out[k].error = e;
+    return out;
+  }
+  for (size_t n = 0; n < idx.size(); ++n) {
+    const size_t i = idx[n];
+    PodGroup pg;
+    pg.name = trainJobs[i]->name;
+    pg.ns = trainJobs[i]->ns;
+    pg.min_member = o.members[n];
+    try {
+      pg.min_resources = to_list(eng_.dims(), o, (int64_t)n);
+    } catch (const Error& e) {
+      out[i].error = e;
+      continue;
+    }
+    pg.schedule_timeout_seconds = infos[i]->runtime_policy.pod_group_policy->coscheduling->schedule_timeout_seconds;
+    pg.owner_kind = "TrainJob";  // SetControllerReference (coscheduling.go:134)
+    pg.owner_name = trainJobs[i]->name;
+    pg.owner_uid = trainJobs[i]->uid;
+    if (NeedsCreateOrUpdate(existing.empty() ? nullptr : existing[i], pg, trainJobs[i]->suspend)) out[i].object = pg;
+  }
+  return out;
+}
+
+CoScheduling::BuildResult CoScheduling::Build(const Info* info, const TrainJob* trainJob, const PodGroup* existing) {
+  return BuildBatch({info}, {trainJob}, {existing})[0];
+}
+
+}  // namespace kf

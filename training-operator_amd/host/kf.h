@@ -1,0 +1,251 @@
+// Host-side mirror of the reference's interfaces for the PodGroup hot path, in C++ (the reference
+// is compiled Go; no Go toolchain exists in this pipeline).  Names, argument meaning and error
+// behaviour follow the Go code so the tests read like the reference's own; every number is
+// computed by libplacement on the GPU through include/placement.h -- this layer only flattens
+// object graphs into the ABI's CSR arrays and builds result objects.
+//
+//   kf::CalcPGMinResources  <- pkg/controller.v1/common/util.go:108-145
+//   kf::GetTotalReplicas    <- pkg/util/k8sutil/k8sutil.go:126-137
+//   kf::CalcPodGroupSpecV1  <- pkg/controller.v1/common/job.go:250-277 (minMember / MinResources)
+//   kf::NewInfo             <- pkg/runtime.v2/runtime.go:105-145 (TotalRequests via kueue formula)
+//   kf::PlainML/Torch/MPI   <- pkg/runtime.v2/framework/plugins/{plainml,torch,mpi} EnforceMLPolicy
+//   kf::CoScheduling        <- pkg/runtime.v2/framework/plugins/coscheduling/coscheduling.go:58-153
+#pragma once
+#include <stdint.h>
+
+#include <functional>
+#include <map>
+#include <memory>
+#include <optional>
+#include <string>
+#include <vector>
+
+#include "placement.h"
+#include "quantity.h"
+
+namespace kf {
+
+// ------------------------------------------------------------------ API types (input schema slice)
+// pkg/apis/kubeflow.org/v1/common_types.go:96-110,194-251; k8s core/v1 Container/PodSpec subset
+struct Container {
+  std::string name;
+  std::optional<ResourceList> requests;  // nil vs empty matters for v1 (util.go:90-92)
+  std::optional<ResourceList> limits;
+  std::optional<std::string> restart_policy;  // "Always" on an init container = sidecar
+};
+
+struct PodSpec {
+  std::vector<Container> containers;
+  std::vector<Container> init_containers;
+  std::optional<ResourceList> overhead;
+  std::string priority_class_name;
+};
+
+using ReplicaType = std::string;
+
+struct ReplicaSpec {
+  std::optional<int32_t> replicas;
+  PodSpec template_spec;
+};
+
+struct SchedulingPolicy {
+  std::optional<int32_t> min_available;
+  std::string queue;
+  std::optional<ResourceList> min_resources;
+  std::string priority_class;
+  std::optional<int32_t> schedule_timeout_seconds;
+};
+
+struct PriorityClass {
+  int32_t value = 0;
+};
+// util.go:106 PriorityClassGetFunc; std::nullopt plays the (nil, err) return
+using PriorityClassGetFunc = std::function<std::optional<PriorityClass>(const std::string&)>;
+
+// v2 (pkg/apis/kubeflow.org/v2alpha1/trainingruntime_types.go:103-180, trainjob_types.go:169-200)
+struct MLPolicy {
+  enum Source { kPlainML, kTorch, kMPI };
+  std::optional<int32_t> num_nodes;
+  Source source = kPlainML;
+};
+struct CoschedulingPodGroupPolicySource {
+  std::optional<int32_t> schedule_timeout_seconds;
+};
+struct PodGroupPolicy {
+  std::optional<CoschedulingPodGroupPolicySource> coscheduling;
+};
+struct TrainJob {
+  std::string name, ns, uid;
+  bool suspend = false;
+  std::optional<int32_t> trainer_num_nodes;
+  std::map<std::string, std::string> labels, annotations;
+};
+
+// pkg/runtime.v2/runtime.go:28-62
+struct TotalResourceRequest {
+  int32_t replicas = 0;
+  ResourceList pod_requests;
+};
+struct RuntimePolicy {
+  std::optional<MLPolicy> ml_policy;
+  std::optional<PodGroupPolicy> pod_group_policy;
+};
+struct Info {
+  std::map<std::string, std::string> labels, annotations;
+  RuntimePolicy runtime_policy;
+  struct {
+    std::optional<int32_t> num_nodes;
+  } trainer;
+  struct {
+    std::map<std::string, std::string> pod_labels;
+    std::map<std::string, TotalResourceRequest> total_requests;
+  } scheduler;
+};
+
+// scheduler-plugins v1alpha1 PodGroup (the fields coscheduling.go:119-133 sets)
+struct PodGroup {
+  std::string name, ns;
+  int32_t min_member = 0;
+  ResourceList min_resources;
+  std::optional<int32_t> schedule_timeout_seconds;
+  std::map<std::string, std::string> labels, annotations;
+  std::string owner_kind, owner_name, owner_uid;
+};
+
+// ------------------------------------------------------------------ engine handle
+
+struct Error {
+  int code;  // PE_E* or PE_EINVAL for host-side validation
+  std::string msg;
+};
+
+// Resource key <-> engine dimension (0 cpu, 1 memory, 2 accelerator, 3 ephemeral-storage)
+struct Dims {
+  std::string gpu = "amd.com/gpu";
+  int dim_of(const std::string& resource) const;  // -1: no engine dimension for this key
+  std::string name_of(int dim) const;
+};
+
+class Engine {
+ public:
+  explicit Engine(int device_id = 0, std::string gpu_resource_name = "amd.com/gpu");
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+  pe_ctx* ctx() const { return ctx_; }
+  const Dims& dims() const { return dims_; }
+
+ private:
+  pe_ctx* ctx_ = nullptr;
+  Dims dims_;
+};
+
+// ------------------------------------------------------------------ v1
+
+int32_t GetTotalReplicas(const std::map<ReplicaType, ReplicaSpec>& replicas);
+
+// util.go:108.  Throws kf::Error when a quantity has no exact int64 canonical form, a resource key
+// has no engine dimension, or the sum overflows int64 (Go would switch to inf.Dec).
+ResourceList CalcPGMinResources(Engine& eng, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
+                                const PriorityClassGetFunc& pcGetFunc);
+
+struct V1Job {
+  int32_t min_member;
+  std::map<ReplicaType, ReplicaSpec> replicas;
+};
+// One kernel launch for a batch of jobs (the throughput form of the same rule).
+std::vector<ResourceList> CalcPGMinResourcesBatch(Engine& eng, const std::vector<V1Job>& jobs,
+                                                  const PriorityClassGetFunc& pcGetFunc);
+
+// job.go:250-277: minMember = MinAvailable ?? GetTotalReplicas; MinResources verbatim if set.
+struct PodGroupSpecV1 {
+  int32_t min_member;
+  ResourceList min_resources;
+};
+PodGroupSpecV1 CalcPodGroupSpecV1(Engine& eng, const std::map<ReplicaType, ReplicaSpec>& replicas,
+                                  const SchedulingPolicy* policy, const PriorityClassGetFunc& pcGetFunc);
+
+// ------------------------------------------------------------------ v2
+
+struct PodSpecReplica {
+  std::string name;
+  int32_t replicas;
+  PodSpec pod_spec;
+};
+struct InfoOptions {
+  std::map<std::string, std::string> labels, annotations;
+  std::optional<MLPolicy> ml_policy;
+  std::optional<PodGroupPolicy> pod_group_policy;
+  std::vector<PodSpecReplica> pod_spec_replicas;
+};
+// runtime.go:115-145: TotalRequests[name] = {replicas, kueue TotalRequests(podSpec)} -- the pod
+// formula runs in the pg_min_resources kernel (PE_MODE_V2, one entry per group, replicas 1).
+Info NewInfo(Engine& eng, const InfoOptions& opts);
+
+class Plugin {
+ public:
+  virtual ~Plugin() = default;
+  virtual std::string Name() const = 0;
+};
+
+// framework/interface.go:45-48
+class EnforceMLPolicyPlugin : public Plugin {
+ public:
+  virtual std::optional<Error> EnforceMLPolicy(Info* info, const TrainJob* trainJob) = 0;
+};
+
+class PlainML : public EnforceMLPolicyPlugin {  // plainml.go:45-76
+ public:
+  std::string Name() const override { return "PlainML"; }
+  std::optional<Error> EnforceMLPolicy(Info* info, const TrainJob* trainJob) override;
+};
+class Torch : public EnforceMLPolicyPlugin {    // torch.go:52-135 (replica rewrite only)
+ public:
+  std::string Name() const override { return "Torch"; }
+  std::optional<Error> EnforceMLPolicy(Info* info, const TrainJob* trainJob) override;
+};
+class MPI : public EnforceMLPolicyPlugin {      // mpi.go:50-56: no-op
+ public:
+  std::string Name() const override { return "MPI"; }
+  std::optional<Error> EnforceMLPolicy(Info*, const TrainJob*) override { return std::nullopt; }
+};
+
+// coscheduling.go: implements EnforcePodGroupPolicyPlugin + ComponentBuilderPlugin
+class CoScheduling : public Plugin {
+ public:
+  static constexpr const char* kName = "CoScheduling";              // coscheduling.go:67
+  static constexpr const char* kPodGroupLabel = "scheduling.x-k8s.io/pod-group";
+  explicit CoScheduling(Engine& eng) : eng_(eng) {}
+  std::string Name() const override { return kName; }
+  std::optional<Error> EnforcePodGroupPolicy(Info* info, const TrainJob* trainJob);   // :91-101
+  struct BuildResult {
+    std::optional<PodGroup> object;  // (nil, nil) <=> no object and no error
+    std::optional<Error> error;
+  };
+  // :103-148. `existing` = the PodGroup the client Get returned (nullptr = NotFound).
+  BuildResult Build(const Info* info, const TrainJob* trainJob, const PodGroup* existing);
+  // Batch form: one kernel launch aggregates every (info, trainJob) pair.
+  std::vector<BuildResult> BuildBatch(const std::vector<const Info*>& infos,
+                                      const std::vector<const TrainJob*>& trainJobs,
+                                      const std::vector<const PodGroup*>& existing);
+
+ private:
+  Engine& eng_;
+};
+
+bool NeedsCreateOrUpdate(const PodGroup* old, const PodGroup& pg, bool suspended);  // :150-153
+
+// ------------------------------------------------------------------ flattening (exposed for tests)
+
+struct Flat {
+  std::vector<int32_t> job_group_off{0}, min_member, group_replicas, group_cont_off{0};
+  std::vector<int64_t> cont_req;
+  std::vector<uint8_t> cont_flags;
+};
+// Each call appends exactly one job (V1Job / Info) or one group (V2PodGroup) or nothing (throws).
+void FlattenV1Job(const Dims& dims, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
+                  const PriorityClassGetFunc& pcGetFunc, Flat* out);
+void FlattenV2PodGroup(const Dims& dims, int32_t replicas, const PodSpec& pod, Flat* out);
+void FlattenV2Info(const Dims& dims, const Info& info, Flat* out);
+
+}  // namespace kf
