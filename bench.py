@@ -173,6 +173,8 @@ def main():
     elapsed = allmax(t1 - t0)
     kern_ms = ev.elapsed_ms(e0, e1) / args.steps
     value = float(N) * J * args.steps / elapsed
+    st0 = eng.stats()
+    fit_path = "coded" if st0["fit_runs_coded"] else ("i32" if st0["fit_runs_i32"] else "i64")
     alg = fit_bytes(Ns, J)
     achieved = alg / (kern_ms * 1e-3) / 1e9
 
@@ -184,7 +186,7 @@ def main():
                    "nodes": N, "jobs": J, "parallelism": f"node-shard x{world}" + (" (host exchange rehearsal)" if host_exchange and world > 1 else ""), "feasible_pairs": feasible},
         "roofline": {"bound": "hbm", "kernel": "fit_mask_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel_ms": kern_ms, "alg_bytes_per_launch": alg,
+                     "kernel_ms": kern_ms, "alg_bytes_per_launch": alg, "fit_path": fit_path,
                      "note": "kernel_ms = hipEvent time on the engine stream / launches (incl. the 8*J-byte "
                              "count memset); per-rank shard; traffic: see profiles/ PMC passes"},
     }

@@ -89,6 +89,8 @@ typedef struct {
   int32_t topk;                  /* best-fit candidates kept per group scan (0 = 64) */
   int32_t window_groups;         /* groups per scan window (0 = 64) */
   int64_t window_pods;           /* pods per scan window (0 = 1024) */
+  int32_t fit_path_mask;         /* allowed fit-mask kernels: bit0 int64 compare, bit1 int32 compare,
+                                    bit2 dictionary-coded; 0 = all (the int64 path is always allowed) */
 } pe_config;
 
 typedef struct {
@@ -105,6 +107,7 @@ typedef struct {
   double greedy_host_ms; /* host time parsing + resolving windows (cumulative) */
   int64_t fit_runs_i32;  /* fit-mask launches on the exact 32-bit path (scaled requests) */
   int64_t fit_runs_i64;  /* fit-mask launches on the general 64-bit path */
+  int64_t fit_runs_coded; /* fit-mask launches on the dictionary-coded SWAR path */
 } pe_stats;
 
 int pe_abi_version(void);
@@ -140,11 +143,14 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
                         uint8_t* out_present, int32_t* out_members, uint8_t* out_overflow);
 
 /* What-if feasibility (config 5): bit (j, n) = fit(job j, node n) against the CURRENT residuals
- * of this shard, device-resident.  Word (j, c) holds nodes 64c..64c+63 (bit n%64) and lives at
- *   ((j / 16) * Wt + c / 4) * 64 + (j % 16) * 4 + c % 4,   Wt = ceil(words_per_row / 4)
- * (tile-major: 16 jobs x 256 nodes per 512-B tile, so the kernel writes whole cache lines);
- * pe_fit_mask_rows hands rows back row-major [n_rows][words_per_row].  Counts are per job over
- * this shard (sum them across shards).
+ * of this shard, device-resident.  The kernel picks the fastest exact path for the batch and the
+ * device layout follows it (pe_fit_mask_layout):
+ *   PE_MASK_NODE_TILES (compare paths): word (j, c) holds nodes 64c..64c+63 (bit n%64) at
+ *     ((j / 16) * Wt + c / 4) * 64 + (j % 16) * 4 + c % 4,   Wt = ceil(words_per_row / 4)
+ *   PE_MASK_JOB_BITS (dictionary-coded path): word (b, n) holds jobs 64b..64b+63 (bit j%64) for
+ *     node n at b * S + n,  S = shard nodes rounded up to 512
+ * Both layouts are written as whole 128-B lines.  pe_fit_mask_rows always hands rows back
+ * row-major [n_rows][words_per_row].  Counts are per job over this shard (sum across shards).
  * One-shot form: upload + compute + counts to host; *dev_mask receives the device pointer. */
 int pe_fit_mask(pe_ctx* ctx, int64_t n_jobs, const int64_t* req /*[j][4]*/, const uint32_t* need,
                 int64_t* out_feasible_count, const uint64_t** dev_mask, int64_t* words_per_row);
@@ -153,6 +159,8 @@ int pe_jobs_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32
 int pe_fit_mask_run(pe_ctx* ctx); /* asynchronous on the context stream */
 int pe_fit_counts(pe_ctx* ctx, int64_t* out_feasible_count); /* synchronizes */
 int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out /*[n_rows][words_per_row]*/);
+enum { PE_MASK_NODE_TILES = 0, PE_MASK_JOB_BITS = 1 };
+int pe_fit_mask_layout(const pe_ctx* ctx, int32_t* layout);
 
 /* Greedy best-fit all-or-nothing gang placement.  Jobs in (priority
  * desc, index asc) order, groups of a job in the given order, pods of a group identical.

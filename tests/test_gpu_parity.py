@@ -149,25 +149,56 @@ def test_fit_mask_edge_values(eng):
     assert counts[0] == N - 1 and counts[4] == 1
 
 
-@pytest.mark.parametrize("path", ["i32", "i64"])
-def test_fit_mask_paths(path):
-    """Same inventory, requests that do / do not admit the exact 32-bit form; residuals span the
-    int32 saturation point after scaling (nodes with TiB of memory)."""
-    e = Engine(0)
-    N, J = 5000, 300
-    inv = synth.make_inventory(N, 71, 0.5)
-    inv.cap[1, ::7] = 1 << 50                   # huge memory: saturates in the 32-bit form
-    req, need = synth.make_fit_jobs(J, 73)
-    if path == "i64":
-        req[5, 1] += 1                           # one odd byte count: no common power of two
+PATHS = {"coded": (0, "fit_runs_coded", 1), "i32": (3, "fit_runs_i32", 0), "i64": (1, "fit_runs_i64", 0)}
+
+
+@pytest.mark.parametrize("path", ["coded", "i32", "i64"])
+@pytest.mark.parametrize("N,J", [(5000, 300), (777, 65), (64, 1)])
+def test_fit_mask_paths(path, N, J):
+    """Every exact fit path on the same data (residuals span the int32 saturation point after
+    scaling: nodes with 2^50 B of memory; over-committed nodes with negative residuals)."""
+    mask_bits, stat, layout = PATHS[path]
+    e = Engine(0, fit_path_mask=mask_bits)
+    inv = synth.make_inventory(N, 71 + N, 0.5)
+    inv.cap[1, ::7] = 1 << 50
+    inv.used[0, 3::11] = inv.cap[0, 3::11] + 1000
+    req, need = synth.make_fit_jobs(J, 73 + J)
     e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     counts = e.fit_mask(req, need)
     o_mask, o_counts = oracle.fit_mask(inv.residual(), inv.labels, req, need)
     np.testing.assert_array_equal(e.fit_mask_rows(0, J), o_mask)
     np.testing.assert_array_equal(counts, o_counts)
     s = e.stats()
-    assert (s["fit_runs_i32"], s["fit_runs_i64"]) == ((1, 0) if path == "i32" else (0, 1))
+    assert s[stat] == 1 and s["fit_runs_coded"] + s["fit_runs_i32"] + s["fit_runs_i64"] == 1
+    assert e.fit_mask_layout() == layout
     e.close()
+
+
+@pytest.mark.parametrize("case", ["many_values", "odd_bytes", "label_antichain"])
+def test_fit_mask_path_fallbacks(eng, case):
+    """Batches the coded word cannot hold fall back to the compare kernels, still exact."""
+    N, J = 3000, 400
+    inv = synth.make_inventory(N, 91, 0.3)
+    req, need = synth.make_fit_jobs(J, 93)
+    if case == "many_values":
+        req[:, 0] = 500 + np.arange(J) * 7          # 400 distinct cpu requests: no 32-bit code word
+        want = "fit_runs_i32"
+    elif case == "odd_bytes":
+        req[:, 1] = req[:, 1] + np.arange(J) % 3     # odd byte counts, 3 extra values -> still coded
+        req[:, 0] = 500 + np.arange(J) * 7
+        req[5, 1] += 1                               # and no common power of two -> int64 compare
+        want = "fit_runs_i64"
+    else:
+        inv.labels[:] = np.arange(N, dtype=np.uint32) % 8
+        need[:] = np.where(np.arange(J) % 2 == 0, 1, 2)   # {1} and {2}: not an inclusion chain
+        want = "fit_runs_i32"
+    eng.reset_stats()
+    eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    counts = eng.fit_mask(req, need)
+    o_mask, o_counts = oracle.fit_mask(inv.residual(), inv.labels, req, need)
+    np.testing.assert_array_equal(eng.fit_mask_rows(0, J), o_mask)
+    np.testing.assert_array_equal(counts, o_counts)
+    assert eng.stats()[want] == 1
 
 
 def test_fit_mask_sharded_columns(eng):

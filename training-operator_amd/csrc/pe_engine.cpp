@@ -108,6 +108,12 @@ struct pe_ctx {
   DevBuf<int32_t> res32;
   bool fit32 = false;      // batch is exactly representable in 32 bits (see ReqRec32)
   int fit_shift[pe::D] = {0, 0, 0, 0};
+  int fit_path = 0;        // 0 int64 compare, 1 int32 compare, 2 dictionary-coded SWAR
+  int fit_path_mask = 7;   // allowed paths (pe_config.fit_path_mask)
+  pe::CodeSpec code{};
+  int64_t code_Jp = 0, node_stride = 0;
+  DevBuf<int64_t> code_vals;
+  DevBuf<uint32_t> code_needs, code_jobs, code_x;
   DevBuf<uint64_t> mask;
   DevBuf<unsigned long long> counts;
   HostBuf<unsigned long long> h_counts;
@@ -130,7 +136,8 @@ struct pe_ctx {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
     res0.release(); res.release(); labels.release(); island.release();
-    fit_jobs.release(); fit_jobs32.release(); res32.release(); mask.release(); counts.release(); h_counts.release();
+    fit_jobs.release(); fit_jobs32.release(); res32.release(); mask.release();
+    code_vals.release(); code_needs.release(); code_jobs.release(); code_x.release(); counts.release(); h_counts.release();
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
@@ -226,6 +233,8 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   ctx->window_groups = cfg->window_groups > 0 ? cfg->window_groups : 64;
   ctx->window_pods = cfg->window_pods > 0 ? cfg->window_pods : 1024;
   ctx->gpu_name = cfg->gpu_resource_name ? cfg->gpu_resource_name : "amd.com/gpu";
+  ctx->fit_path_mask = cfg->fit_path_mask > 0 ? (cfg->fit_path_mask & 7) : 7;
+  if (!(ctx->fit_path_mask & 1)) ctx->fit_path_mask |= 1;   // the int64 path is always available
   int rc = PE_OK;
   try {
     hipchk(hipSetDevice(dev), "hipSetDevice");
@@ -393,6 +402,72 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
 
 // ------------------------------------------------------------------ fit mask
 
+// Dictionary codes of one batch (pe_kernels.h, CodeSpec): per dimension the sorted distinct request
+// values, per job their ranks packed with guard bits; label needs must form an inclusion chain.
+// Returns false when the batch does not fit the 32-bit code word (the compare paths take it).
+static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
+  if (n_jobs == 0) return false;
+  std::vector<int64_t> vals[pe::D];
+  for (int d = 0; d < pe::D; ++d) {
+    vals[d].resize((size_t)n_jobs);
+    for (int64_t j = 0; j < n_jobs; ++j) vals[d][j] = req[j * pe::D + d];
+    std::sort(vals[d].begin(), vals[d].end());
+    vals[d].erase(std::unique(vals[d].begin(), vals[d].end()), vals[d].end());
+    if ((int)vals[d].size() >= pe::CODE_MAXV) return false;
+  }
+  std::vector<uint32_t> needs;
+  for (int64_t j = 0; j < n_jobs; ++j) needs.push_back(need ? need[j] : 0u);
+  std::sort(needs.begin(), needs.end(), [](uint32_t a, uint32_t b) {
+    return __builtin_popcount(a) != __builtin_popcount(b) ? __builtin_popcount(a) < __builtin_popcount(b) : a < b;
+  });
+  needs.erase(std::unique(needs.begin(), needs.end()), needs.end());
+  if ((int)needs.size() >= pe::CODE_MAXV) return false;
+  for (size_t i = 0; i + 1 < needs.size(); ++i)
+    if ((needs[i] & needs[i + 1]) != needs[i]) return false;   // not a chain under inclusion
+  pe::CodeSpec sp{};
+  int off = 0;
+  for (int f = 0; f < pe::CODE_FIELDS; ++f) {
+    const int k = f < pe::D ? (int)vals[f].size() : (int)needs.size();
+    const int bits = 32 - __builtin_clz((unsigned)k);
+    sp.nvals[f] = k;
+    sp.width[f] = bits + 1;
+    sp.off[f] = off;
+    off += bits + 1;
+  }
+  if (off > 32) return false;
+  sp.guard = 0;
+  for (int f = 0; f < pe::CODE_FIELDS; ++f) sp.guard |= 1u << (sp.off[f] + sp.width[f] - 1);
+  const int64_t Jp = round_up(n_jobs, pe::FC_JT);
+  std::vector<uint32_t> jc((size_t)Jp, sp.guard);   // padding jobs: code M never fits
+  for (int64_t j = 0; j < n_jobs; ++j) {
+    uint32_t c = 0;
+    for (int d = 0; d < pe::D; ++d) {
+      const int64_t q = req[j * pe::D + d];
+      const uint32_t rank = (uint32_t)(std::lower_bound(vals[d].begin(), vals[d].end(), q) - vals[d].begin()) + 1;
+      c |= rank << sp.off[d];
+    }
+    const uint32_t nd = need ? need[j] : 0u;
+    const uint32_t rank = (uint32_t)(std::find(needs.begin(), needs.end(), nd) - needs.begin()) + 1;
+    c |= rank << sp.off[4];
+    jc[j] = c;
+  }
+  std::vector<int64_t> vt((size_t)pe::D * pe::CODE_MAXV, INT64_MAX);
+  for (int d = 0; d < pe::D; ++d) std::copy(vals[d].begin(), vals[d].end(), vt.begin() + (size_t)d * pe::CODE_MAXV);
+  std::vector<uint32_t> nt((size_t)pe::CODE_MAXV, 0xFFFFFFFFu);
+  std::copy(needs.begin(), needs.end(), nt.begin());
+  ctx->code = sp;
+  ctx->code_Jp = Jp;
+  ctx->node_stride = round_up(std::max<int64_t>(ctx->Ns, 1), 64 * pe::FC_CH);
+  hipchk(ctx->code_vals.ensure(vt.size()), "alloc code vals");
+  hipchk(ctx->code_needs.ensure(nt.size()), "alloc code needs");
+  hipchk(ctx->code_jobs.ensure(jc.size()), "alloc code jobs");
+  hipchk(ctx->code_x.ensure((size_t)ctx->node_stride), "alloc code x");
+  hipchk(hipMemcpyAsync(ctx->code_vals.p, vt.data(), vt.size() * 8, hipMemcpyHostToDevice, ctx->stream), "H2D vals");
+  hipchk(hipMemcpyAsync(ctx->code_needs.p, nt.data(), nt.size() * 4, hipMemcpyHostToDevice, ctx->stream), "H2D needs");
+  hipchk(hipMemcpyAsync(ctx->code_jobs.p, jc.data(), jc.size() * 4, hipMemcpyHostToDevice, ctx->stream), "H2D codes");
+  return true;
+}
+
 static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
   if (n_jobs < 0) raise(PE_EINVAL, "n_jobs < 0");
   if (!ctx->loaded) raise(PE_ESTATE, "no inventory loaded");
@@ -423,8 +498,8 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
     if (orv & ((int64_t(1) << sh) - 1)) use32 = false;
     ctx->fit_shift[d] = sh;
   }
-  ctx->fit32 = use32;
-  if (use32) {
+  ctx->fit32 = use32 && (ctx->fit_path_mask & 2);
+  if (ctx->fit32) {
     std::vector<pe::ReqRec32> r32((size_t)Jp);
     for (int64_t j = 0; j < Jp; ++j) {
       std::memset(&r32[j], 0, sizeof(pe::ReqRec32));
@@ -442,8 +517,12 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
   ctx->fit_Jp = Jp;
   ctx->Wn = (ctx->Ns + 63) / 64;
   ctx->Wt = (ctx->Wn + 3) / 4;
+  ctx->fit_path = ctx->fit32 ? 1 : 0;
+  if ((ctx->fit_path_mask & 4) && build_codes(ctx, n_jobs, req, need)) ctx->fit_path = 2;
   hipchk(ctx->fit_jobs.ensure(Jp), "alloc fit jobs");
-  hipchk(ctx->mask.ensure((size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4), "alloc fit mask");
+  const size_t mask_words = ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
+                                               : (size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4;
+  hipchk(ctx->mask.ensure(mask_words), "alloc fit mask");
   hipchk(ctx->counts.ensure(Jp), "alloc fit counts");
   hipchk(ctx->h_counts.ensure(Jp), "alloc pinned counts");
   hipchk(hipMemcpyAsync(ctx->fit_jobs.p, recs.data(), Jp * sizeof(ReqRec), hipMemcpyHostToDevice, ctx->stream),
@@ -462,7 +541,19 @@ static void fit_run(pe_ctx* ctx) {
   const int64_t want_x = std::max<int64_t>(1, (16384 + waves_y - 1) / waves_y);
   int64_t tpw = (ctx->Ns + 256 * want_x - 1) / (256 * want_x);
   tpw = std::min<int64_t>(16, std::max<int64_t>(1, tpw));
-  if (ctx->fit32) {
+  if (ctx->fit_path == 2) {
+    const int64_t jblocks = ctx->code_Jp / pe::FC_JT;
+    const int64_t want_x2 = std::max<int64_t>(1, (16384 + jblocks - 1) / jblocks);
+    int64_t tpw2 = (ctx->Ns + 64 * pe::FC_CH * want_x2 - 1) / (64 * pe::FC_CH * want_x2);
+    tpw2 = std::min<int64_t>(64, std::max<int64_t>(1, tpw2));
+    hipchk(pe::launch_encode_nodes(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->node_stride,
+                                   ctx->code, ctx->code_vals.p, ctx->code_needs.p, ctx->code_x.p),
+           "launch encode_nodes");
+    hipchk(pe::launch_fit_mask_coded(ctx->stream, ctx->code_x.p, ctx->Ns, ctx->node_stride, ctx->code_jobs.p,
+                                     ~ctx->code.guard, J, tpw2, ctx->mask.p, ctx->counts.p),
+           "launch fit_mask_coded");
+    ctx->stats.fit_runs_coded += 1;
+  } else if (ctx->fit32) {
     hipchk(pe::launch_compress_res(ctx->stream, ctx->res.p, ctx->res32.p, ctx->stride, ctx->Ns, ctx->fit_shift),
            "launch compress_res");
     hipchk(pe::launch_fit_mask32(ctx->stream, ctx->res32.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->Wt,
@@ -517,6 +608,27 @@ int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out) {
     if (row0 < 0 || n_rows < 0 || row0 + n_rows > ctx->fit_J) raise(PE_EINVAL, "row range");
     if (n_rows == 0 || ctx->Wn == 0) return PE_OK;
     need_ptr(out, "out");
+    if (ctx->fit_path == 2) {
+      // bits-over-jobs layout: copy the 64-job bands, transpose the rows out
+      const int64_t b0 = row0 / 64, b1 = (row0 + n_rows - 1) / 64;
+      const size_t band = (size_t)ctx->node_stride;
+      std::vector<uint64_t> bands((size_t)(b1 - b0 + 1) * band);
+      hipchk(hipMemcpyAsync(bands.data(), ctx->mask.p + (size_t)b0 * band, bands.size() * 8, hipMemcpyDeviceToHost,
+                            ctx->stream),
+             "D2H mask");
+      hipchk(hipStreamSynchronize(ctx->stream), "sync mask");
+      for (int64_t r = 0; r < n_rows; ++r) {
+        const int64_t j = row0 + r;
+        const uint64_t* bw = bands.data() + (size_t)(j / 64 - b0) * band;
+        const int bit = (int)(j % 64);
+        for (int64_t c = 0; c < ctx->Wn; ++c) {
+          uint64_t word = 0;
+          for (int i = 0; i < 64 && c * 64 + i < ctx->Ns; ++i) word |= ((bw[c * 64 + i] >> bit) & 1ull) << i;
+          out[(size_t)r * ctx->Wn + c] = word;
+        }
+      }
+      return PE_OK;
+    }
     // copy the 16-row tile bands covering the rows, then untile into row-major
     const int64_t t0 = row0 / 16, t1 = (row0 + n_rows - 1) / 16;
     const size_t band = (size_t)ctx->Wt * 64;
@@ -677,6 +789,12 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return PE_OK;
   });
+}
+
+int pe_fit_mask_layout(const pe_ctx* ctx, int32_t* layout) {
+  if (!ctx || !layout) return PE_EINVAL;
+  *layout = ctx->fit_path == 2 ? PE_MASK_JOB_BITS : PE_MASK_NODE_TILES;
+  return PE_OK;
 }
 
 int pe_synchronize(pe_ctx* ctx) {

@@ -82,6 +82,31 @@ hipError_t launch_fit_mask32(hipStream_t s, const int32_t* res32, int64_t stride
                              int64_t Ns, int64_t Wt, const ReqRec32* jobs, int64_t J, int64_t tiles_per_wave,
                              uint64_t* mask, unsigned long long* counts);
 
+// ---- dictionary-coded SWAR path (fit mask).  Per batch the host ranks the distinct request
+// values of each dimension (and a chain of label needs); field f of a node's 32-bit code word is
+// (#batch values <= residual) + guard bit, the job's word holds its values' ranks.  Then
+//   fit(j, n)  <=>  ((X[n] - C[j]) | ~M) == 0xFFFFFFFF   (every field keeps its guard bit)
+// exactly, for all 4 dimensions and the labels at once.
+constexpr int CODE_FIELDS = 5;   // cpu, memory, gpu, ephemeral, label-chain
+constexpr int CODE_MAXV = 128;   // distinct values per field the device tables hold
+struct CodeSpec {
+  int off[CODE_FIELDS];
+  int width[CODE_FIELDS];       // code bits + 1 guard bit
+  int nvals[CODE_FIELDS];
+  uint32_t guard;               // M
+};
+constexpr int FC_CH = 8;        // coded fit: 64-node chunks per wave tile (X in 8 VGPRs)
+constexpr int FC_JT = 64;       // coded fit: jobs per wave (one 64-bit word per node)
+
+// vals: [4][CODE_MAXV] sorted int64 request values; needs: [CODE_MAXV] label chain (inclusion order)
+hipError_t launch_encode_nodes(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
+                               int64_t n_pad, CodeSpec spec, const int64_t* vals, const uint32_t* needs, uint32_t* X);
+// Coded-path mask layout (bits over jobs): word (b, n) = jobs 64b..64b+63 at node n (bit j%64),
+// stored at b * node_stride + n, node_stride = ceil(Ns/512)*512.
+hipError_t launch_fit_mask_coded(hipStream_t s, const uint32_t* X, int64_t Ns, int64_t node_stride,
+                                 const uint32_t* jcode, uint32_t not_guard, int64_t J, int64_t tiles_per_wave,
+                                 uint64_t* mask, unsigned long long* counts);
+
 hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
                        uint64_t id_base, const ReqRec* groups, int Wg, uint64_t* cand, int32_t* cnt,
                        uint64_t* bound, int nwaves);

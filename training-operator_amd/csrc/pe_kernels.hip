@@ -279,6 +279,121 @@ hipError_t launch_compress_res(hipStream_t s, const int64_t* res, int32_t* res32
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ coded fit mask (config 5)
+
+__global__ __launch_bounds__(256) void encode_nodes_kernel(const int64_t* __restrict__ res, int64_t stride,
+                                                           const uint32_t* __restrict__ labels, int64_t Ns,
+                                                           int64_t n_pad, CodeSpec spec,
+                                                           const int64_t* __restrict__ vals,
+                                                           const uint32_t* __restrict__ needs,
+                                                           uint32_t* __restrict__ X) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_pad) return;
+  if (n >= Ns) {              // padding node: every field at code 0 -> fails every job (ranks >= 1)
+    X[n] = spec.guard;
+    return;
+  }
+  uint32_t x = 0;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const int64_t r = res[d * stride + n];
+    const int64_t* v = vals + d * CODE_MAXV;
+    int lo = 0, hi = spec.nvals[d];            // code = #{v <= r} (upper bound in sorted values)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (v[mid] <= r) lo = mid + 1;
+      else hi = mid;
+    }
+    x |= ((uint32_t)lo | (1u << (spec.width[d] - 1))) << spec.off[d];
+  }
+  const uint32_t lab = labels[n];
+  int k = 0;                                    // needs form an inclusion chain: satisfied = prefix
+  while (k < spec.nvals[4] && (needs[k] & lab) == needs[k]) ++k;
+  x |= ((uint32_t)k | (1u << (spec.width[4] - 1))) << spec.off[4];
+  X[n] = x;
+}
+
+hipError_t launch_encode_nodes(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
+                               int64_t n_pad, CodeSpec spec, const int64_t* vals, const uint32_t* needs, uint32_t* X) {
+  if (n_pad <= 0) return hipSuccess;
+  hipLaunchKernelGGL(encode_nodes_kernel, dim3((unsigned)((n_pad + 255) / 256)), dim3(256), 0, s, res, stride, labels,
+                     Ns, n_pad, spec, vals, needs, X);
+  return hipGetLastError();
+}
+
+// One (job, chunk) step: tmp = (X - C) | ~M; carry = (tmp + 1 overflows) = fit for this lane;
+// w = 2w + carry shifts the job's bit in.  VCC-style carries between VALU ops need no wait states
+// (the same pattern as a 64-bit add).  Returns the 64-lane fit mask (for the job's popcount).
+__device__ __forceinline__ uint64_t fc_step(uint32_t x, uint32_t code, uint32_t not_guard, uint32_t& w) {
+  uint32_t tmp;
+  uint64_t fit;
+  asm("v_sub_u32_e64 %0, %3, %4\n\t"
+      "v_or_b32_e32 %0, %5, %0\n\t"
+      "v_add_co_u32_e64 %0, %1, %0, 1\n\t"
+      "v_addc_co_u32_e64 %2, vcc, %2, %2, %1"
+      : "=&v"(tmp), "=&s"(fit), "+v"(w)
+      : "v"(x), "s"(code), "s"(not_guard)
+      : "vcc");
+  return fit;
+}
+
+template <int HALF, int JJ>
+__device__ __forceinline__ void fc_jobs(const uint32_t* __restrict__ codes, const uint32_t (&x)[FC_CH],
+                                        uint32_t not_guard, uint32_t (&w)[FC_CH], uint32_t& cnt) {
+  // jobs are shifted in from the top of the half (JJ = 31 first) so job 32*HALF + jj ends in bit jj
+  const uint32_t code = codes[HALF * 32 + JJ];
+  unsigned pc = 0;
+#pragma unroll
+  for (int c = 0; c < FC_CH; ++c) pc += (unsigned)__popcll(fc_step(x[c], code, not_guard, w[c]));
+  const unsigned prev = (unsigned)__builtin_amdgcn_readlane((int)cnt, HALF * 32 + JJ);
+  cnt = writelane<HALF * 32 + JJ>(cnt, prev + pc);
+  if constexpr (JJ > 0) fc_jobs<HALF, JJ - 1>(codes, x, not_guard, w, cnt);
+}
+
+// Wave tile = FC_CH chunks x 64 nodes of code words (8 VGPRs) x FC_JT jobs whose code words are
+// wave-uniform (scalar loads).  4 VALU per (job, chunk) = per 64 fit evaluations, the words leave
+// as whole-line 512-B stores (bits over jobs), per-job counts are s_bcnt1 of the carry masks.
+__global__ __launch_bounds__(256) void fit_mask_coded_kernel(const uint32_t* __restrict__ X, int64_t Ns,
+                                                             int64_t node_stride, const uint32_t* __restrict__ jcode,
+                                                             uint32_t not_guard, int64_t J, int64_t tiles_per_wave,
+                                                             uint64_t* __restrict__ mask,
+                                                             unsigned long long* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_id = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t node_base = wave_id * tiles_per_wave * (64 * FC_CH);
+  if (node_base >= Ns) return;
+  const int64_t jb = (int64_t)blockIdx.y * FC_JT;      // 64 jobs; codes padded with M (never fits)
+  const int64_t ntile = min(tiles_per_wave, (Ns - node_base + 64 * FC_CH - 1) / (64 * FC_CH));
+  uint32_t cnt = 0;                                    // lane i counts job jb + i
+  uint64_t* row = mask + (jb >> 6) * node_stride + node_base + lane;
+  for (int64_t t = 0; t < ntile; ++t) {
+    uint32_t x[FC_CH];
+#pragma unroll
+    for (int c = 0; c < FC_CH; ++c) x[c] = X[node_base + t * (64 * FC_CH) + c * 64 + lane];   // padded
+    uint32_t lo[FC_CH], hi[FC_CH];
+#pragma unroll
+    for (int c = 0; c < FC_CH; ++c) lo[c] = hi[c] = 0;
+    fc_jobs<0, 31>(jcode + jb, x, not_guard, lo, cnt);
+    fc_jobs<1, 31>(jcode + jb, x, not_guard, hi, cnt);
+#pragma unroll
+    for (int c = 0; c < FC_CH; ++c) row[t * (64 * FC_CH) + c * 64] = ((uint64_t)hi[c] << 32) | lo[c];
+  }
+  const int64_t j = jb + lane;
+  if (j < J && cnt) atomicAdd(&counts[j], (unsigned long long)cnt);
+}
+
+hipError_t launch_fit_mask_coded(hipStream_t s, const uint32_t* X, int64_t Ns, int64_t node_stride,
+                                 const uint32_t* jcode, uint32_t not_guard, int64_t J, int64_t tiles_per_wave,
+                                 uint64_t* mask, unsigned long long* counts) {
+  if (J <= 0 || Ns <= 0) return hipSuccess;
+  const int64_t span = tiles_per_wave * 64 * FC_CH;
+  const int64_t waves = (Ns + span - 1) / span;
+  dim3 grid((unsigned)((waves + 3) / 4), (unsigned)((J + FC_JT - 1) / FC_JT));
+  hipLaunchKernelGGL(fit_mask_coded_kernel, grid, dim3(256), 0, s, X, Ns, node_stride, jcode, not_guard, J,
+                     tiles_per_wave, mask, counts);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ best-fit scan (configs 2-4)
 
 // Appendix B key: fit ? (score << 24) | gid : NO_KEY, score = min(a+b+c+d, 2^40-1) with

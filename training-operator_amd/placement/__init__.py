@@ -52,7 +52,7 @@ class Engine:
 
     def __init__(self, device_id: int = 0, rank: int = 0, world_size: int = 1, comm: Optional[bytes] = None,
                  exchange=None, max_nodes: int = 0, gpu_resource_name: str = "amd.com/gpu", topk: int = 0,
-                 window_groups: int = 0, window_pods: int = 0):
+                 window_groups: int = 0, window_pods: int = 0, fit_path_mask: int = 0):
         self.lib = _abi.load()
         self._keep = []
         cfg = _abi.PeConfig()
@@ -81,6 +81,7 @@ class Engine:
         cfg.topk = topk
         cfg.window_groups = window_groups
         cfg.window_pods = window_pods
+        cfg.fit_path_mask = fit_path_mask
         self._cfg = cfg
         h = ctypes.c_void_p()
         rc = self.lib.pe_create(ctypes.byref(cfg), ctypes.byref(h))
@@ -174,6 +175,11 @@ class Engine:
         self.fit_jobs = req.shape[0]
         self.words_per_row = wpr.value
         return counts
+
+    def fit_mask_layout(self) -> int:
+        v = ctypes.c_int32()
+        self._chk(self.lib.pe_fit_mask_layout(self.h, ctypes.byref(v)), "pe_fit_mask_layout")
+        return v.value
 
     def fit_mask_rows(self, row0: int, n_rows: int) -> np.ndarray:
         b, e = self.shard_range()

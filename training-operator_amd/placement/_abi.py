@@ -32,7 +32,7 @@ class PeConfig(ctypes.Structure):
     _fields_ = [("device_id", ctypes.c_int32), ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32),
                 ("comm_id", ctypes.c_void_p), ("exchange", ALLGATHER_FN), ("exchange_user", ctypes.c_void_p),
                 ("max_nodes", ctypes.c_int64), ("gpu_resource_name", ctypes.c_char_p), ("topk", ctypes.c_int32),
-                ("window_groups", ctypes.c_int32), ("window_pods", ctypes.c_int64)]
+                ("window_groups", ctypes.c_int32), ("window_pods", ctypes.c_int64), ("fit_path_mask", ctypes.c_int32)]
 
 
 class PeStats(ctypes.Structure):
@@ -40,7 +40,7 @@ class PeStats(ctypes.Structure):
                 ("rescans", ctypes.c_int64), ("groups_scanned", ctypes.c_int64), ("pods_placed", ctypes.c_int64),
                 ("jobs_placed", ctypes.c_int64), ("jobs_failed", ctypes.c_int64), ("last_greedy_ms", ctypes.c_double),
                 ("greedy_wait_ms", ctypes.c_double), ("greedy_host_ms", ctypes.c_double),
-                ("fit_runs_i32", ctypes.c_int64), ("fit_runs_i64", ctypes.c_int64)]
+                ("fit_runs_i32", ctypes.c_int64), ("fit_runs_i64", ctypes.c_int64), ("fit_runs_coded", ctypes.c_int64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -66,6 +66,7 @@ SIGNATURES = {
     "pe_fit_mask_run": (ctypes.c_int, [P]),
     "pe_fit_counts": (ctypes.c_int, [P, P]),
     "pe_fit_mask_rows": (ctypes.c_int, [P, i64, i64, P]),
+    "pe_fit_mask_layout": (ctypes.c_int, [P, ctypes.POINTER(i32)]),
     "pe_place_greedy": (ctypes.c_int, [P, i64, P, P, P, P, P, P, P]),
     "pe_resolver_create": (ctypes.c_int, [i64, P, P, P, P, P, ctypes.POINTER(P)]),
     "pe_resolver_destroy": (None, [P]),
