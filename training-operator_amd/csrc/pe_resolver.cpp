@@ -4,7 +4,6 @@
 #include <algorithm>
 #include <cstring>
 #include <numeric>
-#include <set>
 #include <utility>
 
 namespace pe {
@@ -32,6 +31,77 @@ uint64_t key_of(const int64_t res[RD], uint32_t labels, const int64_t q[RD], uin
     left[d] = res[d] - q[d];
   }
   return (score_of(left) << 24) | gid;
+}
+
+// ------------------------------------------------------------------ DirtySet
+
+int32_t DirtySet::upsert(int64_t g, const NodeState& st) {
+  if (g >= (int64_t)slot_.size()) slot_.resize((size_t)std::max<int64_t>(g + 1, 2 * (int64_t)slot_.size()), -1);
+  int32_t i = slot_[g];
+  if (i < 0) {
+    i = (int32_t)gid.size();
+    slot_[g] = i;
+    gid.push_back(g);
+    r0.push_back(0);
+    r1.push_back(0);
+    r2.push_back(0);
+    r3.push_back(0);
+    lab.push_back(0);
+  }
+  set(i, st);
+  return i;
+}
+
+void DirtySet::set(int32_t i, const NodeState& st) {
+  r0[i] = st.res[0];
+  r1[i] = st.res[1];
+  r2[i] = st.res[2];
+  r3[i] = st.res[3];
+  lab[i] = st.labels;
+}
+
+NodeState DirtySet::get(int32_t i) const {
+  NodeState st;
+  st.res[0] = r0[i];
+  st.res[1] = r1[i];
+  st.res[2] = r2[i];
+  st.res[3] = r3[i];
+  st.labels = lab[i];
+  return st;
+}
+
+void DirtySet::clear() {
+  for (int64_t g : gid) slot_[g] = -1;
+  gid.clear();
+  r0.clear();
+  r1.clear();
+  r2.clear();
+  r3.clear();
+  lab.clear();
+}
+
+// Branch-free Appendix-B key (same arithmetic as the device's node_key)
+static inline uint64_t key_bf(int64_t x0, int64_t x1, int64_t x2, int64_t x3, uint32_t l, const int64_t q[RD],
+                              uint32_t need, uint64_t g) {
+  const bool fit = ((l & need) == need) & (q[0] <= x0) & (q[1] <= x1) & (q[2] <= x2) & (q[3] <= x3);
+  const uint64_t a = (uint64_t)x0 - (uint64_t)q[0];
+  const uint64_t b = ((uint64_t)x1 - (uint64_t)q[1]) >> 20;
+  const uint64_t c = (uint64_t)x2 - (uint64_t)q[2];
+  const uint64_t d = ((uint64_t)x3 - (uint64_t)q[3]) >> 24;
+  const bool big = (a > kScoreMax) | (b > kScoreMax) | (c >= (1ull << 20)) | (d > kScoreMax);
+  const uint64_t sum = a + b + (c << 20) + d;
+  const uint64_t score = (big | (sum > kScoreMax)) ? kScoreMax : sum;
+  return fit ? ((score << 24) | g) : kNoKey;
+}
+
+void DirtySet::keys(const int64_t q[RD], uint32_t need, std::vector<uint64_t>& out) const {
+  const size_t n = gid.size();
+  out.resize(n);
+  for (size_t i = 0; i < n; ++i) out[i] = key_bf(r0[i], r1[i], r2[i], r3[i], lab[i], q, need, (uint64_t)gid[i]);
+}
+
+uint64_t DirtySet::key_at(int32_t i, const int64_t q[RD], uint32_t need) const {
+  return key_bf(r0[i], r1[i], r2[i], r3[i], lab[i], q, need, (uint64_t)gid[i]);
 }
 
 void merge_shards(const std::vector<const GroupCands*>& parts, GroupCands& out) {
@@ -124,7 +194,7 @@ void Resolver::finish_job(bool ok) {
         --pods_placed_;
       }
     }
-    for (const auto& kv : job_nodes_) dirty_[kv.first] = kv.second;
+    for (const auto& kv : job_nodes_) dirty_.upsert(kv.first, kv.second);
     job_status_[j] = 1;
     ++jobs_failed_;
   }
@@ -163,63 +233,68 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
                        std::vector<Update>& updates) {
   bool consumed = true;
   size_t wi = 0;
-  std::set<std::pair<uint64_t, int64_t>> dk;  // dirty nodes that fit the current group, by key
-  std::unordered_map<int64_t, uint64_t> dkey;
+  std::vector<uint64_t>& dk = dk_;  // keys of the dirty nodes for the current group
+  auto argmin = [&dk]() -> int32_t {
+    int32_t b = -1;
+    uint64_t bk = kNoKey;
+    for (size_t i = 0; i < dk.size(); ++i)
+      if (dk[i] < bk) {
+        bk = dk[i];
+        b = (int32_t)i;
+      }
+    return b;
+  };
   while (!done() && wi < groups.size()) {
     while (wi < groups.size() && groups[wi] != g_) ++wi;  // groups of failed jobs are skipped
     if (wi == groups.size()) break;
     const GroupCands& gc = cands[wi];
     const int64_t* q = req_ + (int64_t)g_ * RD;
     const uint32_t need = need_[g_];
-    dk.clear();
-    dkey.clear();
-    for (const auto& kv : dirty_) {
-      const uint64_t k = key_of(kv.second.res, kv.second.labels, q, need, (uint64_t)kv.first);
-      if (k != kNoKey) {
-        dk.emplace(k, kv.first);
-        dkey[kv.first] = k;
-      }
-    }
+    dirty_.keys(q, need, dk);
+    int32_t best = argmin();
     size_t ptr = 0;
     bool failed = false;
     while (p_ < cnt_[g_]) {
-      while (ptr < gc.list.size() && dirty_.count((int64_t)(gc.list[ptr].key & 0xFFFFFFull))) ++ptr;
+      while (ptr < gc.list.size() && dirty_.find((int64_t)(gc.list[ptr].key & 0xFFFFFFull)) >= 0) ++ptr;
       const uint64_t kc = ptr < gc.list.size() ? gc.list[ptr].key : kNoKey;
-      const uint64_t kd = dk.empty() ? kNoKey : dk.begin()->first;
+      const uint64_t kd = best >= 0 ? dk[best] : kNoKey;
       if (ptr == gc.list.size() && gc.limit != kNoKey && kd >= gc.limit) {
         consumed = false;  // clean nodes beyond the limit could win: rescan from this pod
         break;
       }
-      const uint64_t best = std::min(kc, kd);
-      if (best == kNoKey) {
+      const uint64_t bkey = std::min(kc, kd);
+      if (bkey == kNoKey) {
         failed = true;
         break;
       }
-      const int64_t gid = (int64_t)(best & 0xFFFFFFull);
+      const int64_t gid = (int64_t)(bkey & 0xFFFFFFull);
       NodeState st;
-      if (best == kd) {
-        st = dirty_[gid];
+      int32_t slot;
+      if (bkey == kd) {
+        slot = best;
+        st = dirty_.get(slot);
       } else {
         const Cand& c = gc.list[ptr];
         for (int d = 0; d < RD; ++d) st.res[d] = c.res[d];
         st.labels = c.labels;
+        slot = -1;
       }
       for (int d = 0; d < RD; ++d) st.res[d] -= q[d];
-      dirty_[gid] = st;
+      if (slot < 0) {
+        slot = dirty_.upsert(gid, st);
+        dk.push_back(kNoKey);
+      } else {
+        dirty_.set(slot, st);
+      }
       job_nodes_[gid] = st;
       pod_node_[pod_off_[g_] + p_] = (int32_t)gid;
       ++p_;
       ++pods_placed_;
-      auto it = dkey.find(gid);
-      if (it != dkey.end()) {
-        dk.erase({it->second, gid});
-        dkey.erase(it);
-      }
-      const uint64_t nk = key_of(st.res, st.labels, q, need, (uint64_t)gid);
-      if (nk != kNoKey) {
-        dk.emplace(nk, gid);
-        dkey[gid] = nk;
-      }
+      // the chosen node's key only falls while it still fits (its leftovers shrink), so it stays
+      // the minimum; once it no longer fits the next minimum is searched
+      dk[slot] = dirty_.key_at(slot, q, need);
+      if (dk[slot] != kNoKey) best = slot;
+      else if (best == slot) best = argmin();
     }
     if (!consumed) break;
     if (failed) {
@@ -232,10 +307,11 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     }
     ++wi;
   }
-  for (const auto& kv : dirty_) {
+  for (size_t i = 0; i < dirty_.size(); ++i) {
     Update u;
-    u.gid = kv.first;
-    for (int d = 0; d < RD; ++d) u.res[d] = kv.second.res[d];
+    u.gid = dirty_.gid[i];
+    const NodeState st = dirty_.get((int32_t)i);
+    for (int d = 0; d < RD; ++d) u.res[d] = st.res[d];
     updates.push_back(u);
   }
   dirty_.clear();

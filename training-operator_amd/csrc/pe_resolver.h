@@ -10,6 +10,7 @@
 // the device and the next window rescans from the current pod.  Pure C++, no HIP: the same code
 // runs behind every shard (all ranks resolve identically) and under the CPU tests.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #include <unordered_map>
@@ -51,6 +52,26 @@ void merge_shards(const std::vector<const GroupCands*>& parts, GroupCands& out);
 // what the merge kernel writes.  Parses and merges the shards into cands[n_groups].
 void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands);
 
+// Nodes modified since the window's snapshot, as flat struct-of-arrays so the per-group re-score
+// is one branch-free (vectorisable) loop; gid -> slot is a direct-mapped array grown on demand.
+class DirtySet {
+ public:
+  int32_t find(int64_t gid) const { return gid < (int64_t)slot_.size() ? slot_[gid] : -1; }
+  int32_t upsert(int64_t gid, const NodeState& st);
+  void set(int32_t i, const NodeState& st);
+  NodeState get(int32_t i) const;
+  size_t size() const { return gid.size(); }
+  void clear();
+  // keys of every dirty node for request (q, need) -> out (NO_KEY where it does not fit)
+  void keys(const int64_t q[RD], uint32_t need, std::vector<uint64_t>& out) const;
+  uint64_t key_at(int32_t i, const int64_t q[RD], uint32_t need) const;
+  std::vector<int64_t> gid, r0, r1, r2, r3;
+  std::vector<uint32_t> lab;
+
+ private:
+  std::vector<int32_t> slot_;
+};
+
 class Resolver {
  public:
   Resolver(int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority, const int32_t* group_count,
@@ -90,7 +111,8 @@ class Resolver {
   int32_t g_ = 0;   // global group index inside the current job
   int32_t p_ = 0;   // next pod of group g_
   // window state
-  std::unordered_map<int64_t, NodeState> dirty_;
+  DirtySet dirty_;
+  std::vector<uint64_t> dk_;
   // nodes touched by the current job (exact current residuals, survive window flushes)
   std::unordered_map<int64_t, NodeState> job_nodes_;
   int64_t jobs_placed_ = 0, jobs_failed_ = 0, pods_placed_ = 0, rescans_ = 0;
