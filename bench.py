@@ -174,7 +174,7 @@ def main():
     kern_ms = ev.elapsed_ms(e0, e1) / args.steps
     value = float(N) * J * args.steps / elapsed
     st0 = eng.stats()
-    fit_path = "coded" if st0["fit_runs_coded"] else ("i32" if st0["fit_runs_i32"] else "i64")
+    fit_path = ("coded-therm" if st0["fit_runs_therm"] else "coded-swar") if st0["fit_runs_coded"] else ("i32" if st0["fit_runs_i32"] else "i64")
     alg = fit_bytes(Ns, J)
     achieved = alg / (kern_ms * 1e-3) / 1e9
 

@@ -90,7 +90,9 @@ typedef struct {
   int32_t window_groups;         /* groups per scan window (0 = 64) */
   int64_t window_pods;           /* pods per scan window (0 = 1024) */
   int32_t fit_path_mask;         /* allowed fit-mask kernels: bit0 int64 compare, bit1 int32 compare,
-                                    bit2 dictionary-coded; 0 = all (the int64 path is always allowed) */
+                                    bit2 dictionary-coded; bit3 set = no thermometer form of the
+                                    coded kernel; bits 0-2 all clear = all kernels (the int64 path is
+                                    always allowed) */
 } pe_config;
 
 typedef struct {
@@ -107,7 +109,8 @@ typedef struct {
   double greedy_host_ms; /* host time parsing + resolving windows (cumulative) */
   int64_t fit_runs_i32;  /* fit-mask launches on the exact 32-bit path (scaled requests) */
   int64_t fit_runs_i64;  /* fit-mask launches on the general 64-bit path */
-  int64_t fit_runs_coded; /* fit-mask launches on the dictionary-coded SWAR path */
+  int64_t fit_runs_coded; /* fit-mask launches on the dictionary-coded path (SWAR or thermometer) */
+  int64_t fit_runs_therm; /* ... of which used the thermometer code (3 VALU per 64 evaluations) */
 } pe_stats;
 
 int pe_abi_version(void);

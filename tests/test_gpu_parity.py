@@ -149,10 +149,10 @@ def test_fit_mask_edge_values(eng):
     assert counts[0] == N - 1 and counts[4] == 1
 
 
-PATHS = {"coded": (0, "fit_runs_coded", 1), "i32": (3, "fit_runs_i32", 0), "i64": (1, "fit_runs_i64", 0)}
+PATHS = {"therm": (0, "fit_runs_therm", 1), "swar": (8, "fit_runs_coded", 1), "i32": (3, "fit_runs_i32", 0), "i64": (1, "fit_runs_i64", 0)}
 
 
-@pytest.mark.parametrize("path", ["coded", "i32", "i64"])
+@pytest.mark.parametrize("path", ["therm", "swar", "i32", "i64"])
 @pytest.mark.parametrize("N,J", [(5000, 300), (777, 65), (64, 1)])
 def test_fit_mask_paths(path, N, J):
     """Every exact fit path on the same data (residuals span the int32 saturation point after
@@ -170,6 +170,7 @@ def test_fit_mask_paths(path, N, J):
     np.testing.assert_array_equal(counts, o_counts)
     s = e.stats()
     assert s[stat] == 1 and s["fit_runs_coded"] + s["fit_runs_i32"] + s["fit_runs_i64"] == 1
+    assert s["fit_runs_therm"] == (path == "therm")
     assert e.fit_mask_layout() == layout
     e.close()
 

@@ -233,8 +233,9 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   ctx->window_groups = cfg->window_groups > 0 ? cfg->window_groups : 64;
   ctx->window_pods = cfg->window_pods > 0 ? cfg->window_pods : 1024;
   ctx->gpu_name = cfg->gpu_resource_name ? cfg->gpu_resource_name : "amd.com/gpu";
-  ctx->fit_path_mask = cfg->fit_path_mask > 0 ? (cfg->fit_path_mask & 7) : 7;
-  if (!(ctx->fit_path_mask & 1)) ctx->fit_path_mask |= 1;   // the int64 path is always available
+  ctx->fit_path_mask = cfg->fit_path_mask > 0 ? (cfg->fit_path_mask & 15) : 7;
+  if (!(ctx->fit_path_mask & 7)) ctx->fit_path_mask |= 7;   // no kernel bits = all kernels
+  ctx->fit_path_mask |= 1;                                    // the int64 path is always available
   int rc = PE_OK;
   try {
     hipchk(hipSetDevice(dev), "hipSetDevice");
@@ -425,20 +426,27 @@ static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const u
   for (size_t i = 0; i + 1 < needs.size(); ++i)
     if ((needs[i] & needs[i + 1]) != needs[i]) return false;   // not a chain under inclusion
   pe::CodeSpec sp{};
+  int therm_bits = 0;
+  for (int f = 0; f < pe::CODE_FIELDS; ++f) therm_bits += f < pe::D ? (int)vals[f].size() : (int)needs.size();
+  // thermometer fields (one bit per distinct value) when they fit 31 bits -- bit 31 stays free for
+  // the never-fitting padding jobs -- else log-width SWAR fields with guard bits
+  sp.therm = (ctx->fit_path_mask & 8) == 0 && therm_bits <= 31 ? 1 : 0;
   int off = 0;
   for (int f = 0; f < pe::CODE_FIELDS; ++f) {
     const int k = f < pe::D ? (int)vals[f].size() : (int)needs.size();
     const int bits = 32 - __builtin_clz((unsigned)k);
     sp.nvals[f] = k;
-    sp.width[f] = bits + 1;
+    sp.width[f] = sp.therm ? k : bits + 1;
     sp.off[f] = off;
-    off += bits + 1;
+    off += sp.width[f];
   }
   if (off > 32) return false;
   sp.guard = 0;
-  for (int f = 0; f < pe::CODE_FIELDS; ++f) sp.guard |= 1u << (sp.off[f] + sp.width[f] - 1);
+  if (!sp.therm)
+    for (int f = 0; f < pe::CODE_FIELDS; ++f) sp.guard |= 1u << (sp.off[f] + sp.width[f] - 1);
   const int64_t Jp = round_up(n_jobs, pe::FC_JT);
-  std::vector<uint32_t> jc((size_t)Jp, sp.guard);   // padding jobs: code M never fits
+  // padding jobs never fit: SWAR code M (every field fails); thermometer ~Y with bit 31 cleared
+  std::vector<uint32_t> jc((size_t)Jp, sp.therm ? ~(1u << 31) : sp.guard);
   for (int64_t j = 0; j < n_jobs; ++j) {
     uint32_t c = 0;
     for (int d = 0; d < pe::D; ++d) {
@@ -449,6 +457,14 @@ static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const u
     const uint32_t nd = need ? need[j] : 0u;
     const uint32_t rank = (uint32_t)(std::find(needs.begin(), needs.end(), nd) - needs.begin()) + 1;
     c |= rank << sp.off[4];
+    if (sp.therm) {
+      uint32_t y = 0;   // one bit per field: rank c <=> bit c-1
+      for (int f = 0; f < pe::CODE_FIELDS; ++f) {
+        const uint32_t r = (c >> sp.off[f]) & ((1u << sp.width[f]) - 1);   // ranks < 2^width here
+        y |= 1u << (sp.off[f] + r - 1);
+      }
+      c = ~y;
+    }
     jc[j] = c;
   }
   std::vector<int64_t> vt((size_t)pe::D * pe::CODE_MAXV, INT64_MAX);
@@ -549,10 +565,11 @@ static void fit_run(pe_ctx* ctx) {
     hipchk(pe::launch_encode_nodes(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->node_stride,
                                    ctx->code, ctx->code_vals.p, ctx->code_needs.p, ctx->code_x.p),
            "launch encode_nodes");
-    hipchk(pe::launch_fit_mask_coded(ctx->stream, ctx->code_x.p, ctx->Ns, ctx->node_stride, ctx->code_jobs.p,
+    hipchk(pe::launch_fit_mask_coded(ctx->stream, ctx->code.therm, ctx->code_x.p, ctx->Ns, ctx->node_stride, ctx->code_jobs.p,
                                      ~ctx->code.guard, J, tpw2, ctx->mask.p, ctx->counts.p),
            "launch fit_mask_coded");
     ctx->stats.fit_runs_coded += 1;
+    ctx->stats.fit_runs_therm += ctx->code.therm;
   } else if (ctx->fit32) {
     hipchk(pe::launch_compress_res(ctx->stream, ctx->res.p, ctx->res32.p, ctx->stride, ctx->Ns, ctx->fit_shift),
            "launch compress_res");

@@ -91,11 +91,12 @@ constexpr int CODE_FIELDS = 5;   // cpu, memory, gpu, ephemeral, label-chain
 constexpr int CODE_MAXV = 128;   // distinct values per field the device tables hold
 struct CodeSpec {
   int off[CODE_FIELDS];
-  int width[CODE_FIELDS];       // code bits + 1 guard bit
+  int width[CODE_FIELDS];       // SWAR: code bits + 1 guard bit; thermometer: nvals bits
   int nvals[CODE_FIELDS];
-  uint32_t guard;               // M
+  uint32_t guard;               // SWAR: M (guard bits); thermometer: unused
+  int therm;                    // 1: thermometer fields, fit <=> (X | ~Y) == ~0 (3 VALU per 64 evals)
 };
-constexpr int FC_CH = 8;        // coded fit: 64-node chunks per wave tile (X in 8 VGPRs)
+constexpr int FC_CH = 16;       // coded fit: 64-node chunks per wave tile (X in 16 VGPRs)
 constexpr int FC_JT = 64;       // coded fit: jobs per wave (one 64-bit word per node)
 
 // vals: [4][CODE_MAXV] sorted int64 request values; needs: [CODE_MAXV] label chain (inclusion order)
@@ -103,7 +104,8 @@ hipError_t launch_encode_nodes(hipStream_t s, const int64_t* res, int64_t stride
                                int64_t n_pad, CodeSpec spec, const int64_t* vals, const uint32_t* needs, uint32_t* X);
 // Coded-path mask layout (bits over jobs): word (b, n) = jobs 64b..64b+63 at node n (bit j%64),
 // stored at b * node_stride + n, node_stride = ceil(Ns/512)*512.
-hipError_t launch_fit_mask_coded(hipStream_t s, const uint32_t* X, int64_t Ns, int64_t node_stride,
+// therm = 0: jcode = C (ranks), k = ~M;   therm = 1: jcode = ~Y (one bit per field cleared), k unused
+hipError_t launch_fit_mask_coded(hipStream_t s, int therm, const uint32_t* X, int64_t Ns, int64_t node_stride,
                                  const uint32_t* jcode, uint32_t not_guard, int64_t J, int64_t tiles_per_wave,
                                  uint64_t* mask, unsigned long long* counts);
 

@@ -290,10 +290,10 @@ __global__ __launch_bounds__(256) void encode_nodes_kernel(const int64_t* __rest
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= n_pad) return;
   if (n >= Ns) {              // padding node: every field at code 0 -> fails every job (ranks >= 1)
-    X[n] = spec.guard;
+    X[n] = spec.therm ? 0u : spec.guard;
     return;
   }
-  uint32_t x = 0;
+  int code[CODE_FIELDS];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     const int64_t r = res[d * stride + n];
@@ -304,12 +304,19 @@ __global__ __launch_bounds__(256) void encode_nodes_kernel(const int64_t* __rest
       if (v[mid] <= r) lo = mid + 1;
       else hi = mid;
     }
-    x |= ((uint32_t)lo | (1u << (spec.width[d] - 1))) << spec.off[d];
+    code[d] = lo;
   }
   const uint32_t lab = labels[n];
   int k = 0;                                    // needs form an inclusion chain: satisfied = prefix
   while (k < spec.nvals[4] && (needs[k] & lab) == needs[k]) ++k;
-  x |= ((uint32_t)k | (1u << (spec.width[4] - 1))) << spec.off[4];
+  code[4] = k;
+  uint32_t x = 0;
+#pragma unroll
+  for (int f = 0; f < CODE_FIELDS; ++f) {
+    // SWAR: code + guard bit; thermometer: code ones (job rank c fits <=> bit c-1 is set)
+    const uint32_t fv = spec.therm ? (uint32_t)((1ull << code[f]) - 1) : ((uint32_t)code[f] | (1u << (spec.width[f] - 1)));
+    x |= fv << spec.off[f];
+  }
   X[n] = x;
 }
 
@@ -322,37 +329,68 @@ hipError_t launch_encode_nodes(hipStream_t s, const int64_t* res, int64_t stride
 }
 
 // One (job, chunk) step: tmp = (X - C) | ~M; carry = (tmp + 1 overflows) = fit for this lane;
-// w = 2w + carry shifts the job's bit in.  VCC-style carries between VALU ops need no wait states
-// (the same pattern as a 64-bit add).  Returns the 64-lane fit mask (for the job's popcount).
-__device__ __forceinline__ uint64_t fc_step(uint32_t x, uint32_t code, uint32_t not_guard, uint32_t& w) {
-  uint32_t tmp;
+// w = 2w + carry shifts the job's bit in, pc += popcount(carry) counts it.  The carry lives only
+// inside the asm block: left to the scheduler, 16 carries (SGPR pairs) were computed ahead of their
+// popcounts and spilled into VGPR lanes.  VALU->SALU SGPR reads are interlocked (no wait states).
+__device__ __forceinline__ void fc_step(uint32_t x, uint32_t code, uint32_t not_guard, uint32_t& w, uint32_t& pc) {
+  uint32_t tmp, t;
   uint64_t fit;
-  asm("v_sub_u32_e64 %0, %3, %4\n\t"
-      "v_or_b32_e32 %0, %5, %0\n\t"
+  asm("v_sub_u32_e64 %0, %5, %6\n\t"
+      "v_or_b32_e32 %0, %7, %0\n\t"
       "v_add_co_u32_e64 %0, %1, %0, 1\n\t"
-      "v_addc_co_u32_e64 %2, vcc, %2, %2, %1"
-      : "=&v"(tmp), "=&s"(fit), "+v"(w)
+      "v_addc_co_u32_e64 %2, vcc, %2, %2, %1\n\t"
+      "s_bcnt1_i32_b64 %4, %1\n\t"
+      "s_add_u32 %3, %3, %4"
+      : "=&v"(tmp), "=&s"(fit), "+v"(w), "+s"(pc), "=&s"(t)
       : "v"(x), "s"(code), "s"(not_guard)
-      : "vcc");
-  return fit;
+      : "vcc", "scc");
 }
 
-template <int HALF, int JJ>
+// Thermometer step: tmp = X | ~Y; carry = (tmp + 1 overflows) = every field holds the job's bit.
+__device__ __forceinline__ void ft_step(uint32_t x, uint32_t not_y, uint32_t& w, uint32_t& pc) {
+  uint32_t tmp, t;
+  uint64_t fit;
+  asm("v_or_b32_e32 %0, %5, %6\n\t"
+      "v_add_co_u32_e64 %0, %1, %0, 1\n\t"
+      "v_addc_co_u32_e64 %2, vcc, %2, %2, %1\n\t"
+      "s_bcnt1_i32_b64 %4, %1\n\t"
+      "s_add_u32 %3, %3, %4"
+      : "=&v"(tmp), "=&s"(fit), "+v"(w), "+s"(pc), "=&s"(t)
+      : "s"(not_y), "v"(x)
+      : "vcc", "scc");
+}
+
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+
+// 8 job codes per scalar load, issued inside the tile loop: a volatile load cannot be hoisted, so
+// the 64 codes of the wave never sit in SGPRs at once (hoisting them spilled SGPRs into VGPR lanes).
+__device__ __forceinline__ u32x8 load_codes8(const uint32_t* __restrict__ p) {
+  u32x8 v;
+  asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+
+template <int THERM, int HALF, int JJ>
 __device__ __forceinline__ void fc_jobs(const uint32_t* __restrict__ codes, const uint32_t (&x)[FC_CH],
-                                        uint32_t not_guard, uint32_t (&w)[FC_CH], uint32_t& cnt) {
+                                        uint32_t not_guard, uint32_t (&w)[FC_CH], uint32_t& cnt, u32x8& c8) {
   // jobs are shifted in from the top of the half (JJ = 31 first) so job 32*HALF + jj ends in bit jj
-  const uint32_t code = codes[HALF * 32 + JJ];
-  unsigned pc = 0;
+  if constexpr (JJ % 8 == 7) c8 = load_codes8(codes + HALF * 32 + JJ - 7);
+  const uint32_t code = c8[JJ % 8];
+  uint32_t pc = 0;
 #pragma unroll
-  for (int c = 0; c < FC_CH; ++c) pc += (unsigned)__popcll(fc_step(x[c], code, not_guard, w[c]));
+  for (int c = 0; c < FC_CH; ++c) {
+    if constexpr (THERM) ft_step(x[c], code, w[c], pc);
+    else fc_step(x[c], code, not_guard, w[c], pc);
+  }
   const unsigned prev = (unsigned)__builtin_amdgcn_readlane((int)cnt, HALF * 32 + JJ);
   cnt = writelane<HALF * 32 + JJ>(cnt, prev + pc);
-  if constexpr (JJ > 0) fc_jobs<HALF, JJ - 1>(codes, x, not_guard, w, cnt);
+  if constexpr (JJ > 0) fc_jobs<THERM, HALF, JJ - 1>(codes, x, not_guard, w, cnt, c8);
 }
 
 // Wave tile = FC_CH chunks x 64 nodes of code words (8 VGPRs) x FC_JT jobs whose code words are
 // wave-uniform (scalar loads).  4 VALU per (job, chunk) = per 64 fit evaluations, the words leave
 // as whole-line 512-B stores (bits over jobs), per-job counts are s_bcnt1 of the carry masks.
+template <int THERM>
 __global__ __launch_bounds__(256) void fit_mask_coded_kernel(const uint32_t* __restrict__ X, int64_t Ns,
                                                              int64_t node_stride, const uint32_t* __restrict__ jcode,
                                                              uint32_t not_guard, int64_t J, int64_t tiles_per_wave,
@@ -373,8 +411,9 @@ __global__ __launch_bounds__(256) void fit_mask_coded_kernel(const uint32_t* __r
     uint32_t lo[FC_CH], hi[FC_CH];
 #pragma unroll
     for (int c = 0; c < FC_CH; ++c) lo[c] = hi[c] = 0;
-    fc_jobs<0, 31>(jcode + jb, x, not_guard, lo, cnt);
-    fc_jobs<1, 31>(jcode + jb, x, not_guard, hi, cnt);
+    u32x8 c8;
+    fc_jobs<THERM, 0, 31>(jcode + jb, x, not_guard, lo, cnt, c8);
+    fc_jobs<THERM, 1, 31>(jcode + jb, x, not_guard, hi, cnt, c8);
 #pragma unroll
     for (int c = 0; c < FC_CH; ++c) row[t * (64 * FC_CH) + c * 64] = ((uint64_t)hi[c] << 32) | lo[c];
   }
@@ -382,15 +421,19 @@ __global__ __launch_bounds__(256) void fit_mask_coded_kernel(const uint32_t* __r
   if (j < J && cnt) atomicAdd(&counts[j], (unsigned long long)cnt);
 }
 
-hipError_t launch_fit_mask_coded(hipStream_t s, const uint32_t* X, int64_t Ns, int64_t node_stride,
+hipError_t launch_fit_mask_coded(hipStream_t s, int therm, const uint32_t* X, int64_t Ns, int64_t node_stride,
                                  const uint32_t* jcode, uint32_t not_guard, int64_t J, int64_t tiles_per_wave,
                                  uint64_t* mask, unsigned long long* counts) {
   if (J <= 0 || Ns <= 0) return hipSuccess;
   const int64_t span = tiles_per_wave * 64 * FC_CH;
   const int64_t waves = (Ns + span - 1) / span;
   dim3 grid((unsigned)((waves + 3) / 4), (unsigned)((J + FC_JT - 1) / FC_JT));
-  hipLaunchKernelGGL(fit_mask_coded_kernel, grid, dim3(256), 0, s, X, Ns, node_stride, jcode, not_guard, J,
-                     tiles_per_wave, mask, counts);
+  if (therm)
+    hipLaunchKernelGGL(fit_mask_coded_kernel<1>, grid, dim3(256), 0, s, X, Ns, node_stride, jcode, not_guard, J,
+                       tiles_per_wave, mask, counts);
+  else
+    hipLaunchKernelGGL(fit_mask_coded_kernel<0>, grid, dim3(256), 0, s, X, Ns, node_stride, jcode, not_guard, J,
+                       tiles_per_wave, mask, counts);
   return hipGetLastError();
 }
 
