@@ -29,6 +29,12 @@ from placement import Engine, comm_id, synth  # noqa: E402
 
 METRIC = "job×node fit evals/sec + gang placements/sec, 1M-node inventory, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# chip-wide integer VALU issue ceiling, wave-instructions/s: profiles/r1_ubench_valu.txt
+# (v_add_u32 / v_addc_co at 8 waves per SIMD: 4.24 cycles per wave-instruction per SIMD, 256 CUs x 4 SIMDs)
+VALU_ISSUE_CEILING = 5.79e11
+KERNEL_OF_PATH = {"coded-therm": "pe::fit_mask_coded_kernel", "coded-swar": "pe::fit_mask_coded_kernel",
+                  "i32": "pe::fit_mask_kernel", "i64": "pe::fit_mask_kernel"}
+PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 
 
 class HipEvents:
@@ -62,6 +68,24 @@ def fit_bytes(n_nodes: int, n_jobs: int) -> int:
     node residuals 4x8 B + labels 4 B read once, job request 4x8 B + need 4 B read once,
     mask J*ceil(N/64)*8 B written once, per-job counts 8 B written."""
     return n_nodes * 36 + n_jobs * 36 + n_jobs * ((n_nodes + 63) // 64) * 8 + n_jobs * 8
+
+
+def profiled_traffic(kernel: str, n_nodes: int, n_jobs: int):
+    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/LATEST names the
+    directory; FETCH_SIZE doubled per MI355X_MICROARCH.md, + WRITE_SIZE), if they were taken on this
+    same workload.  None when no matching profile exists."""
+    try:
+        tag = open(os.path.join(PROFILES, "LATEST")).read().strip()
+        summ = json.load(open(os.path.join(PROFILES, tag, "summary.json")))
+    except (OSError, ValueError):
+        return None, None
+    wl = summ.get("workload", {})
+    if wl.get("nodes") != n_nodes or wl.get("jobs") != n_jobs:
+        return None, None
+    for k, p in summ.get("pmc", {}).items():
+        if k.startswith(kernel) and "hbm_traffic_bytes" in p:
+            return p["hbm_traffic_bytes"], f"profiles/{tag}/summary.json (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)"
+    return None, None
 
 
 def cpu_model() -> str:
@@ -177,6 +201,11 @@ def main():
     fit_path = ("coded-therm" if st0["fit_runs_therm"] else "coded-swar") if st0["fit_runs_coded"] else ("i32" if st0["fit_runs_i32"] else "i64")
     alg = fit_bytes(Ns, J)
     achieved = alg / (kern_ms * 1e-3) / 1e9
+    kname = KERNEL_OF_PATH[fit_path]
+    traffic, tsrc = profiled_traffic(kname, Ns, J)
+    valu_frac = None
+    if fit_path == "coded-therm":   # 3 VALU per (job, 64 nodes): or, add_co, addc
+        valu_frac = 3.0 * (-(-J // 64) * 64) * (Ns / 64.0) / (kern_ms * 1e-3) / VALU_ISSUE_CEILING
 
     out = {
         "metric": METRIC, "value": value, "unit": "job*node fit evals/s", "n_gpus": world, "steps": args.steps,
@@ -184,11 +213,13 @@ def main():
         "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic (splitmix64, SURVEY.md 8d)",
         "config": {"workload": "cfg5: fit bitmask, 1M-node inventory x 100k jobs, device-resident",
                    "nodes": N, "jobs": J, "parallelism": f"node-shard x{world}" + (" (host exchange rehearsal)" if host_exchange and world > 1 else ""), "feasible_pairs": feasible},
-        "roofline": {"bound": "hbm", "kernel": "fit_mask_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel_ms": kern_ms, "alg_bytes_per_launch": alg, "fit_path": fit_path,
-                     "note": "kernel_ms = hipEvent time on the engine stream / launches (incl. the 8*J-byte "
-                             "count memset); per-rank shard; traffic: see profiles/ PMC passes"},
+        "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": tsrc, "kernel_ms": kern_ms, "alg_bytes_per_launch": alg,
+                     "fit_path": fit_path, "valu_issue_frac": valu_frac,
+                     "note": "kernel_ms = hipEvent time on the engine stream / fit_mask_run (one count memset, "
+                             "the node encode and the fit kernel); per-rank shard; the fit kernel is VALU-issue-"
+                             "bound (valu_issue_frac = its VALU wave-instructions / measured issue ceiling)"},
     }
 
     if not args.no_greedy:

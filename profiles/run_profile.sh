@@ -21,4 +21,5 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_
   -d $OUT/sq -o sq --output-format csv -- python3 bench.py $BENCH_SMALL "$@" > $OUT/bench_sq.json 2> $OUT/sq.err
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INST_CYCLES_SALU SQ_INSTS_SMEM SQ_BUSY_CU_CYCLES SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_INT32 \
   -d $OUT/sq2 -o sq2 --output-format csv -- python3 bench.py $BENCH_SMALL "$@" > $OUT/bench_sq2.json 2> $OUT/sq2.err
+python3 profiles/summarize.py $OUT > $OUT/summary.json
 echo "profile $TAG done"

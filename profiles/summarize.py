@@ -30,6 +30,14 @@ def main(d):
             p["hbm_write_bytes"] = p["WRITE_SIZE"] * 1024
         if "FETCH_SIZE" in p and "WRITE_SIZE" in p:
             p["hbm_traffic_bytes"] = p["hbm_read_bytes_corrected"] + p["hbm_write_bytes"]
+    # the workload the passes ran (bench.py's JSON line under the kernel trace)
+    for f in glob.glob(os.path.join(d, "bench_trace.json")):
+        lines = [ln for ln in open(f) if ln.startswith("{")]
+        if lines:
+            b = json.loads(lines[-1])
+            out["workload"] = {"nodes": b["config"]["nodes"], "jobs": b["config"]["jobs"],
+                               "fit_path": b["roofline"].get("fit_path"), "bench_value": b["value"],
+                               "bench_kernel_ms": b["roofline"].get("kernel_ms")}
     json.dump(out, sys.stdout, indent=1)
     print()
 
