@@ -32,7 +32,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # chip-wide integer VALU issue ceiling, wave-instructions/s: profiles/r1_ubench_valu.txt
 # (v_add_u32 / v_addc_co at 8 waves per SIMD: 4.24 cycles per wave-instruction per SIMD, 256 CUs x 4 SIMDs)
 VALU_ISSUE_CEILING = 5.79e11
-KERNEL_OF_PATH = {"coded-therm": "pe::fit_mask_coded_kernel", "coded-swar": "pe::fit_mask_coded_kernel",
+KERNEL_OF_PATH = {"planes": "pe::fit_mask_planes_kernel", "coded-therm": "pe::fit_mask_coded_kernel", "coded-swar": "pe::fit_mask_coded_kernel",
                   "i32": "pe::fit_mask_kernel", "i64": "pe::fit_mask_kernel"}
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 
@@ -198,7 +198,9 @@ def main():
     kern_ms = ev.elapsed_ms(e0, e1) / args.steps
     value = float(N) * J * args.steps / elapsed
     st0 = eng.stats()
-    fit_path = ("coded-therm" if st0["fit_runs_therm"] else "coded-swar") if st0["fit_runs_coded"] else ("i32" if st0["fit_runs_i32"] else "i64")
+    fit_path = ("planes" if st0["fit_runs_planes"] else
+                (("coded-therm" if st0["fit_runs_therm"] else "coded-swar") if st0["fit_runs_coded"] else
+                 ("i32" if st0["fit_runs_i32"] else "i64")))
     alg = fit_bytes(Ns, J)
     achieved = alg / (kern_ms * 1e-3) / 1e9
     kname = KERNEL_OF_PATH[fit_path]

@@ -33,7 +33,7 @@ def test_abi_version_and_structs():
     assert lib.pe_abi_version() == 1
     # pe_config / pe_stats layouts mirrored in _abi must match the C sizes (x86-64)
     assert ctypes.sizeof(_abi.PeConfig) == 80
-    assert ctypes.sizeof(_abi.PeStats) == 120
+    assert ctypes.sizeof(_abi.PeStats) == 128
 
 
 def test_no_cpu_fallback_without_gpu():

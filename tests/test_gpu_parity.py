@@ -149,10 +149,11 @@ def test_fit_mask_edge_values(eng):
     assert counts[0] == N - 1 and counts[4] == 1
 
 
-PATHS = {"therm": (0, "fit_runs_therm", 1), "swar": (8, "fit_runs_coded", 1), "i32": (3, "fit_runs_i32", 0), "i64": (1, "fit_runs_i64", 0)}
+PATHS = {"planes": (0, "fit_runs_planes", 2), "therm": (5, "fit_runs_therm", 1), "swar": (13, "fit_runs_coded", 1),
+         "i32": (3, "fit_runs_i32", 0), "i64": (1, "fit_runs_i64", 0)}
 
 
-@pytest.mark.parametrize("path", ["therm", "swar", "i32", "i64"])
+@pytest.mark.parametrize("path", ["planes", "therm", "swar", "i32", "i64"])
 @pytest.mark.parametrize("N,J", [(5000, 300), (777, 65), (64, 1)])
 def test_fit_mask_paths(path, N, J):
     """Every exact fit path on the same data (residuals span the int32 saturation point after
@@ -169,15 +170,15 @@ def test_fit_mask_paths(path, N, J):
     np.testing.assert_array_equal(e.fit_mask_rows(0, J), o_mask)
     np.testing.assert_array_equal(counts, o_counts)
     s = e.stats()
-    assert s[stat] == 1 and s["fit_runs_coded"] + s["fit_runs_i32"] + s["fit_runs_i64"] == 1
+    assert s[stat] == 1 and s["fit_runs_planes"] + s["fit_runs_coded"] + s["fit_runs_i32"] + s["fit_runs_i64"] == 1
     assert s["fit_runs_therm"] == (path == "therm")
     assert e.fit_mask_layout() == layout
     e.close()
 
 
-@pytest.mark.parametrize("case", ["many_values", "odd_bytes", "label_antichain"])
+@pytest.mark.parametrize("case", ["many_values", "odd_bytes", "label_antichain", "many_planes", "extreme_values"])
 def test_fit_mask_path_fallbacks(eng, case):
-    """Batches the coded word cannot hold fall back to the compare kernels, still exact."""
+    """Each batch shape lands on the path that can hold it (planes > coded > int32 > int64), exact."""
     N, J = 3000, 400
     inv = synth.make_inventory(N, 91, 0.3)
     req, need = synth.make_fit_jobs(J, 93)
@@ -189,10 +190,18 @@ def test_fit_mask_path_fallbacks(eng, case):
         req[:, 0] = 500 + np.arange(J) * 7
         req[5, 1] += 1                               # and no common power of two -> int64 compare
         want = "fit_runs_i64"
-    else:
+    elif case == "label_antichain":
         inv.labels[:] = np.arange(N, dtype=np.uint32) % 8
-        need[:] = np.where(np.arange(J) % 2 == 0, 1, 2)   # {1} and {2}: not an inclusion chain
-        want = "fit_runs_i32"
+        need[:] = np.where(np.arange(J) % 2 == 0, 1, 2)   # {1} and {2}: no chain, but 2 planes
+        want = "fit_runs_planes"
+    elif case == "many_planes":
+        req[:, 0] = 500 + (np.arange(J) % 40) * 7    # 40 distinct cpu values: > 32 planes, SWAR-coded
+        want = "fit_runs_coded"
+    else:
+        req[0] = [np.iinfo(np.int64).max, 0, 0, 0]   # int64 extremes are just two more planes
+        req[1] = [0, np.iinfo(np.int64).max, 0, np.iinfo(np.int64).max]
+        inv.used[0, :7] = inv.cap[0, :7] + 5         # over-committed nodes: no request fits them
+        want = "fit_runs_planes"
     eng.reset_stats()
     eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     counts = eng.fit_mask(req, need)

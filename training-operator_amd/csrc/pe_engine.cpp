@@ -80,6 +80,10 @@ void ncclchk(ncclResult_t r, const char* what) {
 
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// pe_config.fit_path_mask bits
+constexpr int PATH_I64 = 1, PATH_I32 = 2, PATH_CODED = 4, PATH_NO_THERM = 8, PATH_PLANES = 16;
+constexpr int PATHS_ALL = PATH_I64 | PATH_I32 | PATH_CODED | PATH_PLANES;
+
 }  // namespace
 
 struct pe_ctx {
@@ -108,8 +112,11 @@ struct pe_ctx {
   DevBuf<int32_t> res32;
   bool fit32 = false;      // batch is exactly representable in 32 bits (see ReqRec32)
   int fit_shift[pe::D] = {0, 0, 0, 0};
-  int fit_path = 0;        // 0 int64 compare, 1 int32 compare, 2 dictionary-coded SWAR
-  int fit_path_mask = 7;   // allowed paths (pe_config.fit_path_mask)
+  int fit_path = 0;        // 0 int64 compare, 1 int32 compare, 2 dictionary-coded, 3 bit planes
+  int fit_path_mask = PATHS_ALL;   // allowed paths (pe_config.fit_path_mask)
+  pe::PlaneSpec plane{};
+  int64_t pl_nblk = 0, row_words = 0;   // planes path: 8192-node blocks, mask row stride (u32)
+  DevBuf<uint32_t> planes, plane_jobs;
   pe::CodeSpec code{};
   int64_t code_Jp = 0, node_stride = 0;
   DevBuf<int64_t> code_vals;
@@ -138,6 +145,7 @@ struct pe_ctx {
     res0.release(); res.release(); labels.release(); island.release();
     fit_jobs.release(); fit_jobs32.release(); res32.release(); mask.release();
     code_vals.release(); code_needs.release(); code_jobs.release(); code_x.release(); counts.release(); h_counts.release();
+    planes.release(); plane_jobs.release();
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
@@ -233,9 +241,9 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   ctx->window_groups = cfg->window_groups > 0 ? cfg->window_groups : 64;
   ctx->window_pods = cfg->window_pods > 0 ? cfg->window_pods : 1024;
   ctx->gpu_name = cfg->gpu_resource_name ? cfg->gpu_resource_name : "amd.com/gpu";
-  ctx->fit_path_mask = cfg->fit_path_mask > 0 ? (cfg->fit_path_mask & 15) : 7;
-  if (!(ctx->fit_path_mask & 7)) ctx->fit_path_mask |= 7;   // no kernel bits = all kernels
-  ctx->fit_path_mask |= 1;                                    // the int64 path is always available
+  ctx->fit_path_mask = cfg->fit_path_mask > 0 ? (cfg->fit_path_mask & (PATHS_ALL | PATH_NO_THERM)) : PATHS_ALL;
+  if (!(ctx->fit_path_mask & PATHS_ALL)) ctx->fit_path_mask |= PATHS_ALL;   // no kernel bits = all kernels
+  ctx->fit_path_mask |= PATH_I64;                                           // always available
   int rc = PE_OK;
   try {
     hipchk(hipSetDevice(dev), "hipSetDevice");
@@ -430,7 +438,7 @@ static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const u
   for (int f = 0; f < pe::CODE_FIELDS; ++f) therm_bits += f < pe::D ? (int)vals[f].size() : (int)needs.size();
   // thermometer fields (one bit per distinct value) when they fit 31 bits -- bit 31 stays free for
   // the never-fitting padding jobs -- else log-width SWAR fields with guard bits
-  sp.therm = (ctx->fit_path_mask & 8) == 0 && therm_bits <= 31 ? 1 : 0;
+  sp.therm = (ctx->fit_path_mask & PATH_NO_THERM) == 0 && therm_bits <= 31 ? 1 : 0;
   int off = 0;
   for (int f = 0; f < pe::CODE_FIELDS; ++f) {
     const int k = f < pe::D ? (int)vals[f].size() : (int)needs.size();
@@ -484,6 +492,47 @@ static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const u
   return true;
 }
 
+// Bit planes of one batch (pe_kernels.h, PlaneSpec): one plane per distinct request value of each
+// dimension and per distinct label need, each job selecting five.  Any int64 values and any need
+// sets; returns false when the batch needs more than PL_MAX planes.
+static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
+  if (n_jobs == 0) return false;
+  pe::PlaneSpec sp{};
+  std::vector<int64_t> vals[pe::D + 1];
+  int off[pe::D + 1];
+  for (int f = 0; f <= pe::D; ++f) {
+    vals[f].resize((size_t)n_jobs);
+    for (int64_t j = 0; j < n_jobs; ++j) vals[f][j] = f < pe::D ? req[j * pe::D + f] : (int64_t)(need ? need[j] : 0u);
+    std::sort(vals[f].begin(), vals[f].end());
+    vals[f].erase(std::unique(vals[f].begin(), vals[f].end()), vals[f].end());
+    off[f] = sp.n;
+    if (sp.n + (int64_t)vals[f].size() > pe::PL_MAX) return false;
+    for (int64_t v : vals[f]) {
+      sp.kind[sp.n] = f;
+      sp.val[sp.n] = v;
+      ++sp.n;
+    }
+  }
+  std::vector<uint32_t> jc((size_t)n_jobs);
+  for (int64_t j = 0; j < n_jobs; ++j) {
+    uint32_t c = 0;
+    for (int f = 0; f <= pe::D; ++f) {
+      const int64_t q = f < pe::D ? req[j * pe::D + f] : (int64_t)(need ? need[j] : 0u);
+      const int64_t i = std::lower_bound(vals[f].begin(), vals[f].end(), q) - vals[f].begin();
+      c |= (uint32_t)(off[f] + i) << (5 * f);
+    }
+    jc[j] = c;
+  }
+  ctx->plane = sp;
+  ctx->pl_nblk = (std::max<int64_t>(ctx->Ns, 1) + pe::PL_BLK - 1) / pe::PL_BLK;
+  ctx->row_words = round_up((ctx->Ns + 31) / 32, 4);
+  hipchk(ctx->planes.ensure((size_t)ctx->pl_nblk * pe::PL_MAX * 64 * pe::PL_R), "alloc planes");
+  hipchk(ctx->plane_jobs.ensure(jc.size()), "alloc plane jobs");
+  hipchk(hipMemcpyAsync(ctx->plane_jobs.p, jc.data(), jc.size() * 4, hipMemcpyHostToDevice, ctx->stream),
+         "H2D plane jobs");
+  return true;
+}
+
 static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
   if (n_jobs < 0) raise(PE_EINVAL, "n_jobs < 0");
   if (!ctx->loaded) raise(PE_ESTATE, "no inventory loaded");
@@ -514,7 +563,7 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
     if (orv & ((int64_t(1) << sh) - 1)) use32 = false;
     ctx->fit_shift[d] = sh;
   }
-  ctx->fit32 = use32 && (ctx->fit_path_mask & 2);
+  ctx->fit32 = use32 && (ctx->fit_path_mask & PATH_I32);
   if (ctx->fit32) {
     std::vector<pe::ReqRec32> r32((size_t)Jp);
     for (int64_t j = 0; j < Jp; ++j) {
@@ -534,10 +583,12 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
   ctx->Wn = (ctx->Ns + 63) / 64;
   ctx->Wt = (ctx->Wn + 3) / 4;
   ctx->fit_path = ctx->fit32 ? 1 : 0;
-  if ((ctx->fit_path_mask & 4) && build_codes(ctx, n_jobs, req, need)) ctx->fit_path = 2;
+  if ((ctx->fit_path_mask & PATH_PLANES) && build_planes(ctx, n_jobs, req, need)) ctx->fit_path = 3;
+  else if ((ctx->fit_path_mask & PATH_CODED) && build_codes(ctx, n_jobs, req, need)) ctx->fit_path = 2;
   hipchk(ctx->fit_jobs.ensure(Jp), "alloc fit jobs");
-  const size_t mask_words = ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
-                                               : (size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4;
+  const size_t mask_words = ctx->fit_path == 3   ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->row_words / 2
+                            : ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
+                                                 : (size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4;
   hipchk(ctx->mask.ensure(mask_words), "alloc fit mask");
   hipchk(ctx->counts.ensure(Jp), "alloc fit counts");
   hipchk(ctx->h_counts.ensure(Jp), "alloc pinned counts");
@@ -557,7 +608,18 @@ static void fit_run(pe_ctx* ctx) {
   const int64_t want_x = std::max<int64_t>(1, (16384 + waves_y - 1) / waves_y);
   int64_t tpw = (ctx->Ns + 256 * want_x - 1) / (256 * want_x);
   tpw = std::min<int64_t>(16, std::max<int64_t>(1, tpw));
-  if (ctx->fit_path == 2) {
+  if (ctx->fit_path == 3) {
+    // ~16k waves: every 8192-node block times enough job ranges, at least 64 jobs per wave
+    const int64_t ranges = std::max<int64_t>(1, (16384 + ctx->pl_nblk - 1) / ctx->pl_nblk);
+    const int64_t jpw = std::max<int64_t>(64, (J + ranges - 1) / ranges);
+    hipchk(pe::launch_encode_planes(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->pl_nblk,
+                                    ctx->plane, ctx->planes.p),
+           "launch encode_planes");
+    hipchk(pe::launch_fit_mask_planes(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p, J, jpw,
+                                      ctx->row_words, reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p),
+           "launch fit_mask_planes");
+    ctx->stats.fit_runs_planes += 1;
+  } else if (ctx->fit_path == 2) {
     const int64_t jblocks = ctx->code_Jp / pe::FC_JT;
     const int64_t want_x2 = std::max<int64_t>(1, (16384 + jblocks - 1) / jblocks);
     int64_t tpw2 = (ctx->Ns + 64 * pe::FC_CH * want_x2 - 1) / (64 * pe::FC_CH * want_x2);
@@ -625,6 +687,14 @@ int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out) {
     if (row0 < 0 || n_rows < 0 || row0 + n_rows > ctx->fit_J) raise(PE_EINVAL, "row range");
     if (n_rows == 0 || ctx->Wn == 0) return PE_OK;
     need_ptr(out, "out");
+    if (ctx->fit_path == 3) {   // row-major already: strided copy (u64 word c = nodes 64c..64c+63)
+      hipchk(hipMemcpy2DAsync(out, (size_t)ctx->Wn * 8, ctx->mask.p + (size_t)row0 * (ctx->row_words / 2),
+                              (size_t)ctx->row_words * 4, (size_t)ctx->Wn * 8, (size_t)n_rows, hipMemcpyDeviceToHost,
+                              ctx->stream),
+             "D2H mask rows");
+      hipchk(hipStreamSynchronize(ctx->stream), "sync mask");
+      return PE_OK;
+    }
     if (ctx->fit_path == 2) {
       // bits-over-jobs layout: copy the 64-job bands, transpose the rows out
       const int64_t b0 = row0 / 64, b1 = (row0 + n_rows - 1) / 64;
@@ -810,7 +880,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
 
 int pe_fit_mask_layout(const pe_ctx* ctx, int32_t* layout) {
   if (!ctx || !layout) return PE_EINVAL;
-  *layout = ctx->fit_path == 2 ? PE_MASK_JOB_BITS : PE_MASK_NODE_TILES;
+  *layout = ctx->fit_path == 3 ? PE_MASK_ROW_MAJOR : ctx->fit_path == 2 ? PE_MASK_JOB_BITS : PE_MASK_NODE_TILES;
   return PE_OK;
 }
 

@@ -109,6 +109,31 @@ hipError_t launch_fit_mask_coded(hipStream_t s, int therm, const uint32_t* X, in
                                  const uint32_t* jcode, uint32_t not_guard, int64_t J, int64_t tiles_per_wave,
                                  uint64_t* mask, unsigned long long* counts);
 
+// ---- bit-plane path (fit mask).  Per batch the host lists the distinct request values of each
+// dimension and the distinct label needs; plane p of a node is one predicate, evaluated exactly in
+// int64 when the planes are encoded:
+//   kind d < 4:  res[d][n] >= val        kind 4:  (labels[n] & need) == need
+// and is stored transposed, 32 nodes per u32 word (padding nodes 0).  A job selects one plane per
+// dimension and one for its need, so for 32 nodes at once
+//   fit word = P[i0] & P[i1] & P[i2] & P[i3] & P[i4]
+// -- two v_bitop3 per 2048 (job, node) pairs per wave instead of one VALU op per 64.
+constexpr int PL_MAX = 32;      // planes a batch may use (held in VGPRs, dynamic index via gpr_idx)
+constexpr int PL_R = 4;         // u32 node words per lane: one 16-B store per job and lane
+constexpr int PL_BLK = 64 * PL_R * 32;   // nodes per wave block (8192)
+struct PlaneSpec {
+  int32_t n;                    // planes in use
+  int32_t kind[PL_MAX];         // 0..3 resource dimension, 4 label need
+  int64_t val[PL_MAX];          // request value (kind < 4) or need bits (kind 4)
+};
+// planes: [nblk][PL_MAX][64 * PL_R] u32; word w of block b covers nodes b*PL_BLK + 32w .. +31
+hipError_t launch_encode_planes(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
+                                int64_t Ns, int64_t nblk, const PlaneSpec& spec, uint32_t* planes);
+// jcode[j] = 5 plane indices, 5 bits each (dims 0..3, need).  Mask row-major: row j at
+// mask + j * row_words (u32 words, row_words a multiple of 4), word w = nodes 32w..32w+31.
+hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint32_t* jcode,
+                                  int64_t J, int64_t jobs_per_wave, int64_t row_words, uint32_t* mask,
+                                  unsigned long long* counts);
+
 hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
                        uint64_t id_base, const ReqRec* groups, int Wg, uint64_t* cand, int32_t* cnt,
                        uint64_t* bound, int nwaves);

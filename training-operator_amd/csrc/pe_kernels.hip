@@ -437,6 +437,134 @@ hipError_t launch_fit_mask_coded(hipStream_t s, int therm, const uint32_t* X, in
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ bit-plane fit mask
+
+// One wave = 64 nodes; per plane one predicate per lane, ballot -> two transposed u32 words.
+__global__ __launch_bounds__(256) void encode_planes_kernel(const int64_t* __restrict__ res, int64_t stride,
+                                                            const uint32_t* __restrict__ labels, int64_t Ns,
+                                                            int64_t nblk, PlaneSpec spec,
+                                                            uint32_t* __restrict__ planes) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n0 = g * 64;
+  if (n0 >= nblk * PL_BLK) return;
+  const int64_t n = n0 + lane;
+  const bool valid = n < Ns;
+  int64_t r[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) r[d] = valid ? res[d * stride + n] : 0;
+  const uint32_t lab = valid ? labels[n] : 0u;
+  const int64_t blk = n0 / PL_BLK;
+  const int64_t w0 = (n0 % PL_BLK) / 32;           // even: this wave's two words
+  uint32_t* out = planes + blk * PL_MAX * (64 * PL_R) + w0;
+#pragma unroll
+  for (int p = 0; p < PL_MAX; ++p) {
+    bool pr = false;
+    if (p < spec.n) {
+      const int k = spec.kind[p];
+      const int64_t v = spec.val[p];
+      int64_t rv = r[0];
+      rv = k == 1 ? r[1] : rv;
+      rv = k == 2 ? r[2] : rv;
+      rv = k == 3 ? r[3] : rv;
+      pr = valid && (k == 4 ? (lab & (uint32_t)v) == (uint32_t)v : rv >= v);
+    }
+    const uint64_t b = __builtin_amdgcn_ballot_w64(pr);
+    if (lane < 2) out[p * (64 * PL_R) + lane] = (uint32_t)(lane ? b >> 32 : b);
+  }
+}
+
+hipError_t launch_encode_planes(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
+                                int64_t Ns, int64_t nblk, const PlaneSpec& spec, uint32_t* planes) {
+  if (nblk <= 0) return hipSuccess;
+  const int64_t waves = nblk * PL_BLK / 64;
+  hipLaunchKernelGGL(encode_planes_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, res, stride, labels, Ns,
+                     nblk, spec, planes);
+  return hipGetLastError();
+}
+
+typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Sum over the 64 lanes, result wave-uniform: quad, half-row and row sums by DPP, then the rows
+// by row_bcast:15 / row_bcast:31 into lane 63.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);    // quad_perm [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);    // quad_perm [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);   // row_half_mirror
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false);   // row_mirror
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// v[lane] = x for one wave-uniform lane.  Data and lane select cannot both be SGPRs (one constant
+// bus read), so the select goes through M0; 4 wait states after the VALU write of x.
+__device__ __forceinline__ uint32_t writelane_s(uint32_t v, uint32_t x, uint32_t lane) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 3\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "s"(lane) : "m0");
+  return v;
+}
+
+// One wave = one 8192-node block (4 words x 32 nodes per lane, PL_MAX planes each in VGPRs) x a job
+// range.  Per job: 5 uniform plane indices (gpr_idx moves), two 3-input ANDs per word, one 16-B
+// store per lane (1 KiB per wave, whole lines), the popcount summed over the wave; lane k gathers
+// the count of the k-th job of each 64 and flushes them with one 64-lane atomic.
+__global__ __launch_bounds__(256) void fit_mask_planes_kernel(const uint32_t* __restrict__ planes, int64_t nblk,
+                                                              const uint32_t* __restrict__ jcode, int64_t J,
+                                                              int64_t jobs_per_wave, int64_t row_words,
+                                                              uint32_t* __restrict__ mask,
+                                                              unsigned long long* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t blk = wave_id % nblk;
+  const int64_t j0 = (wave_id / nblk) * jobs_per_wave;
+  if (j0 >= J) return;
+  const int64_t j1 = min(J, j0 + jobs_per_wave);
+  u32x32 P0, P1, P2, P3;
+  const uint4* pb = reinterpret_cast<const uint4*>(planes + blk * PL_MAX * (64 * PL_R)) + lane;
+#pragma unroll
+  for (int p = 0; p < PL_MAX; ++p) {
+    const uint4 v = pb[p * 64];
+    P0[p] = v.x;
+    P1[p] = v.y;
+    P2[p] = v.z;
+    P3[p] = v.w;
+  }
+  const int64_t col = blk * (64 * PL_R) + lane * PL_R;     // first u32 word of this lane in a row
+  const bool in_row = col < row_words;
+  u32x4* out = reinterpret_cast<u32x4*>(mask + col);
+  const int64_t row4 = row_words / 4;
+  uint32_t acc = 0;
+  for (int64_t j = j0; j < j1; ++j) {
+    const uint32_t c = jcode[j];
+    const uint32_t i0 = c & 31, i1 = (c >> 5) & 31, i2 = (c >> 10) & 31, i3 = (c >> 15) & 31, i4 = (c >> 20) & 31;
+    u32x4 f;
+    f.x = P0[i0] & P0[i1] & P0[i2] & P0[i3] & P0[i4];
+    f.y = P1[i0] & P1[i1] & P1[i2] & P1[i3] & P1[i4];
+    f.z = P2[i0] & P2[i1] & P2[i2] & P2[i3] & P2[i4];
+    f.w = P3[i0] & P3[i1] & P3[i2] & P3[i3] & P3[i4];
+    if (in_row) out[j * row4] = f;
+    const uint32_t n = wave_sum(__popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w));
+    const uint32_t k = (uint32_t)((j - j0) & 63);
+    acc = writelane_s(acc, n, k);
+    if (k == 63 || j + 1 == j1) {
+      const int64_t jb = j - k;
+      if ((uint32_t)lane <= k && acc) atomicAdd(&counts[jb + lane], (unsigned long long)acc);
+      acc = 0;
+    }
+  }
+}
+
+hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint32_t* jcode,
+                                  int64_t J, int64_t jobs_per_wave, int64_t row_words, uint32_t* mask,
+                                  unsigned long long* counts) {
+  if (J <= 0 || nblk <= 0) return hipSuccess;
+  const int64_t waves = nblk * ((J + jobs_per_wave - 1) / jobs_per_wave);
+  hipLaunchKernelGGL(fit_mask_planes_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, planes, nblk, jcode, J,
+                     jobs_per_wave, row_words, mask, counts);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ best-fit scan (configs 2-4)
 
 // Appendix B key: fit ? (score << 24) | gid : NO_KEY, score = min(a+b+c+d, 2^40-1) with

@@ -41,7 +41,7 @@ class PeStats(ctypes.Structure):
                 ("jobs_placed", ctypes.c_int64), ("jobs_failed", ctypes.c_int64), ("last_greedy_ms", ctypes.c_double),
                 ("greedy_wait_ms", ctypes.c_double), ("greedy_host_ms", ctypes.c_double),
                 ("fit_runs_i32", ctypes.c_int64), ("fit_runs_i64", ctypes.c_int64), ("fit_runs_coded", ctypes.c_int64),
-                ("fit_runs_therm", ctypes.c_int64)]
+                ("fit_runs_therm", ctypes.c_int64), ("fit_runs_planes", ctypes.c_int64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
