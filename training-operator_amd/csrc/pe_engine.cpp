@@ -115,8 +115,9 @@ struct pe_ctx {
   int fit_path = 0;        // 0 int64 compare, 1 int32 compare, 2 dictionary-coded, 3 bit planes
   int fit_path_mask = PATHS_ALL;   // allowed paths (pe_config.fit_path_mask)
   pe::PlaneSpec plane{};
-  int64_t pl_nblk = 0, row_words = 0;   // planes path: 8192-node blocks, mask row stride (u32)
-  DevBuf<uint32_t> planes, plane_jobs;
+  int64_t pl_nblk = 0;                   // planes path: 8192-node blocks
+  DevBuf<uint32_t> planes;
+  DevBuf<uint64_t> plane_jobs;
   pe::CodeSpec code{};
   int64_t code_Jp = 0, node_stride = 0;
   DevBuf<int64_t> code_vals;
@@ -513,22 +514,21 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const 
       ++sp.n;
     }
   }
-  std::vector<uint32_t> jc((size_t)n_jobs);
+  std::vector<uint64_t> jc((size_t)n_jobs);
   for (int64_t j = 0; j < n_jobs; ++j) {
-    uint32_t c = 0;
+    uint64_t c = 0;
     for (int f = 0; f <= pe::D; ++f) {
       const int64_t q = f < pe::D ? req[j * pe::D + f] : (int64_t)(need ? need[j] : 0u);
       const int64_t i = std::lower_bound(vals[f].begin(), vals[f].end(), q) - vals[f].begin();
-      c |= (uint32_t)(off[f] + i) << (5 * f);
+      c |= (uint64_t)(4 * (off[f] + i)) << (7 * f);    // register offset of the plane (4 words each)
     }
     jc[j] = c;
   }
   ctx->plane = sp;
   ctx->pl_nblk = (std::max<int64_t>(ctx->Ns, 1) + pe::PL_BLK - 1) / pe::PL_BLK;
-  ctx->row_words = round_up((ctx->Ns + 31) / 32, 4);
   hipchk(ctx->planes.ensure((size_t)ctx->pl_nblk * pe::PL_MAX * 64 * pe::PL_R), "alloc planes");
   hipchk(ctx->plane_jobs.ensure(jc.size()), "alloc plane jobs");
-  hipchk(hipMemcpyAsync(ctx->plane_jobs.p, jc.data(), jc.size() * 4, hipMemcpyHostToDevice, ctx->stream),
+  hipchk(hipMemcpyAsync(ctx->plane_jobs.p, jc.data(), jc.size() * 8, hipMemcpyHostToDevice, ctx->stream),
          "H2D plane jobs");
   return true;
 }
@@ -586,7 +586,7 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
   if ((ctx->fit_path_mask & PATH_PLANES) && build_planes(ctx, n_jobs, req, need)) ctx->fit_path = 3;
   else if ((ctx->fit_path_mask & PATH_CODED) && build_codes(ctx, n_jobs, req, need)) ctx->fit_path = 2;
   hipchk(ctx->fit_jobs.ensure(Jp), "alloc fit jobs");
-  const size_t mask_words = ctx->fit_path == 3   ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->row_words / 2
+  const size_t mask_words = ctx->fit_path == 3   ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->pl_nblk * 128
                             : ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
                                                  : (size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4;
   hipchk(ctx->mask.ensure(mask_words), "alloc fit mask");
@@ -616,7 +616,7 @@ static void fit_run(pe_ctx* ctx) {
                                     ctx->plane, ctx->planes.p),
            "launch encode_planes");
     hipchk(pe::launch_fit_mask_planes(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p, J, jpw,
-                                      ctx->row_words, reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p),
+                                      reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p),
            "launch fit_mask_planes");
     ctx->stats.fit_runs_planes += 1;
   } else if (ctx->fit_path == 2) {
@@ -687,11 +687,13 @@ int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out) {
     if (row0 < 0 || n_rows < 0 || row0 + n_rows > ctx->fit_J) raise(PE_EINVAL, "row range");
     if (n_rows == 0 || ctx->Wn == 0) return PE_OK;
     need_ptr(out, "out");
-    if (ctx->fit_path == 3) {   // row-major already: strided copy (u64 word c = nodes 64c..64c+63)
-      hipchk(hipMemcpy2DAsync(out, (size_t)ctx->Wn * 8, ctx->mask.p + (size_t)row0 * (ctx->row_words / 2),
-                              (size_t)ctx->row_words * 4, (size_t)ctx->Wn * 8, (size_t)n_rows, hipMemcpyDeviceToHost,
-                              ctx->stream),
-             "D2H mask rows");
+    if (ctx->fit_path == 3) {   // block-major: one strided copy per 8192-node block (128 u64 per row)
+      for (int64_t b = 0; b * 128 < ctx->Wn; ++b) {
+        const int64_t w = std::min<int64_t>(128, ctx->Wn - b * 128);
+        hipchk(hipMemcpy2DAsync(out + b * 128, (size_t)ctx->Wn * 8, ctx->mask.p + ((size_t)b * ctx->fit_J + row0) * 128,
+                                128 * 8, (size_t)w * 8, (size_t)n_rows, hipMemcpyDeviceToHost, ctx->stream),
+               "D2H mask rows");
+      }
       hipchk(hipStreamSynchronize(ctx->stream), "sync mask");
       return PE_OK;
     }
@@ -880,7 +882,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
 
 int pe_fit_mask_layout(const pe_ctx* ctx, int32_t* layout) {
   if (!ctx || !layout) return PE_EINVAL;
-  *layout = ctx->fit_path == 3 ? PE_MASK_ROW_MAJOR : ctx->fit_path == 2 ? PE_MASK_JOB_BITS : PE_MASK_NODE_TILES;
+  *layout = ctx->fit_path == 3 ? PE_MASK_NODE_BLOCKS : ctx->fit_path == 2 ? PE_MASK_JOB_BITS : PE_MASK_NODE_TILES;
   return PE_OK;
 }
 

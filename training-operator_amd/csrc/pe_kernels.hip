@@ -505,45 +505,75 @@ __device__ __forceinline__ uint32_t writelane_s(uint32_t v, uint32_t x, uint32_t
   return v;
 }
 
-// One wave = one 8192-node block (4 words x 32 nodes per lane, PL_MAX planes each in VGPRs) x a job
-// range.  Per job: 5 uniform plane indices (gpr_idx moves), two 3-input ANDs per word, one 16-B
-// store per lane (1 KiB per wave, whole lines), the popcount summed over the wave; lane k gathers
-// the count of the k-th job of each 64 and flushes them with one 64-lane atomic.
+// Plane registers.  Plane p = 8q + s lives in tuple q (pinned to v[32+32q : 63+32q]) at elements
+// 4s..4s+3 = its 4 node words, i.e. word r of plane p is v(32 + 4p + r): one dwordx4 load per plane
+// lands in place, and ONE gpr_idx region with index 4p addresses all four words (src0 = v32..v35
+// + M0).  The compiler's own dynamic indexing opened a region per element (8 SALU per field).
+__device__ __forceinline__ u32x32 load_planes8(const u32x4* __restrict__ p) {
+  u32x32 r;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const u32x4 v = p[s * 64];
+    r[4 * s] = v.x;
+    r[4 * s + 1] = v.y;
+    r[4 * s + 2] = v.z;
+    r[4 * s + 3] = v.w;
+  }
+  return r;
+}
+
+// a = plane[idx4 / 4] (4 words)
+__device__ __forceinline__ void plane_sel(u32x4& a, uint32_t idx4, const u32x32& A, const u32x32& B, const u32x32& C,
+                                          const u32x32& Dq) {
+  asm volatile("s_set_gpr_idx_on %4, gpr_idx(SRC0)\n\t"
+               "v_mov_b32_e32 %0, v32\n\tv_mov_b32_e32 %1, v33\n\tv_mov_b32_e32 %2, v34\n\tv_mov_b32_e32 %3, v35\n\t"
+               "s_set_gpr_idx_off"
+               : "=v"(a.x), "=v"(a.y), "=v"(a.z), "=v"(a.w)
+               : "s"(idx4), "{v[32:63]}"(A), "{v[64:95]}"(B), "{v[96:127]}"(C), "{v[128:159]}"(Dq));
+}
+
+// a &= plane[idx4 / 4]
+__device__ __forceinline__ void plane_and(u32x4& a, uint32_t idx4, const u32x32& A, const u32x32& B, const u32x32& C,
+                                          const u32x32& Dq) {
+  asm volatile("s_set_gpr_idx_on %4, gpr_idx(SRC0)\n\t"
+               "v_and_b32_e32 %0, v32, %0\n\tv_and_b32_e32 %1, v33, %1\n\tv_and_b32_e32 %2, v34, %2\n\t"
+               "v_and_b32_e32 %3, v35, %3\n\ts_set_gpr_idx_off"
+               : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w)
+               : "s"(idx4), "{v[32:63]}"(A), "{v[64:95]}"(B), "{v[96:127]}"(C), "{v[128:159]}"(Dq));
+}
+
+// One wave = one 8192-node block (4 words x 32 nodes per lane, 32 planes in v32..v159) x a job
+// range.  Per job: 5 planes selected by wave-uniform index (one gpr_idx region each, the AND folded
+// into the indexed instruction: 20 VOP2 per 8192 pairs), one 16-B store per lane (1 KiB per wave,
+// whole lines), the popcount summed over the wave; lane k gathers the count of the k-th job of each
+// 64 and flushes them with one 64-lane atomic.  Output block-major (pe_kernels.h): the wave's
+// stores form one sequential stream (1 KiB per job), which the HBM takes at ~5 TB/s where the
+// same bytes scattered 1 KiB per 125 KB row ran at 3.6.
 __global__ __launch_bounds__(256) void fit_mask_planes_kernel(const uint32_t* __restrict__ planes, int64_t nblk,
-                                                              const uint32_t* __restrict__ jcode, int64_t J,
-                                                              int64_t jobs_per_wave, int64_t row_words,
-                                                              uint32_t* __restrict__ mask,
+                                                              const uint64_t* __restrict__ jcode, int64_t J,
+                                                              int64_t jobs_per_wave, uint32_t* __restrict__ mask,
                                                               unsigned long long* __restrict__ counts) {
+  static_assert(PL_MAX == 32 && PL_R == 4, "register map assumes 32 planes x 4 words");
   const int lane = threadIdx.x & 63;
   const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = wave_id % nblk;
   const int64_t j0 = (wave_id / nblk) * jobs_per_wave;
   if (j0 >= J) return;
   const int64_t j1 = min(J, j0 + jobs_per_wave);
-  u32x32 P0, P1, P2, P3;
-  const uint4* pb = reinterpret_cast<const uint4*>(planes + blk * PL_MAX * (64 * PL_R)) + lane;
-#pragma unroll
-  for (int p = 0; p < PL_MAX; ++p) {
-    const uint4 v = pb[p * 64];
-    P0[p] = v.x;
-    P1[p] = v.y;
-    P2[p] = v.z;
-    P3[p] = v.w;
-  }
-  const int64_t col = blk * (64 * PL_R) + lane * PL_R;     // first u32 word of this lane in a row
-  const bool in_row = col < row_words;
-  u32x4* out = reinterpret_cast<u32x4*>(mask + col);
-  const int64_t row4 = row_words / 4;
+  const u32x4* pb = reinterpret_cast<const u32x4*>(planes + blk * PL_MAX * (64 * PL_R)) + lane;
+  const u32x32 A = load_planes8(pb), B = load_planes8(pb + 8 * 64), C = load_planes8(pb + 16 * 64),
+               Dq = load_planes8(pb + 24 * 64);
+  u32x4* out = reinterpret_cast<u32x4*>(mask + blk * J * (64 * PL_R)) + lane;   // (blk, job 0, lane)
   uint32_t acc = 0;
   for (int64_t j = j0; j < j1; ++j) {
-    const uint32_t c = jcode[j];
-    const uint32_t i0 = c & 31, i1 = (c >> 5) & 31, i2 = (c >> 10) & 31, i3 = (c >> 15) & 31, i4 = (c >> 20) & 31;
+    const uint64_t c = jcode[j];                          // 5 x 7-bit fields = 4 x plane index
     u32x4 f;
-    f.x = P0[i0] & P0[i1] & P0[i2] & P0[i3] & P0[i4];
-    f.y = P1[i0] & P1[i1] & P1[i2] & P1[i3] & P1[i4];
-    f.z = P2[i0] & P2[i1] & P2[i2] & P2[i3] & P2[i4];
-    f.w = P3[i0] & P3[i1] & P3[i2] & P3[i3] & P3[i4];
-    if (in_row) out[j * row4] = f;
+    plane_sel(f, (uint32_t)c & 127, A, B, C, Dq);
+    plane_and(f, (uint32_t)(c >> 7) & 127, A, B, C, Dq);
+    plane_and(f, (uint32_t)(c >> 14) & 127, A, B, C, Dq);
+    plane_and(f, (uint32_t)(c >> 21) & 127, A, B, C, Dq);
+    plane_and(f, (uint32_t)(c >> 28) & 127, A, B, C, Dq);
+    out[j * 64] = f;
     const uint32_t n = wave_sum(__popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w));
     const uint32_t k = (uint32_t)((j - j0) & 63);
     acc = writelane_s(acc, n, k);
@@ -555,13 +585,12 @@ __global__ __launch_bounds__(256) void fit_mask_planes_kernel(const uint32_t* __
   }
 }
 
-hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint32_t* jcode,
-                                  int64_t J, int64_t jobs_per_wave, int64_t row_words, uint32_t* mask,
-                                  unsigned long long* counts) {
+hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
+                                  int64_t J, int64_t jobs_per_wave, uint32_t* mask, unsigned long long* counts) {
   if (J <= 0 || nblk <= 0) return hipSuccess;
   const int64_t waves = nblk * ((J + jobs_per_wave - 1) / jobs_per_wave);
   hipLaunchKernelGGL(fit_mask_planes_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, planes, nblk, jcode, J,
-                     jobs_per_wave, row_words, mask, counts);
+                     jobs_per_wave, mask, counts);
   return hipGetLastError();
 }
 
