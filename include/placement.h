@@ -126,6 +126,21 @@ const char* pe_last_error(const pe_ctx* ctx); /* valid until the next call on ct
 int pe_load_nodes(pe_ctx* ctx, int64_t n, const int64_t* cap, const int64_t* used, const uint32_t* labels,
                   const int32_t* island);
 int pe_reset_residuals(pe_ctx* ctx); /* residual := cap - used (device-side copy) */
+/* Incremental inventory ingestion (Node list/watch -> SoA deltas).  The
+ * loaded inventory is a table of n_total slots; the caller (the Node informer's event handler)
+ * keeps the node-name -> slot map and a free-slot list, so an added node takes a free slot, an
+ * updated node rewrites its slot and a deleted node empties it.  Per update i:
+ *   op[i] = PE_NODE_SET:    cap[i][4], used[i][4], labels[i], island[i] replace slot slots[i]; its
+ *                           residual (and the pe_reset_residuals snapshot) becomes cap - used,
+ *                           replacing whatever placements had taken from it
+ *   op[i] = PE_NODE_REMOVE: the slot is empty (nothing fits it, no labels, island -1)
+ * Later entries for the same slot win.  Every rank of a sharded context gets the whole batch and
+ * scatters the slots of its own shard on the device.  The batch is validated before anything is
+ * applied (slot out of range, unknown op, negative capacity/usage: PE_EINVAL, nothing changes).
+ * labels / island may be NULL (0 / -1). */
+enum { PE_NODE_SET = 0, PE_NODE_REMOVE = 1 };
+int pe_update_nodes(pe_ctx* ctx, int64_t n, const int64_t* slots, const uint8_t* op, const int64_t* cap /*[n][4]*/,
+                    const int64_t* used /*[n][4]*/, const uint32_t* labels, const int32_t* island);
 int pe_shard_range(const pe_ctx* ctx, int64_t* begin, int64_t* end);
 int pe_read_residuals(pe_ctx* ctx, int64_t* res_out /* [4][end-begin] of this shard */);
 

@@ -372,6 +372,74 @@ TEST_GPU(TestCalcPGMinResourcesBatchAndOverflow) {
   CHECK(threw);
 }
 
+// ------------------------------------------------------------------ GPU: node inventory (8f row 3)
+
+static Node MkNode(const char* name, const char* cpu, const char* mem, const char* gpu, const char* req_cpu,
+                   const char* req_mem, uint32_t labels = 0) {
+  Node n;
+  n.name = name;
+  n.allocatable = RL({{"cpu", cpu}, {"memory", mem}, {"amd.com/gpu", gpu}, {"pods", "110"}});
+  n.requested = RL({{"cpu", req_cpu}, {"memory", req_mem}});
+  n.label_bits = labels;
+  return n;
+}
+
+static std::vector<int64_t> Residuals(Engine& e, int64_t slots) {
+  std::vector<int64_t> r((size_t)PE_DIMS * slots);
+  CHECK(pe_read_residuals(e.ctx(), r.data()) == PE_OK);
+  return r;
+}
+
+TEST_GPU(TestNodeInventoryInformer) {
+  Engine e(0, "amd.com/gpu");
+  NodeInventory inv(e, 6);
+  inv.OnAdd(MkNode("cpu-a", "64", "256Gi", "0", "8", "32Gi"));
+  inv.OnAdd(MkNode("gpu-a", "128", "1Ti", "8", "0", "0", 1));
+  inv.OnAdd(MkNode("cpu-b", "32", "128Gi", "0", "31", "1Gi"));
+  CHECK(inv.Flush() == 3 && inv.Pending() == 0);
+  CHECK(*inv.SlotOf("cpu-a") == 0 && *inv.SlotOf("gpu-a") == 1 && *inv.SlotOf("cpu-b") == 2);
+  auto r = Residuals(e, 6);
+  CHECK(r[0 * 6 + 0] == 56000 && r[1 * 6 + 0] == (224LL << 30));   // cpu milli, memory bytes
+  CHECK(r[2 * 6 + 1] == 8 && r[0 * 6 + 2] == 1000);
+  CHECK(r[0 * 6 + 3] == INT64_MIN);                                 // empty slot: nothing fits
+
+  // delete + add reuse the lowest free slot; update rewrites in place; one flush for all three
+  inv.OnDelete("gpu-a");
+  inv.OnAdd(MkNode("gpu-b", "192", "2Ti", "8", "16", "64Gi", 1));
+  inv.OnUpdate(MkNode("cpu-a", "64", "256Gi", "0", "60", "32Gi"));
+  CHECK(inv.Flush() == 3);
+  CHECK(*inv.SlotOf("gpu-b") == 1 && !inv.SlotOf("gpu-a") && inv.Size() == 3);
+  r = Residuals(e, 6);
+  CHECK(r[0 * 6 + 1] == 176000 && r[2 * 6 + 1] == 8 && r[0 * 6 + 0] == 4000);
+
+  // the fit mask sees the live inventory: cpu 2 + mem 1Gi fits cpu-b? no (1 core left); cpu-a yes
+  const int64_t req[2 * PE_DIMS] = {2000, 1LL << 30, 0, 0, 1000, 1LL << 30, 1, 0};
+  const uint32_t need[2] = {0, 1};
+  int64_t counts[2] = {-1, -1};
+  CHECK(pe_fit_mask(e.ctx(), 2, req, need, counts, nullptr, nullptr) == PE_OK);
+  CHECK(counts[0] == 2 && counts[1] == 1);                          // cpu-a + gpu-b; gpu-b only
+  uint64_t rows[2];
+  CHECK(pe_fit_mask_rows(e.ctx(), 0, 2, rows) == PE_OK);
+  CHECK(rows[0] == 0b011 && rows[1] == 0b010);
+
+  // a node whose quantity has no exact canonical value changes nothing; a full table refuses
+  bool threw = false;
+  try {
+    inv.OnAdd(MkNode("bad", "0.0001", "1Gi", "0", "0", "0"));
+  } catch (const Error& err) {
+    threw = err.code == PE_EINVAL;
+  }
+  CHECK(threw && inv.Pending() == 0 && !inv.SlotOf("bad"));
+  for (int i = 0; i < 3; ++i) inv.OnAdd(MkNode(("n" + std::to_string(i)).c_str(), "8", "8Gi", "0", "0", "0"));
+  threw = false;
+  try {
+    inv.OnAdd(MkNode("overflow", "8", "8Gi", "0", "0", "0"));
+  } catch (const Error& err) {
+    threw = err.code == PE_ENOMEM;
+  }
+  CHECK(threw && inv.Size() == 6 && inv.Flush() == 3);
+}
+
 int main(int argc, char** argv) {
   bool cpu = true, gpu = false;
   for (int i = 1; i < argc; ++i) {

@@ -30,5 +30,6 @@ def test_host_mirror_cpu_cases():
 @pytest.mark.gpu
 def test_host_mirror_gpu_cases():
     out = run("--gpu")
-    for name in ("TestNewInfo", "TestTrainingRuntimeNewObjects", "TestIntegrationPodGroup", "TestCalcPGMinResourcesMnist"):
+    for name in ("TestNewInfo", "TestTrainingRuntimeNewObjects", "TestIntegrationPodGroup", "TestCalcPGMinResourcesMnist",
+                 "TestNodeInventoryInformer"):
         assert "ok   " + name in out

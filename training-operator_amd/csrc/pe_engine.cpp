@@ -13,6 +13,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "pe_kernels.h"
@@ -104,6 +105,7 @@ struct pe_ctx {
   DevBuf<int64_t> res0, res;
   DevBuf<uint32_t> labels;
   DevBuf<int32_t> island;
+  DevBuf<pe::NodeUpd> n_upd;   // pe_update_nodes staging
   // fit mask
   int64_t fit_J = 0, fit_Jp = 0, Wn = 0, Wt = 0;
   bool fit_uploaded = false;
@@ -143,7 +145,7 @@ struct pe_ctx {
   ~pe_ctx() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
-    res0.release(); res.release(); labels.release(); island.release();
+    res0.release(); res.release(); labels.release(); island.release(); n_upd.release();
     fit_jobs.release(); fit_jobs32.release(); res32.release(); mask.release();
     code_vals.release(); code_needs.release(); code_jobs.release(); code_x.release(); counts.release(); h_counts.release();
     planes.release(); plane_jobs.release();
@@ -310,6 +312,65 @@ int pe_load_nodes(pe_ctx* ctx, int64_t n, const int64_t* cap, const int64_t* use
     hipchk(hipMemcpyAsync(ctx->island.p, isl.data(), isl.size() * 4, hipMemcpyHostToDevice, ctx->stream), "H2D isl");
     hipchk(hipStreamSynchronize(ctx->stream), "sync load");
     ctx->loaded = true;
+    return PE_OK;
+  });
+}
+
+int pe_update_nodes(pe_ctx* ctx, int64_t n, const int64_t* slots, const uint8_t* op, const int64_t* cap,
+                    const int64_t* used, const uint32_t* labels, const int32_t* island) {
+  return guarded(ctx, [&]() -> int {
+    if (!ctx->loaded) raise(PE_ESTATE, "no inventory loaded");
+    if (n < 0) raise(PE_EINVAL, "n < 0");
+    if (n == 0) return PE_OK;
+    need_ptr(slots, "slots");
+    need_ptr(op, "op");
+    // validate the whole batch first: nothing is applied unless every entry is valid
+    bool any_set = false;
+    for (int64_t i = 0; i < n; ++i) {
+      if (slots[i] < 0 || slots[i] >= ctx->n_total) raise(PE_EINVAL, "slot out of range");
+      if (op[i] != PE_NODE_SET && op[i] != PE_NODE_REMOVE) raise(PE_EINVAL, "unknown node op");
+      any_set |= op[i] == PE_NODE_SET;
+    }
+    if (any_set) {
+      need_ptr(cap, "cap");
+      need_ptr(used, "used");
+      for (int64_t i = 0; i < n; ++i)
+        if (op[i] == PE_NODE_SET)
+          for (int d = 0; d < pe::D; ++d)
+            if (cap[i * pe::D + d] < 0 || used[i * pe::D + d] < 0) raise(PE_EINVAL, "negative capacity/usage");
+    }
+    // last entry per slot wins; keep only this shard's slots
+    std::unordered_map<int64_t, int64_t> last;
+    last.reserve((size_t)n * 2);
+    for (int64_t i = 0; i < n; ++i)
+      if (slots[i] >= ctx->begin && slots[i] < ctx->end) last[slots[i]] = i;
+    std::vector<pe::NodeUpd> upd;
+    upd.reserve(last.size());
+    for (int64_t i = 0; i < n; ++i) {
+      auto it = last.find(slots[i]);
+      if (it == last.end() || it->second != i) continue;
+      pe::NodeUpd u{};
+      u.local = slots[i] - ctx->begin;
+      if (op[i] == PE_NODE_SET) {
+        for (int d = 0; d < pe::D; ++d) u.res[d] = cap[i * pe::D + d] - used[i * pe::D + d];
+        u.labels = labels ? labels[i] : 0u;
+        u.island = island ? island[i] : -1;
+      } else {
+        for (int d = 0; d < pe::D; ++d) u.res[d] = pe::NEVER;
+        u.labels = 0u;
+        u.island = -1;
+      }
+      upd.push_back(u);
+    }
+    if (upd.empty()) return PE_OK;
+    hipchk(ctx->n_upd.ensure(upd.size()), "alloc node updates");
+    hipchk(hipMemcpyAsync(ctx->n_upd.p, upd.data(), upd.size() * sizeof(pe::NodeUpd), hipMemcpyHostToDevice,
+                          ctx->stream),
+           "H2D node updates");
+    hipchk(pe::launch_scatter_nodes(ctx->stream, ctx->res.p, ctx->res0.p, ctx->stride, ctx->labels.p, ctx->island.p,
+                                    ctx->n_upd.p, (int64_t)upd.size()),
+           "launch scatter_nodes");
+    hipchk(hipStreamSynchronize(ctx->stream), "sync node updates");   // the host vector dies here
     return PE_OK;
   });
 }

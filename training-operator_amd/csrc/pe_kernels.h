@@ -145,4 +145,16 @@ hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt,
 // upd: [n] records {local node (i64), res[4]} -> res[d][node] = value (absolute)
 hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n);
 
+// Inventory delta for one slot of this shard (pe_update_nodes): residual written to both the
+// live and the reset copy, labels and island replaced.  Slots are unique within a launch.
+struct NodeUpd {
+  int64_t local;
+  int64_t res[D];
+  uint32_t labels;
+  int32_t island;
+};
+static_assert(sizeof(NodeUpd) == 48, "NodeUpd must be 48 B");
+hipError_t launch_scatter_nodes(hipStream_t s, int64_t* res, int64_t* res0, int64_t stride, uint32_t* labels,
+                                int32_t* island, const NodeUpd* upd, int64_t n);
+
 }  // namespace pe

@@ -818,4 +818,30 @@ hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ inventory deltas (sec. 8f row 3)
+
+__global__ __launch_bounds__(256) void scatter_nodes_kernel(int64_t* __restrict__ res, int64_t* __restrict__ res0,
+                                                            int64_t stride, uint32_t* __restrict__ labels,
+                                                            int32_t* __restrict__ island,
+                                                            const NodeUpd* __restrict__ upd, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const NodeUpd u = upd[i];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    res[d * stride + u.local] = u.res[d];
+    res0[d * stride + u.local] = u.res[d];
+  }
+  labels[u.local] = u.labels;
+  island[u.local] = u.island;
+}
+
+hipError_t launch_scatter_nodes(hipStream_t s, int64_t* res, int64_t* res0, int64_t stride, uint32_t* labels,
+                                int32_t* island, const NodeUpd* upd, int64_t n) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_nodes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, res, res0, stride,
+                     labels, island, upd, n);
+  return hipGetLastError();
+}
+
 }  // namespace pe

@@ -313,4 +313,89 @@ CoScheduling::BuildResult CoScheduling::Build(const Info* info, const TrainJob* 
   return BuildBatch({info}, {trainJob}, {existing})[0];
 }
 
+// ------------------------------------------------------------------ node inventory
+
+NodeInventory::NodeInventory(Engine& eng, int64_t slots) : eng_(eng), slots_(slots) {
+  if (slots < 0) throw Error{PE_EINVAL, "slots < 0"};
+  std::vector<int64_t> zero((size_t)PE_DIMS * (size_t)slots, 0);
+  int rc = pe_load_nodes(eng_.ctx(), slots, zero.data(), zero.data(), nullptr, nullptr);
+  if (rc != PE_OK) throw Error{rc, pe_last_error(eng_.ctx())};
+  std::vector<int64_t> ids((size_t)slots);
+  for (int64_t i = 0; i < slots; ++i) ids[i] = i;
+  std::vector<uint8_t> ops((size_t)slots, (uint8_t)PE_NODE_REMOVE);
+  rc = pe_update_nodes(eng_.ctx(), slots, ids.data(), ops.data(), nullptr, nullptr, nullptr, nullptr);
+  if (rc != PE_OK) throw Error{rc, pe_last_error(eng_.ctx())};
+  for (int64_t i = 0; i < slots; ++i) free_.insert(free_.end(), i);
+}
+
+void NodeInventory::stage(int64_t slot, const Node* node) {
+  int64_t cap[PE_DIMS] = {0, 0, 0, 0}, used[PE_DIMS] = {0, 0, 0, 0};
+  if (node) {
+    const Dims& dims = eng_.dims();
+    auto conv = [&](const ResourceList& rl, int64_t* out) {
+      for (const auto& kv : rl) {
+        const int d = dims.dim_of(kv.first);
+        if (d < 0) continue;
+        try {
+          out[d] = kv.second.Canonical(kv.first);
+        } catch (const QuantityError& e) {
+          throw Error{PE_EINVAL, "node " + node->name + ": " + e.msg};
+        }
+      }
+    };
+    conv(node->allocatable, cap);   // converted before anything is staged: a bad node changes nothing
+    conv(node->requested, used);
+  }
+  p_slot_.push_back(slot);
+  p_op_.push_back((uint8_t)(node ? PE_NODE_SET : PE_NODE_REMOVE));
+  p_cap_.insert(p_cap_.end(), cap, cap + PE_DIMS);
+  p_used_.insert(p_used_.end(), used, used + PE_DIMS);
+  p_lab_.push_back(node ? node->label_bits : 0u);
+  p_isl_.push_back(node ? node->island : -1);
+}
+
+void NodeInventory::OnAdd(const Node& node) {
+  if (slot_of_.count(node.name)) return OnUpdate(node);
+  if (free_.empty()) throw Error{PE_ENOMEM, "node inventory full (" + std::to_string(slots_) + " slots)"};
+  const int64_t slot = *free_.begin();
+  stage(slot, &node);
+  free_.erase(free_.begin());
+  slot_of_[node.name] = slot;
+}
+
+void NodeInventory::OnUpdate(const Node& node) {
+  auto it = slot_of_.find(node.name);
+  if (it == slot_of_.end()) return OnAdd(node);
+  stage(it->second, &node);
+}
+
+void NodeInventory::OnDelete(const std::string& name) {
+  auto it = slot_of_.find(name);
+  if (it == slot_of_.end()) return;
+  stage(it->second, nullptr);
+  free_.insert(it->second);
+  slot_of_.erase(it);
+}
+
+int64_t NodeInventory::Flush() {
+  const int64_t n = (int64_t)p_slot_.size();
+  if (n == 0) return 0;
+  const int rc = pe_update_nodes(eng_.ctx(), n, p_slot_.data(), p_op_.data(), p_cap_.data(), p_used_.data(),
+                                 p_lab_.data(), p_isl_.data());
+  if (rc != PE_OK) throw Error{rc, pe_last_error(eng_.ctx())};
+  p_slot_.clear();
+  p_op_.clear();
+  p_cap_.clear();
+  p_used_.clear();
+  p_lab_.clear();
+  p_isl_.clear();
+  return n;
+}
+
+std::optional<int64_t> NodeInventory::SlotOf(const std::string& name) const {
+  auto it = slot_of_.find(name);
+  if (it == slot_of_.end()) return std::nullopt;
+  return it->second;
+}
+
 }  // namespace kf

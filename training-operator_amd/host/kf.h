@@ -17,6 +17,7 @@
 #include <map>
 #include <memory>
 #include <optional>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -234,6 +235,43 @@ class CoScheduling : public Plugin {
 };
 
 bool NeedsCreateOrUpdate(const PodGroup* old, const PodGroup& pg, bool suspended);  // :150-153
+
+// ------------------------------------------------------------------ node inventory
+// The Node informer's event-handler side of pe_update_nodes: node name -> slot map, lowest-free-slot
+// reuse, and a pending delta batch flushed in one call.  A Node carries status.allocatable and the
+// summed requests of the pods bound to it (the scheduler cache's view); keys without an engine
+// dimension (pods, hugepages-*) are not part of the fit and are ignored.
+struct Node {
+  std::string name;
+  ResourceList allocatable;
+  ResourceList requested;
+  uint32_t label_bits = 0;   // the node's labels as the engine's label bits (placement.h `need`)
+  int32_t island = -1;
+};
+
+class NodeInventory {
+ public:
+  // Loads `slots` empty slots on the engine (nothing fits a slot until a node arrives in it).
+  NodeInventory(Engine& eng, int64_t slots);
+  void OnAdd(const Node& node);              // lowest free slot; Error{PE_ENOMEM} when every slot is used
+  void OnUpdate(const Node& node);           // rewrites the node's slot (an unknown node is added)
+  void OnDelete(const std::string& name);    // empties the slot (unknown names are ignored)
+  int64_t Flush();                           // one pe_update_nodes call; returns the entries sent
+  std::optional<int64_t> SlotOf(const std::string& name) const;
+  int64_t Size() const { return (int64_t)slot_of_.size(); }
+  int64_t Pending() const { return (int64_t)p_slot_.size(); }
+
+ private:
+  void stage(int64_t slot, const Node* node);   // nullptr: remove
+  Engine& eng_;
+  int64_t slots_;
+  std::map<std::string, int64_t> slot_of_;
+  std::set<int64_t> free_;
+  std::vector<int64_t> p_slot_, p_cap_, p_used_;
+  std::vector<uint8_t> p_op_;
+  std::vector<uint32_t> p_lab_;
+  std::vector<int32_t> p_isl_;
+};
 
 // ------------------------------------------------------------------ flattening (exposed for tests)
 

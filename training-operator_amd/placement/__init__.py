@@ -17,12 +17,13 @@ import numpy as np
 
 from . import _abi
 from ._abi import (PE_JOB_PLACED, PE_JOB_UNSCHEDULABLE, PE_KIND_CONTAINER, PE_KIND_INIT, PE_KIND_OVERHEAD,
-                   PE_KIND_SHIFT, PE_KIND_SIDECAR, PE_MODE_V1, PE_MODE_V2)
+                   PE_KIND_SHIFT, PE_KIND_SIDECAR, PE_MODE_V1, PE_MODE_V2, PE_NODE_REMOVE, PE_NODE_SET)
 
 V1, V2 = PE_MODE_V1, PE_MODE_V2
 
 __all__ = ["Engine", "Resolver", "PlacementError", "V1", "V2", "PE_JOB_PLACED", "PE_JOB_UNSCHEDULABLE",
-           "PE_KIND_CONTAINER", "PE_KIND_INIT", "PE_KIND_SIDECAR", "PE_KIND_OVERHEAD", "PE_KIND_SHIFT", "comm_id"]
+           "PE_KIND_CONTAINER", "PE_KIND_INIT", "PE_KIND_SIDECAR", "PE_KIND_OVERHEAD", "PE_KIND_SHIFT", "comm_id",
+           "PE_NODE_SET", "PE_NODE_REMOVE"]
 
 
 class PlacementError(RuntimeError):
@@ -116,6 +117,19 @@ class Engine:
         isl = None if island is None else _c(island, np.int32)
         self._chk(self.lib.pe_load_nodes(self.h, n, _p(cap), _p(used), _p(lab), _p(isl)), "pe_load_nodes")
         self.n_nodes = n
+
+    def update_nodes(self, slots, op, cap=None, used=None, labels=None, island=None):
+        """pe_update_nodes: per entry op 0 (NODE_SET: cap[i][4], used[i][4], labels, island replace
+        the slot) or 1 (NODE_REMOVE).  cap/used are row-major [n][4]."""
+        slots = _c(slots, np.int64)
+        op = _c(op, np.uint8)
+        n = slots.shape[0]
+        cap = None if cap is None else _c(cap, np.int64)
+        used = None if used is None else _c(used, np.int64)
+        lab = None if labels is None else _c(labels, np.uint32)
+        isl = None if island is None else _c(island, np.int32)
+        self._chk(self.lib.pe_update_nodes(self.h, n, _p(slots), _p(op), _p(cap), _p(used), _p(lab), _p(isl)),
+                  "pe_update_nodes")
 
     def reset_residuals(self):
         self._chk(self.lib.pe_reset_residuals(self.h), "pe_reset_residuals")

@@ -16,6 +16,7 @@ HEADER = os.path.join(REPO_ROOT, "include", "placement.h")
 
 PE_OK, PE_EINVAL, PE_EOVERFLOW, PE_ENOMEM, PE_EHIP, PE_ERCCL, PE_ESTATE, PE_ENODEV = 0, -1, -2, -3, -4, -5, -6, -7
 PE_MODE_V1, PE_MODE_V2 = 1, 2
+PE_NODE_SET, PE_NODE_REMOVE = 0, 1
 PE_JOB_PLACED, PE_JOB_UNSCHEDULABLE = 0, 1
 PE_KIND_CONTAINER, PE_KIND_INIT, PE_KIND_SIDECAR, PE_KIND_OVERHEAD = 0, 1, 2, 3
 PE_KIND_SHIFT = 4
@@ -59,6 +60,7 @@ SIGNATURES = {
     "pe_last_error": (ctypes.c_char_p, [P]),
     "pe_load_nodes": (ctypes.c_int, [P, i64, P, P, P, P]),
     "pe_reset_residuals": (ctypes.c_int, [P]),
+    "pe_update_nodes": (ctypes.c_int, [P, i64, P, P, P, P, P, P]),
     "pe_shard_range": (ctypes.c_int, [P, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
     "pe_read_residuals": (ctypes.c_int, [P, P]),
     "pe_pg_min_resources": (ctypes.c_int, [P, i32, i64, P, P, P, P, P, P, P, P, P, P]),
