@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """Benchmark of the gang-placement hot path (BASELINE.json metric).
 
-A "step" = one fit-mask pass (config 5): every job of a 100k-job batch evaluated against every
-node of the 1M-node inventory, mask + per-job counts written to HBM, inputs already resident.
+A "step" = one fit-mask pass (config 5): every job of the batch evaluated against every node of
+the 1M-node inventory, mask + per-job counts written to HBM, inputs already resident.  The
+inventory is node-sharded over the ranks (north_star); scaling is weak: the batch holds
+100k x n_gpus jobs, so every rank evaluates 100k jobs x 1M nodes worth of pairs (its 1M/N-node
+shard x the whole batch) per step with no collective on the data path.
 `value` = job x node fit evaluations per second for the whole job (all ranks).  The second half
 of the metric, gang placements/s, is measured on the same 1M-node inventory with a 10k-job
 mixed PyTorch/MPI/JAX batch (config 3 mix) and reported in the "greedy" object.
@@ -32,7 +35,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # chip-wide integer VALU issue ceiling, wave-instructions/s: profiles/r1_ubench_valu.txt
 # (v_add_u32 / v_addc_co at 8 waves per SIMD: 4.24 cycles per wave-instruction per SIMD, 256 CUs x 4 SIMDs)
 VALU_ISSUE_CEILING = 5.79e11
-KERNEL_OF_PATH = {"planes": "pe::fit_mask_planes_kernel", "coded-therm": "pe::fit_mask_coded_kernel", "coded-swar": "pe::fit_mask_coded_kernel",
+KERNEL_OF_PATH = {"planes": "pe::fit_mask_planes_rows_kernel", "planes-blocks": "pe::fit_mask_planes_kernel", "coded-therm": "pe::fit_mask_coded_kernel", "coded-swar": "pe::fit_mask_coded_kernel",
                   "i32": "pe::fit_mask_kernel", "i64": "pe::fit_mask_kernel"}
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 
@@ -88,6 +91,10 @@ def profiled_traffic(kernel: str, n_nodes: int, n_jobs: int):
     return None, None
 
 
+def _count(n: int) -> str:
+    return f"{n // 1_000_000}M" if n % 1_000_000 == 0 else (f"{n // 1000}k" if n % 1000 == 0 else str(n))
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -113,7 +120,10 @@ def main():
     ap.add_argument("--window-pods", type=int, default=0)
     ap.add_argument("--no-greedy", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-jobs", type=int, default=1000)
+    ap.add_argument("--cpu-sample-jobs", type=int, default=20000)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: batch = fit-jobs x n_gpus (fixed per-rank work); strong: batch = fit-jobs")
+    ap.add_argument("--fit-path-mask", type=int, default=0, help="pe_config.fit_path_mask (0 = every kernel)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -166,10 +176,11 @@ def main():
         def allsum(x):
             return x
 
-    N, J = args.nodes, args.fit_jobs
+    N = args.nodes
+    J = args.fit_jobs * (world if args.scaling == "weak" else 1)
     inv = synth.make_inventory(N, synth.SEED["cfg5"], gpu_frac=0.2)
     eng = Engine(device, rank=rank, world_size=world, comm=cid, exchange=exchange, max_nodes=N, topk=args.topk,
-                 window_groups=args.window_groups, window_pods=args.window_pods)
+                 window_groups=args.window_groups, window_pods=args.window_pods, fit_path_mask=args.fit_path_mask)
     eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     b, e = eng.shard_range()
     Ns = e - b
@@ -198,7 +209,7 @@ def main():
     kern_ms = ev.elapsed_ms(e0, e1) / args.steps
     value = float(N) * J * args.steps / elapsed
     st0 = eng.stats()
-    fit_path = ("planes" if st0["fit_runs_planes"] else
+    fit_path = (("planes-blocks" if args.fit_path_mask & 32 else "planes") if st0["fit_runs_planes"] else
                 (("coded-therm" if st0["fit_runs_therm"] else "coded-swar") if st0["fit_runs_coded"] else
                  ("i32" if st0["fit_runs_i32"] else "i64")))
     alg = fit_bytes(Ns, J)
@@ -212,16 +223,20 @@ def main():
     out = {
         "metric": METRIC, "value": value, "unit": "job*node fit evals/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "int64", "data": "synthetic (splitmix64, SURVEY.md 8d)",
-        "config": {"workload": "cfg5: fit bitmask, 1M-node inventory x 100k jobs, device-resident",
-                   "nodes": N, "jobs": J, "parallelism": f"node-shard x{world}" + (" (host exchange rehearsal)" if host_exchange and world > 1 else ""), "feasible_pairs": feasible},
+        "scaling": args.scaling, "vs_baseline": None, "dtype": "int64", "data": "synthetic (splitmix64, SURVEY.md 8d)",
+        "config": {"workload": f"cfg5: fit bitmask, {_count(N)}-node inventory x {_count(args.fit_jobs)} jobs"
+                               f"{' per GPU' if args.scaling == 'weak' else ''} ({J} jobs in all), device-resident",
+                   "nodes": N, "jobs": J, "jobs_per_gpu": J // world if args.scaling == "weak" else J,
+                   "shard_nodes": Ns,
+                   "parallelism": f"node-shard x{world}" + (" (host exchange rehearsal)" if host_exchange and world > 1 else ""), "feasible_pairs": feasible},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": tsrc, "kernel_ms": kern_ms, "alg_bytes_per_launch": alg,
                      "fit_path": fit_path, "valu_issue_frac": valu_frac,
                      "note": "kernel_ms = hipEvent time on the engine stream / fit_mask_run (one count memset, "
-                             "the node encode and the fit kernel); per-rank shard; the fit kernel is VALU-issue-"
-                             "bound (valu_issue_frac = its VALU wave-instructions / measured issue ceiling)"},
+                             "the node encode and the fit kernel) on this rank's shard; achieved = algorithmic "
+                             "bytes (shard nodes x 36 + jobs x 44 + jobs x ceil(shard/64) x 8) / kernel_ms; the "
+                             "fit kernel is bound by its mask stores (HBM write)"},
     }
 
     if not args.no_greedy:

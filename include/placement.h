@@ -91,7 +91,9 @@ typedef struct {
   int64_t window_pods;           /* pods per scan window (0 = 1024) */
   int32_t fit_path_mask;         /* allowed fit-mask kernels: bit0 int64 compare, bit1 int32 compare,
                                     bit2 dictionary-coded, bit4 bit planes; bit3 set = no thermometer
-                                    form of the coded kernel; no kernel bit set = all kernels (the
+                                    form of the coded kernel; bit5 set = bit planes through the
+                                    block-major kernel (PE_MASK_NODE_BLOCKS) instead of the row-major
+                                    sweep (PE_MASK_ROWS); no kernel bit set = all kernels (the
                                     int64 path is always allowed) */
 } pe_config;
 
@@ -168,8 +170,10 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
  *     ((j / 16) * Wt + c / 4) * 64 + (j % 16) * 4 + c % 4,   Wt = ceil(words_per_row / 4)
  *   PE_MASK_JOB_BITS (dictionary-coded path): word (b, n) holds jobs 64b..64b+63 (bit j%64) for
  *     node n at b * S + n,  S = shard nodes rounded up to 512
- *   PE_MASK_NODE_BLOCKS (bit-plane path): word (j, c) at ((c / 128) * J + j) * 128 + c % 128, i.e.
- *     per 8192-node block a [J][128]-word slab (J = jobs of the batch)
+ *   PE_MASK_ROWS (bit-plane path, default): row-major, word (j, c) at j * ceil(S / 8192) * 128 + c
+ *     (S = shard nodes; rows padded to whole 8192-node blocks, padding bits 0)
+ *   PE_MASK_NODE_BLOCKS (bit-plane path, fit_path_mask bit5): word (j, c) at
+ *     ((c / 128) * J + j) * 128 + c % 128, i.e. per 8192-node block a [J][128]-word slab
  * All layouts are written as whole 128-B lines.  pe_fit_mask_rows always hands rows back
  * row-major [n_rows][words_per_row].  Counts are per job over this shard (sum across shards).
  * One-shot form: upload + compute + counts to host; *dev_mask receives the device pointer. */
@@ -180,7 +184,7 @@ int pe_jobs_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32
 int pe_fit_mask_run(pe_ctx* ctx); /* asynchronous on the context stream */
 int pe_fit_counts(pe_ctx* ctx, int64_t* out_feasible_count); /* synchronizes */
 int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out /*[n_rows][words_per_row]*/);
-enum { PE_MASK_NODE_TILES = 0, PE_MASK_JOB_BITS = 1, PE_MASK_NODE_BLOCKS = 2 };
+enum { PE_MASK_NODE_TILES = 0, PE_MASK_JOB_BITS = 1, PE_MASK_NODE_BLOCKS = 2, PE_MASK_ROWS = 3 };
 int pe_fit_mask_layout(const pe_ctx* ctx, int32_t* layout);
 
 /* Greedy best-fit all-or-nothing gang placement.  Jobs in (priority

@@ -149,12 +149,13 @@ def test_fit_mask_edge_values(eng):
     assert counts[0] == N - 1 and counts[4] == 1
 
 
-PATHS = {"planes": (0, "fit_runs_planes", 2), "therm": (5, "fit_runs_therm", 1), "swar": (13, "fit_runs_coded", 1),
+PATHS = {"planes": (0, "fit_runs_planes", 3), "planes_blocks": (16 | 32, "fit_runs_planes", 2),
+         "therm": (5, "fit_runs_therm", 1), "swar": (13, "fit_runs_coded", 1),
          "i32": (3, "fit_runs_i32", 0), "i64": (1, "fit_runs_i64", 0)}
 
 
-@pytest.mark.parametrize("path", ["planes", "therm", "swar", "i32", "i64"])
-@pytest.mark.parametrize("N,J", [(5000, 300), (777, 65), (64, 1)])
+@pytest.mark.parametrize("path", ["planes", "planes_blocks", "therm", "swar", "i32", "i64"])
+@pytest.mark.parametrize("N,J", [(5000, 300), (777, 65), (64, 1), (600_000, 2085)])
 def test_fit_mask_paths(path, N, J):
     """Every exact fit path on the same data (residuals span the int32 saturation point after
     scaling: nodes with 2^50 B of memory; over-committed nodes with negative residuals)."""

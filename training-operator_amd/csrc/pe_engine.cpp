@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -82,7 +83,7 @@ void ncclchk(ncclResult_t r, const char* what) {
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // pe_config.fit_path_mask bits
-constexpr int PATH_I64 = 1, PATH_I32 = 2, PATH_CODED = 4, PATH_NO_THERM = 8, PATH_PLANES = 16;
+constexpr int PATH_I64 = 1, PATH_I32 = 2, PATH_CODED = 4, PATH_NO_THERM = 8, PATH_PLANES = 16, PATH_PLANES_BLOCKS = 32;
 constexpr int PATHS_ALL = PATH_I64 | PATH_I32 | PATH_CODED | PATH_PLANES;
 
 }  // namespace
@@ -118,6 +119,8 @@ struct pe_ctx {
   int fit_path_mask = PATHS_ALL;   // allowed paths (pe_config.fit_path_mask)
   pe::PlaneSpec plane{};
   int64_t pl_nblk = 0;                   // planes path: 8192-node blocks
+  bool pl_rows = true;                   // planes path: row-major sweep kernel (else block-major streams)
+  int64_t pl_R = 1;                      // row-major kernel: job phases of the uploaded batch
   DevBuf<uint32_t> planes;
   DevBuf<uint64_t> plane_jobs;
   pe::CodeSpec code{};
@@ -244,7 +247,8 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   ctx->window_groups = cfg->window_groups > 0 ? cfg->window_groups : 64;
   ctx->window_pods = cfg->window_pods > 0 ? cfg->window_pods : 1024;
   ctx->gpu_name = cfg->gpu_resource_name ? cfg->gpu_resource_name : "amd.com/gpu";
-  ctx->fit_path_mask = cfg->fit_path_mask > 0 ? (cfg->fit_path_mask & (PATHS_ALL | PATH_NO_THERM)) : PATHS_ALL;
+  ctx->fit_path_mask = cfg->fit_path_mask & (PATHS_ALL | PATH_NO_THERM | PATH_PLANES_BLOCKS);
+  ctx->pl_rows = !(ctx->fit_path_mask & PATH_PLANES_BLOCKS);
   if (!(ctx->fit_path_mask & PATHS_ALL)) ctx->fit_path_mask |= PATHS_ALL;   // no kernel bits = all kernels
   ctx->fit_path_mask |= PATH_I64;                                           // always available
   int rc = PE_OK;
@@ -581,12 +585,22 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const 
     for (int f = 0; f <= pe::D; ++f) {
       const int64_t q = f < pe::D ? req[j * pe::D + f] : (int64_t)(need ? need[j] : 0u);
       const int64_t i = std::lower_bound(vals[f].begin(), vals[f].end(), q) - vals[f].begin();
-      c |= (uint64_t)(4 * (off[f] + i)) << (7 * f);    // register offset of the plane (4 words each)
+      // register offset of the plane (4 words each); dims at bits 0, 7, 14, 21, the need at bit 32
+      c |= (uint64_t)(4 * (off[f] + i)) << (f < pe::D ? 7 * f : 32);
     }
     jc[j] = c;
   }
   ctx->plane = sp;
   ctx->pl_nblk = (std::max<int64_t>(ctx->Ns, 1) + pe::PL_BLK - 1) / pe::PL_BLK;
+  if (ctx->pl_rows) {
+    // one wave per SIMD (1024 on 256 CUs) = nblk x R job phases; codes phase-major
+    const int64_t R = std::min<int64_t>(n_jobs, std::max<int64_t>(1, 1024 / ctx->pl_nblk));
+    const int64_t Jr = ((n_jobs + R - 1) / R + 3) / 4 * 4;   // = the kernel's phase stride
+    std::vector<uint64_t> perm((size_t)(R * Jr), 0);
+    for (int64_t j = 0; j < n_jobs; ++j) perm[(size_t)((j % R) * Jr + j / R)] = jc[j];
+    jc.swap(perm);
+    ctx->pl_R = R;
+  }
   hipchk(ctx->planes.ensure((size_t)ctx->pl_nblk * pe::PL_MAX * 64 * pe::PL_R), "alloc planes");
   hipchk(ctx->plane_jobs.ensure(jc.size()), "alloc plane jobs");
   hipchk(hipMemcpyAsync(ctx->plane_jobs.p, jc.data(), jc.size() * 8, hipMemcpyHostToDevice, ctx->stream),
@@ -651,8 +665,9 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
                             : ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
                                                  : (size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4;
   hipchk(ctx->mask.ensure(mask_words), "alloc fit mask");
-  hipchk(ctx->counts.ensure(Jp), "alloc fit counts");
-  hipchk(ctx->h_counts.ensure(Jp), "alloc pinned counts");
+  const int64_t n_counts = std::max<int64_t>(Jp, ctx->fit_path == 3 && ctx->pl_rows ? ctx->pl_R * (((n_jobs + ctx->pl_R - 1) / ctx->pl_R + 3) / 4 * 4) : 0);
+  hipchk(ctx->counts.ensure(n_counts), "alloc fit counts");
+  hipchk(ctx->h_counts.ensure(n_counts), "alloc pinned counts");
   hipchk(hipMemcpyAsync(ctx->fit_jobs.p, recs.data(), Jp * sizeof(ReqRec), hipMemcpyHostToDevice, ctx->stream),
          "H2D fit jobs");
   hipchk(hipStreamSynchronize(ctx->stream), "sync fit upload");
@@ -671,14 +686,20 @@ static void fit_run(pe_ctx* ctx) {
   tpw = std::min<int64_t>(16, std::max<int64_t>(1, tpw));
   if (ctx->fit_path == 3) {
     // ~16k waves: every 8192-node block times enough job ranges, at least 64 jobs per wave
-    const int64_t ranges = std::max<int64_t>(1, (16384 + ctx->pl_nblk - 1) / ctx->pl_nblk);
-    const int64_t jpw = std::max<int64_t>(64, (J + ranges - 1) / ranges);
     hipchk(pe::launch_encode_planes(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->pl_nblk,
                                     ctx->plane, ctx->planes.p),
            "launch encode_planes");
-    hipchk(pe::launch_fit_mask_planes(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p, J, jpw,
-                                      reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p),
-           "launch fit_mask_planes");
+    if (ctx->pl_rows) {
+      hipchk(pe::launch_fit_mask_planes_rows(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p, J, ctx->pl_R,
+                                             reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p),
+             "launch fit_mask_planes_rows");
+    } else {
+      const int64_t ranges = std::max<int64_t>(1, (16384 + ctx->pl_nblk - 1) / ctx->pl_nblk);
+      const int64_t jpw = std::max<int64_t>(64, (J + ranges - 1) / ranges);
+      hipchk(pe::launch_fit_mask_planes(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p, J, jpw,
+                                        reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p),
+             "launch fit_mask_planes");
+    }
     ctx->stats.fit_runs_planes += 1;
   } else if (ctx->fit_path == 2) {
     const int64_t jblocks = ctx->code_Jp / pe::FC_JT;
@@ -712,11 +733,13 @@ static void fit_run(pe_ctx* ctx) {
 static void fit_counts(pe_ctx* ctx, int64_t* out) {
   const int64_t J = ctx->fit_J;
   if (J == 0) return;
-  hipchk(hipMemcpyAsync(ctx->h_counts.p, ctx->counts.p, J * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+  const bool phased = ctx->fit_path == 3 && ctx->pl_rows;
+  const int64_t R = phased ? ctx->pl_R : 1, Jr = phased ? ((J + R - 1) / R + 3) / 4 * 4 : J;
+  hipchk(hipMemcpyAsync(ctx->h_counts.p, ctx->counts.p, R * Jr * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                         ctx->stream),
          "D2H counts");
   hipchk(hipStreamSynchronize(ctx->stream), "sync counts");
-  for (int64_t j = 0; j < J; ++j) out[j] = (int64_t)ctx->h_counts.p[j];
+  for (int64_t j = 0; j < J; ++j) out[j] = (int64_t)ctx->h_counts.p[(j % R) * Jr + j / R];
 }
 
 int pe_jobs_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
@@ -748,6 +771,14 @@ int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out) {
     if (row0 < 0 || n_rows < 0 || row0 + n_rows > ctx->fit_J) raise(PE_EINVAL, "row range");
     if (n_rows == 0 || ctx->Wn == 0) return PE_OK;
     need_ptr(out, "out");
+    if (ctx->fit_path == 3 && ctx->pl_rows) {   // row-major, rows padded to whole 8192-node blocks
+      hipchk(hipMemcpy2DAsync(out, (size_t)ctx->Wn * 8, ctx->mask.p + (size_t)row0 * ctx->pl_nblk * 128,
+                              (size_t)ctx->pl_nblk * 128 * 8, (size_t)ctx->Wn * 8, (size_t)n_rows,
+                              hipMemcpyDeviceToHost, ctx->stream),
+             "D2H mask rows");
+      hipchk(hipStreamSynchronize(ctx->stream), "sync mask");
+      return PE_OK;
+    }
     if (ctx->fit_path == 3) {   // block-major: one strided copy per 8192-node block (128 u64 per row)
       for (int64_t b = 0; b * 128 < ctx->Wn; ++b) {
         const int64_t w = std::min<int64_t>(128, ctx->Wn - b * 128);
@@ -943,7 +974,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
 
 int pe_fit_mask_layout(const pe_ctx* ctx, int32_t* layout) {
   if (!ctx || !layout) return PE_EINVAL;
-  *layout = ctx->fit_path == 3 ? PE_MASK_NODE_BLOCKS : ctx->fit_path == 2 ? PE_MASK_JOB_BITS : PE_MASK_NODE_TILES;
+  *layout = ctx->fit_path == 3 ? (ctx->pl_rows ? PE_MASK_ROWS : PE_MASK_NODE_BLOCKS) : ctx->fit_path == 2 ? PE_MASK_JOB_BITS : PE_MASK_NODE_TILES;
   return PE_OK;
 }
 

@@ -128,11 +128,17 @@ struct PlaneSpec {
 // planes: [nblk][PL_MAX][64 * PL_R] u32; word w of block b covers nodes b*PL_BLK + 32w .. +31
 hipError_t launch_encode_planes(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
                                 int64_t Ns, int64_t nblk, const PlaneSpec& spec, uint32_t* planes);
-// jcode[j] = 5 fields of 7 bits (dims 0..3, need), each 4 x the plane index.  Mask block-major:
+// jcode[j] = 5 fields of 7 bits (dims 0..3 at bits 0/7/14/21, need at bit 32), each 4 x the plane index.  Mask block-major:
 // u32 word w of row j (nodes 32w..32w+31) at (w / 256 * J + j) * 256 + w % 256, i.e. per 8192-node
 // block a [J][1 KiB] slab.
 hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
                                   int64_t J, int64_t jobs_per_wave, uint32_t* mask, unsigned long long* counts);
+// Row-major form (the default): nblk x R persistent waves, one per SIMD, R job phases; wave
+// (blk, r) takes jobs r, r+R, ...; u32 word w of row j at j * nblk * 256 + w.  jcode and counts are
+// phase-major: entry r * Jr + i belongs to job r + R * i (Jr = ceil(J / R) rounded up to 4), so
+// every wave reads and counts a contiguous run.
+hipError_t launch_fit_mask_planes_rows(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
+                                       int64_t J, int64_t R, uint32_t* mask, unsigned long long* counts);
 
 hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
                        uint64_t id_base, const ReqRec* groups, int Wg, uint64_t* cand, int32_t* cnt,

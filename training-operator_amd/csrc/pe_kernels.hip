@@ -572,7 +572,7 @@ __global__ __launch_bounds__(256) void fit_mask_planes_kernel(const uint32_t* __
     plane_and(f, (uint32_t)(c >> 7) & 127, A, B, C, Dq);
     plane_and(f, (uint32_t)(c >> 14) & 127, A, B, C, Dq);
     plane_and(f, (uint32_t)(c >> 21) & 127, A, B, C, Dq);
-    plane_and(f, (uint32_t)(c >> 28) & 127, A, B, C, Dq);
+    plane_and(f, (uint32_t)(c >> 32) & 127, A, B, C, Dq);
     out[j * 64] = f;
     const uint32_t n = wave_sum(__popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w));
     const uint32_t k = (uint32_t)((j - j0) & 63);
@@ -583,6 +583,170 @@ __global__ __launch_bounds__(256) void fit_mask_planes_kernel(const uint32_t* __
       acc = 0;
     }
   }
+}
+
+typedef __attribute__((address_space(1))) u32x4 gu32x4;   // global (not flat) stores
+
+// f = AND of the 5 planes of batch job K, whose code is lane K of (lo, hi): the code read-out and
+// field extraction sit in the same asm block as the indexed ANDs, so the compiler cannot hoist 128
+// readlanes of a batch into SGPRs (it did, and spilled them).  VALU -> SALU SGPR reads interlock.
+template <int K>
+__device__ __forceinline__ void plane_job(u32x4& f, uint32_t lo, uint32_t hi, const u32x32& A, const u32x32& B,
+                                          const u32x32& C, const u32x32& Dq) {
+  uint32_t c, c4, t;
+  asm volatile(
+      "v_readlane_b32 %[c], %[lo], %[k]\n\t"
+      "v_readlane_b32 %[c4], %[hi], %[k]\n\t"
+      "s_and_b32 %[t], %[c], 0x7f\n\t"
+      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      "v_mov_b32_e32 %[f0], v32\n\tv_mov_b32_e32 %[f1], v33\n\tv_mov_b32_e32 %[f2], v34\n\tv_mov_b32_e32 %[f3], v35\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_bfe_u32 %[t], %[c], 0x70007\n\t"
+      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_bfe_u32 %[t], %[c], 0x7000e\n\t"
+      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_bfe_u32 %[t], %[c], 0x70015\n\t"
+      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_and_b32 %[t], %[c4], 0x7f\n\t"
+      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
+      "s_set_gpr_idx_off"
+      : [f0] "=&v"(f.x), [f1] "=&v"(f.y), [f2] "=&v"(f.z), [f3] "=&v"(f.w), [c] "=&s"(c), [c4] "=&s"(c4),
+        [t] "=&s"(t)
+      : [lo] "v"(lo), [hi] "v"(hi), [k] "i"(K), "{v[32:63]}"(A), "{v[64:95]}"(B), "{v[96:127]}"(C),
+        "{v[128:159]}"(Dq)
+      : "scc");
+}
+
+// Column sums of a 64 x 64 block: p[k] holds, per lane, a partial count of job k; returns F with
+// F[l] = sum over all 64 lanes of p[sigma(l)] for a fixed permutation sigma of 0..63 (find it by
+// reducing a probe, p[k] = (lane == 0) ? k : 0).  Six halving levels, each pairing two registers
+// into one that carries both jobs on half the lanes: permlane32_swap (halves), permlane16_swap
+// (rows), then DPP row_ror:8, row_half_mirror, quad_perm [2,3,0,1], [1,0,3,2] with a lane select.
+// 141 VALU per 64 jobs, no dependent chains: 2.2 per job where a per-job wave sum costs ~12.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_pair(uint32_t x, uint32_t y, bool take_y) {
+  const uint32_t tx = x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+  const uint32_t ty = y + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)y, CTRL, 0xf, 0xf, false);
+  return take_y ? ty : tx;
+}
+
+__device__ __forceinline__ uint32_t reduce64x64(const uint32_t (&p)[64], int lane) {
+  uint32_t s1[32], s2[16], s3[8], s4[4], s5[2];
+#pragma unroll
+  for (int m = 0; m < 32; ++m) {
+    const auto r = __builtin_amdgcn_permlane32_swap(p[2 * m], p[2 * m + 1], false, false);
+    s1[m] = r[0] + r[1];
+  }
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const auto r = __builtin_amdgcn_permlane16_swap(s1[2 * m], s1[2 * m + 1], false, false);
+    s2[m] = r[0] + r[1];
+  }
+  const bool b8 = lane & 8, b4 = lane & 4, b2 = lane & 2, b1 = lane & 1;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) s3[m] = dpp_pair<0x128>(s2[2 * m], s2[2 * m + 1], b8);   // row_ror:8
+#pragma unroll
+  for (int m = 0; m < 4; ++m) s4[m] = dpp_pair<0x141>(s3[2 * m], s3[2 * m + 1], b4);   // row_half_mirror
+#pragma unroll
+  for (int m = 0; m < 2; ++m) s5[m] = dpp_pair<0x4e>(s4[2 * m], s4[2 * m + 1], b2);   // quad_perm [2,3,0,1]
+  return dpp_pair<0xb1>(s5[0], s5[1], b1);                                          // quad_perm [1,0,3,2]
+}
+
+// Jobs K .. 63 of a batch: select, store (row stride `step` u32x4), per-lane popcount into p[K].
+// `row` is wave-uniform (kept in SGPRs by the empty asm, which also stops the compiler from
+// precomputing 64 row offsets and spilling them); the store is row + lane.
+template <int K>
+__device__ __forceinline__ void rows_batch(uint32_t (&p)[64], uint32_t lo, uint32_t hi, const u32x32& A,
+                                           const u32x32& B, const u32x32& C, const u32x32& Dq, gu32x4* row,
+                                           int64_t step, uint32_t lane_off) {
+  u32x4 f;
+  plane_job<K>(f, lo, hi, A, B, C, Dq);
+  *(gu32x4*)((__attribute__((address_space(1))) char*)row + lane_off) = f;
+  p[K] = __popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w);
+  if constexpr (K + 1 < 64) {
+    row += step;
+    asm volatile("" : "+s"(row));
+    rows_batch<K + 1>(p, lo, hi, A, B, C, Dq, row, step, lane_off);
+  }
+}
+
+// Row-major variant: the same per-job select, but the grid is ONE resident wave per SIMD
+// (nblk x R waves, R job phases) and wave (blk, r) takes jobs r, r + R, r + 2R, ...  So at step i
+// every wave writes into rows iR .. iR + R - 1: the chip's stores in flight cover one contiguous
+// window of R x nblk KiB that sweeps the mask once, instead of ~2k independent streams (HBM takes
+// the sweep at ~6.5 TB/s and the streams at ~5.3: profiles/r5_write_patterns.txt).  With one wave
+// per SIMD nothing hides latency, so per 64 jobs: the codes come in one vector load issued a
+// batch ahead (read out with v_readlane), and the per-job counts are one 64 x 64 column-sum
+// (reduce64x64) instead of 64 dependent wave sums.  Mask layout row-major: u32 word w of row j at
+// j * row_words + w, row_words = nblk * 256.
+__global__ __launch_bounds__(256) void fit_mask_planes_rows_kernel(const uint32_t* __restrict__ planes, int64_t nblk,
+                                                                   const uint64_t* __restrict__ jcode, int64_t J,
+                                                                   int64_t R, int64_t Jr, uint32_t* __restrict__ mask,
+                                                                   unsigned long long* __restrict__ counts) {
+  static_assert(PL_MAX == 32 && PL_R == 4, "register map assumes 32 planes x 4 words");
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t blk = wave_id % nblk;
+  const int64_t r = wave_id / nblk;
+  if (r >= R || r >= J) return;
+  const u32x4* pb = reinterpret_cast<const u32x4*>(planes + blk * PL_MAX * (64 * PL_R)) + lane;
+  const u32x32 A = load_planes8(pb), B = load_planes8(pb + 8 * 64), C = load_planes8(pb + 16 * 64),
+               Dq = load_planes8(pb + 24 * 64);
+  const int64_t row_vec = nblk * 64;           // u32x4 per row
+  u32x4* const rows0 = reinterpret_cast<u32x4*>(mask) + blk * 64;   // this block's column, row 0
+  u32x4* out = rows0 + lane;
+  const uint64_t* jc = jcode + r * Jr;         // this phase's codes, contiguous
+  unsigned long long* cnt = counts + r * Jr;   // and its counts (the host un-permutes)
+  const int64_t ni = (J - r + R - 1) / R;      // jobs of this phase
+  uint32_t sigma;                              // lane l of a batch sum counts batch job sigma
+  {
+    uint32_t probe[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) probe[k] = lane == 0 ? (uint32_t)k : 0u;
+    sigma = reduce64x64(probe, lane);
+  }
+  int64_t i0 = 0;
+  uint64_t cv = ni >= 64 ? jc[lane] : 0;       // lane l: code of batch job l
+  for (; i0 + 64 <= ni; i0 += 64) {
+    const uint32_t lo = (uint32_t)cv, hi = (uint32_t)(cv >> 32);
+    if (i0 + 128 <= ni) cv = jc[i0 + 64 + lane];   // next batch, in flight during this one
+    uint32_t p[64];
+    rows_batch<0>(p, lo, hi, A, B, C, Dq, (gu32x4*)(rows0 + (r + i0 * R) * row_vec), R * row_vec,
+                       (uint32_t)lane * 16u);
+    const uint32_t F = reduce64x64(p, lane);
+    if (F) atomicAdd(&cnt[i0 + sigma], (unsigned long long)F);
+  }
+  uint32_t acc = 0;                            // tail (< 64 jobs): per-job wave sums
+  for (int64_t i = i0; i < ni; ++i) {
+    const uint64_t c = jc[i];
+    u32x4 f;
+    plane_sel(f, (uint32_t)c & 127, A, B, C, Dq);
+    plane_and(f, (uint32_t)(c >> 7) & 127, A, B, C, Dq);
+    plane_and(f, (uint32_t)(c >> 14) & 127, A, B, C, Dq);
+    plane_and(f, (uint32_t)(c >> 21) & 127, A, B, C, Dq);
+    plane_and(f, (uint32_t)(c >> 32) & 127, A, B, C, Dq);
+    *(gu32x4*)(out + (r + i * R) * row_vec) = f;
+    const uint32_t n = wave_sum(__popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w));
+    acc = writelane_s(acc, n, (uint32_t)(i - i0));
+  }
+  if (lane < ni - i0 && acc) atomicAdd(&cnt[i0 + lane], (unsigned long long)acc);
+}
+
+hipError_t launch_fit_mask_planes_rows(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
+                                       int64_t J, int64_t R, uint32_t* mask, unsigned long long* counts) {
+  if (J <= 0 || nblk <= 0 || R <= 0) return hipSuccess;
+  const int64_t Jr = ((J + R - 1) / R + 3) / 4 * 4;   // phase stride (the engine pads codes alike)
+  const int64_t waves = nblk * R;
+  hipLaunchKernelGGL(fit_mask_planes_rows_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, planes, nblk,
+                     jcode, J, R, Jr, mask, counts);
+  return hipGetLastError();
 }
 
 hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
