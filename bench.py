@@ -120,6 +120,7 @@ def main():
     ap.add_argument("--window-pods", type=int, default=0)
     ap.add_argument("--no-greedy", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the cfg2-4 greedy lines")
     ap.add_argument("--cpu-sample-jobs", type=int, default=20000)
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: batch = fit-jobs x n_gpus (fixed per-rank work); strong: batch = fit-jobs")
@@ -150,9 +151,16 @@ def main():
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
             tdev = "cuda"
+
+        def new_comm():
+            """A fresh RCCL unique id per engine (an id bootstraps exactly one communicator)."""
+            if host_exchange:
+                return None
             ids = [comm_id() if rank == 0 else None]
             dist.broadcast_object_list(ids, src=0)
-            cid = ids[0]
+            return ids[0]
+
+        cid = new_comm()
 
         def barrier():
             dist.barrier()
@@ -167,6 +175,9 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
             return int(t.item())
     else:
+        def new_comm():
+            return None
+
         def barrier():
             pass
 
@@ -265,6 +276,37 @@ def main():
                          "device_wait_ms_per_batch": s["greedy_wait_ms"] / (args.greedy_steps + 1),
                          "host_resolve_ms_per_batch": s["greedy_host_ms"] / (args.greedy_steps + 1),
                          "naive_pod_x_node_evals_per_s": batch.n_pods * float(N) / gt}
+
+    if not args.no_configs:
+        # BASELINE.json configs 2-4 at their own sizes (greedy best-fit, all-or-nothing); every rank
+        # holds its shard of each inventory and makes the same calls
+        out["configs"] = {}
+        for cfg, mix, n_nodes, n_jobs, gpu_frac, what in (
+                ("cfg2", "pytorch", 10_000, 1_000, 0.2, "10k nodes x 1k PyTorchJobs (Master 1 + Worker 0-15)"),
+                ("cfg3", "mixed", 100_000, 10_000, 0.2, "100k nodes x 10k jobs, 50% PyTorch / 25% MPI / 25% JAX"),
+                ("cfg4", "gang8", 100_000, 10_000, 1.0,
+                 "100k 8-GPU nodes x 10k gangs of 1-16 pods x 8 GPUs, label-constrained, all-or-nothing")):
+            cinv = synth.make_inventory(n_nodes, synth.SEED[cfg], gpu_frac)
+            cb = synth.make_jobs(n_jobs, synth.SEED[cfg], mix)
+            ce = Engine(device, rank=rank, world_size=world, comm=new_comm(), exchange=exchange, max_nodes=n_nodes)
+            ce.load_nodes(cinv.cap, cinv.used, cinv.labels, cinv.island)
+            ce.place_batch(cb)                       # warm-up
+            ts = []
+            for _ in range(3):
+                ce.reset_residuals()
+                ce.synchronize()
+                barrier()
+                g0 = time.perf_counter()
+                _, cst = ce.place_batch(cb)
+                barrier()
+                ts.append(allmax(time.perf_counter() - g0))
+            ct = float(np.median(ts))
+            cs = ce.stats()
+            out["configs"][cfg] = {"workload": what, "nodes": n_nodes, "jobs": n_jobs, "pods": cb.n_pods,
+                                   "jobs_placed": int((cst == 0).sum()), "gang_placements_per_s": n_jobs / ct,
+                                   "ms_per_batch": ct * 1e3, "windows_per_batch": cs["windows"] / 4.0,
+                                   "group_x_node_evals_per_s": cs["scan_evals"] / 4.0 * world / ct}
+            ce.close()
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle
