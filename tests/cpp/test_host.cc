@@ -85,6 +85,84 @@ TEST_CPU(TestQuantityParse) {
   CHECK(Quantity::FromCanonical("memory", 404LL << 30).String() == "404Gi");
 }
 
+
+// apimachinery quantity.go String() (CanonicalizeBytes): canonical print forms
+TEST_CPU(TestQuantityString) {
+  struct {
+    const char *in, *want;
+  } tcs[] = {{"0", "0"},           {"1", "1"},          {"1000m", "1"},        {"100m", "100m"},
+             {"0.5", "500m"},      {"1.5", "1500m"},    {"0.1", "100m"},       {"10m", "10m"},
+             {"1n", "1n"},         {"5u", "5u"},        {"1000", "1k"},        {"1000M", "1G"},
+             {"12345", "12345"},   {"12.345", "12345m"}, {"1e3", "1e3"},       {"129e6", "129e6"},
+             {"1.5e3", "1500"},    {"1Gi", "1Gi"},      {"1024Mi", "1Gi"},     {"1.5Gi", "1536Mi"},
+             {"1536Ki", "1536Ki"}, {"2000Mi", "2000Mi"}, {"0.5Ki", "512"},     {"1Ki", "1Ki"},
+             {"100Ki", "100Ki"},   {"1E", "1E"},        {"2k", "2k"},          {"8Gi", "8Gi"}};
+  for (auto& tc : tcs) {
+    const std::string got = Quantity::Parse(tc.in).String();
+    if (got != tc.want) std::fprintf(stderr, "  %s -> %s (want %s)\n", tc.in, got.c_str(), tc.want);
+    CHECK(got == tc.want);
+  }
+  CHECK(Quantity::Parse("4Gi").format() == Format::kBinarySI);
+  CHECK(Quantity::Parse("1e3").format() == Format::kDecimalExponent);
+  CHECK(Quantity::Parse("1E").format() == Format::kDecimalSI);
+  CHECK(Quantity::FromCanonical("memory", 404LL << 30, Format::kBinarySI).String() == "404Gi");
+  CHECK(Quantity::FromCanonical("cpu", 101000, Format::kDecimalSI).String() == "101");
+  CHECK(Quantity::FromCanonical("cpu", 1600).String() == "1600m");
+  // DecimalSI memory that is not a multiple of 1000: plain digits
+  CHECK(Quantity::FromCanonical("memory", 1000000000LL + (1LL << 30), Format::kDecimalSI).String() == "2073741824");
+}
+
+// util.go:79-104 AddResourceList + quantity.go Add: the first nonzero contribution's format wins
+TEST_CPU(TestMinResourcesFormatsV1) {
+  ReplicaSpec m, w;
+  m.replicas = 1;
+  m.template_spec.containers = {Ctr(RL({{"memory", "0"}, {"cpu", "500m"}}))};
+  w.replicas = 3;
+  w.template_spec.containers = {Ctr(RL({{"memory", "2Gi"}, {"cpu", "1"}}))};
+  auto f = MinResourcesFormatsV1(4, {{"Master", m}, {"Worker", w}}, kNoPC);
+  CHECK(f.at("memory") == Format::kBinarySI);   // Master's 0 (DecimalSI) adopts Worker's BinarySI
+  CHECK(f.at("cpu") == Format::kDecimalSI);
+  // a type that counts no pod contributes no format
+  ReplicaSpec e;
+  e.replicas = 2;
+  e.template_spec.containers = {Ctr(RL({{"memory", "1e9"}}))};
+  auto g = MinResourcesFormatsV1(1, {{"A", w}, {"B", e}}, kNoPC);
+  CHECK(g.at("memory") == Format::kBinarySI && g.size() == 2);
+  auto h = MinResourcesFormatsV1(4, {{"A", w}, {"B", e}}, kNoPC);   // A's 3 pods, then one B pod
+  CHECK(h.at("memory") == Format::kBinarySI);
+}
+
+// Go JSON of the objects the operator sends (field order of the Go types, omitempty, sorted maps)
+TEST_CPU(TestPodGroupJSON) {
+  PodGroup pg;
+  pg.name = "mnist";
+  pg.ns = "kubeflow";
+  pg.min_member = 2;
+  pg.min_resources = {{"nvidia.com/gpu", Quantity::FromCanonical("nvidia.com/gpu", 2, Format::kDecimalSI)}};
+  pg.owner_api_version = "kubeflow.org/v1";
+  pg.owner_kind = "PyTorchJob";
+  pg.owner_name = "mnist";
+  pg.owner_uid = "u-1";
+  pg.annotations = {{"b", "x<y"}, {"a", "q\"r"}};
+  const std::string want_sp =
+      "{\"kind\":\"PodGroup\",\"apiVersion\":\"scheduling.x-k8s.io/v1alpha1\",\"metadata\":{\"name\":\"mnist\","
+      "\"namespace\":\"kubeflow\",\"creationTimestamp\":null,\"annotations\":{\"a\":\"q\\\"r\",\"b\":\"x\\u003cy\"},"
+      "\"ownerReferences\":[{\"apiVersion\":\"kubeflow.org/v1\",\"kind\":\"PyTorchJob\",\"name\":\"mnist\",\"uid\":\"u-1\","
+      "\"controller\":true,\"blockOwnerDeletion\":true}]},\"spec\":{\"minMember\":2,\"minResources\":{\"nvidia.com/gpu\":\"2\"}},"
+      "\"status\":{\"scheduleStartTime\":null}}";
+  CHECK(PodGroupJSON(pg) == want_sp);
+  pg.flavour = GangScheduler::kVolcano;
+  pg.queue = "default";
+  pg.annotations.clear();
+  pg.min_resources.clear();
+  const std::string want_v =
+      "{\"kind\":\"PodGroup\",\"apiVersion\":\"scheduling.volcano.sh/v1beta1\",\"metadata\":{\"name\":\"mnist\","
+      "\"namespace\":\"kubeflow\",\"creationTimestamp\":null,\"ownerReferences\":[{\"apiVersion\":\"kubeflow.org/v1\","
+      "\"kind\":\"PyTorchJob\",\"name\":\"mnist\",\"uid\":\"u-1\",\"controller\":true,\"blockOwnerDeletion\":true}]},"
+      "\"spec\":{\"minMember\":2,\"queue\":\"default\",\"minResources\":{}},\"status\":{}}";
+  CHECK(PodGroupJSON(pg) == want_v);
+}
+
 // ------------------------------------------------------------------ CPU: flattening (host logic)
 
 static std::map<ReplicaType, ReplicaSpec> mnist(int workers) {
@@ -310,6 +388,59 @@ TEST_GPU(TestRunComponentBuilderPlugins) {
   CHECK(r.object && r.object->min_member == 101);
   CHECK(EqualResourceList(r.object->min_resources, RL({{"cpu", "101"}, {"memory", "404Gi"}})));
   CHECK(r.object->schedule_timeout_seconds == 300);
+}
+
+// job.go:250-313 + scheduling.go:32-73 through the GPU aggregation, both PodGroup flavours
+TEST_GPU(TestSyncPodGroupV1) {
+  JobMeta job;
+  job.name = "pytorch-dist-mnist-nccl";
+  job.ns = "kubeflow";
+  job.uid = "uid-1";
+  auto c = SyncPodGroupV1(eng(), GangScheduler::kSchedulerPlugins, job, mnist(1), nullptr, kNoPC, nullptr);
+  CHECK(c.action == SyncPodGroupResult::kCreate && c.object.min_member == 2);
+  CHECK(c.object.min_resources.at("nvidia.com/gpu").String() == "2");
+  const std::string js = PodGroupJSON(c.object);
+  CHECK(js.find("\"spec\":{\"minMember\":2,\"minResources\":{\"nvidia.com/gpu\":\"2\"}}") != std::string::npos);
+  CHECK(js.find("\"ownerReferences\":[{\"apiVersion\":\"kubeflow.org/v1\",\"kind\":\"PyTorchJob\"") != std::string::npos);
+  // Volcano: queue / priorityClass from the SchedulingPolicy, no timeout field
+  SchedulingPolicy pol;
+  pol.queue = "q1";
+  pol.priority_class = "high";
+  pol.schedule_timeout_seconds = 30;
+  auto v = SyncPodGroupV1(eng(), GangScheduler::kVolcano, job, mnist(3), &pol, kNoPC, nullptr);
+  CHECK(v.object.queue == "q1" && v.object.priority_class_name == "high" && !v.object.schedule_timeout_seconds);
+  CHECK(PodGroupJSON(v.object).find("\"spec\":{\"minMember\":4,\"queue\":\"q1\",\"priorityClassName\":\"high\","
+                                    "\"minResources\":{\"nvidia.com/gpu\":\"4\"}}") != std::string::npos);
+  // existing Volcano PodGroup keeps its queue; an existing object is always updated
+  PodGroup old = v.object;
+  old.queue = "keep";
+  auto u = SyncPodGroupV1(eng(), GangScheduler::kVolcano, job, mnist(3), &pol, kNoPC, &old);
+  CHECK(u.action == SyncPodGroupResult::kUpdate && u.object.queue == "keep");
+  auto same = SyncPodGroupV1(eng(), GangScheduler::kVolcano, job, mnist(3), &pol, kNoPC, &u.object);
+  CHECK(same.action == SyncPodGroupResult::kUpdate);
+  // MinResources given: used verbatim (job.go:267-269), printed as given
+  pol.min_resources = RL({{"cpu", "1500m"}, {"memory", "1024Mi"}});
+  auto g = SyncPodGroupV1(eng(), GangScheduler::kSchedulerPlugins, job, mnist(1), &pol, kNoPC, nullptr);
+  CHECK(PodGroupJSON(g.object).find("\"minResources\":{\"cpu\":\"1500m\",\"memory\":\"1Gi\"},\"scheduleTimeoutSeconds\":30") !=
+        std::string::npos);
+  // mixed formats: DecimalSI first nonzero wins; 1G + 1Gi prints as plain digits
+  ReplicaSpec a, b;
+  a.replicas = 1;
+  a.template_spec.containers = {Ctr(RL({{"memory", "1G"}}))};
+  b.replicas = 1;
+  b.template_spec.containers = {Ctr(RL({{"memory", "1Gi"}}))};
+  auto mix = CalcPGMinResources(eng(), 2, {{"A", a}, {"B", b}}, kNoPC);
+  CHECK(mix.at("memory").String() == "2073741824");
+}
+
+// framework_test.go:398-486 pin (101 CPU, 404Gi, timeout 300) as the wire object
+TEST_GPU(TestBuildWireV2) {
+  auto r = RunBuild(RL({{"cpu", "1"}, {"memory", "4Gi"}}), 100, std::nullopt, 300, false);
+  CHECK(r.object);
+  const std::string js = PodGroupJSON(*r.object);
+  CHECK(js.find("\"spec\":{\"minMember\":101,\"minResources\":{\"cpu\":\"101\",\"memory\":\"404Gi\"},"
+                "\"scheduleTimeoutSeconds\":300}") != std::string::npos);
+  CHECK(js.find("\"apiVersion\":\"kubeflow.org/v2alpha1\",\"kind\":\"TrainJob\"") != std::string::npos);
 }
 
 TEST_GPU(TestBuildNilPolicyAndExistingPodGroup) {

@@ -31,5 +31,5 @@ def test_host_mirror_cpu_cases():
 def test_host_mirror_gpu_cases():
     out = run("--gpu")
     for name in ("TestNewInfo", "TestTrainingRuntimeNewObjects", "TestIntegrationPodGroup", "TestCalcPGMinResourcesMnist",
-                 "TestNodeInventoryInformer"):
+                 "TestNodeInventoryInformer", "TestSyncPodGroupV1", "TestBuildWireV2"):
         assert "ok   " + name in out

@@ -163,13 +163,38 @@ static AggOut run_agg(Engine& eng, int mode, const Flat& f) {
   return o;
 }
 
-static ResourceList to_list(const Dims& eng, const AggOut& o, int64_t j) {
+static ResourceList to_list(const Dims& eng, const AggOut& o, int64_t j,
+                            const std::map<std::string, Format>* formats = nullptr) {
   if (o.overflow[j]) throw Error{PE_EOVERFLOW, "int64 overflow: the reference would switch to inf.Dec"};
   ResourceList rl;
-  for (int d = 0; d < PE_DIMS; ++d)
-    if (o.present[j] & (1u << d)) rl[eng.name_of(d)] = Quantity::FromCanonical(eng.name_of(d), o.res[j * PE_DIMS + d]);
+  for (int d = 0; d < PE_DIMS; ++d) {
+    if (!(o.present[j] & (1u << d))) continue;
+    const std::string key = eng.name_of(d);
+    const auto f = formats ? formats->find(key) : std::map<std::string, Format>::const_iterator{};
+    rl[key] = formats && f != formats->end() ? Quantity::FromCanonical(key, o.res[j * PE_DIMS + d], f->second)
+                                             : Quantity::FromCanonical(key, o.res[j * PE_DIMS + d]);
+  }
   return rl;
 }
+
+// Quantity.Add's format rule (quantity.go Add: `if q.i.value == 0 { q.Format = y.Format }`, and the
+// same for the inf.Dec branch): the running sum adopts the addend's format while it is still 0.
+struct FormatAcc {
+  std::map<std::string, Format> fmt;
+  std::map<std::string, bool> nonzero;
+  void add(const std::string& key, const Quantity& q, bool first_copies) {
+    auto it = fmt.find(key);
+    if (it == fmt.end()) {
+      // AddResourceList deep-copies the first quantity; Build's zero Quantity{} adopts it on Add
+      fmt[key] = q.format();
+      nonzero[key] = !q.IsZero();
+      (void)first_copies;
+      return;
+    }
+    if (!nonzero[key]) it->second = q.format();
+    if (!q.IsZero()) nonzero[key] = true;
+  }
+};
 
 // ------------------------------------------------------------------ v1
 
@@ -179,11 +204,34 @@ int32_t GetTotalReplicas(const std::map<ReplicaType, ReplicaSpec>& replicas) {
   return total;
 }
 
+std::map<std::string, Format> MinResourcesFormatsV1(int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
+                                                    const PriorityClassGetFunc& pcGetFunc) {
+  // util.go:126-141 walk: only counted pods add, pods of one type are identical, so one pass per
+  // type that counts at least one pod gives the same first-nonzero / last-zero answer
+  FormatAcc acc;
+  int64_t pod_cnt = 0;
+  for (const ReplicaType& t : v1_order(replicas, pcGetFunc)) {
+    const ReplicaSpec& spec = replicas.at(t);
+    if (!spec.replicas) continue;
+    const int64_t k = std::min<int64_t>(*spec.replicas, std::max<int64_t>(0, (int64_t)minMember - pod_cnt));
+    if (k <= 0) continue;
+    pod_cnt += k;
+    for (int64_t pod = 0; pod < std::min<int64_t>(k, 2); ++pod)   // a 2nd pod only re-adds the same formats
+      for (const Container& c : spec.template_spec.containers) {
+        const ResourceList* rl = c.requests ? &*c.requests : (c.limits ? &*c.limits : nullptr);
+        if (rl)
+          for (const auto& kv : *rl) acc.add(kv.first, kv.second, true);
+      }
+  }
+  return acc.fmt;
+}
+
 ResourceList CalcPGMinResources(Engine& eng, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
                                 const PriorityClassGetFunc& pcGetFunc) {
   Flat f;
   FlattenV1Job(eng.dims(), minMember, replicas, pcGetFunc, &f);
-  return to_list(eng.dims(), run_agg(eng, PE_MODE_V1, f), 0);
+  const auto formats = MinResourcesFormatsV1(minMember, replicas, pcGetFunc);
+  return to_list(eng.dims(), run_agg(eng, PE_MODE_V1, f), 0, &formats);
 }
 
 std::vector<ResourceList> CalcPGMinResourcesBatch(Engine& eng, const std::vector<V1Job>& jobs,
@@ -192,7 +240,10 @@ std::vector<ResourceList> CalcPGMinResourcesBatch(Engine& eng, const std::vector
   for (const V1Job& j : jobs) FlattenV1Job(eng.dims(), j.min_member, j.replicas, pcGetFunc, &f);
   AggOut o = run_agg(eng, PE_MODE_V1, f);
   std::vector<ResourceList> out;
-  for (size_t j = 0; j < jobs.size(); ++j) out.push_back(to_list(eng.dims(), o, (int64_t)j));
+  for (size_t j = 0; j < jobs.size(); ++j) {
+    const auto formats = MinResourcesFormatsV1(jobs[j].min_member, jobs[j].replicas, pcGetFunc);
+    out.push_back(to_list(eng.dims(), o, (int64_t)j, &formats));
+  }
   return out;
 }
 
@@ -223,7 +274,20 @@ Info NewInfo(Engine& eng, const InfoOptions& opts) {
   AggOut o = run_agg(eng, PE_MODE_V2, f);
   for (size_t i = 0; i < opts.pod_spec_replicas.size(); ++i) {
     const PodSpecReplica& r = opts.pod_spec_replicas[i];
-    info.scheduler.total_requests[r.name] = TotalResourceRequest{r.replicas, to_list(eng.dims(), o, (int64_t)i)};
+    // Print formats through kueue's merges (containers, then sidecar / init containers, then
+    // overhead, by the Add rule).  kueue v0.6.3 is not in the container: this order is an
+    // assumption ("parity unpinned"); the values are exact either way.
+    FormatAcc acc;
+    for (const Container& c : r.pod_spec.containers)
+      if (c.requests)
+        for (const auto& kv : *c.requests) acc.add(kv.first, kv.second, true);
+    for (const Container& c : r.pod_spec.init_containers)
+      if (c.requests)
+        for (const auto& kv : *c.requests) acc.add(kv.first, kv.second, true);
+    if (r.pod_spec.overhead)
+      for (const auto& kv : *r.pod_spec.overhead) acc.add(kv.first, kv.second, true);
+    info.scheduler.total_requests[r.name] =
+        TotalResourceRequest{r.replicas, to_list(eng.dims(), o, (int64_t)i, &acc.fmt)};
   }
   return info;
 }
@@ -300,8 +364,24 @@ std::vector<CoScheduling::BuildResult> CoScheduling::BuildBatch(const std::vecto
       out[i].error = e;
       continue;
     }
+    // print formats: totalResources[k] starts as a zero Quantity{} and Adds quantity * replicas
+    // (coscheduling.go:110-116); Go ranges TotalRequests in map order (random), we in name order
+    FormatAcc acc;
+    for (const auto& kv : infos[i]->scheduler.total_requests)
+      for (const auto& q : kv.second.pod_requests) {
+        Quantity scaled = q.second.IsZero() || kv.second.replicas == 0
+                              ? Quantity::FromCanonical(q.first, 0, q.second.format())
+                              : q.second;
+        acc.add(q.first, scaled, false);
+      }
+    for (auto& kv : pg.min_resources) {
+      auto f = acc.fmt.find(kv.first);
+      if (f != acc.fmt.end())
+        kv.second = Quantity::FromCanonical(kv.first, kv.second.Canonical(kv.first), f->second);
+    }
     pg.schedule_timeout_seconds = infos[i]->runtime_policy.pod_group_policy->coscheduling->schedule_timeout_seconds;
-    pg.owner_kind = "TrainJob";  // SetControllerReference (coscheduling.go:134)
+    pg.owner_api_version = "kubeflow.org/v2alpha1";   // SetControllerReference (coscheduling.go:134)
+    pg.owner_kind = "TrainJob";
     pg.owner_name = trainJobs[i]->name;
     pg.owner_uid = trainJobs[i]->uid;
     if (NeedsCreateOrUpdate(existing.empty() ? nullptr : existing[i], pg, trainJobs[i]->suspend)) out[i].object = pg;
@@ -311,6 +391,180 @@ std::vector<CoScheduling::BuildResult> CoScheduling::BuildBatch(const std::vecto
 
 CoScheduling::BuildResult CoScheduling::Build(const Info* info, const TrainJob* trainJob, const PodGroup* existing) {
   return BuildBatch({info}, {trainJob}, {existing})[0];
+}
+
+// ------------------------------------------------------------------ v1 SyncPodGroup (8f row 1)
+
+SyncPodGroupResult SyncPodGroupV1(Engine& eng, GangScheduler flavour, const JobMeta& job,
+                                  const std::map<ReplicaType, ReplicaSpec>& replicas, const SchedulingPolicy* policy,
+                                  const PriorityClassGetFunc& pcGetFunc, const PodGroup* existing) {
+  // job.go:251-277
+  int32_t min_member = GetTotalReplicas(replicas);
+  std::string queue = "default", priority_class;
+  std::optional<int32_t> timeout;
+  std::optional<ResourceList> min_resources;
+  if (policy) {
+    if (policy->min_available) min_member = *policy->min_available;
+    if (!policy->queue.empty()) queue = policy->queue;
+    if (!policy->priority_class.empty()) priority_class = policy->priority_class;
+    if (policy->min_resources) min_resources = *policy->min_resources;
+    if (policy->schedule_timeout_seconds) timeout = policy->schedule_timeout_seconds;
+  }
+  if (!min_resources) min_resources = CalcPGMinResources(eng, min_member, replicas, pcGetFunc);
+
+  SyncPodGroupResult r;
+  if (existing) {
+    r.action = SyncPodGroupResult::kUpdate;   // scheduling.go:38-44: the cmp.Diff never matches
+    r.object = *existing;
+  } else {
+    r.action = SyncPodGroupResult::kCreate;   // scheduling.go:49-56
+    r.object = PodGroup{};
+    r.object.name = job.name;
+    r.object.ns = job.ns;
+    r.object.annotations = job.annotations;
+    r.object.owner_api_version = job.api_version;
+    r.object.owner_kind = job.kind;
+    r.object.owner_name = job.name;
+    r.object.owner_uid = job.uid;
+  }
+  PodGroup& pg = r.object;
+  pg.flavour = flavour;
+  // the fill replaces the whole Spec (job.go:291-297, 306-310)
+  pg.min_member = min_member;
+  pg.min_resources = *min_resources;
+  if (flavour == GangScheduler::kVolcano) {
+    if (!pg.queue.empty()) queue = pg.queue;   // job.go:287-289: the object's queue wins
+    pg.queue = queue;
+    pg.priority_class_name = priority_class;
+    pg.schedule_timeout_seconds.reset();
+  } else {
+    pg.schedule_timeout_seconds = timeout;
+    pg.queue.clear();
+    pg.priority_class_name.clear();
+  }
+  return r;
+}
+
+// ------------------------------------------------------------------ PodGroup JSON (8f row 1)
+
+static void json_str(std::string& o, const std::string& s) {
+  // encoding/json: HTML-safe escaping by default (<, >, & as \u00XX), \n \r \t, other controls \u00XX
+  static const char* hex = "0123456789abcdef";
+  o.push_back('"');
+  for (size_t i = 0; i < s.size(); ++i) {
+    const unsigned char c = (unsigned char)s[i];
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\n': o += "\\n"; break;
+      case '\r': o += "\\r"; break;
+      case '\t': o += "\\t"; break;
+      default:
+        if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+          o += "\\u00";
+          o.push_back(hex[c >> 4]);
+          o.push_back(hex[c & 15]);
+        } else if (c == 0xE2 && i + 2 < s.size() && (unsigned char)s[i + 1] == 0x80 &&
+                   ((unsigned char)s[i + 2] == 0xA8 || (unsigned char)s[i + 2] == 0xA9)) {
+          o += (unsigned char)s[i + 2] == 0xA8 ? "\\u2028" : "\\u2029";   // U+2028 / U+2029
+          i += 2;
+        } else {
+          o.push_back((char)c);
+        }
+    }
+  }
+  o.push_back('"');
+}
+
+static void json_map(std::string& o, const std::map<std::string, std::string>& m) {
+  o.push_back('{');
+  bool first = true;
+  for (const auto& kv : m) {   // Go sorts map keys
+    if (!first) o.push_back(',');
+    first = false;
+    json_str(o, kv.first);
+    o.push_back(':');
+    json_str(o, kv.second);
+  }
+  o.push_back('}');
+}
+
+static void json_resources(std::string& o, const ResourceList& rl) {
+  std::map<std::string, std::string> m;
+  for (const auto& kv : rl) m[kv.first] = kv.second.String();
+  json_map(o, m);
+}
+
+std::string PodGroupJSON(const PodGroup& pg) {
+  const bool volcano = pg.flavour == GangScheduler::kVolcano;
+  std::string o = "{\"kind\":\"PodGroup\",\"apiVersion\":";
+  json_str(o, volcano ? "scheduling.volcano.sh/v1beta1" : "scheduling.x-k8s.io/v1alpha1");
+  // metav1.ObjectMeta, declaration order; creationTimestamp is a struct (omitempty never drops it)
+  o += ",\"metadata\":{\"name\":";
+  json_str(o, pg.name);
+  if (!pg.ns.empty()) {
+    o += ",\"namespace\":";
+    json_str(o, pg.ns);
+  }
+  o += ",\"creationTimestamp\":null";
+  if (!pg.labels.empty()) {
+    o += ",\"labels\":";
+    json_map(o, pg.labels);
+  }
+  if (!pg.annotations.empty()) {
+    o += ",\"annotations\":";
+    json_map(o, pg.annotations);
+  }
+  if (!pg.owner_kind.empty()) {
+    o += ",\"ownerReferences\":[{\"apiVersion\":";
+    json_str(o, pg.owner_api_version);
+    o += ",\"kind\":";
+    json_str(o, pg.owner_kind);
+    o += ",\"name\":";
+    json_str(o, pg.owner_name);
+    o += ",\"uid\":";
+    json_str(o, pg.owner_uid);
+    o += ",\"controller\":true,\"blockOwnerDeletion\":true}]";
+  }
+  o += "},\"spec\":{";
+  std::string spec;
+  auto field = [&](const char* name) {
+    if (!spec.empty()) spec.push_back(',');
+    spec += "\"";
+    spec += name;
+    spec += "\":";
+  };
+  if (pg.min_member != 0) {   // int32 omitempty
+    field("minMember");
+    spec += std::to_string(pg.min_member);
+  }
+  if (volcano) {
+    // v1beta1.PodGroupSpec: minMember, minTaskMember, queue, priorityClassName, minResources (*ResourceList)
+    if (!pg.queue.empty()) {
+      field("queue");
+      json_str(spec, pg.queue);
+    }
+    if (!pg.priority_class_name.empty()) {
+      field("priorityClassName");
+      json_str(spec, pg.priority_class_name);
+    }
+    field("minResources");   // a non-nil pointer: written even when the list is empty
+    json_resources(spec, pg.min_resources);
+  } else {
+    // v1alpha1.PodGroupSpec: minMember, minResources (map, omitempty), scheduleTimeoutSeconds (*int32)
+    if (!pg.min_resources.empty()) {
+      field("minResources");
+      json_resources(spec, pg.min_resources);
+    }
+    if (pg.schedule_timeout_seconds) {
+      field("scheduleTimeoutSeconds");
+      spec += std::to_string(*pg.schedule_timeout_seconds);
+    }
+  }
+  o += spec;
+  // status of a new object: every field omitempty except scheduler-plugins' scheduleStartTime (metav1.Time)
+  o += volcano ? "},\"status\":{}}" : "},\"status\":{\"scheduleStartTime\":null}}";
+  return o;
 }
 
 // ------------------------------------------------------------------ node inventory

@@ -103,15 +103,30 @@ struct Info {
   } scheduler;
 };
 
-// scheduler-plugins v1alpha1 PodGroup (the fields coscheduling.go:119-133 sets)
+// Which PodGroup API the operator writes: --gang-scheduler-name (pkg/controller.v1/common/
+// job_controller.go GangSchedulerVolcano / scheduler-plugins default; v2 always scheduler-plugins)
+enum class GangScheduler { kSchedulerPlugins, kVolcano };
+
+// The PodGroup the operator creates: scheduler-plugins v1alpha1 (the fields coscheduling.go:119-133
+// and job.go:302-310 set) or Volcano v1beta1 (job.go:285-299: queue, priorityClassName, minResources
+// as a pointer).  The owner reference is the job's controller reference
+// (job_controller.go:221-233 GenOwnerReference / ctrlutil.SetControllerReference): controller and
+// blockOwnerDeletion true.
 struct PodGroup {
+  GangScheduler flavour = GangScheduler::kSchedulerPlugins;
   std::string name, ns;
   int32_t min_member = 0;
   ResourceList min_resources;
-  std::optional<int32_t> schedule_timeout_seconds;
+  std::optional<int32_t> schedule_timeout_seconds;   // scheduler-plugins only
+  std::string queue, priority_class_name;            // Volcano only
   std::map<std::string, std::string> labels, annotations;
-  std::string owner_kind, owner_name, owner_uid;
+  std::string owner_api_version, owner_kind, owner_name, owner_uid;
 };
+
+// The object as the operator's client sends it to the API server: Go's JSON encoding of the
+// scheduler-plugins / Volcano PodGroup types (struct field order, omitempty, map keys sorted,
+// quantities through Quantity.String(), metav1.Time zero values as null).  SURVEY 8f row 1.
+std::string PodGroupJSON(const PodGroup& pg);
 
 // ------------------------------------------------------------------ engine handle
 
@@ -165,6 +180,35 @@ struct PodGroupSpecV1 {
 };
 PodGroupSpecV1 CalcPodGroupSpecV1(Engine& eng, const std::map<ReplicaType, ReplicaSpec>& replicas,
                                   const SchedulingPolicy* policy, const PriorityClassGetFunc& pcGetFunc);
+
+// Print format of each MinResources key as Go's AddResourceList leaves it (util.go:79-104): a new
+// key deep-copies the first quantity, Quantity.Add adopts the addend's format while the running
+// value is 0 -- so a key prints in the format of its first nonzero contribution (all zero: the
+// last one).  Host-side metadata only; the values come from the GPU.
+std::map<std::string, Format> MinResourcesFormatsV1(int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
+                                                    const PriorityClassGetFunc& pcGetFunc);
+
+// v1 gang branch + SyncPodGroup (job.go:250-313, scheduling.go:32-73): the PodGroup the job
+// controller creates or updates for one job.
+struct JobMeta {
+  std::string name, ns, uid;
+  std::string api_version = "kubeflow.org/v1", kind = "PyTorchJob";
+  std::map<std::string, std::string> annotations;
+};
+struct SyncPodGroupResult {
+  enum Action { kCreate, kUpdate } action;
+  PodGroup object;
+};
+// existing = the PodGroup GetPodGroup returned (nullptr = NotFound).  A new PodGroup takes the
+// job's name, namespace, annotations and controller reference.  For an existing one the spec is
+// refilled in place and the result is ALWAYS kUpdate: SyncPodGroup compares `&podGroup` (a
+// *metav1.Object) with `podGroup` (a metav1.Object) through cmp.Diff, which never reports equal
+// (scheduling.go:38-44) -- reproduced.  Volcano keeps a non-empty queue already on the object
+// (job.go:287-289).  MinResources: SchedulingPolicy.MinResources verbatim, else
+// CalcPGMinResources on the GPU, printed in MinResourcesFormatsV1's formats.
+SyncPodGroupResult SyncPodGroupV1(Engine& eng, GangScheduler flavour, const JobMeta& job,
+                                  const std::map<ReplicaType, ReplicaSpec>& replicas, const SchedulingPolicy* policy,
+                                  const PriorityClassGetFunc& pcGetFunc, const PodGroup* existing);
 
 // ------------------------------------------------------------------ v2
 

@@ -92,7 +92,9 @@ Quantity Quantity::Parse(const std::string& s0) {
   q.mant_ = neg ? -mant : mant;
   q.e10_ = e10 - frac;
   q.e2_ = e2;
-  q.text_ = s0;
+  const std::string suf = s.substr(i);
+  q.format_ = e2 ? Format::kBinarySI
+                 : (suf.size() >= 2 && (suf[0] == 'e' || suf[0] == 'E')) ? Format::kDecimalExponent : Format::kDecimalSI;
   return q;
 }
 
@@ -117,21 +119,14 @@ int64_t Quantity::Canonical(const std::string& resource) const {
 }
 
 Quantity Quantity::FromCanonical(const std::string& resource, int64_t v) {
+  return FromCanonical(resource, v, resource == "cpu" ? Format::kDecimalSI : Format::kBinarySI);
+}
+
+Quantity Quantity::FromCanonical(const std::string& resource, int64_t v, Format f) {
   Quantity q;
   q.mant_ = v;
   q.e10_ = resource == "cpu" ? -3 : 0;
-  if (resource == "cpu") {
-    q.text_ = (v % 1000 == 0) ? std::to_string(v / 1000) : std::to_string(v) + "m";
-  } else {
-    static const char* suf[] = {"", "Ki", "Mi", "Gi", "Ti", "Pi", "Ei"};
-    int k = 0;
-    int64_t m = v;
-    while (m != 0 && k < 6 && m % 1024 == 0) {
-      m /= 1024;
-      ++k;
-    }
-    q.text_ = std::to_string(m) + suf[k];
-  }
+  q.format_ = f;
   return q;
 }
 
@@ -143,9 +138,71 @@ bool Quantity::Equal(const Quantity& o) const {
   return m1 == m2 && a1 == a2 && b1 == b2;
 }
 
+static std::string i128_str(__int128 x) {
+  if (x == 0) return "0";
+  const bool neg = x < 0;
+  std::string s;
+  for (; x != 0; x /= 10) s.push_back((char)('0' + (int)(neg ? -(x % 10) : x % 10)));
+  if (neg) s.push_back('-');
+  return std::string(s.rbegin(), s.rend());
+}
+
 std::string Quantity::String() const {
-  if (!text_.empty()) return text_;
-  return "0";
+  // quantity.go CanonicalizeBytes (apimachinery v0.30.7), restated for the exact value
+  // mant * 10^e10 * 2^e2 (e2 >= 0).
+  if (mant_ == 0) return "0";
+  __int128 a = mant_;                          // value = a * 10^x
+  for (int k = 0; k < e2_; ++k) a *= 2;
+  int x = e10_;
+  Format f = format_;
+  if (f == Format::kBinarySI) {
+    // |v| < 1024 or not an integer: DecimalSI ("This avoids rounding" / "Don't lose precision")
+    __int128 n = a;
+    bool integer = true;
+    for (int k = 0; k < x; ++k) n *= 10;
+    for (int k = 0; k < -x && integer; ++k) {
+      if (n % 10 != 0) integer = false;
+      n /= 10;
+    }
+    if (!integer || (n > -1024 && n < 1024)) {
+      f = Format::kDecimalSI;
+    } else {
+      static const char* bin[] = {"", "Ki", "Mi", "Gi", "Ti", "Pi", "Ei"};
+      int e = 0;                               // AsCanonicalBase1024Bytes: removeInt64Factors(v, 1024)
+      __int128 m = n < 0 ? -n : n;
+      while (m >= 1024 && m % 1024 == 0 && e < 6) {
+        m /= 1024;
+        ++e;
+      }
+      return i128_str(n < 0 ? -m : m) + bin[e];
+    }
+  }
+  // AsCanonicalBytes: move factors of ten into the exponent, then make it a multiple of 3
+  __int128 m = a < 0 ? -a : a;
+  while (m >= 10 && m % 10 == 0) {
+    m /= 10;
+    ++x;
+  }
+  switch (x % 3) {                             // Go's % keeps the dividend's sign
+    case 1: case -2: m *= 10; x -= 1; break;
+    case 2: case -1: m *= 100; x -= 2; break;
+    default: break;
+  }
+  const std::string num = i128_str(a < 0 ? -m : m);
+  if (f == Format::kDecimalExponent) return x == 0 ? num : num + "e" + std::to_string(x);
+  switch (x) {                                 // decimal SI suffixes (suffix.go)
+    case -9: return num + "n";
+    case -6: return num + "u";
+    case -3: return num + "m";
+    case 0: return num;
+    case 3: return num + "k";
+    case 6: return num + "M";
+    case 9: return num + "G";
+    case 12: return num + "T";
+    case 15: return num + "P";
+    case 18: return num + "E";
+    default: return num + "e" + std::to_string(x);   // outside the SI table (no int64 canonical value)
+  }
 }
 
 bool EqualResourceList(const ResourceList& a, const ResourceList& b) {

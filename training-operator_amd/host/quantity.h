@@ -16,25 +16,38 @@ struct QuantityError {
   std::string msg;
 };
 
+// resource.Format: how a quantity prints (apimachinery quantity.go).  Parse takes it from the
+// suffix: Ki..Ei -> BinarySI, e<N>/E<N> exponent -> DecimalExponent, none or n..E -> DecimalSI.
+enum class Format { kDecimalExponent, kBinarySI, kDecimalSI };
+
 class Quantity {
  public:
   Quantity() = default;
   static Quantity Parse(const std::string& s);     // throws QuantityError
   static Quantity MustParse(const std::string& s) { return Parse(s); }
+  // From an engine result.  Default format: DecimalSI for cpu, BinarySI for everything else.
   static Quantity FromCanonical(const std::string& resource, int64_t v);
+  static Quantity FromCanonical(const std::string& resource, int64_t v, Format f);
 
   // canonical int64 for `resource` (cpu: milli); throws QuantityError when inexact / negative / > int64
   int64_t Canonical(const std::string& resource) const;
   // Cmp == 0 semantics
   bool Equal(const Quantity& o) const;
-  std::string String() const;                         // an exact string form (not Go's canonical format)
+  bool IsZero() const { return mant_ == 0; }
+  Format format() const { return format_; }
+  // Go's Quantity.String(): CanonicalizeBytes of the value in its format (quantity.go) --
+  // BinarySI prints as <n>Ki..Ei when |v| >= 1024 and v is an integer, else falls back to
+  // DecimalSI; DecimalSI / DecimalExponent strip factors of ten and round the exponent down to a
+  // multiple of 3 (n u m "" k M G T P E, or e<N>).  "1.5Gi" -> "1536Mi", "1000m" -> "1",
+  // "0.5" -> "500m", "1024Mi" -> "1Gi", "1e3" -> "1e3".  What the JSON encoder writes.
+  std::string String() const;
 
  private:
   // value = mant * 10^e10 * 2^e2, mant signed
   __int128 mant_ = 0;
   int e10_ = 0;
   int e2_ = 0;
-  std::string text_;
+  Format format_ = Format::kDecimalSI;
 };
 
 using ResourceList = std::map<std::string, Quantity>;
