@@ -227,6 +227,39 @@ TEST_CPU(TestFlattenRejectsUnknownResource) {
   CHECK(f.job_group_off.size() == 1 && f.cont_flags.empty());   // all-or-nothing append
 }
 
+// a started PriorityClass informer and the deterministic tie policy
+TEST_CPU(TestPriorityClassInformerAndTiePolicy) {
+  ReplicaSpec m, w, l;
+  m.replicas = 1;
+  m.template_spec.priority_class_name = "";
+  w.replicas = 4;
+  w.template_spec.priority_class_name = "high";
+  l.replicas = 1;
+  l.template_spec.priority_class_name = "low";
+  const std::map<ReplicaType, ReplicaSpec> reps = {{"Master", m}, {"Worker", w}, {"Launcher", l}};
+  PriorityClassInformer inf;
+  // informer not fed (the reference's never-started factory): every Get misses, all tie -> name asc
+  CHECK((ReplicaOrderV1(reps, inf.Lister()) == std::vector<ReplicaType>{"Launcher", "Master", "Worker"}));
+  inf.OnAdd("high", 1000);
+  inf.OnAdd("low", -5);
+  CHECK((ReplicaOrderV1(reps, inf.Lister()) == std::vector<ReplicaType>{"Worker", "Master", "Launcher"}));
+  inf.OnUpdate("high", -10);
+  CHECK((ReplicaOrderV1(reps, inf.Lister()) == std::vector<ReplicaType>{"Master", "Launcher", "Worker"}));
+  inf.OnDelete("high");
+  inf.OnDelete("low");
+  // tie policy: listed types first in the given order, then name asc
+  CHECK((ReplicaOrderV1(reps, inf.Lister(), V1OrderPolicy{{"Worker", "Master"}}) ==
+         std::vector<ReplicaType>{"Worker", "Master", "Launcher"}));
+  // priority still dominates the tie policy
+  inf.OnAdd("low", 7);
+  CHECK((ReplicaOrderV1(reps, inf.Lister(), V1OrderPolicy{{"Worker", "Master"}}) ==
+         std::vector<ReplicaType>{"Launcher", "Worker", "Master"}));
+  // the flattened CSR follows the order
+  Flat f;
+  FlattenV1Job(Dims{"nvidia.com/gpu"}, 2, reps, inf.Lister(), &f, V1OrderPolicy{{"Worker"}});
+  CHECK((f.group_replicas == std::vector<int32_t>{1, 4, 1}));   // Launcher(7), Worker(tie first), Master
+}
+
 TEST_CPU(TestGetTotalReplicas) {
   auto r = mnist(3);
   r["Worker"].replicas.reset();                   // nil counts as 1 (k8sutil.go:131-133)
@@ -441,6 +474,58 @@ TEST_GPU(TestBuildWireV2) {
   CHECK(js.find("\"spec\":{\"minMember\":101,\"minResources\":{\"cpu\":\"101\",\"memory\":\"404Gi\"},"
                 "\"scheduleTimeoutSeconds\":300}") != std::string::npos);
   CHECK(js.find("\"apiVersion\":\"kubeflow.org/v2alpha1\",\"kind\":\"TrainJob\"") != std::string::npos);
+}
+
+// ResourcesPerNode vs TotalRequests.  Reference behaviour (option off): the
+// PodGroup counts the runtime's trainer requests even though the pods run with ResourcesPerNode.
+TEST_GPU(TestResourcesPerNodeTotalRequests) {
+  PodSpec trainer;
+  Container tc = Ctr(RL({{"cpu", "1"}, {"memory", "4Gi"}}));
+  tc.name = "trainer";
+  trainer.containers = {tc, Ctr(RL({{"cpu", "100m"}}))};   // a second (sidecar-style) container keeps its own
+  TrainJob tj;
+  tj.name = "rpn";
+  tj.uid = "u";
+  tj.trainer_num_nodes = 10;
+  tj.resources_per_node = ResourceRequirements{RL({{"cpu", "2"}, {"memory", "8Gi"}}), std::nullopt};
+  auto run = [&](bool fix) {
+    InfoOptions o;
+    o.ml_policy = MLPolicy{std::nullopt, MLPolicy::kTorch};
+    o.pod_group_policy = PodGroupPolicy{CoschedulingPodGroupPolicySource{60}};
+    o.pod_spec_replicas = {{"trainer-node", 1, trainer}};
+    Info info = NewInfo(eng(), o);
+    CHECK(!ApplyTotalRequestsOptions(eng(), TotalRequestsOptions{fix}, &info, &tj, trainer));
+    Torch().EnforceMLPolicy(&info, &tj);
+    return CoScheduling(eng()).Build(&info, &tj, nullptr);
+  };
+  auto ref = run(false);   // 10 x (1 + 0.1) cpu, 10 x 4Gi
+  CHECK(ref.object && ref.object->min_member == 10);
+  CHECK(EqualResourceList(ref.object->min_resources, RL({{"cpu", "11"}, {"memory", "40Gi"}})));
+  auto fixed = run(true);  // 10 x (2 + 0.1) cpu, 10 x 8Gi
+  CHECK(fixed.object && fixed.object->min_member == 10);
+  CHECK(EqualResourceList(fixed.object->min_resources, RL({{"cpu", "21"}, {"memory", "80Gi"}})));
+  PodSpec applied = ApplyTrainerResourcesPerNode(trainer, tj);
+  CHECK(applied.containers[0].requests->at("cpu").Equal(Quantity::Parse("2")) && !applied.containers[0].limits);
+  CHECK(applied.containers[1].requests->at("cpu").Equal(Quantity::Parse("100m")));
+}
+
+// The order decides which pods count toward minMember (util.go:126-141)
+TEST_GPU(TestCalcPGMinResourcesTiePolicy) {
+  ReplicaSpec m, w;
+  m.replicas = 1;
+  m.template_spec.containers = {Ctr(RL({{"cpu", "4"}}))};
+  w.replicas = 3;
+  w.template_spec.containers = {Ctr(RL({{"cpu", "1"}}))};
+  const std::map<ReplicaType, ReplicaSpec> reps = {{"Master", m}, {"Worker", w}};
+  PriorityClassInformer inf;
+  auto dflt = CalcPGMinResources(eng(), 2, reps, inf.Lister());   // Master then one Worker
+  CHECK(dflt.at("cpu").Equal(Quantity::Parse("5")));
+  auto wfirst = CalcPGMinResources(eng(), 2, reps, inf.Lister(), V1OrderPolicy{{"Worker"}});   // two Workers
+  CHECK(wfirst.at("cpu").Equal(Quantity::Parse("2")));
+  w.template_spec.priority_class_name = "hp";
+  inf.OnAdd("hp", 100);
+  auto pri = CalcPGMinResources(eng(), 2, {{"Master", m}, {"Worker", w}}, inf.Lister());
+  CHECK(pri.at("cpu").Equal(Quantity::Parse("2")));
 }
 
 TEST_GPU(TestBuildNilPolicyAndExistingPodGroup) {

@@ -336,3 +336,17 @@ def test_greedy_reset_residuals(eng):
     b = eng.place_batch(batch)
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x, y)
+
+
+def test_v2_total_requests_edge_cases(eng):
+    """kueue pod formula corners (sidecar order, overhead, key union, zero keys) on the GPU, one
+    batch, against hand-derived answers (tests/kueue_cases.py); replicas 3 scales every key."""
+    from kueue_cases import CASES
+    flat = F.Flat()
+    for _, pod, _ in CASES:
+        F.add_v2_pod_group(flat, 3, pod, GPU)
+        flat.end_job(0)
+    out, pres, mem, ovf = eng.pg_min_resources(V2, *flat.arrays())
+    for j, (name, _, want) in enumerate(CASES):
+        assert F.unflatten(out[j], pres[j], GPU) == {k: 3 * v for k, v in want.items()}, name
+        assert mem[j] == 3 and ovf[j] == 0

@@ -31,5 +31,6 @@ def test_host_mirror_cpu_cases():
 def test_host_mirror_gpu_cases():
     out = run("--gpu")
     for name in ("TestNewInfo", "TestTrainingRuntimeNewObjects", "TestIntegrationPodGroup", "TestCalcPGMinResourcesMnist",
-                 "TestNodeInventoryInformer", "TestSyncPodGroupV1", "TestBuildWireV2"):
+                 "TestNodeInventoryInformer", "TestSyncPodGroupV1", "TestBuildWireV2",
+                 "TestResourcesPerNodeTotalRequests", "TestCalcPGMinResourcesTiePolicy"):
         assert "ok   " + name in out

@@ -192,3 +192,19 @@ def test_c_oracle_overflow_and_wrap():
     assert ovf[0] == 1 and ovf[1] == 0
     assert members[1] == -(2**31) + 1
     assert out[1, 0] == (2**31 + 1) * 1000
+
+
+# ----------------------------------------------------------------- kueue TotalRequests edge cases
+
+from kueue_cases import CASES as KUEUE_CASES  # noqa: E402
+
+
+@pytest.mark.parametrize("name,pod,want", KUEUE_CASES, ids=[c[0] for c in KUEUE_CASES])
+def test_total_requests_edge_cases(name, pod, want):
+    """Python restatement and C restatement against hand-derived answers (kueue_cases.py)."""
+    assert F.canonical_list(S.total_requests(pod), GPU) == want
+    flat = F.Flat()
+    F.add_v2_pod_group(flat, 1, pod, GPU)
+    flat.end_job(0)
+    out, pres, mem, ovf = oracle.pg_min_resources(2, *flat.arrays())
+    assert F.unflatten(out[0], pres[0], GPU) == want and mem[0] == 1 and ovf[0] == 0

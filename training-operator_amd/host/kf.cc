@@ -65,21 +65,38 @@ static void end_job(int32_t min_member, Flat* out) {
 }
 
 // util.go:110-124: priority from the PriorityClass lister (error/nil -> 0), sorted DESC.  Go's
-// sort.Sort leaves equal priorities in map-iteration order (random); we take type name ASC.
-static std::vector<ReplicaType> v1_order(const std::map<ReplicaType, ReplicaSpec>& replicas,
-                                         const PriorityClassGetFunc& pcGetFunc) {
-  std::vector<std::pair<int32_t, ReplicaType>> pri;
+// sort.Sort leaves equal priorities in map-iteration order (random); we apply V1OrderPolicy.
+std::vector<ReplicaType> ReplicaOrderV1(const std::map<ReplicaType, ReplicaSpec>& replicas,
+                                        const PriorityClassGetFunc& pcGetFunc, const V1OrderPolicy& order) {
+  struct Ent {
+    int32_t pri;
+    size_t rank;   // position in tie_order, or tie_order.size() for unlisted types
+    ReplicaType t;
+  };
+  std::vector<Ent> pri;
   for (const auto& kv : replicas) {
     std::optional<PriorityClass> pc;
     if (pcGetFunc) pc = pcGetFunc(kv.second.template_spec.priority_class_name);
-    pri.emplace_back(pc ? pc->value : 0, kv.first);
+    const size_t rank = (size_t)(std::find(order.tie_order.begin(), order.tie_order.end(), kv.first) -
+                                 order.tie_order.begin());
+    pri.push_back({pc ? pc->value : 0, rank, kv.first});
   }
-  std::stable_sort(pri.begin(), pri.end(), [](const auto& a, const auto& b) {
-    return a.first != b.first ? a.first > b.first : a.second < b.second;
+  std::sort(pri.begin(), pri.end(), [](const Ent& a, const Ent& b) {
+    if (a.pri != b.pri) return a.pri > b.pri;
+    if (a.rank != b.rank) return a.rank < b.rank;
+    return a.t < b.t;
   });
-  std::vector<ReplicaType> order;
-  for (auto& p : pri) order.push_back(p.second);
-  return order;
+  std::vector<ReplicaType> out;
+  for (auto& p : pri) out.push_back(p.t);
+  return out;
+}
+
+PriorityClassGetFunc PriorityClassInformer::Lister() const {
+  return [this](const std::string& name) -> std::optional<PriorityClass> {
+    auto it = values_.find(name);
+    if (it == values_.end()) return std::nullopt;   // lister NotFound -> priority 0
+    return PriorityClass{it->second};
+  };
 }
 
 // Roll the arrays back to their sizes at entry if a record throws (one job is all-or-nothing).
@@ -102,9 +119,9 @@ struct FlatTxn {
 };
 
 void FlattenV1Job(const Dims& eng, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
-                  const PriorityClassGetFunc& pcGetFunc, Flat* out) {
+                  const PriorityClassGetFunc& pcGetFunc, Flat* out, const V1OrderPolicy& order) {
   FlatTxn txn(out);
-  for (const ReplicaType& t : v1_order(replicas, pcGetFunc)) {
+  for (const ReplicaType& t : ReplicaOrderV1(replicas, pcGetFunc, order)) {
     const ReplicaSpec& spec = replicas.at(t);
     for (const Container& c : spec.template_spec.containers) {
       // AddResourceList (util.go:79-104): Requests keys, or Limits only when Requests is nil
@@ -205,12 +222,13 @@ int32_t GetTotalReplicas(const std::map<ReplicaType, ReplicaSpec>& replicas) {
 }
 
 std::map<std::string, Format> MinResourcesFormatsV1(int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
-                                                    const PriorityClassGetFunc& pcGetFunc) {
+                                                    const PriorityClassGetFunc& pcGetFunc,
+                                                    const V1OrderPolicy& order) {
   // util.go:126-141 walk: only counted pods add, pods of one type are identical, so one pass per
   // type that counts at least one pod gives the same first-nonzero / last-zero answer
   FormatAcc acc;
   int64_t pod_cnt = 0;
-  for (const ReplicaType& t : v1_order(replicas, pcGetFunc)) {
+  for (const ReplicaType& t : ReplicaOrderV1(replicas, pcGetFunc, order)) {
     const ReplicaSpec& spec = replicas.at(t);
     if (!spec.replicas) continue;
     const int64_t k = std::min<int64_t>(*spec.replicas, std::max<int64_t>(0, (int64_t)minMember - pod_cnt));
@@ -227,33 +245,34 @@ std::map<std::string, Format> MinResourcesFormatsV1(int32_t minMember, const std
 }
 
 ResourceList CalcPGMinResources(Engine& eng, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
-                                const PriorityClassGetFunc& pcGetFunc) {
+                                const PriorityClassGetFunc& pcGetFunc, const V1OrderPolicy& order) {
   Flat f;
-  FlattenV1Job(eng.dims(), minMember, replicas, pcGetFunc, &f);
-  const auto formats = MinResourcesFormatsV1(minMember, replicas, pcGetFunc);
+  FlattenV1Job(eng.dims(), minMember, replicas, pcGetFunc, &f, order);
+  const auto formats = MinResourcesFormatsV1(minMember, replicas, pcGetFunc, order);
   return to_list(eng.dims(), run_agg(eng, PE_MODE_V1, f), 0, &formats);
 }
 
 std::vector<ResourceList> CalcPGMinResourcesBatch(Engine& eng, const std::vector<V1Job>& jobs,
-                                                  const PriorityClassGetFunc& pcGetFunc) {
+                                                  const PriorityClassGetFunc& pcGetFunc, const V1OrderPolicy& order) {
   Flat f;
-  for (const V1Job& j : jobs) FlattenV1Job(eng.dims(), j.min_member, j.replicas, pcGetFunc, &f);
+  for (const V1Job& j : jobs) FlattenV1Job(eng.dims(), j.min_member, j.replicas, pcGetFunc, &f, order);
   AggOut o = run_agg(eng, PE_MODE_V1, f);
   std::vector<ResourceList> out;
   for (size_t j = 0; j < jobs.size(); ++j) {
-    const auto formats = MinResourcesFormatsV1(jobs[j].min_member, jobs[j].replicas, pcGetFunc);
+    const auto formats = MinResourcesFormatsV1(jobs[j].min_member, jobs[j].replicas, pcGetFunc, order);
     out.push_back(to_list(eng.dims(), o, (int64_t)j, &formats));
   }
   return out;
 }
 
 PodGroupSpecV1 CalcPodGroupSpecV1(Engine& eng, const std::map<ReplicaType, ReplicaSpec>& replicas,
-                                  const SchedulingPolicy* policy, const PriorityClassGetFunc& pcGetFunc) {
+                                  const SchedulingPolicy* policy, const PriorityClassGetFunc& pcGetFunc,
+                                  const V1OrderPolicy& order) {
   PodGroupSpecV1 pg;
   pg.min_member = GetTotalReplicas(replicas);                                    // job.go:251
   if (policy && policy->min_available) pg.min_member = *policy->min_available;   // job.go:258-260
   if (policy && policy->min_resources) pg.min_resources = *policy->min_resources;  // job.go:267-269
-  else pg.min_resources = CalcPGMinResources(eng, pg.min_member, replicas, pcGetFunc);  // job.go:275-277
+  else pg.min_resources = CalcPGMinResources(eng, pg.min_member, replicas, pcGetFunc, order);  // job.go:275-277
   return pg;
 }
 
@@ -290,6 +309,32 @@ Info NewInfo(Engine& eng, const InfoOptions& opts) {
         TotalResourceRequest{r.replicas, to_list(eng.dims(), o, (int64_t)i, &acc.fmt)};
   }
   return info;
+}
+
+PodSpec ApplyTrainerResourcesPerNode(const PodSpec& pod, const TrainJob& trainJob) {
+  PodSpec out = pod;
+  if (!trainJob.resources_per_node) return out;
+  for (Container& c : out.containers)
+    if (c.name == "trainer") {   // constants.ContainerTrainer
+      c.requests = trainJob.resources_per_node->requests;
+      c.limits = trainJob.resources_per_node->limits;
+    }
+  return out;
+}
+
+std::optional<Error> ApplyTotalRequestsOptions(Engine& eng, const TotalRequestsOptions& opts, Info* info,
+                                               const TrainJob* trainJob, const PodSpec& runtime_trainer_pod) {
+  if (!opts.from_resources_per_node || !info || !trainJob || !trainJob->resources_per_node) return std::nullopt;
+  auto it = info->scheduler.total_requests.find("trainer-node");   // constants.JobTrainerNode
+  if (it == info->scheduler.total_requests.end()) return std::nullopt;
+  try {
+    InfoOptions o;
+    o.pod_spec_replicas = {{"trainer-node", 1, ApplyTrainerResourcesPerNode(runtime_trainer_pod, *trainJob)}};
+    it->second.pod_requests = NewInfo(eng, o).scheduler.total_requests.at("trainer-node").pod_requests;
+  } catch (const Error& e) {
+    return e;
+  }
+  return std::nullopt;
 }
 
 static std::optional<Error> rewrite_trainer_replicas(Info* info, const TrainJob* trainJob) {
@@ -397,7 +442,8 @@ CoScheduling::BuildResult CoScheduling::Build(const Info* info, const TrainJob* 
 
 SyncPodGroupResult SyncPodGroupV1(Engine& eng, GangScheduler flavour, const JobMeta& job,
                                   const std::map<ReplicaType, ReplicaSpec>& replicas, const SchedulingPolicy* policy,
-                                  const PriorityClassGetFunc& pcGetFunc, const PodGroup* existing) {
+                                  const PriorityClassGetFunc& pcGetFunc, const PodGroup* existing,
+                                  const V1OrderPolicy& order) {
   // job.go:251-277
   int32_t min_member = GetTotalReplicas(replicas);
   std::string queue = "default", priority_class;
@@ -410,7 +456,7 @@ SyncPodGroupResult SyncPodGroupV1(Engine& eng, GangScheduler flavour, const JobM
     if (policy->min_resources) min_resources = *policy->min_resources;
     if (policy->schedule_timeout_seconds) timeout = policy->schedule_timeout_seconds;
   }
-  if (!min_resources) min_resources = CalcPGMinResources(eng, min_member, replicas, pcGetFunc);
+  if (!min_resources) min_resources = CalcPGMinResources(eng, min_member, replicas, pcGetFunc, order);
 
   SyncPodGroupResult r;
   if (existing) {

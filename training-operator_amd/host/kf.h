@@ -75,10 +75,14 @@ struct CoschedulingPodGroupPolicySource {
 struct PodGroupPolicy {
   std::optional<CoschedulingPodGroupPolicySource> coscheduling;
 };
+struct ResourceRequirements {
+  std::optional<ResourceList> requests, limits;
+};
 struct TrainJob {
   std::string name, ns, uid;
   bool suspend = false;
   std::optional<int32_t> trainer_num_nodes;
+  std::optional<ResourceRequirements> resources_per_node;   // trainjob_types.go:192 Trainer.ResourcesPerNode
   std::map<std::string, std::string> labels, annotations;
 };
 
@@ -156,6 +160,37 @@ class Engine {
   Dims dims_;
 };
 
+// ------------------------------------------------------------------ priority classes
+// In the reference the PriorityClass lister's shared informer factory is never started
+// (pytorchjob_controller.go:73-86 builds it, nothing calls Start), so every Get misses and every
+// replica type gets priority 0 with a warning (util.go:112-119); the tie is then broken by Go map
+// iteration order through a non-stable sort.Sort (util.go:29-48,124): random.  Two explicit fixes:
+//
+// PriorityClassInformer -- the started informer's store: the PriorityClass watch handlers feed it,
+// Lister() answers Get(name) from it (miss / "" -> nullopt -> priority 0, as the Go lister errors).
+class PriorityClassInformer {
+ public:
+  void OnAdd(const std::string& name, int32_t value) { values_[name] = value; }
+  void OnUpdate(const std::string& name, int32_t value) { values_[name] = value; }
+  void OnDelete(const std::string& name) { values_.erase(name); }
+  bool HasSynced() const { return true; }
+  PriorityClassGetFunc Lister() const;   // reads the live store (valid while the informer lives)
+
+ private:
+  std::map<std::string, int32_t> values_;
+};
+
+// V1OrderPolicy -- the deterministic tie policy: among replica types of equal priority, the types
+// listed in tie_order come first, in that order; the rest by type name ascending (the default,
+// what the kernel fixtures and the oracle's canonical order use).  E.g. {"Master", "Launcher",
+// "Chief"} counts leader pods toward minMember before workers.
+struct V1OrderPolicy {
+  std::vector<ReplicaType> tie_order;
+};
+// The CalcPGMinResources type order under a policy (priority desc, then the tie policy).
+std::vector<ReplicaType> ReplicaOrderV1(const std::map<ReplicaType, ReplicaSpec>& replicas,
+                                        const PriorityClassGetFunc& pcGetFunc, const V1OrderPolicy& order = {});
+
 // ------------------------------------------------------------------ v1
 
 int32_t GetTotalReplicas(const std::map<ReplicaType, ReplicaSpec>& replicas);
@@ -163,7 +198,7 @@ int32_t GetTotalReplicas(const std::map<ReplicaType, ReplicaSpec>& replicas);
 // util.go:108.  Throws kf::Error when a quantity has no exact int64 canonical form, a resource key
 // has no engine dimension, or the sum overflows int64 (Go would switch to inf.Dec).
 ResourceList CalcPGMinResources(Engine& eng, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
-                                const PriorityClassGetFunc& pcGetFunc);
+                                const PriorityClassGetFunc& pcGetFunc, const V1OrderPolicy& order = {});
 
 struct V1Job {
   int32_t min_member;
@@ -171,7 +206,7 @@ struct V1Job {
 };
 // One kernel launch for a batch of jobs (the throughput form of the same rule).
 std::vector<ResourceList> CalcPGMinResourcesBatch(Engine& eng, const std::vector<V1Job>& jobs,
-                                                  const PriorityClassGetFunc& pcGetFunc);
+                                                  const PriorityClassGetFunc& pcGetFunc, const V1OrderPolicy& order = {});
 
 // job.go:250-277: minMember = MinAvailable ?? GetTotalReplicas; MinResources verbatim if set.
 struct PodGroupSpecV1 {
@@ -179,14 +214,16 @@ struct PodGroupSpecV1 {
   ResourceList min_resources;
 };
 PodGroupSpecV1 CalcPodGroupSpecV1(Engine& eng, const std::map<ReplicaType, ReplicaSpec>& replicas,
-                                  const SchedulingPolicy* policy, const PriorityClassGetFunc& pcGetFunc);
+                                  const SchedulingPolicy* policy, const PriorityClassGetFunc& pcGetFunc,
+                                  const V1OrderPolicy& order = {});
 
 // Print format of each MinResources key as Go's AddResourceList leaves it (util.go:79-104): a new
 // key deep-copies the first quantity, Quantity.Add adopts the addend's format while the running
 // value is 0 -- so a key prints in the format of its first nonzero contribution (all zero: the
 // last one).  Host-side metadata only; the values come from the GPU.
 std::map<std::string, Format> MinResourcesFormatsV1(int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
-                                                    const PriorityClassGetFunc& pcGetFunc);
+                                                    const PriorityClassGetFunc& pcGetFunc,
+                                                    const V1OrderPolicy& order = {});
 
 // v1 gang branch + SyncPodGroup (job.go:250-313, scheduling.go:32-73): the PodGroup the job
 // controller creates or updates for one job.
@@ -208,7 +245,8 @@ struct SyncPodGroupResult {
 // CalcPGMinResources on the GPU, printed in MinResourcesFormatsV1's formats.
 SyncPodGroupResult SyncPodGroupV1(Engine& eng, GangScheduler flavour, const JobMeta& job,
                                   const std::map<ReplicaType, ReplicaSpec>& replicas, const SchedulingPolicy* policy,
-                                  const PriorityClassGetFunc& pcGetFunc, const PodGroup* existing);
+                                  const PriorityClassGetFunc& pcGetFunc, const PodGroup* existing,
+                                  const V1OrderPolicy& order = {});
 
 // ------------------------------------------------------------------ v2
 
@@ -226,6 +264,23 @@ struct InfoOptions {
 // runtime.go:115-145: TotalRequests[name] = {replicas, kueue TotalRequests(podSpec)} -- the pod
 // formula runs in the pg_min_resources kernel (PE_MODE_V2, one entry per group, replicas 1).
 Info NewInfo(Engine& eng, const InfoOptions& opts);
+
+// jobset/builder.go:138-163 (Builder.Trainer): the TrainJob's Trainer.ResourcesPerNode replaces the
+// resources of the "trainer" container (constants.ContainerTrainer) of the trainer-node pod.
+PodSpec ApplyTrainerResourcesPerNode(const PodSpec& runtime_trainer_pod, const TrainJob& trainJob);
+
+// the reference computes TotalRequests["trainer-node"] from the RUNTIME's pod spec
+// (runtime.go:133-134; plainml.go:63-66 and torch.go:122-125 carry "TODO: Add support for total
+// requests from the TrainJob's ResourcesPerNode"), while the JobSet it launches runs the pods with
+// ResourcesPerNode -- so the PodGroup's MinResources can disagree with the pods it gates.  Opt-in
+// fix (default off = the reference's behaviour): when the TrainJob sets ResourcesPerNode, recompute
+// the trainer-node pod requests on the GPU from ApplyTrainerResourcesPerNode(runtime pod).  The
+// replica count (MLPolicy rewrite) is untouched.  Call after NewInfo, before Build.
+struct TotalRequestsOptions {
+  bool from_resources_per_node = false;
+};
+std::optional<Error> ApplyTotalRequestsOptions(Engine& eng, const TotalRequestsOptions& opts, Info* info,
+                                               const TrainJob* trainJob, const PodSpec& runtime_trainer_pod);
 
 class Plugin {
  public:
@@ -326,7 +381,7 @@ struct Flat {
 };
 // Each call appends exactly one job (V1Job / Info) or one group (V2PodGroup) or nothing (throws).
 void FlattenV1Job(const Dims& dims, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
-                  const PriorityClassGetFunc& pcGetFunc, Flat* out);
+                  const PriorityClassGetFunc& pcGetFunc, Flat* out, const V1OrderPolicy& order = {});
 void FlattenV2PodGroup(const Dims& dims, int32_t replicas, const PodSpec& pod, Flat* out);
 void FlattenV2Info(const Dims& dims, const Info& info, Flat* out);
 
