@@ -350,3 +350,28 @@ def test_v2_total_requests_edge_cases(eng):
     for j, (name, _, want) in enumerate(CASES):
         assert F.unflatten(out[j], pres[j], GPU) == {k: 3 * v for k, v in want.items()}, name
         assert mem[j] == 3 and ovf[j] == 0
+
+
+@pytest.mark.parametrize("case", ["saturating", "over_committed", "low_bits"])
+def test_greedy_score_corner_nodes(eng, case):
+    """The scan's node-only score terms (K(n) = S(n) << 24 | gid, exact when no term saturates)
+    against the oracle's direct Appendix-B key: nodes whose terms saturate take the full formula
+    (huge cpu / memory / accelerator counts), over-committed nodes fit nothing, and requests whose
+    low memory / ephemeral bits exceed the node's exercise the borrow terms."""
+    N, J = 2500, 200
+    inv = synth.make_inventory(N, 53, 0.3)
+    batch = synth.make_jobs(J, 59, "mixed")
+    if case == "saturating":
+        inv.cap[0, ::97] = 1 << 41                     # left_cpu > SCORE_MAX
+        inv.cap[2, 5::89] = 1 << 21                    # left_gpu << 20 would exceed 2^40
+        inv.cap[1, 7::83] = 1 << 61                    # left_mem >> 20 > SCORE_MAX
+        inv.cap[0, 9::79] = (1 << 40) - 2              # S(n) reaches SCORE_MAX
+    elif case == "over_committed":
+        inv.used[0, ::7] = inv.cap[0, ::7] + 1         # negative cpu residual
+        inv.used[3, 3::11] = inv.cap[3, 3::11] + 5
+    else:
+        inv.cap[1] += np.arange(N, dtype=np.int64) * 4099        # odd memory bytes on every node
+        inv.cap[3] += np.arange(N, dtype=np.int64) * 65537
+        batch.group_req[:, 1] += (np.arange(len(batch.group_count)) % 7) * 131071
+        batch.group_req[:, 3] += (np.arange(len(batch.group_count)) % 5) * 9_999_991
+    check_greedy(eng, inv, batch)

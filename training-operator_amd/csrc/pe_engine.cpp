@@ -140,6 +140,8 @@ struct pe_ctx {
   DevBuf<int32_t> g_cnt;
   DevBuf<uint8_t> g_out, g_gath;
   DevBuf<int64_t> g_upd;
+  DevBuf<uint64_t> g_kn;   // scan: node-only score terms K(n) (prep_nodes), refreshed by apply
+  DevBuf<uint32_t> g_lo;   // scan: lo20(r1) / lo24(r3), [2][stride]
   HostBuf<ReqRec> h_groups;
   HostBuf<uint8_t> h_out, h_own;
   HostBuf<int64_t> h_upd;
@@ -155,7 +157,7 @@ struct pe_ctx {
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
-    g_upd.release(); h_groups.release(); h_out.release(); h_own.release(); h_upd.release();
+    g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_out.release(); h_own.release(); h_upd.release();
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -886,6 +888,12 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       hipchk(ctx->g_gath.ensure((size_t)Wmax * gb * ctx->world), "alloc gather");
       hipchk(ctx->h_own.ensure((size_t)Wmax * gb), "alloc pinned own");
     }
+    hipchk(ctx->g_kn.ensure((size_t)std::max<int64_t>(ctx->stride, 1)), "alloc node keys");
+    hipchk(ctx->g_lo.ensure((size_t)2 * std::max<int64_t>(ctx->stride, 1)), "alloc node lows");
+    // residuals may have changed since the last call (reset, pe_update_nodes): one pass over the shard
+    hipchk(pe::launch_prep_nodes(ctx->stream, ctx->res.p, ctx->stride, ctx->Ns, (uint64_t)ctx->begin, ctx->g_kn.p,
+                                 ctx->g_lo.p),
+           "launch prep_nodes");
     std::vector<int32_t> groups;
     std::vector<pe::GroupCands> cands;
     std::vector<pe::Update> updates;
@@ -902,8 +910,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       hipchk(hipMemcpyAsync(ctx->g_groups.p, ctx->h_groups.p, Wgp * sizeof(ReqRec), hipMemcpyHostToDevice, s),
              "H2D window");
       if (ctx->Ns > 0) {
-        hipchk(pe::launch_scan(s, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, (uint64_t)ctx->begin,
-                               ctx->g_groups.p, Wg, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p, nwaves),
+        hipchk(pe::launch_scan(s, ctx->res.p, ctx->stride, ctx->labels.p, ctx->g_kn.p, ctx->g_lo.p, ctx->Ns,
+                               (uint64_t)ctx->begin, ctx->g_groups.p, Wg, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p,
+                               nwaves),
                "launch scan");
         hipchk(pe::launch_merge(s, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p, nwaves, K, ctx->res.p, ctx->stride,
                                 ctx->labels.p, (uint64_t)ctx->begin, ctx->g_out.p, Wg),
@@ -953,7 +962,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         hipchk(ctx->g_upd.ensure((size_t)nu * (pe::D + 1)), "alloc upd");
         hipchk(hipMemcpyAsync(ctx->g_upd.p, ctx->h_upd.p, (size_t)nu * (pe::D + 1) * 8, hipMemcpyHostToDevice, s),
                "H2D upd");
-        hipchk(pe::launch_apply(s, ctx->res.p, ctx->stride, ctx->g_upd.p, nu), "launch apply");
+        hipchk(pe::launch_apply(s, ctx->res.p, ctx->stride, ctx->g_upd.p, nu, (uint64_t)ctx->begin, ctx->g_kn.p,
+                                ctx->g_lo.p),
+               "launch apply");
       }
       ctx->stats.windows += 1;
       ctx->stats.groups_scanned += Wg;

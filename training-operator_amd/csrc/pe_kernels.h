@@ -51,8 +51,9 @@ __host__ __device__ inline size_t cand_group_bytes(int K) { return sizeof(CandHd
 constexpr int FM_CH = 4;       // fit mask: 64-node chunks per wave tile (256 nodes in VGPRs)
 constexpr int FM_JT = 256;     // fit mask: jobs per wave
 constexpr int SC_M = 16;       // scan: nodes per lane (wave span 1024 nodes)
-constexpr int SC_GT = 8;       // scan: groups per wave (top-2 state in registers)
+constexpr int SC_GT = 4;       // scan: groups per wave (top-2 state in registers)
 constexpr int SC_SPAN = 64 * SC_M;
+constexpr int SC_WPB = 16;     // scan: waves (group tiles) per block, all on one node span
 constexpr int MG_CAP = 8192;   // merge: LDS candidate capacity per group
 constexpr int MG_THREADS = 1024;
 
@@ -140,16 +141,22 @@ hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t
 hipError_t launch_fit_mask_planes_rows(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
                                        int64_t J, int64_t R, uint32_t* mask, unsigned long long* counts);
 
-hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
-                       uint64_t id_base, const ReqRec* groups, int Wg, uint64_t* cand, int32_t* cnt,
-                       uint64_t* bound, int nwaves);
+// kn / lo: the node-only score terms of prep_nodes (K(n) = (S(n) << 24) | gid, lo20(r1), lo24(r3)),
+// kept current by apply; see pe_kernels.hip node_prep for the exactness argument.
+hipError_t launch_prep_nodes(hipStream_t s, const int64_t* res, int64_t stride, int64_t Ns, uint64_t id_base,
+                             uint64_t* kn, uint32_t* lo /* [2][stride] */);
+hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, const uint64_t* kn,
+                       const uint32_t* lo, int64_t Ns, uint64_t id_base, const ReqRec* groups, int Wg, uint64_t* cand,
+                       int32_t* cnt, uint64_t* bound, int nwaves);
 
 hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt, const uint64_t* bound,
                         int nwaves, int K, const int64_t* res, int64_t stride, const uint32_t* labels,
                         uint64_t id_base, uint8_t* out, int Wg);
 
 // upd: [n] records {local node (i64), res[4]} -> res[d][node] = value (absolute)
-hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n);
+// (kn, lo nullable: refreshed for the updated nodes when given)
+hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n, uint64_t id_base,
+                        uint64_t* kn, uint32_t* lo);
 
 // Inventory delta for one slot of this shard (pe_update_nodes): residual written to both the
 // live and the reset copy, labels and island replaced.  Slots are unique within a launch.

@@ -776,44 +776,142 @@ __device__ __forceinline__ uint64_t node_key(int64_t r0, int64_t r1, int64_t r2,
   return fit ? ((score << 24) | gid) : NO_KEY;
 }
 
-__global__ __launch_bounds__(256) void scan_kernel(const int64_t* __restrict__ res, int64_t stride,
-                                                   const uint32_t* __restrict__ labels, int64_t Ns, uint64_t id_base,
+// Node-only part of the Appendix-B score, kept per node for the scan:
+//   S(n) = r0 + (r1 >> 20) + (r2 << 20) + (r3 >> 24),   K(n) = (S << 24) | gid.
+// For a fitting request q and a node whose terms cannot saturate (r0 <= SCORE_MAX, r1 < 2^60,
+// r2 < 2^20, S < SCORE_MAX) the score is exactly
+//   score = S(n) - s(q) - [lo20(r1) < lo20(q1)] - [lo24(r3) < lo24(q3)]
+// (floor((r - q) / 2^k) = (r >> k) - (q >> k) - borrow), so key = K(n) - (s(q) << 24) - borrows << 24.
+// Nodes with a negative residual fit nothing (requests are >= 0): K = 0.  The rest: K = KEY_SLOW
+// and the scan evaluates node_key() for them.
+constexpr uint64_t KEY_SLOW = ~0ull;
+
+__device__ __forceinline__ void node_prep(int64_t r0, int64_t r1, int64_t r2, int64_t r3, uint64_t gid, uint64_t& K,
+                                          uint32_t& l1, uint32_t& l3) {
+  l1 = (uint32_t)r1 & 0xFFFFFu;
+  l3 = (uint32_t)r3 & 0xFFFFFFu;
+  if ((r0 | r1 | r2 | r3) < 0) {
+    K = 0;
+  } else if ((uint64_t)r0 > SCORE_MAX || r1 >= (1ll << 60) || r2 >= (1ll << 20)) {
+    K = KEY_SLOW;
+  } else {
+    const uint64_t S = (uint64_t)r0 + ((uint64_t)r1 >> 20) + ((uint64_t)r2 << 20) + ((uint64_t)r3 >> 24);
+    K = S < SCORE_MAX ? (S << 24) | gid : KEY_SLOW;
+  }
+}
+
+__global__ __launch_bounds__(256) void prep_nodes_kernel(const int64_t* __restrict__ res, int64_t stride, int64_t Ns,
+                                                         uint64_t id_base, uint64_t* __restrict__ kn,
+                                                         uint32_t* __restrict__ lo) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= stride) return;
+  uint64_t K = 0;
+  uint32_t l1 = 0, l3 = 0;
+  if (n < Ns) node_prep(res[n], res[stride + n], res[2 * stride + n], res[3 * stride + n], id_base + (uint64_t)n, K, l1, l3);
+  kn[n] = K;
+  lo[n] = l1;
+  lo[stride + n] = l3;
+}
+
+hipError_t launch_prep_nodes(hipStream_t s, const int64_t* res, int64_t stride, int64_t Ns, uint64_t id_base,
+                             uint64_t* kn, uint32_t* lo) {
+  if (stride <= 0) return hipSuccess;
+  hipLaunchKernelGGL(prep_nodes_kernel, dim3((unsigned)((stride + 255) / 256)), dim3(256), 0, s, res, stride, Ns,
+                     id_base, kn, lo);
+  return hipGetLastError();
+}
+
+// Grid: one block per 1024-node span (SC_WPB waves), wave w of the block takes group tile
+// blockIdx.y * SC_WPB + w.  All waves of a block read the same node chunks at about the same
+// time, so the node data comes from HBM once per window and the re-reads for the other group
+// tiles hit the CU's L1 (a grid of spans x tiles re-read it from MALL once per tile).
+__global__ __launch_bounds__(64 * SC_WPB) void scan_kernel(const int64_t* __restrict__ res, int64_t stride,
+                                                   const uint32_t* __restrict__ labels, const uint64_t* __restrict__ kn,
+                                                   const uint32_t* __restrict__ lo, int64_t Ns, uint64_t id_base,
                                                    const ReqRec* __restrict__ groups, int Wg,
                                                    uint64_t* __restrict__ cand, int32_t* __restrict__ cnt,
                                                    uint64_t* __restrict__ bound, int nwaves) {
   const int lane = threadIdx.x & 63;
-  const int wave_id = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (wave_id >= nwaves) return;
-  const int g0 = blockIdx.y * SC_GT;
+  const int wave_id = blockIdx.x;                                              // node span
+  const int g0 = (blockIdx.y * SC_WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * SC_GT;
+  if (g0 >= Wg) return;
   int64_t q[SC_GT][D];
-  uint32_t need[SC_GT];
+  uint32_t need[SC_GT], ql1[SC_GT], ql3[SC_GT];
+  uint64_t Q[SC_GT];
 #pragma unroll
   for (int g = 0; g < SC_GT; ++g) {                // groups padded to SC_GT on the device
     const ReqRec& gr = groups[g0 + g];
 #pragma unroll
     for (int d = 0; d < D; ++d) q[g][d] = gr.q[d];
     need[g] = gr.need;
+    ql1[g] = (uint32_t)q[g][1] & 0xFFFFFu;
+    ql3[g] = (uint32_t)q[g][3] & 0xFFFFFFu;
+    // s(q) << 24 with the terms clamped where no fast-path node can fit anyway (r0 <= SCORE_MAX,
+    // r1 < 2^60, r2 < 2^20 for every K(n) != KEY_SLOW)
+    const uint64_t t0 = (uint64_t)q[g][0] > SCORE_MAX ? SCORE_MAX : (uint64_t)q[g][0];
+    const uint64_t t1 = (uint64_t)q[g][1] >> 20;
+    const uint64_t t2 = (uint64_t)q[g][2] >= (1ull << 20) ? (1ull << 20) : (uint64_t)q[g][2];
+    Q[g] = (t0 + (t1 > SCORE_MAX ? SCORE_MAX : t1) + (t2 << 20) + ((uint64_t)q[g][3] >> 24)) << 24;
+    // wave-uniform, but kept in VGPRs: the group requests (q, need) already take most of the SGPR
+    // budget, and scalar spills inside the node loop cost more than VGPR operands
+    asm volatile("" : "+v"(Q[g]), "+v"(ql1[g]), "+v"(ql3[g]));
   }
   uint64_t m[SC_GT], s2[SC_GT];
 #pragma unroll
   for (int g = 0; g < SC_GT; ++g) m[g] = s2[g] = NO_KEY;
   const int64_t base = (int64_t)wave_id * SC_SPAN;
-  for (int i = 0; i < SC_M; ++i) {
+  // stride is a multiple of 64, so a 64-node chunk is wholly inside [0, stride) or wholly past it:
+  // a wave-uniform bound, no per-lane masks.  Nodes in [Ns, stride) are padding (residual NEVER,
+  // K = 0): they fit nothing.
+  const int nchunk = (int)min((int64_t)SC_M, (stride - base) / 64);
+  // chunk i+1's node data is loaded while chunk i is scored (the loads' latency was exposed)
+  struct Chunk {
+    int64_t r0, r1, r2, r3;
+    uint64_t K;
+    uint32_t lab, l1, l3;
+  };
+  auto load_chunk = [&](int i) {
     const int64_t n = base + i * 64 + lane;
-    const bool ok = n < Ns;
-    const int64_t r0 = ok ? res[n] : NEVER;
-    const int64_t r1 = ok ? res[stride + n] : NEVER;
-    const int64_t r2 = ok ? res[2 * stride + n] : NEVER;
-    const int64_t r3 = ok ? res[3 * stride + n] : NEVER;
-    const uint32_t lab = ok ? labels[n] : 0u;
+    return Chunk{res[n], res[stride + n], res[2 * stride + n], res[3 * stride + n], kn[n], labels[n], lo[n],
+                 lo[stride + n]};
+  };
+  Chunk nxt = nchunk > 0 ? load_chunk(0) : Chunk{};
+  for (int i = 0; i < nchunk; ++i) {
+    const Chunk c = nxt;
+    if (i + 1 < nchunk) nxt = load_chunk(i + 1);
+    const int64_t n = base + i * 64 + lane;
+    const int64_t r0 = c.r0, r1 = c.r1, r2 = c.r2, r3 = c.r3;
+    const uint32_t lab = c.lab;
+    const uint64_t K = c.K;
+    const uint32_t l1 = c.l1, l3 = c.l3;
     const uint64_t gid = id_base + (uint64_t)n;
+    if (__builtin_expect(__ballot(K == KEY_SLOW) == 0, 1)) {   // wave-uniform: no saturating node here
 #pragma unroll
-    for (int g = 0; g < SC_GT; ++g) {
-      const uint64_t k = node_key(r0, r1, r2, r3, lab, q[g][0], q[g][1], q[g][2], q[g][3], need[g], gid);
-      const bool lt_m = k < m[g];
-      const bool lt_s = k < s2[g];
-      s2[g] = lt_m ? m[g] : (lt_s ? k : s2[g]);
-      m[g] = lt_m ? k : m[g];
+      for (int g = 0; g < SC_GT; ++g) {
+        const bool fit = ((lab & need[g]) == need[g]) & (q[g][0] <= r0) & (q[g][1] <= r1) & (q[g][2] <= r2) &
+                         (q[g][3] <= r3);
+        const uint64_t borrow = ((uint64_t)(l1 < ql1[g]) + (uint64_t)(l3 < ql3[g])) << 24;
+        const uint64_t k = fit ? K - Q[g] - borrow : NO_KEY;
+        const bool lt_m = k < m[g];
+        const bool lt_s = k < s2[g];
+        s2[g] = lt_m ? m[g] : (lt_s ? k : s2[g]);
+        m[g] = lt_m ? k : m[g];
+      }
+    } else {
+      const bool slow = K == KEY_SLOW;
+#pragma unroll
+      for (int g = 0; g < SC_GT; ++g) {
+        const bool fit = ((lab & need[g]) == need[g]) & (q[g][0] <= r0) & (q[g][1] <= r1) & (q[g][2] <= r2) &
+                         (q[g][3] <= r3);
+        const uint64_t borrow = ((uint64_t)(l1 < ql1[g]) + (uint64_t)(l3 < ql3[g])) << 24;
+        const uint64_t k = !fit ? NO_KEY
+                           : slow ? node_key(r0, r1, r2, r3, lab, q[g][0], q[g][1], q[g][2], q[g][3], need[g], gid)
+                                  : K - Q[g] - borrow;
+        const bool lt_m = k < m[g];
+        const bool lt_s = k < s2[g];
+        s2[g] = lt_m ? m[g] : (lt_s ? k : s2[g]);
+        m[g] = lt_m ? k : m[g];
+      }
     }
   }
 #pragma unroll
@@ -832,13 +930,14 @@ __global__ __launch_bounds__(256) void scan_kernel(const int64_t* __restrict__ r
   }
 }
 
-hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
-                       uint64_t id_base, const ReqRec* groups, int Wg, uint64_t* cand, int32_t* cnt, uint64_t* bound,
-                       int nwaves) {
+hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, const uint64_t* kn,
+                       const uint32_t* lo, int64_t Ns, uint64_t id_base, const ReqRec* groups, int Wg, uint64_t* cand,
+                       int32_t* cnt, uint64_t* bound, int nwaves) {
   if (Wg <= 0 || nwaves <= 0) return hipSuccess;
-  dim3 grid((unsigned)((nwaves + 3) / 4), (unsigned)((Wg + SC_GT - 1) / SC_GT));
-  hipLaunchKernelGGL(scan_kernel, grid, dim3(256), 0, s, res, stride, labels, Ns, id_base, groups, Wg, cand, cnt,
-                     bound, nwaves);
+  const int tiles = (Wg + SC_GT - 1) / SC_GT;
+  dim3 grid((unsigned)nwaves, (unsigned)((tiles + SC_WPB - 1) / SC_WPB));
+  hipLaunchKernelGGL(scan_kernel, grid, dim3(64 * SC_WPB), 0, s, res, stride, labels, kn, lo, Ns, id_base, groups, Wg,
+                     cand, cnt, bound, nwaves);
   return hipGetLastError();
 }
 
@@ -967,18 +1066,29 @@ hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt,
 // ------------------------------------------------------------------ apply residual updates
 
 __global__ __launch_bounds__(256) void apply_kernel(int64_t* __restrict__ res, int64_t stride,
-                                                    const int64_t* __restrict__ upd, int64_t n) {
+                                                    const int64_t* __restrict__ upd, int64_t n, uint64_t id_base,
+                                                    uint64_t* __restrict__ kn, uint32_t* __restrict__ lo) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t* u = upd + i * (D + 1);
   const int64_t node = u[0];
 #pragma unroll
   for (int d = 0; d < D; ++d) res[d * stride + node] = u[1 + d];
+  if (kn) {                                   // keep the scan's node-only score terms current
+    uint64_t K;
+    uint32_t l1, l3;
+    node_prep(u[1], u[2], u[3], u[4], id_base + (uint64_t)node, K, l1, l3);
+    kn[node] = K;
+    lo[node] = l1;
+    lo[stride + node] = l3;
+  }
 }
 
-hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n) {
+hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n, uint64_t id_base,
+                        uint64_t* kn, uint32_t* lo) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, res, stride, upd, n);
+  hipLaunchKernelGGL(apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, res, stride, upd, n, id_base,
+                     kn, lo);
   return hipGetLastError();
 }
 

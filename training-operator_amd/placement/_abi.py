@@ -11,7 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(PKG_ROOT, "libplacement.so")
+LIB_PATH = os.environ.get("PE_LIBRARY") or os.path.join(PKG_ROOT, "libplacement.so")   # PE_LIBRARY: A/B builds
 HEADER = os.path.join(REPO_ROOT, "include", "placement.h")
 
 PE_OK, PE_EINVAL, PE_EOVERFLOW, PE_ENOMEM, PE_EHIP, PE_ERCCL, PE_ESTATE, PE_ENODEV = 0, -1, -2, -3, -4, -5, -6, -7
