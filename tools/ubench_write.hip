@@ -153,6 +153,21 @@ __global__ __launch_bounds__(256) void readwrite(u32x4* __restrict__ out, int64_
   if (v.x == 0xdeadbeef) occ[0] = 1;
 }
 
+// Linear sweep with a workgroup barrier every S steps: the 4 waves of a CU stay in lockstep.
+template <int S>
+__global__ __launch_bounds__(256) void linear_bar(u32x4* __restrict__ out, int64_t nwaves, int64_t kib) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  u32x4 v = {(uint32_t)w, 1u, 2u, 3u};
+  const int64_t steps = (kib + nwaves - 1) / nwaves;
+  for (int64_t i = 0; i < steps; ++i) {
+    const int64_t k = i * nwaves + w;
+    v = spin<40>(v);
+    if (k < kib) out[k * 64 + lane] = v;
+    if (i % S == S - 1) __syncthreads();
+  }
+}
+
 static float time_it(void (*launch)(void*), void* arg, hipEvent_t a, hipEvent_t b, int reps = 5) {
   launch(arg);
   hipDeviceSynchronize();
@@ -200,6 +215,11 @@ static void go(const Arg& a) {
     else
       hipLaunchKernelGGL((readwrite<1>), dim3((unsigned)((waves + 3) / 4)), dim3(256), a.lds, 0, a.out, a.kib, a.chunk,
                          a.nwaves, a.src, a.R);
+  } else if (a.kind == 7) {
+    const dim3 g((unsigned)((a.nwaves + 3) / 4));
+    if (a.S == 1) hipLaunchKernelGGL(linear_bar<1>, g, dim3(256), a.lds, 0, a.out, a.nwaves, a.kib);
+    else if (a.S == 4) hipLaunchKernelGGL(linear_bar<4>, g, dim3(256), a.lds, 0, a.out, a.nwaves, a.kib);
+    else hipLaunchKernelGGL(linear_bar<16>, g, dim3(256), a.lds, 0, a.out, a.nwaves, a.kib);
   } else if (a.kind == 3) {
     const int64_t waves = (a.kib + a.chunk - 1) / a.chunk;
     hipLaunchKernelGGL((oneshot<POL, DLY>), dim3((unsigned)((waves + 3) / 4)), dim3(256), a.lds, 0, a.out, a.kib,
@@ -245,17 +265,21 @@ int main() {
   auto rep = [&](const char* name, float ms) { printf("%-58s %7.3f ms  %5.2f TB/s\n", name, ms, bytes / (ms * 1e-3) / 1e12); };
   rep("hipMemsetD32", time_it(memset_launch, &g, a, b));
   char name[160];
-  g.kind = 1;
-  g.lds = 0;
-  for (int pol : {0, 1, 2})
-    for (int dly : {0, 40})
-      for (int64_t W : {984L, 1024L}) {
-        g.pol = pol;
-        g.dly = dly;
-        g.nwaves = W;
-        snprintf(name, sizeof name, "linear W=%ld pol=%d dly=%d", (long)W, pol, dly);
-        rep(name, time_it(launch, &g, a, b));
-      }
+  g.lds = 98304;   // one workgroup (4 waves) per CU, like the rows kernel
+  g.pol = 0;
+  g.dly = 40;
+  for (int64_t W : {984L, 1024L}) {
+    g.kind = 1;
+    g.nwaves = W;
+    snprintf(name, sizeof name, "linear W=%ld dly=40 1 WG/CU", (long)W);
+    rep(name, time_it(launch, &g, a, b));
+    for (int S : {1, 4, 16}) {
+      g.kind = 7;
+      g.S = S;
+      snprintf(name, sizeof name, "linear_bar W=%ld S=%d 1 WG/CU", (long)W, S);
+      rep(name, time_it(launch, &g, a, b));
+    }
+  }
   rep("hipMemsetD32 again", time_it(memset_launch, &g, a, b));
   hipFree(out);
   return 0;
