@@ -821,6 +821,54 @@ hipError_t launch_prep_nodes(hipStream_t s, const int64_t* res, int64_t stride, 
   return hipGetLastError();
 }
 
+#ifndef PE_SCAN_ASM
+#define PE_SCAN_ASM 1
+#endif
+// One group's key on the fast path, scheduled by hand: the compiler lowered the 5-way fit AND of
+// groups 2.. into v_cndmask / v_bitop3 chains and put the key under an exec branch (~40 VALU per
+// group and chunk).  Here: 4 x v_cmp_le_i64 + label test combined by s_and into the fit mask,
+// borrow masks, K - Q - borrows << 24 in a 32-bit carry chain, NO_KEY where the mask is clear.
+// 19 VALU + 4 SALU; the s_nop pairs keep 2 wait states between a VALU carry/mask write and its
+// VALU read (gfx950 hazard; the compiler inserts the same).
+__device__ __forceinline__ uint64_t fast_key(int64_t r0, int64_t r1, int64_t r2, int64_t r3, uint32_t lab, uint64_t K,
+                                             uint32_t l1, uint32_t l3, int64_t q0, int64_t q1, int64_t q2, int64_t q3,
+                                             uint32_t need, uint64_t Q, uint32_t ql1, uint32_t ql3, uint32_t c24) {
+  uint32_t klo, khi, x, y;
+  uint64_t f, t, b1, b3, c;
+  asm volatile(
+      "v_cmp_le_i64_e64 %[f], %[q0], %[r0]\n\t"
+      "v_cmp_le_i64_e64 %[t], %[q1], %[r1]\n\t"
+      "v_and_b32_e32 %[x], %[need], %[lab]\n\t"
+      "s_and_b64 %[f], %[f], %[t]\n\t"
+      "v_cmp_le_i64_e64 %[t], %[q2], %[r2]\n\t"
+      "v_cmp_lt_u32_e64 %[b1], %[l1], %[ql1]\n\t"
+      "s_and_b64 %[f], %[f], %[t]\n\t"
+      "v_cmp_le_i64_e64 %[t], %[q3], %[r3]\n\t"
+      "v_cmp_lt_u32_e64 %[b3], %[l3], %[ql3]\n\t"
+      "s_and_b64 %[f], %[f], %[t]\n\t"
+      "v_cmp_eq_u32_e64 %[t], %[need], %[x]\n\t"
+      "v_sub_co_u32_e64 %[klo], %[c], %[Klo], %[Qlo]\n\t"
+      "s_and_b64 %[f], %[f], %[t]\n\t"
+      "v_cndmask_b32_e64 %[x], 0, %[c24], %[b1]\n\t"
+      "v_cndmask_b32_e64 %[y], 0, %[c24], %[b3]\n\t"
+      "v_subb_co_u32_e64 %[khi], %[c], %[Khi], %[Qhi], %[c]\n\t"
+      "v_add_u32_e32 %[x], %[x], %[y]\n\t"
+      "s_nop 1\n\t"
+      "v_sub_co_u32_e64 %[klo], %[c], %[klo], %[x]\n\t"
+      "s_nop 1\n\t"
+      "v_subbrev_co_u32_e64 %[khi], %[c], 0, %[khi], %[c]\n\t"
+      "v_cndmask_b32_e64 %[klo], -1, %[klo], %[f]\n\t"
+      "v_cndmask_b32_e64 %[khi], -1, %[khi], %[f]"
+      : [klo] "=&v"(klo), [khi] "=&v"(khi), [x] "=&v"(x), [y] "=&v"(y), [f] "=&s"(f), [t] "=&s"(t), [b1] "=&s"(b1),
+        [b3] "=&s"(b3), [c] "=&s"(c)
+      : [r0] "v"(r0), [r1] "v"(r1), [r2] "v"(r2), [r3] "v"(r3), [lab] "v"(lab), [Klo] "v"((uint32_t)K),
+        [Khi] "v"((uint32_t)(K >> 32)), [l1] "v"(l1), [l3] "v"(l3), [q0] "s"(q0), [q1] "s"(q1), [q2] "s"(q2),
+        [q3] "s"(q3), [need] "s"(need), [Qlo] "v"((uint32_t)Q), [Qhi] "v"((uint32_t)(Q >> 32)), [ql1] "v"(ql1),
+        [ql3] "v"(ql3), [c24] "v"(c24)
+      : "scc");
+  return ((uint64_t)khi << 32) | klo;
+}
+
 // Grid: one block per 1024-node span (SC_WPB waves), wave w of the block takes group tile
 // blockIdx.y * SC_WPB + w.  All waves of a block read the same node chunks at about the same
 // time, so the node data comes from HBM once per window and the re-reads for the other group
@@ -859,6 +907,8 @@ __global__ __launch_bounds__(64 * SC_WPB) void scan_kernel(const int64_t* __rest
   uint64_t m[SC_GT], s2[SC_GT];
 #pragma unroll
   for (int g = 0; g < SC_GT; ++g) m[g] = s2[g] = NO_KEY;
+  uint32_t c24 = 1u << 24;                          // a VGPR operand (one SGPR per VALU op)
+  asm volatile("" : "+v"(c24));
   const int64_t base = (int64_t)wave_id * SC_SPAN;
   // stride is a multiple of 64, so a 64-node chunk is wholly inside [0, stride) or wholly past it:
   // a wave-uniform bound, no per-lane masks.  Nodes in [Ns, stride) are padding (residual NEVER,
@@ -888,10 +938,15 @@ __global__ __launch_bounds__(64 * SC_WPB) void scan_kernel(const int64_t* __rest
     if (__builtin_expect(__ballot(K == KEY_SLOW) == 0, 1)) {   // wave-uniform: no saturating node here
 #pragma unroll
       for (int g = 0; g < SC_GT; ++g) {
+#if PE_SCAN_ASM
+        const uint64_t k = fast_key(r0, r1, r2, r3, lab, K, l1, l3, q[g][0], q[g][1], q[g][2], q[g][3], need[g], Q[g],
+                                    ql1[g], ql3[g], c24);
+#else
         const bool fit = ((lab & need[g]) == need[g]) & (q[g][0] <= r0) & (q[g][1] <= r1) & (q[g][2] <= r2) &
                          (q[g][3] <= r3);
         const uint64_t borrow = ((uint64_t)(l1 < ql1[g]) + (uint64_t)(l3 < ql3[g])) << 24;
         const uint64_t k = fit ? K - Q[g] - borrow : NO_KEY;
+#endif
         const bool lt_m = k < m[g];
         const bool lt_s = k < s2[g];
         s2[g] = lt_m ? m[g] : (lt_s ? k : s2[g]);
