@@ -125,6 +125,7 @@ def main():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: batch = fit-jobs x n_gpus (fixed per-rank work); strong: batch = fit-jobs")
     ap.add_argument("--fit-path-mask", type=int, default=0, help="pe_config.fit_path_mask (0 = every kernel)")
+    ap.add_argument("--greedy-flags", type=int, default=0, help="pe_config.greedy_flags (bit0: pipelined windows)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -191,7 +192,8 @@ def main():
     J = args.fit_jobs * (world if args.scaling == "weak" else 1)
     inv = synth.make_inventory(N, synth.SEED["cfg5"], gpu_frac=0.2)
     eng = Engine(device, rank=rank, world_size=world, comm=cid, exchange=exchange, max_nodes=N, topk=args.topk,
-                 window_groups=args.window_groups, window_pods=args.window_pods, fit_path_mask=args.fit_path_mask)
+                 window_groups=args.window_groups, window_pods=args.window_pods, fit_path_mask=args.fit_path_mask,
+                 greedy_flags=args.greedy_flags)
     eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     b, e = eng.shard_range()
     Ns = e - b

@@ -95,6 +95,12 @@ typedef struct {
                                     block-major kernel (PE_MASK_NODE_BLOCKS) instead of the row-major
                                     sweep (PE_MASK_ROWS); no kernel bit set = all kernels (the
                                     int64 path is always allowed) */
+  int32_t greedy_flags;          /* bit0 set = pipelined greedy windows: the GPU scans the next window
+                                    while the host resolves the current one (exact; the current
+                                    window's changes are seeded as dirty).  Off by default: best-fit
+                                    packs consecutive windows onto the same nodes, so the seeded
+                                    nodes shorten the next lists and the extra rescans cost more than
+                                    the overlap saves (profiles/r5_greedy_pipeline.txt) */
 } pe_config;
 
 typedef struct {

@@ -10,7 +10,7 @@ TAG=${1:-r1}; shift || true
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_${TAG}
 mkdir -p $OUT
-BENCH_SMALL="--steps 2 --warmup 1 --no-greedy --no-cpu-baseline"
+BENCH_SMALL="--steps 2 --warmup 1 --no-greedy --no-configs --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- \
   python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > $OUT/bench_trace.json 2> $OUT/trace.err
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- \

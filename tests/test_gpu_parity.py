@@ -375,3 +375,19 @@ def test_greedy_score_corner_nodes(eng, case):
         batch.group_req[:, 1] += (np.arange(len(batch.group_count)) % 7) * 131071
         batch.group_req[:, 3] += (np.arange(len(batch.group_count)) % 5) * 9_999_991
     check_greedy(eng, inv, batch)
+
+
+@pytest.mark.parametrize("mix,N,J,topk,wg", [("mixed", 3000, 400, 64, 64), ("mixed", 1500, 300, 2, 8),
+                                             ("gang8", 500, 150, 4, 16), ("pytorch", 2000, 300, 1, 1)])
+def test_greedy_pipelined_vs_sequential(mix, N, J, topk, wg):
+    """The pipelined window loop (next window scanned while the host resolves the current one,
+    the current window's changes seeded as dirty) against the sequential loop and the oracle --
+    small K / windows force many discarded speculations (rescans) and cross-window rollbacks."""
+    inv = synth.make_inventory(N, 61 + N, 0.4)
+    batch = synth.make_jobs(J, 67 + J, mix)
+    res = {}
+    for flags in (1, 0):     # bit0: pipelined windows
+        e = Engine(0, topk=topk, window_groups=wg, greedy_flags=flags)
+        res[flags] = check_greedy(e, inv, batch)
+        e.close()
+    np.testing.assert_array_equal(res[0], res[1])

@@ -96,6 +96,7 @@ struct pe_ctx {
   pe_allgather_fn exchange = nullptr;
   void* exchange_user = nullptr;
   int topk = 64, window_groups = 64;
+  bool pipeline = false;  // greedy: scan window w+1 while the host resolves window w (opt-in)
   int64_t window_pods = 1024;
   int64_t max_nodes = 0;
   std::string gpu_name, err;
@@ -251,6 +252,7 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   ctx->gpu_name = cfg->gpu_resource_name ? cfg->gpu_resource_name : "amd.com/gpu";
   ctx->fit_path_mask = cfg->fit_path_mask & (PATHS_ALL | PATH_NO_THERM | PATH_PLANES_BLOCKS);
   ctx->pl_rows = !(ctx->fit_path_mask & PATH_PLANES_BLOCKS);
+  ctx->pipeline = (cfg->greedy_flags & 1) != 0;
   if (!(ctx->fit_path_mask & PATHS_ALL)) ctx->fit_path_mask |= PATHS_ALL;   // no kernel bits = all kernels
   ctx->fit_path_mask |= PATH_I64;                                           // always available
   int rc = PE_OK;
@@ -894,13 +896,11 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     hipchk(pe::launch_prep_nodes(ctx->stream, ctx->res.p, ctx->stride, ctx->Ns, (uint64_t)ctx->begin, ctx->g_kn.p,
                                  ctx->g_lo.p),
            "launch prep_nodes");
-    std::vector<int32_t> groups;
     std::vector<pe::GroupCands> cands;
-    std::vector<pe::Update> updates;
     hipStream_t s = ctx->stream;
-    while (!R.done()) {
-      R.next_window(Wmax, ctx->window_pods, groups);
-      if (groups.empty()) break;
+    const bool use_exchange = ctx->exchange && !(ctx->world == 1 && !ctx->comm);
+    // ---- one window on the device: group requests H2D, scan, merge, (RCCL all-gather), blob D2H
+    auto enqueue_window = [&](const std::vector<int32_t>& groups) {
       const int Wg = (int)groups.size();
       const int Wgp = (int)round_up(Wg, pe::SC_GT);
       for (int w = 0; w < Wgp; ++w) {
@@ -927,26 +927,38 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         hipchk(hipStreamSynchronize(s), "sync empty");
       }
       const size_t bytes = (size_t)Wg * gb;
-      const auto tw = std::chrono::steady_clock::now();
       if (ctx->world == 1 && !ctx->comm) {
         hipchk(hipMemcpyAsync(ctx->h_out.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
-        hipchk(hipStreamSynchronize(s), "sync window");
-      } else if (ctx->exchange) {
+      } else if (use_exchange) {
         hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
-        hipchk(hipStreamSynchronize(s), "sync window");
-        if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, ctx->h_out.p, bytes) != 0)
-          raise(PE_ERCCL, "exchange callback failed");
       } else {
         ncclchk(ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
         hipchk(hipMemcpyAsync(ctx->h_out.p, ctx->g_gath.p, bytes * ctx->world, hipMemcpyDeviceToHost, s),
                "D2H gathered");
-        hipchk(hipStreamSynchronize(s), "sync window");
+      }
+      ctx->stats.windows += 1;
+      ctx->stats.groups_scanned += Wg;
+      ctx->stats.scan_evals += (int64_t)Wg * ctx->Ns;
+    };
+    // ---- wait for the window's blob (and run the host exchange when one is configured), parse it
+    auto collect_window = [&](const std::vector<int32_t>& groups) {
+      const int Wg = (int)groups.size();
+      const size_t bytes = (size_t)Wg * gb;
+      const auto tw = std::chrono::steady_clock::now();
+      hipchk(hipStreamSynchronize(s), "sync window");
+      if (use_exchange) {
+        if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, ctx->h_out.p, bytes) != 0)
+          raise(PE_ERCCL, "exchange callback failed");
       }
       const auto th = std::chrono::steady_clock::now();
       ctx->stats.greedy_wait_ms += std::chrono::duration<double, std::milli>(th - tw).count();
       pe::parse_window(ctx->h_out.p, ctx->world, Wg, K, cands);
-      updates.clear();
-      R.resolve(groups, cands, updates);
+      ctx->stats.greedy_host_ms +=
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
+    };
+    // ---- residual updates of this shard H2D + apply (the pinned staging buffer is reused only
+    //      after the next collect_window's stream sync)
+    auto enqueue_apply = [&](const std::vector<pe::Update>& updates) {
       int64_t nu = 0;
       hipchk(ctx->h_upd.ensure(std::max<size_t>(updates.size(), 1) * (pe::D + 1)), "alloc pinned upd");
       for (const pe::Update& u : updates) {
@@ -956,8 +968,6 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         for (int d = 0; d < pe::D; ++d) o[1 + d] = u.res[d];
         ++nu;
       }
-      ctx->stats.greedy_host_ms +=
-          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
       if (nu > 0) {
         hipchk(ctx->g_upd.ensure((size_t)nu * (pe::D + 1)), "alloc upd");
         hipchk(hipMemcpyAsync(ctx->g_upd.p, ctx->h_upd.p, (size_t)nu * (pe::D + 1) * 8, hipMemcpyHostToDevice, s),
@@ -966,9 +976,63 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
                                 ctx->g_lo.p),
                "launch apply");
       }
-      ctx->stats.windows += 1;
-      ctx->stats.groups_scanned += Wg;
-      ctx->stats.scan_evals += (int64_t)Wg * ctx->Ns;
+    };
+    auto timed_resolve = [&](const std::vector<int32_t>& groups, std::vector<pe::Update>& updates,
+                             const std::vector<pe::Update>* seed) {
+      const auto th = std::chrono::steady_clock::now();
+      updates.clear();
+      const bool consumed = R.resolve(groups, cands, updates, seed);
+      ctx->stats.greedy_host_ms +=
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
+      return consumed;
+    };
+
+    std::vector<int32_t> cur, nxt;
+    std::vector<pe::Update> pending, seed;
+    pe::Cursor cur_end, nxt_end;
+    // The host exchange is a synchronous callback: it cannot sit behind queued device work.
+    const bool pipelined = ctx->pipeline && !use_exchange;
+    R.next_window_from(R.cursor(), Wmax, ctx->window_pods, cur, &cur_end);
+    if (!cur.empty()) enqueue_window(cur);
+    while (!cur.empty()) {
+      collect_window(cur);                       // cur's lists: snapshot = device state at its launch
+      if (!pipelined) {
+        std::vector<pe::Update> upd;
+        timed_resolve(cur, upd, nullptr);
+        enqueue_apply(upd);
+        if (R.done()) break;
+        R.next_window_from(R.cursor(), Wmax, ctx->window_pods, cur, &cur_end);
+        if (!cur.empty()) enqueue_window(cur);
+        continue;
+      }
+      // Pipelined (exact): the device applies the previous window's updates and scans the window
+      // that follows cur -- speculating that cur is consumed -- while the host resolves cur.  The
+      // next window's lists then miss only cur's own changes, which its resolution takes as dirty
+      // seeds (current state known here).  A window cut short, or a cursor that did not land where
+      // the speculation started, discards the speculative scan and rescans from the cursor.
+      R.next_window_from(cur_end, Wmax, ctx->window_pods, nxt, &nxt_end);
+      enqueue_apply(pending);                    // device: everything up to the previous window
+      pending.clear();
+      if (!nxt.empty()) enqueue_window(nxt);
+      std::vector<pe::Update> upd;
+      const bool consumed = timed_resolve(cur, upd, &seed);
+      if (R.done()) {
+        hipchk(hipStreamSynchronize(s), "sync speculative");
+        enqueue_apply(upd);
+        break;
+      }
+      if (consumed && !nxt.empty() && R.cursor() == cur_end) {
+        cur.swap(nxt);
+        cur_end = nxt_end;
+        seed = upd;                              // nxt's scan did not see cur's changes
+        pending = std::move(upd);
+        continue;
+      }
+      hipchk(hipStreamSynchronize(s), "sync discarded");   // speculative work done and dropped
+      enqueue_apply(upd);
+      seed.clear();
+      R.next_window_from(R.cursor(), Wmax, ctx->window_pods, cur, &cur_end);
+      if (!cur.empty()) enqueue_window(cur);
     }
     hipchk(hipStreamSynchronize(s), "sync greedy");
     if (P > 0) std::memcpy(out_pod_node, R.pod_node().data(), (size_t)P * 4);

@@ -47,6 +47,7 @@ int32_t DirtySet::upsert(int64_t g, const NodeState& st) {
     r2.push_back(0);
     r3.push_back(0);
     lab.push_back(0);
+    touched.push_back(0);
   }
   set(i, st);
   return i;
@@ -78,6 +79,7 @@ void DirtySet::clear() {
   r2.clear();
   r3.clear();
   lab.clear();
+  touched.clear();
 }
 
 // Branch-free Appendix-B key (same arithmetic as the device's node_key)
@@ -194,7 +196,7 @@ void Resolver::finish_job(bool ok) {
         --pods_placed_;
       }
     }
-    for (const auto& kv : job_nodes_) dirty_.upsert(kv.first, kv.second);
+    for (const auto& kv : job_nodes_) dirty_.mark(dirty_.upsert(kv.first, kv.second));
     job_status_[j] = 1;
     ++jobs_failed_;
   }
@@ -205,12 +207,19 @@ void Resolver::finish_job(bool ok) {
 }
 
 void Resolver::next_window(int max_groups, int64_t max_pods, std::vector<int32_t>& groups) {
+  Cursor end;
+  next_window_from(cursor(), max_groups, max_pods, groups, &end);
+}
+
+void Resolver::next_window_from(const Cursor& from, int max_groups, int64_t max_pods, std::vector<int32_t>& groups,
+                                Cursor* end) const {
   groups.clear();
-  if (done()) return;
+  *end = from;
+  if (from.oi >= (int64_t)order_.size()) return;
   int64_t pods = 0;
-  int64_t oi = oi_;
-  int32_t g = g_;
-  int32_t p = p_;
+  int64_t oi = from.oi;
+  int32_t g = from.g;
+  int32_t p = from.p;
   while (oi < (int64_t)order_.size() && (int)groups.size() < max_groups) {
     const int64_t j = order_[oi];
     if (g >= jgo_[j + 1]) {
@@ -227,11 +236,35 @@ void Resolver::next_window(int max_groups, int64_t max_pods, std::vector<int32_t
     ++g;
     p = 0;
   }
+  // normalise the end like advance_group() would: skip empty groups and finished jobs
+  while (oi < (int64_t)order_.size()) {
+    const int64_t j = order_[oi];
+    if (g >= jgo_[j + 1]) {
+      ++oi;
+      if (oi < (int64_t)order_.size()) g = jgo_[order_[oi]];
+      p = 0;
+      continue;
+    }
+    if (p >= cnt_[g]) {
+      ++g;
+      p = 0;
+      continue;
+    }
+    break;
+  }
+  *end = Cursor{oi, g, p};
 }
 
 bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<GroupCands>& cands,
-                       std::vector<Update>& updates) {
+                       std::vector<Update>& updates, const std::vector<Update>* seed) {
   bool consumed = true;
+  if (seed)
+    for (const Update& u : *seed) {
+      NodeState st;
+      for (int d = 0; d < RD; ++d) st.res[d] = u.res[d];
+      st.labels = u.labels;
+      dirty_.upsert(u.gid, st);   // dirty but untouched: not flushed again unless changed here
+    }
   size_t wi = 0;
   std::vector<uint64_t>& dk = dk_;  // keys of the dirty nodes for the current group
   auto argmin = [&dk]() -> int32_t {
@@ -286,6 +319,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       } else {
         dirty_.set(slot, st);
       }
+      dirty_.mark(slot);
       job_nodes_[gid] = st;
       pod_node_[pod_off_[g_] + p_] = (int32_t)gid;
       ++p_;
@@ -308,10 +342,12 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     ++wi;
   }
   for (size_t i = 0; i < dirty_.size(); ++i) {
+    if (!dirty_.touched[i]) continue;
     Update u;
     u.gid = dirty_.gid[i];
     const NodeState st = dirty_.get((int32_t)i);
     for (int d = 0; d < RD; ++d) u.res[d] = st.res[d];
+    u.labels = st.labels;
     updates.push_back(u);
   }
   dirty_.clear();

@@ -39,6 +39,15 @@ struct GroupCands {
 struct Update {
   int64_t gid;
   int64_t res[RD];
+  uint32_t labels;
+};
+
+// Position of the resolver in the (priority-ordered) pod sequence.
+struct Cursor {
+  int64_t oi = 0;  // position in the job order
+  int32_t g = 0;   // group index
+  int32_t p = 0;   // next pod of the group
+  bool operator==(const Cursor& o) const { return oi == o.oi && g == o.g && p == o.p; }
 };
 
 uint64_t score_of(const int64_t left[RD]);
@@ -59,6 +68,7 @@ class DirtySet {
   int32_t find(int64_t gid) const { return gid < (int64_t)slot_.size() ? slot_[gid] : -1; }
   int32_t upsert(int64_t gid, const NodeState& st);
   void set(int32_t i, const NodeState& st);
+  void mark(int32_t i) { touched[i] = 1; }
   NodeState get(int32_t i) const;
   size_t size() const { return gid.size(); }
   void clear();
@@ -67,6 +77,7 @@ class DirtySet {
   uint64_t key_at(int32_t i, const int64_t q[RD], uint32_t need) const;
   std::vector<int64_t> gid, r0, r1, r2, r3;
   std::vector<uint32_t> lab;
+  std::vector<uint8_t> touched;   // changed in this window (seeded entries start untouched)
 
  private:
   std::vector<int32_t> slot_;
@@ -78,12 +89,19 @@ class Resolver {
            const int64_t* group_req, const uint32_t* group_need);
 
   bool done() const { return oi_ >= (int64_t)order_.size(); }
-  // Groups (global ids, count > 0) of the next window, starting at the cursor.
+  // Groups (global ids, count > 0) of the next window, starting at the cursor (or at `from`);
+  // *end receives the cursor just past the window (where it stands if the window is consumed).
   void next_window(int max_groups, int64_t max_pods, std::vector<int32_t>& groups);
+  void next_window_from(const Cursor& from, int max_groups, int64_t max_pods, std::vector<int32_t>& groups,
+                        Cursor* end) const;
+  Cursor cursor() const { return Cursor{oi_, g_, p_}; }
   // Resolve with candidates for exactly the groups returned by next_window (same order).
   // Appends the residual updates to flush; returns true if the whole window was consumed.
+  // seed (pipelined form): nodes changed since the snapshot the candidates were scanned on, with
+  // their current state -- they start dirty, so the lists' clean entries stay exact; only nodes
+  // changed in THIS window are returned as updates.
   bool resolve(const std::vector<int32_t>& groups, const std::vector<GroupCands>& cands,
-               std::vector<Update>& updates);
+               std::vector<Update>& updates, const std::vector<Update>* seed = nullptr);
 
   const std::vector<int32_t>& pod_node() const { return pod_node_; }
   const std::vector<int32_t>& job_status() const { return job_status_; }

@@ -33,7 +33,8 @@ class PeConfig(ctypes.Structure):
     _fields_ = [("device_id", ctypes.c_int32), ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32),
                 ("comm_id", ctypes.c_void_p), ("exchange", ALLGATHER_FN), ("exchange_user", ctypes.c_void_p),
                 ("max_nodes", ctypes.c_int64), ("gpu_resource_name", ctypes.c_char_p), ("topk", ctypes.c_int32),
-                ("window_groups", ctypes.c_int32), ("window_pods", ctypes.c_int64), ("fit_path_mask", ctypes.c_int32)]
+                ("window_groups", ctypes.c_int32), ("window_pods", ctypes.c_int64), ("fit_path_mask", ctypes.c_int32),
+                ("greedy_flags", ctypes.c_int32)]
 
 
 class PeStats(ctypes.Structure):
