@@ -899,6 +899,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     std::vector<pe::GroupCands> cands;
     hipStream_t s = ctx->stream;
     const bool use_exchange = ctx->exchange && !(ctx->world == 1 && !ctx->comm);
+    // The host exchange is a synchronous callback: it cannot sit behind queued device work.
+    const bool pipelined = ctx->pipeline && !use_exchange;
     // ---- one window on the device: group requests H2D, scan, merge, (RCCL all-gather), blob D2H
     auto enqueue_window = [&](const std::vector<int32_t>& groups) {
       const int Wg = (int)groups.size();
@@ -952,7 +954,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       const auto th = std::chrono::steady_clock::now();
       ctx->stats.greedy_wait_ms += std::chrono::duration<double, std::milli>(th - tw).count();
-      pe::parse_window(ctx->h_out.p, ctx->world, Wg, K, cands);
+      // in place unless the pipelined loop will D2H the next blob into h_out before resolving
+      pe::parse_window(ctx->h_out.p, ctx->world, Wg, K, cands, pipelined);
       ctx->stats.greedy_host_ms +=
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
     };
@@ -990,8 +993,6 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     std::vector<int32_t> cur, nxt;
     std::vector<pe::Update> pending, seed;
     pe::Cursor cur_end, nxt_end;
-    // The host exchange is a synchronous callback: it cannot sit behind queued device work.
-    const bool pipelined = ctx->pipeline && !use_exchange;
     R.next_window_from(R.cursor(), Wmax, ctx->window_pods, cur, &cur_end);
     if (!cur.empty()) enqueue_window(cur);
     while (!cur.empty()) {

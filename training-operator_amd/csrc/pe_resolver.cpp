@@ -107,16 +107,19 @@ uint64_t DirtySet::key_at(int32_t i, const int64_t q[RD], uint32_t need) const {
 }
 
 void merge_shards(const std::vector<const GroupCands*>& parts, GroupCands& out) {
-  out.list.clear();
+  out.own.clear();
   out.limit = kNoKey;
   for (const GroupCands* p : parts) out.limit = std::min(out.limit, p->limit);
   for (const GroupCands* p : parts)
-    for (const Cand& c : p->list)
-      if (c.key < out.limit) out.list.push_back(c);
-  std::sort(out.list.begin(), out.list.end(), [](const Cand& a, const Cand& b) { return a.key < b.key; });
+    for (size_t i = 0; i < p->n; ++i)
+      if ((*p)[i].key < out.limit) out.own.push_back((*p)[i]);
+  std::sort(out.own.begin(), out.own.end(), [](const Cand& a, const Cand& b) { return a.key < b.key; });
+  out.data = out.own.data();
+  out.n = out.own.size();
 }
 
-void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands) {
+void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands,
+                  bool copy_blob) {
   const size_t gb = 16 + (size_t)K * 48;
   const size_t shard_bytes = (size_t)n_groups * gb;
   cands.resize((size_t)n_groups);
@@ -131,14 +134,11 @@ void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::v
       std::memcpy(&limit, base + 8, 8);
       GroupCands& gc = n_shards == 1 ? cands[w] : parts[r];
       gc.limit = limit;
-      gc.list.resize((size_t)std::max(n, 0));
-      for (int i = 0; i < n; ++i) {
-        const uint8_t* rec = base + 16 + (size_t)i * 48;
-        uint64_t lab;
-        std::memcpy(&gc.list[i].key, rec, 8);
-        std::memcpy(gc.list[i].res, rec + 8, 32);
-        std::memcpy(&lab, rec + 40, 8);
-        gc.list[i].labels = (uint32_t)lab;
+      gc.n = (size_t)std::max(n, 0);
+      gc.data = reinterpret_cast<const Cand*>(base + 16);   // 16-B aligned records in the blob
+      if (copy_blob && n_shards == 1) {
+        gc.own.assign(gc.data, gc.data + gc.n);
+        gc.data = gc.own.data();
       }
       pp[r] = &parts[r];
     }
@@ -288,10 +288,10 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     size_t ptr = 0;
     bool failed = false;
     while (p_ < cnt_[g_]) {
-      while (ptr < gc.list.size() && dirty_.find((int64_t)(gc.list[ptr].key & 0xFFFFFFull)) >= 0) ++ptr;
-      const uint64_t kc = ptr < gc.list.size() ? gc.list[ptr].key : kNoKey;
+      while (ptr < gc.size() && dirty_.find((int64_t)(gc[ptr].key & 0xFFFFFFull)) >= 0) ++ptr;
+      const uint64_t kc = ptr < gc.size() ? gc[ptr].key : kNoKey;
       const uint64_t kd = best >= 0 ? dk[best] : kNoKey;
-      if (ptr == gc.list.size() && gc.limit != kNoKey && kd >= gc.limit) {
+      if (ptr == gc.size() && gc.limit != kNoKey && kd >= gc.limit) {
         consumed = false;  // clean nodes beyond the limit could win: rescan from this pod
         break;
       }
@@ -307,7 +307,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         slot = best;
         st = dirty_.get(slot);
       } else {
-        const Cand& c = gc.list[ptr];
+        const Cand& c = gc[ptr];
         for (int d = 0; d < RD; ++d) st.res[d] = c.res[d];
         st.labels = c.labels;
         slot = -1;

@@ -25,15 +25,23 @@ struct NodeState {
   uint32_t labels;
 };
 
+// One candidate, byte-identical to the device's CandRec (labels in the low half of a u64), so a
+// single-shard window blob is read in place.
 struct Cand {
   uint64_t key;
   int64_t res[RD];
   uint32_t labels;
+  uint32_t pad_;
 };
+static_assert(sizeof(Cand) == 48, "Cand must match the 48-B device record");
 
 struct GroupCands {
-  std::vector<Cand> list;  // ascending keys, all clean at the snapshot
-  uint64_t limit = ~0ull;  // every clean node with key < limit is in list
+  const Cand* data = nullptr;  // ascending keys, all clean at the snapshot
+  size_t n = 0;
+  uint64_t limit = ~0ull;      // every clean node with key < limit is listed
+  std::vector<Cand> own;       // storage when the list is a copy (shard merge, or copy_blob)
+  size_t size() const { return n; }
+  const Cand& operator[](size_t i) const { return data[i]; }
 };
 
 struct Update {
@@ -59,7 +67,9 @@ void merge_shards(const std::vector<const GroupCands*>& parts, GroupCands& out);
 // Window blob = n_shards consecutive shard blocks, each n_groups x (16-B header {int32 n,
 // int32 flags, uint64 limit} + K x 48-B records {u64 key, i64 res[4], u64 labels}) -- exactly
 // what the merge kernel writes.  Parses and merges the shards into cands[n_groups].
-void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands);
+// With one shard and copy_blob = false the lists point INTO the blob, which must outlive them.
+void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands,
+                  bool copy_blob = false);
 
 // Nodes modified since the window's snapshot, as flat struct-of-arrays so the per-group re-score
 // is one branch-free (vectorisable) loop; gid -> slot is a direct-mapped array grown on demand.
