@@ -56,6 +56,7 @@ constexpr int SC_SPAN = 64 * SC_M;
 constexpr int SC_WPB = 16;     // scan: waves (group tiles) per block, all on one node span
 constexpr int MG_CAP = 8192;   // merge: LDS candidate capacity per group
 constexpr int MG_THREADS = 1024;
+constexpr int MG_SEL = 1024;   // merge: keys kept after the histogram cut (sorted instead of all)
 
 // ---- launch wrappers (return hipError_t of the launch)
 hipError_t launch_pg_min_resources(hipStream_t s, int mode, int64_t n_jobs, const int32_t* job_group_off,

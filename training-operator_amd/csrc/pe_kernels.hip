@@ -1005,15 +1005,30 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
                                                            const uint32_t* __restrict__ labels, uint64_t id_base,
                                                            uint8_t* __restrict__ out) {
   __shared__ uint64_t keys[MG_CAP];
+  __shared__ uint64_t sel[MG_SEL];
   __shared__ uint64_t red[MG_THREADS / 64];
-  __shared__ int total;
+  __shared__ int hist[256];
+  __shared__ int total, sel_n, sel_bin;
   const int g = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t gbase = (size_t)g * (size_t)nwaves;
 
-  // phase A: min bound over the wave lists (one list per thread, coalesced)
+  // Phase A+B in one round trip: each thread loads its wave list's bound, count and first PRE
+  // keys together (independent loads; list slots always exist); G = block min of the bounds; the
+  // loaded keys below G are appended to LDS with one atomic per wave (ballot/mbcnt ranks).
+  constexpr int PRE = 8;
   uint64_t b = NO_KEY;
-  for (int w = tid; w < nwaves; w += MG_THREADS) b = umin64(b, bound[gbase + w]);
+  int c0 = 0;
+  uint64_t k0[PRE];
+  {
+    const bool has = tid < nwaves;
+    b = has ? bound[gbase + tid] : NO_KEY;
+    c0 = has ? cnt[gbase + tid] : 0;
+    const uint64_t* lst = cand + (gbase + (has ? tid : 0)) * 64;
+#pragma unroll
+    for (int u = 0; u < PRE; ++u) k0[u] = lst[u];
+  }
+  for (int w = tid + MG_THREADS; w < nwaves; w += MG_THREADS) b = umin64(b, bound[gbase + w]);
   b = wave_min_u64(b);
   if (lane == 0) red[wave] = b;
   if (tid == 0) total = 0;
@@ -1021,14 +1036,23 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
   uint64_t G = NO_KEY;
 #pragma unroll
   for (int i = 0; i < MG_THREADS / 64; ++i) G = umin64(G, red[i]);
-  __syncthreads();
-
-  // phase B: every thread walks one list with independent loads (latency overlapped across the
-  // block instead of one dependent list per wave); keys below G are appended to LDS.
+  __syncthreads();                            // red[] is reused by the selection below
+  auto append = [&](uint64_t k, bool take) {
+    const uint64_t bal = __ballot(take);
+    if (bal == 0) return;
+    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+    int base = 0;
+    if (take && rank == 0) base = atomicAdd(&total, __popcll(bal));
+    base = __shfl(base, __ffsll((unsigned long long)bal) - 1, 64);
+    if (take && base + rank < MG_CAP) keys[base + rank] = k;
+  };
+#pragma unroll
+  for (int u = 0; u < PRE; ++u) append(k0[u], u < c0 && k0[u] < G);
+  // the rest of longer lists, and lists beyond the first MG_THREADS
   for (int w = tid; w < nwaves; w += MG_THREADS) {
-    const int c = cnt[gbase + w];
+    const int c = w == tid ? c0 : cnt[gbase + w];
     const uint64_t* lst = cand + (gbase + w) * 64;
-    for (int i0 = 0; i0 < c; i0 += 8) {
+    for (int i0 = w == tid ? PRE : 0; i0 < c; i0 += 8) {
       uint64_t k[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) k[u] = i0 + u < c ? lst[i0 + u] : NO_KEY;
@@ -1065,20 +1089,81 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
     limit = mn + 1;
     flags = 1;
   } else {
+    // Only the K + 1 smallest of the T candidates matter (K records + the limit).  For large T a
+    // 256-bin histogram of (key - min) >> shift finds the bin holding the (K+1)-th smallest; the
+    // keys up to that bin (typically ~K + a bin) are sorted instead of all T.
+    uint64_t* sk = keys;
+    int C = T;
+    if (T > 2 * (K + 1) && K + 1 <= MG_SEL) {
+      uint64_t mn = NO_KEY;
+      for (int i = tid; i < T; i += MG_THREADS) mn = umin64(mn, keys[i]);
+      mn = wave_min_u64(mn);
+      if (lane == 0) red[wave] = mn;
+      for (int i = tid; i < 256; i += MG_THREADS) hist[i] = 0;
+      if (tid == 0) sel_n = 0;
+      __syncthreads();
+      uint64_t kmin = NO_KEY;
+#pragma unroll
+      for (int i = 0; i < MG_THREADS / 64; ++i) kmin = umin64(kmin, red[i]);
+      const uint64_t span = G - kmin;   // every candidate is < G (G may be NO_KEY: no wave had a 2nd best)
+      const int bits = 64 - __clzll((long long)(span | 1));
+      const int sh = bits > 8 ? bits - 8 : 0;
+      for (int i = tid; i < T; i += MG_THREADS) atomicAdd(&hist[(int)((keys[i] - kmin) >> sh)], 1);
+      __syncthreads();
+      if (wave == 0) {                       // inclusive scan of 256 bins, 4 per lane
+        int h[4], sum = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          h[u] = hist[lane * 4 + u];
+          sum += h[u];
+        }
+        int incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const int o = __shfl_up(incl, off, 64);
+          if (lane >= off) incl += o;
+        }
+        int run = incl - sum, cut = 1 << 30;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          run += h[u];
+          if (run >= K + 1 && cut == (1 << 30)) cut = lane * 4 + u;
+        }
+        // first lane holding a cut bin
+        const uint64_t bal = __ballot(cut != (1 << 30));
+        const int first = __ffsll((unsigned long long)bal) - 1;
+        const int cb = __shfl(cut, first < 0 ? 0 : first, 64);
+        if (lane == 0) sel_bin = first < 0 ? 255 : cb;
+      }
+      __syncthreads();
+      const int cb = sel_bin;
+      for (int i = tid; i < T; i += MG_THREADS) {
+        const uint64_t k = keys[i];
+        if ((int)((k - kmin) >> sh) <= cb) {
+          const int pos = atomicAdd(&sel_n, 1);
+          if (pos < MG_SEL) sel[pos] = k;
+        }
+      }
+      __syncthreads();
+      if (sel_n <= MG_SEL) {                 // else (one bin held too many): sort all T
+        sk = sel;
+        C = sel_n;
+      }
+    }
     int P = 2;
-    while (P < T) P <<= 1;
-    for (int i = T + tid; i < P; i += MG_THREADS) keys[i] = NO_KEY;
+    while (P < C) P <<= 1;
+    for (int i = C + tid; i < P; i += MG_THREADS) sk[i] = NO_KEY;
     __syncthreads();
     for (int k = 2; k <= P; k <<= 1) {
       for (int j = k >> 1; j > 0; j >>= 1) {
         for (int i = tid; i < P; i += MG_THREADS) {
           const int ixj = i ^ j;
           if (ixj > i) {
-            const uint64_t a = keys[i], c = keys[ixj];
+            const uint64_t a = sk[i], c = sk[ixj];
             const bool up = (i & k) == 0;
             if ((a > c) == up) {
-              keys[i] = c;
-              keys[ixj] = a;
+              sk[i] = c;
+              sk[ixj] = a;
             }
           }
         }
@@ -1086,7 +1171,10 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
       }
     }
     nout = T < K ? T : K;
-    limit = T > K ? keys[K] : G;
+    limit = T > K ? sk[K] : G;     // sk holds the K + 1 smallest of all T in order
+    if (sk != keys)
+      for (int i = tid; i < nout; i += MG_THREADS) keys[i] = sk[i];
+    __syncthreads();
   }
   uint8_t* og = out + (size_t)g * cand_group_bytes(K);
   CandRec* recs = reinterpret_cast<CandRec*>(og + sizeof(CandHdr));
