@@ -176,8 +176,9 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
  *     ((j / 16) * Wt + c / 4) * 64 + (j % 16) * 4 + c % 4,   Wt = ceil(words_per_row / 4)
  *   PE_MASK_JOB_BITS (dictionary-coded path): word (b, n) holds jobs 64b..64b+63 (bit j%64) for
  *     node n at b * S + n,  S = shard nodes rounded up to 512
- *   PE_MASK_ROWS (bit-plane path, default): row-major, word (j, c) at j * ceil(S / 8192) * 128 + c
- *     (S = shard nodes; rows padded to whole 8192-node blocks, padding bits 0)
+ *   PE_MASK_ROWS (bit-plane path, default): row-major, word (j, c) at j * P + c, P =
+ *     pe_fit_mask_row_pitch (a whole number of 8192-node blocks, >= ceil(S / 8192) * 128 words;
+ *     S = shard nodes; padding bits 0)
  *   PE_MASK_NODE_BLOCKS (bit-plane path, fit_path_mask bit5): word (j, c) at
  *     ((c / 128) * J + j) * 128 + c % 128, i.e. per 8192-node block a [J][128]-word slab
  * All layouts are written as whole 128-B lines.  pe_fit_mask_rows always hands rows back
@@ -192,6 +193,9 @@ int pe_fit_counts(pe_ctx* ctx, int64_t* out_feasible_count); /* synchronizes */
 int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out /*[n_rows][words_per_row]*/);
 enum { PE_MASK_NODE_TILES = 0, PE_MASK_JOB_BITS = 1, PE_MASK_NODE_BLOCKS = 2, PE_MASK_ROWS = 3 };
 int pe_fit_mask_layout(const pe_ctx* ctx, int32_t* layout);
+/* u64 words between consecutive job rows of the device mask in the PE_MASK_ROWS layout (0 for
+ * the other layouts). */
+int pe_fit_mask_row_pitch(const pe_ctx* ctx, int64_t* words);
 
 /* Greedy best-fit all-or-nothing gang placement.  Jobs in (priority
  * desc, index asc) order, groups of a job in the given order, pods of a group identical.

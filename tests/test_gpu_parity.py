@@ -177,6 +177,24 @@ def test_fit_mask_paths(path, N, J):
     e.close()
 
 
+@pytest.mark.parametrize("N,J,pitch_blocks", [(62 * 8192 - 100, 300, 62), (123 * 8192 - 5000, 64, 123),
+                                              (100 * 8192, 70, 100), (5000, 8, 1)])
+def test_fit_mask_rows_pitch(N, J, pitch_blocks):
+    """Row-major planes mask: the reported row pitch, zero padding bits past the last node (counts
+    would include them otherwise), rows handed back exact (first and last rows)."""
+    e = Engine(0)
+    inv = synth.make_inventory(N, 17 + N % 97, 0.4)
+    req, need = synth.make_fit_jobs(J, 19 + J)
+    e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    counts = e.fit_mask(req, need)
+    o_mask, o_counts = oracle.fit_mask(inv.residual(), inv.labels, req, need)
+    assert e.fit_mask_layout() == 3 and e.fit_mask_row_pitch() == pitch_blocks * 128
+    np.testing.assert_array_equal(counts, o_counts)
+    np.testing.assert_array_equal(e.fit_mask_rows(0, J), o_mask)
+    np.testing.assert_array_equal(e.fit_mask_rows(J - 3, 3), o_mask[J - 3:])
+    e.close()
+
+
 @pytest.mark.parametrize("case", ["many_values", "odd_bytes", "label_antichain", "many_planes", "extreme_values"])
 def test_fit_mask_path_fallbacks(eng, case):
     """Each batch shape lands on the path that can hold it (planes > coded > int32 > int64), exact."""

@@ -168,6 +168,21 @@ __global__ __launch_bounds__(256) void linear_bar(u32x4* __restrict__ out, int64
   }
 }
 
+// The rows fit pattern: wave (blk, r) writes KiB (r + i*R) * pitch + blk for its jobs i (row pitch
+// `pitch` KiB, `nblk` KiB written per row; pitch > nblk leaves a hole at the end of every row).
+__global__ __launch_bounds__(256) void rows(u32x4* __restrict__ out, int64_t nblk, int64_t pitch, int64_t J,
+                                            int64_t R) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t blk = w % nblk, r = w / nblk;
+  if (r >= R) return;
+  u32x4 v = {(uint32_t)w, 1u, 2u, 3u};
+  for (int64_t j = r; j < J; j += R) {
+    v = spin<40>(v);
+    out[(j * pitch + blk) * 64 + lane] = v;
+  }
+}
+
 static float time_it(void (*launch)(void*), void* arg, hipEvent_t a, hipEvent_t b, int reps = 5) {
   launch(arg);
   hipDeviceSynchronize();
@@ -220,6 +235,9 @@ static void go(const Arg& a) {
     if (a.S == 1) hipLaunchKernelGGL(linear_bar<1>, g, dim3(256), a.lds, 0, a.out, a.nwaves, a.kib);
     else if (a.S == 4) hipLaunchKernelGGL(linear_bar<4>, g, dim3(256), a.lds, 0, a.out, a.nwaves, a.kib);
     else hipLaunchKernelGGL(linear_bar<16>, g, dim3(256), a.lds, 0, a.out, a.nwaves, a.kib);
+  } else if (a.kind == 8) {
+    hipLaunchKernelGGL(rows, dim3((unsigned)((a.nblk * a.R + 3) / 4)), dim3(256), a.lds, 0, a.out, a.nblk, a.chunk,
+                       a.J, (int64_t)a.R);
   } else if (a.kind == 3) {
     const int64_t waves = (a.kib + a.chunk - 1) / a.chunk;
     hipLaunchKernelGGL((oneshot<POL, DLY>), dim3((unsigned)((waves + 3) / 4)), dim3(256), a.lds, 0, a.out, a.kib,
@@ -253,7 +271,7 @@ int main() {
   const int64_t kib = nblk * J;   // 12.6 GB
   const double bytes = (double)kib * 1024.0;
   u32x4* out;
-  CHK(hipMalloc(&out, (size_t)bytes));
+  CHK(hipMalloc(&out, (size_t)(132 * J) * 1024));
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
@@ -268,18 +286,21 @@ int main() {
   g.lds = 98304;   // one workgroup (4 waves) per CU, like the rows kernel
   g.pol = 0;
   g.dly = 40;
-  for (int64_t W : {984L, 1024L}) {
-    g.kind = 1;
-    g.nwaves = W;
-    snprintf(name, sizeof name, "linear W=%ld dly=40 1 WG/CU", (long)W);
-    rep(name, time_it(launch, &g, a, b));
-    for (int S : {1, 4, 16}) {
-      g.kind = 7;
-      g.S = S;
-      snprintf(name, sizeof name, "linear_bar W=%ld S=%d 1 WG/CU", (long)W, S);
-      rep(name, time_it(launch, &g, a, b));
+  struct RowCase { int64_t nblk, pitch, R; };
+  for (int pass = 0; pass < 2; ++pass)
+    for (RowCase c : {RowCase{123, 123, 8}, RowCase{123, 128, 8}, RowCase{128, 128, 8}, RowCase{123, 123, 16},
+                      RowCase{123, 128, 16}, RowCase{128, 128, 16}, RowCase{123, 124, 8}, RowCase{123, 132, 8}}) {
+      g.kind = 8;
+      g.nblk = c.nblk;
+      g.chunk = c.pitch;
+      g.R = (int)c.R;
+      g.lds = c.R == 8 ? 98304 : 0;
+      const float ms = time_it(launch, &g, a, b);
+      snprintf(name, sizeof name, "rows nblk=%ld pitch=%ld R=%ld (bytes/written %.3f)", (long)c.nblk, (long)c.pitch,
+               (long)c.R, (double)c.nblk / 123.0);
+      // rate over the bytes actually written
+      printf("%-58s %7.3f ms  %5.2f TB/s written\n", name, ms, bytes * (double)c.nblk / 123.0 / (ms * 1e-3) / 1e12);
     }
-  }
   rep("hipMemsetD32 again", time_it(memset_launch, &g, a, b));
   hipFree(out);
   return 0;

@@ -597,7 +597,9 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const 
   ctx->plane = sp;
   ctx->pl_nblk = (std::max<int64_t>(ctx->Ns, 1) + pe::PL_BLK - 1) / pe::PL_BLK;
   if (ctx->pl_rows) {
-    // one wave per SIMD (1024 on 256 CUs) = nblk x R job phases; codes phase-major
+    // one wave per SIMD (1024 on 256 CUs) = nblk x R job phases; codes phase-major.  (Padding the
+    // row to 1024 / R blocks, i.e. an aligned 1 MiB store window, was measured no faster:
+    // profiles/r5c_row_pitch.txt.)
     const int64_t R = std::min<int64_t>(n_jobs, std::max<int64_t>(1, 1024 / ctx->pl_nblk));
     const int64_t Jr = ((n_jobs + R - 1) / R + 3) / 4 * 4;   // = the kernel's phase stride
     std::vector<uint64_t> perm((size_t)(R * Jr), 0);
@@ -775,7 +777,7 @@ int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out) {
     if (row0 < 0 || n_rows < 0 || row0 + n_rows > ctx->fit_J) raise(PE_EINVAL, "row range");
     if (n_rows == 0 || ctx->Wn == 0) return PE_OK;
     need_ptr(out, "out");
-    if (ctx->fit_path == 3 && ctx->pl_rows) {   // row-major, rows padded to whole 8192-node blocks
+    if (ctx->fit_path == 3 && ctx->pl_rows) {   // row-major, row pitch pl_nblk 8192-node blocks
       hipchk(hipMemcpy2DAsync(out, (size_t)ctx->Wn * 8, ctx->mask.p + (size_t)row0 * ctx->pl_nblk * 128,
                               (size_t)ctx->pl_nblk * 128 * 8, (size_t)ctx->Wn * 8, (size_t)n_rows,
                               hipMemcpyDeviceToHost, ctx->stream),
@@ -1051,6 +1053,12 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
 int pe_fit_mask_layout(const pe_ctx* ctx, int32_t* layout) {
   if (!ctx || !layout) return PE_EINVAL;
   *layout = ctx->fit_path == 3 ? (ctx->pl_rows ? PE_MASK_ROWS : PE_MASK_NODE_BLOCKS) : ctx->fit_path == 2 ? PE_MASK_JOB_BITS : PE_MASK_NODE_TILES;
+  return PE_OK;
+}
+
+int pe_fit_mask_row_pitch(const pe_ctx* ctx, int64_t* words) {
+  if (!ctx || !words) return PE_EINVAL;
+  *words = ctx->fit_path == 3 && ctx->pl_rows ? ctx->pl_nblk * 128 : 0;
   return PE_OK;
 }
 

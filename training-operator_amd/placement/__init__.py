@@ -196,6 +196,11 @@ class Engine:
         self._chk(self.lib.pe_fit_mask_layout(self.h, ctypes.byref(v)), "pe_fit_mask_layout")
         return v.value
 
+    def fit_mask_row_pitch(self) -> int:
+        v = ctypes.c_int64()
+        self._chk(self.lib.pe_fit_mask_row_pitch(self.h, ctypes.byref(v)), "pe_fit_mask_row_pitch")
+        return v.value
+
     def fit_mask_rows(self, row0: int, n_rows: int) -> np.ndarray:
         b, e = self.shard_range()
         w = (e - b + 63) // 64

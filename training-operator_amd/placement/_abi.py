@@ -71,6 +71,7 @@ SIGNATURES = {
     "pe_fit_counts": (ctypes.c_int, [P, P]),
     "pe_fit_mask_rows": (ctypes.c_int, [P, i64, i64, P]),
     "pe_fit_mask_layout": (ctypes.c_int, [P, ctypes.POINTER(i32)]),
+    "pe_fit_mask_row_pitch": (ctypes.c_int, [P, ctypes.POINTER(i64)]),
     "pe_place_greedy": (ctypes.c_int, [P, i64, P, P, P, P, P, P, P]),
     "pe_resolver_create": (ctypes.c_int, [i64, P, P, P, P, P, ctypes.POINTER(P)]),
     "pe_resolver_destroy": (None, [P]),
