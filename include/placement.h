@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 1
+#define PE_ABI_VERSION 2
 #define PE_DIMS 4
 #define PE_COMM_ID_BYTES 128
 #define PE_MAX_NODES (1LL << 24) /* node ids live in the low 24 bits of the best-fit key */
@@ -100,12 +100,16 @@ typedef struct {
                                     window's changes are seeded as dirty).  Off by default: best-fit
                                     packs consecutive windows onto the same nodes, so the seeded
                                     nodes shorten the next lists and the extra rescans cost more than
-                                    the overlap saves (profiles/r5_greedy_pipeline.txt) */
+                                    the overlap saves (profiles/r5_greedy_pipeline.txt).
+                                    bit1 set = every window scans all nodes of the shard (scan +
+                                    merge kernels) instead of the sorted walk */
+  int32_t resort_nodes;          /* sorted walk: rebuild the sorted index once this many node updates
+                                    were applied since the last build (0 = 4096) */
 } pe_config;
 
 typedef struct {
   int64_t fit_evals;     /* job x node fit evaluations (fit mask) */
-  int64_t scan_evals;    /* group x node key evaluations (greedy scans) */
+  int64_t scan_evals;    /* group x node key evaluations (greedy full scans, greedy_flags bit1) */
   int64_t windows;       /* greedy scan windows */
   int64_t rescans;       /* windows cut short because a candidate list ran dry */
   int64_t groups_scanned;
@@ -120,6 +124,7 @@ typedef struct {
   int64_t fit_runs_coded; /* fit-mask launches on the dictionary-coded path (SWAR or thermometer) */
   int64_t fit_runs_therm; /* ... of which used the thermometer code (3 VALU per 64 evaluations) */
   int64_t fit_runs_planes; /* fit-mask launches on the bit-plane path (5-way AND per 32 nodes) */
+  int64_t resorts;       /* sorted-walk index builds (greedy) */
 } pe_stats;
 
 int pe_abi_version(void);

@@ -1,6 +1,7 @@
 """The C-ABI library loads and exports exactly what include/placement.h declares (no GPU)."""
 import ctypes
 import os
+import subprocess
 import re
 
 import pytest
@@ -28,12 +29,24 @@ def test_every_declared_symbol_is_exported():
     assert set(declared) == set(_abi.SIGNATURES), set(declared) ^ set(_abi.SIGNATURES)
 
 
-def test_abi_version_and_structs():
+def test_abi_version_and_structs(tmp_path):
     lib = _abi.load()
-    assert lib.pe_abi_version() == 1
-    # pe_config / pe_stats layouts mirrored in _abi must match the C sizes (x86-64)
-    assert ctypes.sizeof(_abi.PeConfig) == 80
-    assert ctypes.sizeof(_abi.PeStats) == 128
+    assert lib.pe_abi_version() == 2
+    # pe_config / pe_stats layouts mirrored in _abi must match the C compiler's (size and offsets)
+    src = tmp_path / "sz.c"
+    fields = [f for f, _ in _abi.PeConfig._fields_]
+    sfields = [f for f, _ in _abi.PeStats._fields_]
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "placement.h"\nint main(void){'
+                   'printf("%zu %zu\\n", sizeof(pe_config), sizeof(pe_stats));'
+                   + "".join(f'printf("%zu\\n", offsetof(pe_config, {f}));' for f in fields)
+                   + "".join(f'printf("%zu\\n", offsetof(pe_stats, {f}));' for f in sfields) + "return 0;}")
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(_abi.HEADER), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    assert int(out[0]) == ctypes.sizeof(_abi.PeConfig) and int(out[1]) == ctypes.sizeof(_abi.PeStats)
+    offs = [int(x) for x in out[2:]]
+    assert offs[:len(fields)] == [getattr(_abi.PeConfig, f).offset for f in fields]
+    assert offs[len(fields):] == [getattr(_abi.PeStats, f).offset for f in sfields]
 
 
 def test_no_cpu_fallback_without_gpu():

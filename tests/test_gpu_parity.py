@@ -409,3 +409,35 @@ def test_greedy_pipelined_vs_sequential(mix, N, J, topk, wg):
         res[flags] = check_greedy(e, inv, batch)
         e.close()
     np.testing.assert_array_equal(res[0], res[1])
+
+
+@pytest.mark.parametrize("flags,resort", [(2, 0), (0, 1), (0, 64), (1, 16), (3, 0)])
+@pytest.mark.parametrize("mix,N,J,gpu_frac,topk,wg", [("mixed", 3000, 300, 0.3, 64, 64), ("pytorch", 2500, 300, 0.2, 2, 8),
+                                                       ("gang8", 700, 150, 1.0, 4, 16), ("mixed", 5000, 200, 0.5, 1, 1)])
+def test_greedy_walk_and_full_scan(flags, resort, mix, N, J, gpu_frac, topk, wg):
+    """Both window paths against the oracle: the sorted walk (default; resort_nodes 1 rebuilds the
+    sorted index after every applied window, 64 / 16 let the overlay grow across many windows) and
+    the full scan + merge (greedy_flags bit1), sequential and pipelined (bit0)."""
+    e = Engine(0, topk=topk, window_groups=wg, greedy_flags=flags, resort_nodes=resort)
+    inv = synth.make_inventory(N, 71 + N, gpu_frac)
+    batch = synth.make_jobs(J, 73 + J, mix)
+    check_greedy(e, inv, batch)
+    s = e.stats()
+    assert (s["resorts"] > 0) == (not flags & 2)
+    assert (s["scan_evals"] > 0) == bool(flags & 2)
+    if resort == 1:
+        assert s["resorts"] >= s["windows"] // 2
+    e.close()
+
+
+def test_greedy_walk_overlay_compaction():
+    """Overlay larger than the LDS candidate buffer (every node updated, resort never triggers):
+    the walk's in-loop compaction to the K + 1 smallest keeps the lists exact."""
+    N = 20_000
+    e = Engine(0, topk=64, resort_nodes=1 << 30)
+    inv = synth.make_inventory(N, 83, 0.3)
+    batch = synth.make_jobs(4000, 89, "mixed")
+    check_greedy(e, inv, batch)
+    s = e.stats()
+    assert s["resorts"] == 1
+    e.close()

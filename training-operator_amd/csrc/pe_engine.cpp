@@ -146,6 +146,15 @@ struct pe_ctx {
   HostBuf<ReqRec> h_groups;
   HostBuf<uint8_t> h_out, h_own;
   HostBuf<int64_t> h_upd;
+  // greedy sorted walk (pe_kernels.h WalkIndex; the default window path, greedy_flags bit1 = full scan)
+  bool walk = true;
+  int64_t resort_nodes = 4096;   // re-sort once this many applied updates joined the overlay
+  int64_t w_est = 0;             // updates applied since the last sort (>= overlay size)
+  DevBuf<uint64_t> w_sk, w_kin, w_rmin;
+  DevBuf<int64_t> w_sr, w_rmax;
+  DevBuf<uint32_t> w_sl, w_pos, w_ror, w_inovl;
+  DevBuf<int32_t> w_ovl, w_ovln;
+  DevBuf<uint8_t> w_temp;
   pe_stats stats{};
 
   ~pe_ctx() {
@@ -159,6 +168,8 @@ struct pe_ctx {
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
     g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_out.release(); h_own.release(); h_upd.release();
+    w_sk.release(); w_kin.release(); w_rmin.release(); w_sr.release(); w_rmax.release(); w_sl.release(); w_pos.release();
+    w_ror.release(); w_inovl.release(); w_ovl.release(); w_ovln.release(); w_temp.release();
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -253,6 +264,9 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   ctx->fit_path_mask = cfg->fit_path_mask & (PATHS_ALL | PATH_NO_THERM | PATH_PLANES_BLOCKS);
   ctx->pl_rows = !(ctx->fit_path_mask & PATH_PLANES_BLOCKS);
   ctx->pipeline = (cfg->greedy_flags & 1) != 0;
+  ctx->walk = (cfg->greedy_flags & 2) == 0;
+  if (cfg->resort_nodes < 0) raise(PE_EINVAL, "resort_nodes < 0");
+  ctx->resort_nodes = cfg->resort_nodes > 0 ? cfg->resort_nodes : 4096;
   if (!(ctx->fit_path_mask & PATHS_ALL)) ctx->fit_path_mask |= PATHS_ALL;   // no kernel bits = all kernels
   ctx->fit_path_mask |= PATH_I64;                                           // always available
   int rc = PE_OK;
@@ -846,6 +860,57 @@ int pe_fit_mask(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t*
 
 // ------------------------------------------------------------------ greedy placement
 
+// The sorted-walk index of the shard over the current residuals (g_kn must be current): sort the
+// walkable nodes by K(n), gather the sorted SoA copy and the round summaries, empty the overlay
+// (then holding only the saturating nodes).
+static pe::WalkIndex walk_index(pe_ctx* ctx) {
+  pe::WalkIndex w{};
+  w.sk = ctx->w_sk.p;
+  w.sr = ctx->w_sr.p;
+  w.sl = ctx->w_sl.p;
+  w.pos = ctx->w_pos.p;
+  w.rmin = ctx->w_rmin.p;
+  w.rmax = ctx->w_rmax.p;
+  w.ror = ctx->w_ror.p;
+  w.ovl = ctx->w_ovl.p;
+  w.ovl_n = ctx->w_ovln.p;
+  w.in_ovl = ctx->w_inovl.p;
+  w.sstride = ctx->stride;
+  w.nr = (ctx->Ns + pe::WK_ROUND - 1) / pe::WK_ROUND;
+  return w;
+}
+
+static void walk_resort(pe_ctx* ctx) {
+  hipStream_t s = ctx->stream;
+  const int64_t Ns = ctx->Ns, st = std::max<int64_t>(ctx->stride, 1);
+  const int64_t nr = std::max<int64_t>(1, (Ns + pe::WK_ROUND - 1) / pe::WK_ROUND);
+  if (nr > pe::WK_MAXR) raise(PE_EINVAL, "shard too large for the sorted walk");
+  hipchk(ctx->w_sk.ensure(st), "alloc walk keys");
+  hipchk(ctx->w_kin.ensure(st), "alloc walk keys");
+  hipchk(ctx->w_sr.ensure((size_t)pe::D * st), "alloc walk residuals");
+  hipchk(ctx->w_sl.ensure(st), "alloc walk labels");
+  hipchk(ctx->w_pos.ensure(st), "alloc walk pos");
+  hipchk(ctx->w_rmin.ensure(nr), "alloc walk rounds");
+  hipchk(ctx->w_rmax.ensure((size_t)pe::D * nr), "alloc walk rounds");
+  hipchk(ctx->w_ror.ensure(nr), "alloc walk rounds");
+  hipchk(ctx->w_ovl.ensure(st), "alloc overlay");
+  hipchk(ctx->w_ovln.ensure(1), "alloc overlay");
+  hipchk(ctx->w_inovl.ensure(st), "alloc overlay");
+  size_t tb = 0;
+  hipchk(pe::sort_keys_u64(nullptr, &tb, ctx->w_kin.p, ctx->w_sk.p, Ns, s), "sort size");
+  hipchk(ctx->w_temp.ensure(tb), "alloc sort scratch");
+  const pe::WalkIndex w = walk_index(ctx);
+  hipchk(hipMemsetAsync(ctx->w_ovln.p, 0, sizeof(int32_t), s), "memset overlay");
+  hipchk(hipMemsetAsync(ctx->w_inovl.p, 0, (size_t)st * 4, s), "memset overlay");
+  hipchk(hipMemsetAsync(ctx->w_pos.p, 0xFF, (size_t)st * 4, s), "memset pos");
+  hipchk(pe::launch_walk_prep(s, ctx->res.p, ctx->stride, Ns, ctx->g_kn.p, ctx->w_kin.p, w), "launch walk_prep");
+  hipchk(pe::sort_keys_u64(ctx->w_temp.p, &tb, ctx->w_kin.p, ctx->w_sk.p, Ns, s), "sort walk keys");
+  hipchk(pe::launch_walk_build(s, ctx->res.p, ctx->stride, ctx->labels.p, Ns, (uint64_t)ctx->begin, w),
+         "launch walk_build");
+  ctx->w_est = 0;
+  ctx->stats.resorts += 1;
+}
+
 int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority,
                     const int32_t* group_count, const int64_t* group_req, const uint32_t* group_need,
                     int32_t* out_pod_node, int32_t* out_job_status) {
@@ -898,6 +963,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     hipchk(pe::launch_prep_nodes(ctx->stream, ctx->res.p, ctx->stride, ctx->Ns, (uint64_t)ctx->begin, ctx->g_kn.p,
                                  ctx->g_lo.p),
            "launch prep_nodes");
+    const bool walk = ctx->walk && ctx->Ns > 0;
+    if (walk) walk_resort(ctx);
     std::vector<pe::GroupCands> cands;
     hipStream_t s = ctx->stream;
     const bool use_exchange = ctx->exchange && !(ctx->world == 1 && !ctx->comm);
@@ -913,7 +980,12 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       hipchk(hipMemcpyAsync(ctx->g_groups.p, ctx->h_groups.p, Wgp * sizeof(ReqRec), hipMemcpyHostToDevice, s),
              "H2D window");
-      if (ctx->Ns > 0) {
+      if (walk) {
+        if (ctx->w_est > ctx->resort_nodes) walk_resort(ctx);
+        hipchk(pe::launch_walk(s, ctx->g_groups.p, Wg, K, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p,
+                               ctx->Ns, (uint64_t)ctx->begin, ctx->g_out.p),
+               "launch walk");
+      } else if (ctx->Ns > 0) {
         hipchk(pe::launch_scan(s, ctx->res.p, ctx->stride, ctx->labels.p, ctx->g_kn.p, ctx->g_lo.p, ctx->Ns,
                                (uint64_t)ctx->begin, ctx->g_groups.p, Wg, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p,
                                nwaves),
@@ -942,7 +1014,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       ctx->stats.windows += 1;
       ctx->stats.groups_scanned += Wg;
-      ctx->stats.scan_evals += (int64_t)Wg * ctx->Ns;
+      if (!walk) ctx->stats.scan_evals += (int64_t)Wg * ctx->Ns;
     };
     // ---- wait for the window's blob (and run the host exchange when one is configured), parse it
     auto collect_window = [&](const std::vector<int32_t>& groups) {
@@ -977,9 +1049,11 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         hipchk(ctx->g_upd.ensure((size_t)nu * (pe::D + 1)), "alloc upd");
         hipchk(hipMemcpyAsync(ctx->g_upd.p, ctx->h_upd.p, (size_t)nu * (pe::D + 1) * 8, hipMemcpyHostToDevice, s),
                "H2D upd");
+        const pe::WalkIndex w = walk_index(ctx);
         hipchk(pe::launch_apply(s, ctx->res.p, ctx->stride, ctx->g_upd.p, nu, (uint64_t)ctx->begin, ctx->g_kn.p,
-                                ctx->g_lo.p),
+                                ctx->g_lo.p, walk ? &w : nullptr),
                "launch apply");
+        ctx->w_est += nu;
       }
     };
     auto timed_resolve = [&](const std::vector<int32_t>& groups, std::vector<pe::Update>& updates,

@@ -154,10 +154,48 @@ hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt,
                         int nwaves, int K, const int64_t* res, int64_t stride, const uint32_t* labels,
                         uint64_t id_base, uint8_t* out, int Wg);
 
+// ---- sorted walk (the default greedy window path).  The shard's nodes sorted by the node-only
+// key K(n) = (S(n) << 24) | gid, copied into sorted SoA order and summarised per 1024-entry round
+// (max residual per dimension, OR of labels, first key).  A fitting node has S(n) >= s(q), and its
+// key is K(n) - ((s(q) + borrows) << 24) with borrows <= 2, so a group walks the rounds from the
+// first that can hold K >= s(q) << 24 and stops once K + 1 collected keys lie below every key the
+// unvisited rounds can produce.  Nodes changed since the sort (apply) and nodes whose terms can
+// saturate form the overlay, evaluated in full by every group; their sorted entries are
+// invalidated (WK_INVALID).  Negative-residual nodes fit nothing and appear in neither.
+constexpr int WK_ROUND = 1024;          // sorted entries per round = walk threads per group
+constexpr int WK_MAXR = 16384;          // rounds per shard (PE_MAX_NODES / WK_ROUND)
+constexpr uint64_t WK_INVALID = ~0ull;
+struct WalkIndex {
+  uint64_t* sk;        // [Ns] sorted keys (WK_INVALID = not walked)
+  int64_t* sr;         // [4][sstride] residuals in sorted order
+  uint32_t* sl;        // [Ns] labels in sorted order
+  uint32_t* pos;       // [stride] sorted index of each local node (~0u = none)
+  uint64_t* rmin;      // [nr] first key of each round (at sort time)
+  int64_t* rmax;       // [4][nr] max residual per dimension over the round's valid entries
+  uint32_t* ror;       // [nr] OR of the round's labels
+  int32_t* ovl;        // [stride] overlay local node ids
+  int32_t* ovl_n;      // overlay size
+  uint32_t* in_ovl;    // [stride] 1 = in the overlay
+  int64_t sstride, nr;
+};
+// kin[n] = K(n) of a walkable node (no negative residual, not saturating), else WK_INVALID; the
+// saturating ones are appended to the overlay (cleared by the caller beforehand).
+hipError_t launch_walk_prep(hipStream_t s, const int64_t* res, int64_t stride, int64_t Ns, const uint64_t* kn,
+                            uint64_t* kin, const WalkIndex& w);
+// hipcub radix sort of n u64 keys (temp == nullptr: *temp_bytes = the scratch size needed).
+hipError_t sort_keys_u64(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n, hipStream_t s);
+// Sorted SoA copy, pos[], round summaries from the sorted keys w.sk.
+hipError_t launch_walk_build(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
+                             uint64_t id_base, const WalkIndex& w);
+// One block per group: overlay + walk, exact top-K records and limit, same blob as merge.
+hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const WalkIndex& w, const int64_t* res,
+                       int64_t stride, const uint32_t* labels, int64_t Ns, uint64_t id_base, uint8_t* out);
+
 // upd: [n] records {local node (i64), res[4]} -> res[d][node] = value (absolute)
-// (kn, lo nullable: refreshed for the updated nodes when given)
+// (kn, lo nullable: refreshed for the updated nodes when given; w nullable: the updated nodes
+// leave the sorted walk and join its overlay)
 hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n, uint64_t id_base,
-                        uint64_t* kn, uint32_t* lo);
+                        uint64_t* kn, uint32_t* lo, const WalkIndex* w);
 
 // Inventory delta for one slot of this shard (pe_update_nodes): residual written to both the
 // live and the reset copy, labels and island replaced.  Slots are unique within a launch.

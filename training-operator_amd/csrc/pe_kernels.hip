@@ -998,17 +998,164 @@ hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const 
 
 // ------------------------------------------------------------------ merge: per-group exact top-K
 
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = umax64(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// LDS working set of one top-K block (merge or walk), MG_THREADS threads.
+struct TopkShared {
+  uint64_t keys[MG_CAP];
+  uint64_t sel[MG_SEL];
+  uint64_t red[2 * (MG_THREADS / 64)];
+  int hist[256];
+  int total, sel_n, sel_bin;
+};
+
+// Wave-aggregated append of the lanes' keys with `take` to s.keys: one LDS atomic per wave
+// (ballot / mbcnt ranks).  Keys past MG_CAP are counted in s.total but dropped.
+__device__ __forceinline__ void topk_append(TopkShared& s, uint64_t k, bool take) {
+  const uint64_t bal = __ballot(take);
+  if (bal == 0) return;
+  const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+  int base = 0;
+  if (take && rank == 0) base = atomicAdd(&s.total, __popcll(bal));
+  base = __shfl(base, __ffsll((unsigned long long)bal) - 1, 64);
+  if (take && base + rank < MG_CAP) s.keys[base + rank] = k;
+}
+
+// Block-wide: sorts (at least) the K + 1 smallest of s.keys[0..T) ascending and returns the array
+// holding them at its front (s.keys or s.sel).  Only the K + 1 smallest matter (K records + the
+// limit), so for T > 2(K+1) a 256-bin histogram of (key - min) >> shift over [min, max] finds the
+// bin holding the (K+1)-th smallest and only the keys up to that bin are bitonic-sorted (typically
+// ~K + a bin instead of all T).  T <= MG_CAP.  Starts and ends with a block barrier.
+__device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __syncthreads();
+  uint64_t* sk = s.keys;
+  int C = T;
+  if (T > 2 * (K + 1) && K + 1 <= MG_SEL) {
+    uint64_t mn = NO_KEY, mx = 0;
+    for (int i = tid; i < T; i += MG_THREADS) {
+      mn = umin64(mn, s.keys[i]);
+      mx = umax64(mx, s.keys[i]);
+    }
+    mn = wave_min_u64(mn);
+    mx = wave_max_u64(mx);
+    if (lane == 0) {
+      s.red[wave] = mn;
+      s.red[MG_THREADS / 64 + wave] = mx;
+    }
+    for (int i = tid; i < 256; i += MG_THREADS) s.hist[i] = 0;
+    if (tid == 0) s.sel_n = 0;
+    __syncthreads();
+    uint64_t kmin = NO_KEY, kmax = 0;
+#pragma unroll
+    for (int i = 0; i < MG_THREADS / 64; ++i) {
+      kmin = umin64(kmin, s.red[i]);
+      kmax = umax64(kmax, s.red[MG_THREADS / 64 + i]);
+    }
+    const int bits = 64 - __clzll((long long)((kmax - kmin) | 1));
+    const int sh = bits > 8 ? bits - 8 : 0;
+    for (int i = tid; i < T; i += MG_THREADS) atomicAdd(&s.hist[(int)((s.keys[i] - kmin) >> sh)], 1);
+    __syncthreads();
+    if (wave == 0) {                       // inclusive scan of 256 bins, 4 per lane
+      int h[4], sum = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        h[u] = s.hist[lane * 4 + u];
+        sum += h[u];
+      }
+      int incl = sum;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += o;
+      }
+      int run = incl - sum, cut = 1 << 30;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        run += h[u];
+        if (run >= K + 1 && cut == (1 << 30)) cut = lane * 4 + u;
+      }
+      const uint64_t bal = __ballot(cut != (1 << 30));   // first lane holding a cut bin
+      const int first = __ffsll((unsigned long long)bal) - 1;
+      const int cb = __shfl(cut, first < 0 ? 0 : first, 64);
+      if (lane == 0) s.sel_bin = first < 0 ? 255 : cb;
+    }
+    __syncthreads();
+    const int cb = s.sel_bin;
+    for (int i = tid; i < T; i += MG_THREADS) {
+      const uint64_t k = s.keys[i];
+      if ((int)((k - kmin) >> sh) <= cb) {
+        const int pos = atomicAdd(&s.sel_n, 1);
+        if (pos < MG_SEL) s.sel[pos] = k;
+      }
+    }
+    __syncthreads();
+    if (s.sel_n <= MG_SEL) {               // else (one bin held too many): sort all T
+      sk = s.sel;
+      C = s.sel_n;
+    }
+  }
+  int P = 2;
+  while (P < C) P <<= 1;
+  for (int i = C + tid; i < P; i += MG_THREADS) sk[i] = NO_KEY;
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P; i += MG_THREADS) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = sk[i], c = sk[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > c) == up) {
+            sk[i] = c;
+            sk[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  return sk;
+}
+
+// Group blob: header + the first nout keys of sk as records {key, residual now, labels}.
+__device__ void write_group(const uint64_t* sk, int nout, int flags, uint64_t limit, int K, int g,
+                            const int64_t* __restrict__ res, int64_t stride, const uint32_t* __restrict__ labels,
+                            uint64_t id_base, uint8_t* __restrict__ out) {
+  uint8_t* og = out + (size_t)g * cand_group_bytes(K);
+  CandRec* recs = reinterpret_cast<CandRec*>(og + sizeof(CandHdr));
+  for (int i = threadIdx.x; i < nout; i += blockDim.x) {
+    const uint64_t key = sk[i];
+    const int64_t n = (int64_t)((key & 0xFFFFFFull) - id_base);
+    CandRec r;
+    r.key = key;
+#pragma unroll
+    for (int d = 0; d < D; ++d) r.res[d] = res[d * stride + n];
+    r.labels = labels[n];
+    recs[i] = r;
+  }
+  if (threadIdx.x == 0) {
+    CandHdr h;
+    h.n = nout;
+    h.flags = flags;
+    h.limit = limit;
+    *reinterpret_cast<CandHdr*>(og) = h;
+  }
+}
+
 __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __restrict__ cand,
                                                            const int32_t* __restrict__ cnt,
                                                            const uint64_t* __restrict__ bound, int nwaves, int K,
                                                            const int64_t* __restrict__ res, int64_t stride,
                                                            const uint32_t* __restrict__ labels, uint64_t id_base,
                                                            uint8_t* __restrict__ out) {
-  __shared__ uint64_t keys[MG_CAP];
-  __shared__ uint64_t sel[MG_SEL];
-  __shared__ uint64_t red[MG_THREADS / 64];
-  __shared__ int hist[256];
-  __shared__ int total, sel_n, sel_bin;
+  __shared__ TopkShared s;
   const int g = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t gbase = (size_t)g * (size_t)nwaves;
@@ -1030,24 +1177,14 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
   }
   for (int w = tid + MG_THREADS; w < nwaves; w += MG_THREADS) b = umin64(b, bound[gbase + w]);
   b = wave_min_u64(b);
-  if (lane == 0) red[wave] = b;
-  if (tid == 0) total = 0;
+  if (lane == 0) s.red[wave] = b;
+  if (tid == 0) s.total = 0;
   __syncthreads();
   uint64_t G = NO_KEY;
 #pragma unroll
-  for (int i = 0; i < MG_THREADS / 64; ++i) G = umin64(G, red[i]);
-  __syncthreads();                            // red[] is reused by the selection below
-  auto append = [&](uint64_t k, bool take) {
-    const uint64_t bal = __ballot(take);
-    if (bal == 0) return;
-    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-    int base = 0;
-    if (take && rank == 0) base = atomicAdd(&total, __popcll(bal));
-    base = __shfl(base, __ffsll((unsigned long long)bal) - 1, 64);
-    if (take && base + rank < MG_CAP) keys[base + rank] = k;
-  };
+  for (int i = 0; i < MG_THREADS / 64; ++i) G = umin64(G, s.red[i]);
 #pragma unroll
-  for (int u = 0; u < PRE; ++u) append(k0[u], u < c0 && k0[u] < G);
+  for (int u = 0; u < PRE; ++u) topk_append(s, k0[u], u < c0 && k0[u] < G);
   // the rest of longer lists, and lists beyond the first MG_THREADS
   for (int w = tid; w < nwaves; w += MG_THREADS) {
     const int c = w == tid ? c0 : cnt[gbase + w];
@@ -1059,15 +1196,13 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         if (k[u] < G) {
-          const int pos = atomicAdd(&total, 1);
-          if (pos < MG_CAP) keys[pos] = k[u];
+          const int pos = atomicAdd(&s.total, 1);
+          if (pos < MG_CAP) s.keys[pos] = k[u];
         }
     }
   }
   __syncthreads();
-  const int T = total;
-  int nout, flags = 0;
-  uint64_t limit;
+  const int T = s.total;
   if (T > MG_CAP) {
     // Overflow (pathological): keep only the exact minimum over every candidate.
     uint64_t mn = NO_KEY;
@@ -1076,125 +1211,20 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
       for (int i = 0; i < c; ++i) mn = umin64(mn, cand[(gbase + w) * 64 + i]);
     }
     mn = wave_min_u64(mn);
-    __syncthreads();
-    if (lane == 0) red[wave] = mn;
+    __syncthreads();                       // every thread has read G from s.red
+    if (lane == 0) s.red[wave] = mn;
     __syncthreads();
     mn = NO_KEY;
 #pragma unroll
-    for (int i = 0; i < MG_THREADS / 64; ++i) mn = umin64(mn, red[i]);
+    for (int i = 0; i < MG_THREADS / 64; ++i) mn = umin64(mn, s.red[i]);
+    if (tid == 0) s.keys[0] = mn;
     __syncthreads();
-    if (tid == 0) keys[0] = mn;
-    __syncthreads();
-    nout = 1;
-    limit = mn + 1;
-    flags = 1;
-  } else {
-    // Only the K + 1 smallest of the T candidates matter (K records + the limit).  For large T a
-    // 256-bin histogram of (key - min) >> shift finds the bin holding the (K+1)-th smallest; the
-    // keys up to that bin (typically ~K + a bin) are sorted instead of all T.
-    uint64_t* sk = keys;
-    int C = T;
-    if (T > 2 * (K + 1) && K + 1 <= MG_SEL) {
-      uint64_t mn = NO_KEY;
-      for (int i = tid; i < T; i += MG_THREADS) mn = umin64(mn, keys[i]);
-      mn = wave_min_u64(mn);
-      if (lane == 0) red[wave] = mn;
-      for (int i = tid; i < 256; i += MG_THREADS) hist[i] = 0;
-      if (tid == 0) sel_n = 0;
-      __syncthreads();
-      uint64_t kmin = NO_KEY;
-#pragma unroll
-      for (int i = 0; i < MG_THREADS / 64; ++i) kmin = umin64(kmin, red[i]);
-      const uint64_t span = G - kmin;   // every candidate is < G (G may be NO_KEY: no wave had a 2nd best)
-      const int bits = 64 - __clzll((long long)(span | 1));
-      const int sh = bits > 8 ? bits - 8 : 0;
-      for (int i = tid; i < T; i += MG_THREADS) atomicAdd(&hist[(int)((keys[i] - kmin) >> sh)], 1);
-      __syncthreads();
-      if (wave == 0) {                       // inclusive scan of 256 bins, 4 per lane
-        int h[4], sum = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          h[u] = hist[lane * 4 + u];
-          sum += h[u];
-        }
-        int incl = sum;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          const int o = __shfl_up(incl, off, 64);
-          if (lane >= off) incl += o;
-        }
-        int run = incl - sum, cut = 1 << 30;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          run += h[u];
-          if (run >= K + 1 && cut == (1 << 30)) cut = lane * 4 + u;
-        }
-        // first lane holding a cut bin
-        const uint64_t bal = __ballot(cut != (1 << 30));
-        const int first = __ffsll((unsigned long long)bal) - 1;
-        const int cb = __shfl(cut, first < 0 ? 0 : first, 64);
-        if (lane == 0) sel_bin = first < 0 ? 255 : cb;
-      }
-      __syncthreads();
-      const int cb = sel_bin;
-      for (int i = tid; i < T; i += MG_THREADS) {
-        const uint64_t k = keys[i];
-        if ((int)((k - kmin) >> sh) <= cb) {
-          const int pos = atomicAdd(&sel_n, 1);
-          if (pos < MG_SEL) sel[pos] = k;
-        }
-      }
-      __syncthreads();
-      if (sel_n <= MG_SEL) {                 // else (one bin held too many): sort all T
-        sk = sel;
-        C = sel_n;
-      }
-    }
-    int P = 2;
-    while (P < C) P <<= 1;
-    for (int i = C + tid; i < P; i += MG_THREADS) sk[i] = NO_KEY;
-    __syncthreads();
-    for (int k = 2; k <= P; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < P; i += MG_THREADS) {
-          const int ixj = i ^ j;
-          if (ixj > i) {
-            const uint64_t a = sk[i], c = sk[ixj];
-            const bool up = (i & k) == 0;
-            if ((a > c) == up) {
-              sk[i] = c;
-              sk[ixj] = a;
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-    nout = T < K ? T : K;
-    limit = T > K ? sk[K] : G;     // sk holds the K + 1 smallest of all T in order
-    if (sk != keys)
-      for (int i = tid; i < nout; i += MG_THREADS) keys[i] = sk[i];
-    __syncthreads();
+    write_group(s.keys, 1, 1, mn + 1, K, g, res, stride, labels, id_base, out);
+    return;
   }
-  uint8_t* og = out + (size_t)g * cand_group_bytes(K);
-  CandRec* recs = reinterpret_cast<CandRec*>(og + sizeof(CandHdr));
-  for (int i = tid; i < nout; i += MG_THREADS) {
-    const uint64_t key = keys[i];
-    const int64_t n = (int64_t)((key & 0xFFFFFFull) - id_base);
-    CandRec r;
-    r.key = key;
-#pragma unroll
-    for (int d = 0; d < D; ++d) r.res[d] = res[d * stride + n];
-    r.labels = labels[n];
-    recs[i] = r;
-  }
-  if (tid == 0) {
-    CandHdr h;
-    h.n = nout;
-    h.flags = flags;
-    h.limit = limit;
-    *reinterpret_cast<CandHdr*>(og) = h;
-  }
+  const uint64_t* sk = topk_sort(s, T, K);
+  // sk holds the K + 1 smallest of all T in order; keys >= G were never listed
+  write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : G, K, g, res, stride, labels, id_base, out);
 }
 
 hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt, const uint64_t* bound, int nwaves,
@@ -1206,11 +1236,233 @@ hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt,
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ sorted walk (greedy default)
+
+__global__ __launch_bounds__(256) void walk_prep_kernel(const int64_t* __restrict__ res, int64_t stride, int64_t Ns,
+                                                        const uint64_t* __restrict__ kn, uint64_t* __restrict__ kin,
+                                                        int32_t* __restrict__ ovl, int32_t* __restrict__ ovl_n,
+                                                        uint32_t* __restrict__ in_ovl) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= Ns) return;
+  const bool neg = (res[n] | res[stride + n] | res[2 * stride + n] | res[3 * stride + n]) < 0;
+  const uint64_t K = kn[n];
+  uint64_t k = K;
+  if (neg) {
+    k = WK_INVALID;                  // fits nothing
+  } else if (K == KEY_SLOW) {
+    k = WK_INVALID;                  // saturating terms: evaluated in full through the overlay
+    in_ovl[n] = 1u;
+    ovl[atomicAdd(ovl_n, 1)] = (int32_t)n;
+  }
+  kin[n] = k;
+}
+
+hipError_t launch_walk_prep(hipStream_t s, const int64_t* res, int64_t stride, int64_t Ns, const uint64_t* kn,
+                            uint64_t* kin, const WalkIndex& w) {
+  if (Ns <= 0) return hipSuccess;
+  hipLaunchKernelGGL(walk_prep_kernel, dim3((unsigned)((Ns + 255) / 256)), dim3(256), 0, s, res, stride, Ns, kn, kin,
+                     w.ovl, w.ovl_n, w.in_ovl);
+  return hipGetLastError();
+}
+
+// One block per round: gather the sorted SoA copy, pos[], and the round's summary.
+__global__ __launch_bounds__(WK_ROUND) void walk_build_kernel(const int64_t* __restrict__ res, int64_t stride,
+                                                              const uint32_t* __restrict__ labels, int64_t Ns,
+                                                              uint64_t id_base, WalkIndex w) {
+  __shared__ int64_t mx[D][WK_ROUND / 64];
+  __shared__ uint32_t orl[WK_ROUND / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r = blockIdx.x;
+  const int64_t i = r * WK_ROUND + tid;
+  const uint64_t K = i < Ns ? w.sk[i] : WK_INVALID;
+  int64_t v[D] = {INT64_MIN, INT64_MIN, INT64_MIN, INT64_MIN};
+  uint32_t lab = 0;
+  if (K != WK_INVALID) {
+    const int64_t n = (int64_t)((K & 0xFFFFFFull) - id_base);
+    w.pos[n] = (uint32_t)i;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      v[d] = res[d * stride + n];
+      w.sr[d * w.sstride + i] = v[d];
+    }
+    lab = labels[n];
+    w.sl[i] = lab;
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    for (int off = 32; off >= 1; off >>= 1) {
+      const int64_t o = __shfl_xor(v[d], off, 64);
+      v[d] = o > v[d] ? o : v[d];
+    }
+  for (int off = 32; off >= 1; off >>= 1) lab |= __shfl_xor(lab, off, 64);
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) mx[d][wave] = v[d];
+    orl[wave] = lab;
+  }
+  __syncthreads();
+  if (tid < D) {
+    int64_t m = INT64_MIN;
+    for (int k = 0; k < WK_ROUND / 64; ++k) m = mx[tid][k] > m ? mx[tid][k] : m;
+    w.rmax[tid * w.nr + r] = m;
+  } else if (tid == D) {
+    uint32_t o = 0;
+    for (int k = 0; k < WK_ROUND / 64; ++k) o |= orl[k];
+    w.ror[r] = o;
+    w.rmin[r] = w.sk[r * WK_ROUND];       // sorted: the round's smallest key
+  }
+}
+
+hipError_t launch_walk_build(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
+                             uint64_t id_base, const WalkIndex& w) {
+  if (Ns <= 0) return hipSuccess;
+  hipLaunchKernelGGL(walk_build_kernel, dim3((unsigned)w.nr), dim3(WK_ROUND), 0, s, res, stride, labels, Ns, id_base,
+                     w);
+  return hipGetLastError();
+}
+
+// One block of WK_ROUND threads per group of the window:
+//  1. per round (all rounds at once): can it hold a fit (q <= max residual per dimension, need in
+//     the OR of labels)?  -> LDS bitmap; and how many rounds start below s(q) << 24 -> the first
+//     round worth walking;
+//  2. the overlay in full (current residuals);
+//  3. the candidate rounds in sorted order, one node per thread, until >= K + 1 collected keys lie
+//     below X = rmin(next round) - ((s(q) + 2) << 24), a lower bound of every key the unvisited
+//     rounds can produce (their K(n) >= rmin, key = K(n) - ((s(q) + borrows) << 24)).
+// Then the same exact selection and blob as merge: top-K records, limit = the (K+1)-th key (or
+// NO_KEY once every candidate round was walked and at most K fit).
+__global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict__ groups, int K, WalkIndex w,
+                                                        const int64_t* __restrict__ res, int64_t stride,
+                                                        const uint32_t* __restrict__ labels, int64_t Ns,
+                                                        uint64_t id_base, uint8_t* __restrict__ out) {
+  static_assert(WK_ROUND == MG_THREADS, "the walk uses the merge's block-wide selection");
+  __shared__ TopkShared s;
+  __shared__ uint32_t cbits[WK_MAXR / 32];
+  __shared__ int start_cnt, below;
+  const int g = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const ReqRec rq = groups[g];
+  const int64_t q0 = rq.q[0], q1 = rq.q[1], q2 = rq.q[2], q3 = rq.q[3];
+  const uint32_t need = rq.need;
+  // s(q), saturated: a walkable node has S(n) < SCORE_MAX, so s(q) >= SCORE_MAX fits none of them
+  uint64_t sq = (uint64_t)q0 + ((uint64_t)q1 >> 20) + ((uint64_t)q3 >> 24);
+  sq = (uint64_t)q0 > SCORE_MAX || (uint64_t)q2 >= (1ull << 20) || sq >= SCORE_MAX ? SCORE_MAX : sq;
+  sq = sq < SCORE_MAX ? sq + ((uint64_t)q2 << 20) : sq;
+  const bool walk = sq < SCORE_MAX;
+  const uint64_t KQ = walk ? sq << 24 : 0;
+  const uint64_t KQ2 = !walk ? 0 : sq + 2 >= (1ull << 40) ? ~0ull : (sq + 2) << 24;   // (s(q) + 2) << 24, saturated
+  const int64_t nr = w.nr;
+  const int nwords = (int)((nr + 31) / 32);
+  for (int i = tid; i < nwords; i += WK_ROUND) cbits[i] = 0u;
+  if (tid == 0) {
+    s.total = 0;
+    start_cnt = 0;
+  }
+  __syncthreads();
+  if (walk) {
+    int cnt = 0;
+    for (int64_t r = tid; r < nr; r += WK_ROUND) {
+      cnt += w.rmin[r] < KQ;
+      const bool can = q0 <= w.rmax[r] && q1 <= w.rmax[nr + r] && q2 <= w.rmax[2 * nr + r] &&
+                       q3 <= w.rmax[3 * nr + r] && (w.ror[r] & need) == need;
+      if (can) atomicOr(&cbits[r >> 5], 1u << (r & 31));
+    }
+    for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if (lane == 0 && cnt) atomicAdd(&start_cnt, cnt);
+  }
+  // overlay: every node changed since the sort (and the saturating ones), current values
+  const int no = *w.ovl_n;
+  for (int i0 = 0; i0 < no; i0 += WK_ROUND) {
+    const int i = i0 + tid;
+    uint64_t k = NO_KEY;
+    if (i < no) {
+      const int64_t n = w.ovl[i];
+      k = node_key(res[n], res[stride + n], res[2 * stride + n], res[3 * stride + n], labels[n], q0, q1, q2, q3, need,
+                   id_base + (uint64_t)n);
+    }
+    topk_append(s, k, k != NO_KEY);
+    __syncthreads();
+    if (s.total > MG_CAP - WK_ROUND) {     // keep the K + 1 smallest (the rest can never matter)
+      const int T = s.total;
+      const uint64_t* sk = topk_sort(s, T, K);
+      const int m = T < K + 1 ? T : K + 1;
+      uint64_t v = tid < m ? sk[tid] : 0;
+      __syncthreads();
+      if (tid < m) s.keys[tid] = v;
+      if (tid == 0) s.total = m;
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  bool done = !walk;
+  int64_t r = walk ? (start_cnt > 0 ? start_cnt - 1 : 0) : nr;
+  auto next_round = [&](int64_t from) -> int64_t {   // first candidate round >= from (uniform)
+    int64_t wi = from >> 5;
+    if (wi >= nwords) return nr;
+    uint32_t bits = cbits[wi] & (~0u << (from & 31));
+    while (bits == 0) {
+      if (++wi >= nwords) return nr;
+      bits = cbits[wi];
+    }
+    return wi * 32 + __ffs(bits) - 1;
+  };
+  if (!done) r = next_round(r);
+  while (!done && r < nr) {
+    const int T = s.total;
+    if (T >= K + 1) {                      // stop once K + 1 keys lie below every unvisited key
+      const uint64_t rm = w.rmin[r];
+      const uint64_t X = rm > KQ2 ? rm - KQ2 : 0;
+      int c = 0;
+      for (int i = tid; i < T; i += WK_ROUND) c += s.keys[i] < X;
+      for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
+      if (tid == 0) below = 0;
+      __syncthreads();
+      if (lane == 0 && c) atomicAdd(&below, c);
+      __syncthreads();
+      if (below >= K + 1) break;
+    }
+    const int64_t i = r * WK_ROUND + tid;
+    uint64_t k = NO_KEY;
+    if (i < Ns) {
+      const uint64_t Kn = w.sk[i];
+      if (Kn != WK_INVALID)
+        k = node_key(w.sr[i], w.sr[w.sstride + i], w.sr[2 * w.sstride + i], w.sr[3 * w.sstride + i], w.sl[i], q0, q1,
+                     q2, q3, need, Kn & 0xFFFFFFull);
+    }
+    topk_append(s, k, k != NO_KEY);
+    __syncthreads();
+    if (s.total > MG_CAP - WK_ROUND) {
+      const int T2 = s.total;
+      const uint64_t* sk = topk_sort(s, T2, K);
+      const int m = T2 < K + 1 ? T2 : K + 1;
+      uint64_t v = tid < m ? sk[tid] : 0;
+      __syncthreads();
+      if (tid < m) s.keys[tid] = v;
+      if (tid == 0) s.total = m;
+      __syncthreads();
+    }
+    r = next_round(r + 1);
+  }
+  const int T = s.total;
+  const uint64_t* sk = topk_sort(s, T, K);
+  write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : NO_KEY, K, g, res, stride, labels, id_base, out);
+}
+
+hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const WalkIndex& w, const int64_t* res,
+                       int64_t stride, const uint32_t* labels, int64_t Ns, uint64_t id_base, uint8_t* out) {
+  if (Wg <= 0) return hipSuccess;
+  if (w.nr > WK_MAXR || K + 1 > WK_ROUND) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(walk_kernel, dim3((unsigned)Wg), dim3(WK_ROUND), 0, s, groups, K, w, res, stride, labels, Ns,
+                     id_base, out);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ apply residual updates
 
 __global__ __launch_bounds__(256) void apply_kernel(int64_t* __restrict__ res, int64_t stride,
                                                     const int64_t* __restrict__ upd, int64_t n, uint64_t id_base,
-                                                    uint64_t* __restrict__ kn, uint32_t* __restrict__ lo) {
+                                                    uint64_t* __restrict__ kn, uint32_t* __restrict__ lo,
+                                                    WalkIndex w, int walk) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t* u = upd + i * (D + 1);
@@ -1225,13 +1477,22 @@ __global__ __launch_bounds__(256) void apply_kernel(int64_t* __restrict__ res, i
     lo[node] = l1;
     lo[stride + node] = l3;
   }
+  if (walk) {                                 // leave the sorted walk, join the overlay (once)
+    const uint32_t p = w.pos[node];
+    if (p != ~0u) {
+      w.sk[p] = WK_INVALID;
+      w.pos[node] = ~0u;
+    }
+    if (atomicExch(&w.in_ovl[node], 1u) == 0u) w.ovl[atomicAdd(w.ovl_n, 1)] = (int32_t)node;
+  }
 }
 
 hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n, uint64_t id_base,
-                        uint64_t* kn, uint32_t* lo) {
+                        uint64_t* kn, uint32_t* lo, const WalkIndex* w) {
   if (n <= 0) return hipSuccess;
+  const WalkIndex none{};
   hipLaunchKernelGGL(apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, res, stride, upd, n, id_base,
-                     kn, lo);
+                     kn, lo, w ? *w : none, w ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -53,7 +53,8 @@ class Engine:
 
     def __init__(self, device_id: int = 0, rank: int = 0, world_size: int = 1, comm: Optional[bytes] = None,
                  exchange=None, max_nodes: int = 0, gpu_resource_name: str = "amd.com/gpu", topk: int = 0,
-                 window_groups: int = 0, window_pods: int = 0, fit_path_mask: int = 0, greedy_flags: int = 0):
+                 window_groups: int = 0, window_pods: int = 0, fit_path_mask: int = 0, greedy_flags: int = 0,
+                 resort_nodes: int = 0):
         self.lib = _abi.load()
         self._keep = []
         cfg = _abi.PeConfig()
@@ -84,6 +85,7 @@ class Engine:
         cfg.window_pods = window_pods
         cfg.fit_path_mask = fit_path_mask
         cfg.greedy_flags = greedy_flags
+        cfg.resort_nodes = resort_nodes
         self._cfg = cfg
         h = ctypes.c_void_p()
         rc = self.lib.pe_create(ctypes.byref(cfg), ctypes.byref(h))

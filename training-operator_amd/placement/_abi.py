@@ -34,7 +34,7 @@ class PeConfig(ctypes.Structure):
                 ("comm_id", ctypes.c_void_p), ("exchange", ALLGATHER_FN), ("exchange_user", ctypes.c_void_p),
                 ("max_nodes", ctypes.c_int64), ("gpu_resource_name", ctypes.c_char_p), ("topk", ctypes.c_int32),
                 ("window_groups", ctypes.c_int32), ("window_pods", ctypes.c_int64), ("fit_path_mask", ctypes.c_int32),
-                ("greedy_flags", ctypes.c_int32)]
+                ("greedy_flags", ctypes.c_int32), ("resort_nodes", ctypes.c_int32)]
 
 
 class PeStats(ctypes.Structure):
@@ -43,7 +43,7 @@ class PeStats(ctypes.Structure):
                 ("jobs_placed", ctypes.c_int64), ("jobs_failed", ctypes.c_int64), ("last_greedy_ms", ctypes.c_double),
                 ("greedy_wait_ms", ctypes.c_double), ("greedy_host_ms", ctypes.c_double),
                 ("fit_runs_i32", ctypes.c_int64), ("fit_runs_i64", ctypes.c_int64), ("fit_runs_coded", ctypes.c_int64),
-                ("fit_runs_therm", ctypes.c_int64), ("fit_runs_planes", ctypes.c_int64)]
+                ("fit_runs_therm", ctypes.c_int64), ("fit_runs_planes", ctypes.c_int64), ("resorts", ctypes.c_int64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
