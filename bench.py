@@ -125,7 +125,9 @@ def main():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: batch = fit-jobs x n_gpus (fixed per-rank work); strong: batch = fit-jobs")
     ap.add_argument("--fit-path-mask", type=int, default=0, help="pe_config.fit_path_mask (0 = every kernel)")
-    ap.add_argument("--greedy-flags", type=int, default=0, help="pe_config.greedy_flags (bit0: pipelined windows)")
+    ap.add_argument("--greedy-flags", type=int, default=0,
+                    help="pe_config.greedy_flags (bit0: pipelined windows, bit1: full scan instead of the sorted walk)")
+    ap.add_argument("--resort-nodes", type=int, default=0, help="pe_config.resort_nodes (0 = default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -193,7 +195,7 @@ def main():
     inv = synth.make_inventory(N, synth.SEED["cfg5"], gpu_frac=0.2)
     eng = Engine(device, rank=rank, world_size=world, comm=cid, exchange=exchange, max_nodes=N, topk=args.topk,
                  window_groups=args.window_groups, window_pods=args.window_pods, fit_path_mask=args.fit_path_mask,
-                 greedy_flags=args.greedy_flags)
+                 greedy_flags=args.greedy_flags, resort_nodes=args.resort_nodes)
     eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     b, e = eng.shard_range()
     Ns = e - b

@@ -42,7 +42,7 @@ int main() {
       float best = 1e9f;
       for (int r = 0; r < 10; ++r) {
         hipEventRecord(a, 0);
-        pe::launch_merge(0, d_cand, d_cnt, d_bound, nw, K, d_res, stride, d_lab, 0, d_out, G);
+        pe::launch_merge(0, d_cand, d_cnt, d_bound, nw, K, d_out, G);
         hipEventRecord(b, 0);
         hipEventSynchronize(b);
         float ms; hipEventElapsedTime(&ms, a, b); best = std::min(best, ms);

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -45,25 +46,30 @@ struct DevBuf {
   }
 };
 
+// Pinned host buffer.  Coherent (fine-grained) ones are also read and written by kernels directly
+// (dev = the device-side address): per-window inputs and the candidate blob skip the copy engines.
 template <class T>
 struct HostBuf {
   T* p = nullptr;
+  T* dev = nullptr;
   size_t n = 0;
-  hipError_t ensure(size_t count) {
+  hipError_t ensure(size_t count, unsigned flags = hipHostMallocDefault) {
     if (count <= n && p) return hipSuccess;
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dev = nullptr;
     n = 0;
-    hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault);
+    hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T), flags);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&dev, p, 0);
     if (e == hipSuccess) n = count;
     return e;
   }
   void release() {
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dev = nullptr;
     n = 0;
   }
 };
+constexpr unsigned kZeroCopy = hipHostMallocCoherent | hipHostMallocMapped;
 
 struct PeError {
   int code;
@@ -104,6 +110,10 @@ struct pe_ctx {
   // inventory shard
   int64_t n_total = 0, begin = 0, end = 0, Ns = 0, stride = 0;
   bool loaded = false;
+  // host mirror of the GLOBAL inventory (residual SoA [4][n_total], its reset copy, labels): the
+  // greedy windows ship candidate keys only and the resolver reads node states here
+  std::vector<int64_t> m_res, m_res0;
+  std::vector<uint32_t> m_lab;
   DevBuf<int64_t> res0, res;
   DevBuf<uint32_t> labels;
   DevBuf<int32_t> island;
@@ -144,7 +154,7 @@ struct pe_ctx {
   DevBuf<uint64_t> g_kn;   // scan: node-only score terms K(n) (prep_nodes), refreshed by apply
   DevBuf<uint32_t> g_lo;   // scan: lo20(r1) / lo24(r3), [2][stride]
   HostBuf<ReqRec> h_groups;
-  HostBuf<uint8_t> h_out, h_own;
+  HostBuf<uint8_t> h_out, h_out2, h_own;   // h_out2: the pipelined loop's second blob buffer
   HostBuf<int64_t> h_upd;
   // greedy sorted walk (pe_kernels.h WalkIndex; the default window path, greedy_flags bit1 = full scan)
   bool walk = true;
@@ -167,7 +177,7 @@ struct pe_ctx {
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
-    g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_out.release(); h_own.release(); h_upd.release();
+    g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_out.release(); h_out2.release(); h_own.release(); h_upd.release();
     w_sk.release(); w_kin.release(); w_rmin.release(); w_sr.release(); w_rmax.release(); w_sl.release(); w_pos.release();
     w_ror.release(); w_inovl.release(); w_ovl.release(); w_ovln.release(); w_temp.release();
     if (comm) (void)ncclCommDestroy(comm);
@@ -324,6 +334,14 @@ int pe_load_nodes(pe_ctx* ctx, int64_t n, const int64_t* cap, const int64_t* use
       lab[i] = labels ? labels[ctx->begin + i] : 0u;
       isl[i] = island ? island[ctx->begin + i] : -1;
     }
+    ctx->m_res.resize((size_t)pe::D * n);
+    for (int64_t k = 0; k < pe::D * n; ++k) {
+      if (cap[k] < 0 || used[k] < 0) raise(PE_EINVAL, "negative capacity/usage");
+      ctx->m_res[k] = cap[k] - used[k];
+    }
+    ctx->m_res0 = ctx->m_res;
+    ctx->m_lab.assign((size_t)n, 0u);
+    if (labels) std::copy(labels, labels + n, ctx->m_lab.begin());
     hipchk(ctx->res0.ensure(cells), "alloc res0");
     hipchk(ctx->res.ensure(cells), "alloc res");
     hipchk(ctx->labels.ensure((size_t)ctx->stride), "alloc labels");
@@ -360,6 +378,16 @@ int pe_update_nodes(pe_ctx* ctx, int64_t n, const int64_t* slots, const uint8_t*
         if (op[i] == PE_NODE_SET)
           for (int d = 0; d < pe::D; ++d)
             if (cap[i * pe::D + d] < 0 || used[i * pe::D + d] < 0) raise(PE_EINVAL, "negative capacity/usage");
+    }
+    // the host mirror takes every entry in order (global inventory)
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t g = slots[i];
+      for (int d = 0; d < pe::D; ++d) {
+        const int64_t v = op[i] == PE_NODE_SET ? cap[i * pe::D + d] - used[i * pe::D + d] : pe::NEVER;
+        ctx->m_res[(size_t)d * ctx->n_total + g] = v;
+        ctx->m_res0[(size_t)d * ctx->n_total + g] = v;
+      }
+      ctx->m_lab[g] = op[i] == PE_NODE_SET && labels ? labels[i] : 0u;
     }
     // last entry per slot wins; keep only this shard's slots
     std::unordered_map<int64_t, int64_t> last;
@@ -403,6 +431,7 @@ int pe_reset_residuals(pe_ctx* ctx) {
     hipchk(hipMemcpyAsync(ctx->res.p, ctx->res0.p, (size_t)pe::D * ctx->stride * 8, hipMemcpyDeviceToDevice,
                           ctx->stream),
            "D2D reset");
+    ctx->m_res = ctx->m_res0;
     return PE_OK;
   });
 }
@@ -941,18 +970,37 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       group_need = no_need.data();
     }
     pe::Resolver R(n_jobs, job_group_off, priority, group_count, group_req, group_need);
+    R.set_mirror(pe::Mirror{ctx->m_res.data(), ctx->n_total, ctx->m_lab.data()});
+    // PE_DUMP_WINDOWS=<file>: record the batch and every window's groups + blob (host resolver
+    // replay, tools/replay_resolver.cc); diagnostics only
+    FILE* dump = nullptr;
+    if (const char* dp = std::getenv("PE_DUMP_WINDOWS")) {
+      dump = std::fopen(dp, "wb");
+      if (dump) {
+        const int64_t hdr[3] = {n_jobs, G, (int64_t)ctx->topk};
+        std::fwrite(hdr, 8, 3, dump);
+        std::fwrite(job_group_off, 4, (size_t)n_jobs + 1, dump);
+        std::fwrite(priority, 4, (size_t)n_jobs, dump);
+        std::fwrite(group_count, 4, (size_t)G, dump);
+        std::fwrite(group_req, 8, (size_t)G * pe::D, dump);
+        std::fwrite(group_need, 4, (size_t)G, dump);
+      }
+    }
+    struct DumpClose { FILE*& f; ~DumpClose() { if (f) std::fclose(f); } } dump_close{dump};
+    int64_t dump_left = std::getenv("PE_DUMP_MAX_WINDOWS") ? std::atoll(std::getenv("PE_DUMP_MAX_WINDOWS")) : INT64_MAX;
     const int K = ctx->topk;
     const size_t gb = pe::cand_group_bytes(K);
     const int Wmax = ctx->window_groups;
     const int Wpad = (int)round_up(Wmax, pe::SC_GT);
     const int nwaves = (int)std::max<int64_t>(1, (ctx->Ns + pe::SC_SPAN - 1) / pe::SC_SPAN);
     hipchk(ctx->g_groups.ensure(Wpad), "alloc groups");
-    hipchk(ctx->h_groups.ensure(Wpad), "alloc pinned groups");
+    hipchk(ctx->h_groups.ensure(Wpad, kZeroCopy), "alloc pinned groups");
     hipchk(ctx->g_cand.ensure((size_t)Wpad * nwaves * 64), "alloc cand");
     hipchk(ctx->g_cnt.ensure((size_t)Wpad * nwaves), "alloc cnt");
     hipchk(ctx->g_bound.ensure((size_t)Wpad * nwaves), "alloc bound");
     hipchk(ctx->g_out.ensure((size_t)Wmax * gb), "alloc out");
-    hipchk(ctx->h_out.ensure((size_t)Wmax * gb * ctx->world), "alloc pinned out");
+    hipchk(ctx->h_out.ensure((size_t)Wmax * gb * ctx->world, kZeroCopy), "alloc pinned out");
+    if (ctx->pipeline) hipchk(ctx->h_out2.ensure((size_t)Wmax * gb * ctx->world, kZeroCopy), "alloc pinned out");
     if (ctx->world > 1 || ctx->comm) {
       hipchk(ctx->g_gath.ensure((size_t)Wmax * gb * ctx->world), "alloc gather");
       hipchk(ctx->h_own.ensure((size_t)Wmax * gb), "alloc pinned own");
@@ -971,27 +1019,34 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // The host exchange is a synchronous callback: it cannot sit behind queued device work.
     const bool pipelined = ctx->pipeline && !use_exchange;
     // ---- one window on the device: group requests H2D, scan, merge, (RCCL all-gather), blob D2H
-    auto enqueue_window = [&](const std::vector<int32_t>& groups) {
+    int cb = 0;   // the blob buffer of the window being resolved
+    // blob buffer b (0: h_out, 1: h_out2): the pipelined loop D2Hs the next window's blob while the
+    // host still resolves from the current one's
+    auto outbuf = [&](int b) { return b ? ctx->h_out2.p : ctx->h_out.p; };
+    auto outbufdev = [&](int b) { return b ? ctx->h_out2.dev : ctx->h_out.dev; };
+    const bool direct_out = ctx->world == 1 && !ctx->comm;
+    auto enqueue_window = [&](const std::vector<int32_t>& groups, int b) {
       const int Wg = (int)groups.size();
       const int Wgp = (int)round_up(Wg, pe::SC_GT);
       for (int w = 0; w < Wgp; ++w) {
         const int g = groups[std::min(w, Wg - 1)];
         fill_req(ctx->h_groups.p[w], group_req + (int64_t)g * pe::D, group_need[g]);
       }
-      hipchk(hipMemcpyAsync(ctx->g_groups.p, ctx->h_groups.p, Wgp * sizeof(ReqRec), hipMemcpyHostToDevice, s),
-             "H2D window");
-      if (walk) {
+      // unsharded: the kernel writes the blob straight into pinned host memory (no D2H copy)
+      uint8_t* const dst = direct_out ? outbufdev(b) : ctx->g_out.p;
+      if (walk) {   // one 64-B request per block: read from pinned host memory, no H2D copy
         if (ctx->w_est > ctx->resort_nodes) walk_resort(ctx);
-        hipchk(pe::launch_walk(s, ctx->g_groups.p, Wg, K, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p,
-                               ctx->Ns, (uint64_t)ctx->begin, ctx->g_out.p),
+        hipchk(pe::launch_walk(s, ctx->h_groups.dev, Wg, K, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p,
+                               ctx->Ns, (uint64_t)ctx->begin, dst),
                "launch walk");
       } else if (ctx->Ns > 0) {
+        hipchk(hipMemcpyAsync(ctx->g_groups.p, ctx->h_groups.p, Wgp * sizeof(ReqRec), hipMemcpyHostToDevice, s),
+               "H2D window");
         hipchk(pe::launch_scan(s, ctx->res.p, ctx->stride, ctx->labels.p, ctx->g_kn.p, ctx->g_lo.p, ctx->Ns,
                                (uint64_t)ctx->begin, ctx->g_groups.p, Wg, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p,
                                nwaves),
                "launch scan");
-        hipchk(pe::launch_merge(s, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p, nwaves, K, ctx->res.p, ctx->stride,
-                                ctx->labels.p, (uint64_t)ctx->begin, ctx->g_out.p, Wg),
+        hipchk(pe::launch_merge(s, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p, nwaves, K, dst, Wg),
                "launch merge");
       } else {
         std::vector<uint8_t> empty((size_t)Wg * gb, 0);
@@ -999,17 +1054,21 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           pe::CandHdr h{0, 0, pe::NO_KEY};
           std::memcpy(empty.data() + (size_t)w * gb, &h, sizeof(h));
         }
-        hipchk(hipMemcpyAsync(ctx->g_out.p, empty.data(), empty.size(), hipMemcpyHostToDevice, s), "H2D empty");
-        hipchk(hipStreamSynchronize(s), "sync empty");
+        if (direct_out) {
+          std::memcpy(outbuf(b), empty.data(), empty.size());
+        } else {
+          hipchk(hipMemcpyAsync(dst, empty.data(), empty.size(), hipMemcpyHostToDevice, s), "H2D empty");
+          hipchk(hipStreamSynchronize(s), "sync empty");
+        }
       }
       const size_t bytes = (size_t)Wg * gb;
-      if (ctx->world == 1 && !ctx->comm) {
-        hipchk(hipMemcpyAsync(ctx->h_out.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
+      if (direct_out) {
+        // written in place
       } else if (use_exchange) {
         hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
       } else {
         ncclchk(ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
-        hipchk(hipMemcpyAsync(ctx->h_out.p, ctx->g_gath.p, bytes * ctx->world, hipMemcpyDeviceToHost, s),
+        hipchk(hipMemcpyAsync(outbuf(b), ctx->g_gath.p, bytes * ctx->world, hipMemcpyDeviceToHost, s),
                "D2H gathered");
       }
       ctx->stats.windows += 1;
@@ -1017,19 +1076,19 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (!walk) ctx->stats.scan_evals += (int64_t)Wg * ctx->Ns;
     };
     // ---- wait for the window's blob (and run the host exchange when one is configured), parse it
-    auto collect_window = [&](const std::vector<int32_t>& groups) {
+    auto collect_window = [&](const std::vector<int32_t>& groups, int b) {
       const int Wg = (int)groups.size();
       const size_t bytes = (size_t)Wg * gb;
       const auto tw = std::chrono::steady_clock::now();
       hipchk(hipStreamSynchronize(s), "sync window");
       if (use_exchange) {
-        if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, ctx->h_out.p, bytes) != 0)
+        if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, outbuf(b), bytes) != 0)
           raise(PE_ERCCL, "exchange callback failed");
       }
       const auto th = std::chrono::steady_clock::now();
       ctx->stats.greedy_wait_ms += std::chrono::duration<double, std::milli>(th - tw).count();
-      // in place unless the pipelined loop will D2H the next blob into h_out before resolving
-      pe::parse_window(ctx->h_out.p, ctx->world, Wg, K, cands, pipelined);
+      pe::parse_window_keys(outbuf(b), ctx->world, Wg, K, cands);   // lists point into the blob
+
       ctx->stats.greedy_host_ms +=
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
     };
@@ -1037,7 +1096,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     //      after the next collect_window's stream sync)
     auto enqueue_apply = [&](const std::vector<pe::Update>& updates) {
       int64_t nu = 0;
-      hipchk(ctx->h_upd.ensure(std::max<size_t>(updates.size(), 1) * (pe::D + 1)), "alloc pinned upd");
+      hipchk(ctx->h_upd.ensure(std::max<size_t>(updates.size(), 1) * (pe::D + 1), kZeroCopy), "alloc pinned upd");
       for (const pe::Update& u : updates) {
         if (u.gid < ctx->begin || u.gid >= ctx->end) continue;
         int64_t* o = ctx->h_upd.p + nu * (pe::D + 1);
@@ -1045,12 +1104,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         for (int d = 0; d < pe::D; ++d) o[1 + d] = u.res[d];
         ++nu;
       }
-      if (nu > 0) {
-        hipchk(ctx->g_upd.ensure((size_t)nu * (pe::D + 1)), "alloc upd");
-        hipchk(hipMemcpyAsync(ctx->g_upd.p, ctx->h_upd.p, (size_t)nu * (pe::D + 1) * 8, hipMemcpyHostToDevice, s),
-               "H2D upd");
+      if (nu > 0) {   // the kernel reads the pinned records directly (no H2D copy)
         const pe::WalkIndex w = walk_index(ctx);
-        hipchk(pe::launch_apply(s, ctx->res.p, ctx->stride, ctx->g_upd.p, nu, (uint64_t)ctx->begin, ctx->g_kn.p,
+        hipchk(pe::launch_apply(s, ctx->res.p, ctx->stride, ctx->h_upd.dev, nu, (uint64_t)ctx->begin, ctx->g_kn.p,
                                 ctx->g_lo.p, walk ? &w : nullptr),
                "launch apply");
         ctx->w_est += nu;
@@ -1058,9 +1114,23 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     };
     auto timed_resolve = [&](const std::vector<int32_t>& groups, std::vector<pe::Update>& updates,
                              const std::vector<pe::Update>* seed) {
+      if (dump && dump_left-- == 0) {   // PE_DUMP_MAX_WINDOWS reached
+        std::fclose(dump);
+        dump = nullptr;
+      }
+      if (dump) {   // {Wg, groups, blob, n_seed, seeds}: what this resolve call reads
+        const int32_t wg = (int32_t)groups.size(), ns = seed ? (int32_t)seed->size() : 0;
+        std::fwrite(&wg, 4, 1, dump);
+        std::fwrite(groups.data(), 4, (size_t)wg, dump);
+        std::fwrite(outbuf(cb), 1, (size_t)wg * gb * ctx->world, dump);
+        std::fwrite(&ns, 4, 1, dump);
+        if (ns) std::fwrite(seed->data(), sizeof(pe::Update), (size_t)ns, dump);
+      }
       const auto th = std::chrono::steady_clock::now();
       updates.clear();
       const bool consumed = R.resolve(groups, cands, updates, seed);
+      for (const pe::Update& u : updates)          // the mirror follows every placement (all shards)
+        for (int d = 0; d < pe::D; ++d) ctx->m_res[(size_t)d * ctx->n_total + u.gid] = u.res[d];
       ctx->stats.greedy_host_ms +=
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
       return consumed;
@@ -1070,16 +1140,16 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     std::vector<pe::Update> pending, seed;
     pe::Cursor cur_end, nxt_end;
     R.next_window_from(R.cursor(), Wmax, ctx->window_pods, cur, &cur_end);
-    if (!cur.empty()) enqueue_window(cur);
+    if (!cur.empty()) enqueue_window(cur, cb);
     while (!cur.empty()) {
-      collect_window(cur);                       // cur's lists: snapshot = device state at its launch
+      collect_window(cur, cb);                   // cur's lists: snapshot = device state at its launch
       if (!pipelined) {
         std::vector<pe::Update> upd;
         timed_resolve(cur, upd, nullptr);
         enqueue_apply(upd);
         if (R.done()) break;
         R.next_window_from(R.cursor(), Wmax, ctx->window_pods, cur, &cur_end);
-        if (!cur.empty()) enqueue_window(cur);
+        if (!cur.empty()) enqueue_window(cur, cb);
         continue;
       }
       // Pipelined (exact): the device applies the previous window's updates and scans the window
@@ -1090,7 +1160,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       R.next_window_from(cur_end, Wmax, ctx->window_pods, nxt, &nxt_end);
       enqueue_apply(pending);                    // device: everything up to the previous window
       pending.clear();
-      if (!nxt.empty()) enqueue_window(nxt);
+      if (!nxt.empty()) enqueue_window(nxt, 1 - cb);   // the other buffer: cur's lists stay valid
       std::vector<pe::Update> upd;
       const bool consumed = timed_resolve(cur, upd, &seed);
       if (R.done()) {
@@ -1101,6 +1171,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (consumed && !nxt.empty() && R.cursor() == cur_end) {
         cur.swap(nxt);
         cur_end = nxt_end;
+        cb = 1 - cb;
         seed = upd;                              // nxt's scan did not see cur's changes
         pending = std::move(upd);
         continue;
@@ -1109,7 +1180,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       enqueue_apply(upd);
       seed.clear();
       R.next_window_from(R.cursor(), Wmax, ctx->window_pods, cur, &cur_end);
-      if (!cur.empty()) enqueue_window(cur);
+      if (!cur.empty()) enqueue_window(cur, cb);
     }
     hipchk(hipStreamSynchronize(s), "sync greedy");
     if (P > 0) std::memcpy(out_pod_node, R.pod_node().data(), (size_t)P * 4);

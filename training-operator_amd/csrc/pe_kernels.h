@@ -30,22 +30,17 @@ struct alignas(32) ReqRec32 {
 };
 static_assert(sizeof(ReqRec32) == 32, "ReqRec32 must be 32 B");
 
-// Candidate record shipped to the host resolver: key + the node's residual at scan time.
-struct CandRec {
-  uint64_t key;
-  int64_t res[D];
-  uint64_t labels;
-};
-static_assert(sizeof(CandRec) == 48, "CandRec must be 48 B");
-
+// Per-group candidate list shipped to the host resolver: a header + K keys (ascending).  The keys
+// carry the node id (low 24 bits); the host reads the node's residual snapshot from its own mirror
+// of the inventory, so the device ships 8 B per candidate instead of a 48-B record.
 struct CandHdr {
-  int32_t n;       // valid records (sorted by key ascending)
+  int32_t n;       // valid keys (ascending)
   int32_t flags;   // bit0: merge overflowed LDS, list truncated to the exact minimum
   uint64_t limit;  // every clean node with key < limit is in the list
 };
 static_assert(sizeof(CandHdr) == 16, "CandHdr must be 16 B");
 
-__host__ __device__ inline size_t cand_group_bytes(int K) { return sizeof(CandHdr) + (size_t)K * sizeof(CandRec); }
+__host__ __device__ inline size_t cand_group_bytes(int K) { return sizeof(CandHdr) + (size_t)K * sizeof(uint64_t); }
 
 // ---- geometry shared by host and device
 constexpr int FM_CH = 4;       // fit mask: 64-node chunks per wave tile (256 nodes in VGPRs)
@@ -151,8 +146,7 @@ hipError_t launch_scan(hipStream_t s, const int64_t* res, int64_t stride, const 
                        int32_t* cnt, uint64_t* bound, int nwaves);
 
 hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt, const uint64_t* bound,
-                        int nwaves, int K, const int64_t* res, int64_t stride, const uint32_t* labels,
-                        uint64_t id_base, uint8_t* out, int Wg);
+                        int nwaves, int K, uint8_t* out, int Wg);
 
 // ---- sorted walk (the default greedy window path).  The shard's nodes sorted by the node-only
 // key K(n) = (S(n) << 24) | gid, copied into sorted SoA order and summarised per 1024-entry round
@@ -187,7 +181,7 @@ hipError_t sort_keys_u64(void* temp, size_t* temp_bytes, const uint64_t* in, uin
 // Sorted SoA copy, pos[], round summaries from the sorted keys w.sk.
 hipError_t launch_walk_build(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
                              uint64_t id_base, const WalkIndex& w);
-// One block per group: overlay + walk, exact top-K records and limit, same blob as merge.
+// One block per group: overlay + walk, exact top-K keys and limit, same blob as merge.
 hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const WalkIndex& w, const int64_t* res,
                        int64_t stride, const uint32_t* labels, int64_t Ns, uint64_t id_base, uint8_t* out);
 

@@ -1124,22 +1124,12 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
   return sk;
 }
 
-// Group blob: header + the first nout keys of sk as records {key, residual now, labels}.
+// Group blob: header + the first nout keys of sk.
 __device__ void write_group(const uint64_t* sk, int nout, int flags, uint64_t limit, int K, int g,
-                            const int64_t* __restrict__ res, int64_t stride, const uint32_t* __restrict__ labels,
-                            uint64_t id_base, uint8_t* __restrict__ out) {
+                            uint8_t* __restrict__ out) {
   uint8_t* og = out + (size_t)g * cand_group_bytes(K);
-  CandRec* recs = reinterpret_cast<CandRec*>(og + sizeof(CandHdr));
-  for (int i = threadIdx.x; i < nout; i += blockDim.x) {
-    const uint64_t key = sk[i];
-    const int64_t n = (int64_t)((key & 0xFFFFFFull) - id_base);
-    CandRec r;
-    r.key = key;
-#pragma unroll
-    for (int d = 0; d < D; ++d) r.res[d] = res[d * stride + n];
-    r.labels = labels[n];
-    recs[i] = r;
-  }
+  uint64_t* keys = reinterpret_cast<uint64_t*>(og + sizeof(CandHdr));
+  for (int i = threadIdx.x; i < nout; i += blockDim.x) keys[i] = sk[i];
   if (threadIdx.x == 0) {
     CandHdr h;
     h.n = nout;
@@ -1152,8 +1142,6 @@ __device__ void write_group(const uint64_t* sk, int nout, int flags, uint64_t li
 __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __restrict__ cand,
                                                            const int32_t* __restrict__ cnt,
                                                            const uint64_t* __restrict__ bound, int nwaves, int K,
-                                                           const int64_t* __restrict__ res, int64_t stride,
-                                                           const uint32_t* __restrict__ labels, uint64_t id_base,
                                                            uint8_t* __restrict__ out) {
   __shared__ TopkShared s;
   const int g = blockIdx.x;
@@ -1219,20 +1207,18 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
     for (int i = 0; i < MG_THREADS / 64; ++i) mn = umin64(mn, s.red[i]);
     if (tid == 0) s.keys[0] = mn;
     __syncthreads();
-    write_group(s.keys, 1, 1, mn + 1, K, g, res, stride, labels, id_base, out);
+    write_group(s.keys, 1, 1, mn + 1, K, g, out);
     return;
   }
   const uint64_t* sk = topk_sort(s, T, K);
   // sk holds the K + 1 smallest of all T in order; keys >= G were never listed
-  write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : G, K, g, res, stride, labels, id_base, out);
+  write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : G, K, g, out);
 }
 
 hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt, const uint64_t* bound, int nwaves,
-                        int K, const int64_t* res, int64_t stride, const uint32_t* labels, uint64_t id_base,
-                        uint8_t* out, int Wg) {
+                        int K, uint8_t* out, int Wg) {
   if (Wg <= 0) return hipSuccess;
-  hipLaunchKernelGGL(merge_kernel, dim3(Wg), dim3(MG_THREADS), 0, s, cand, cnt, bound, nwaves, K, res, stride, labels,
-                     id_base, out);
+  hipLaunchKernelGGL(merge_kernel, dim3(Wg), dim3(MG_THREADS), 0, s, cand, cnt, bound, nwaves, K, out);
   return hipGetLastError();
 }
 
@@ -1340,7 +1326,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   __shared__ uint32_t cbits[WK_MAXR / 32];
   __shared__ int start_cnt, below;
   const int g = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
   const ReqRec rq = groups[g];
   const int64_t q0 = rq.q[0], q1 = rq.q[1], q2 = rq.q[2], q3 = rq.q[3];
   const uint32_t need = rq.need;
@@ -1445,7 +1431,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   }
   const int T = s.total;
   const uint64_t* sk = topk_sort(s, T, K);
-  write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : NO_KEY, K, g, res, stride, labels, id_base, out);
+  write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : NO_KEY, K, g, out);
 }
 
 hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const WalkIndex& w, const int64_t* res,

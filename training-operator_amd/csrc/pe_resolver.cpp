@@ -5,8 +5,24 @@
 #include <cstring>
 #include <numeric>
 #include <utility>
+#include <cstdio>
+
+#include <immintrin.h>
+#ifdef PE_RES_PROF
+#include <x86intrin.h>
+#endif
 
 namespace pe {
+#ifdef PE_RES_PROF   // section cycle counts for tools/replay_resolver (-DPE_RES_PROF)
+struct ResProf { unsigned long long seed = 0, keys = 0, skip = 0, place = 0, fin = 0, other = 0; long skips = 0, pods = 0;
+  ~ResProf() { std::fprintf(stderr, "cycles seed %.1fM keys %.1fM skip %.1fM place %.1fM fin %.1fM | skips %ld pods %ld\n", seed / 1e6, keys / 1e6, skip / 1e6, place / 1e6, fin / 1e6, skips, pods); } };
+static ResProf rp;
+#define RP_T() __rdtsc()
+#define RP_ADD(f, t) (rp.f += __rdtsc() - (t))
+#else
+#define RP_T() 0ull
+#define RP_ADD(f, t) (void)(t)
+#endif
 
 static constexpr uint64_t kNoKey = ~0ull;
 static constexpr uint64_t kScoreMax = (1ull << 40) - 1;
@@ -36,21 +52,33 @@ uint64_t key_of(const int64_t res[RD], uint32_t labels, const int64_t q[RD], uin
 // ------------------------------------------------------------------ DirtySet
 
 int32_t DirtySet::upsert(int64_t g, const NodeState& st) {
-  if (g >= (int64_t)slot_.size()) slot_.resize((size_t)std::max<int64_t>(g + 1, 2 * (int64_t)slot_.size()), -1);
-  int32_t i = slot_[g];
-  if (i < 0) {
-    i = (int32_t)gid.size();
-    slot_[g] = i;
+  int32_t i = slot_.insert(g, (int32_t)gid.size());
+  if (i == (int32_t)gid.size()) {
+    const size_t w = (size_t)g >> 6;
+    if (w >= bits_.size()) bits_.resize(std::max(w + 1, 2 * bits_.size()), 0);
+    bits_[w] |= 1ull << (g & 63);
     gid.push_back(g);
     r0.push_back(0);
     r1.push_back(0);
     r2.push_back(0);
     r3.push_back(0);
     lab.push_back(0);
+    kn.push_back(0);
     touched.push_back(0);
   }
   set(i, st);
   return i;
+}
+
+// Node-only key of the device scan (pe_kernels.hip node_prep): (S << 24) | gid with
+// S = r0 + (r1 >> 20) + (r2 << 20) + (r3 >> 24), or ~0 where a term can saturate or a residual is
+// negative (such nodes are always scored in full).
+static uint64_t node_only_key(const NodeState& st, int64_t g) {
+  const int64_t* r = st.res;
+  if ((r[0] | r[1] | r[2] | r[3]) < 0 || (uint64_t)r[0] > kScoreMax || r[1] >= (1ll << 60) || r[2] >= (1ll << 20))
+    return kNoKey;
+  const uint64_t S = (uint64_t)r[0] + ((uint64_t)r[1] >> 20) + ((uint64_t)r[2] << 20) + ((uint64_t)r[3] >> 24);
+  return S < kScoreMax ? (S << 24) | (uint64_t)g : kNoKey;
 }
 
 void DirtySet::set(int32_t i, const NodeState& st) {
@@ -59,6 +87,7 @@ void DirtySet::set(int32_t i, const NodeState& st) {
   r2[i] = st.res[2];
   r3[i] = st.res[3];
   lab[i] = st.labels;
+  kn[i] = node_only_key(st, gid[i]);
 }
 
 NodeState DirtySet::get(int32_t i) const {
@@ -72,13 +101,15 @@ NodeState DirtySet::get(int32_t i) const {
 }
 
 void DirtySet::clear() {
-  for (int64_t g : gid) slot_[g] = -1;
+  slot_.clear(gid.begin(), gid.end());
+  for (int64_t g : gid) bits_[(size_t)g >> 6] = 0;
   gid.clear();
   r0.clear();
   r1.clear();
   r2.clear();
   r3.clear();
   lab.clear();
+  kn.clear();
   touched.clear();
 }
 
@@ -96,10 +127,36 @@ static inline uint64_t key_bf(int64_t x0, int64_t x1, int64_t x2, int64_t x3, ui
   return fit ? ((score << 24) | g) : kNoKey;
 }
 
-void DirtySet::keys(const int64_t q[RD], uint32_t need, std::vector<uint64_t>& out) const {
+void DirtySet::keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
+                    std::vector<int32_t>& idx) const {
   const size_t n = gid.size();
-  out.resize(n);
-  for (size_t i = 0; i < n; ++i) out[i] = key_bf(r0[i], r1[i], r2[i], r3[i], lab[i], q, need, (uint64_t)gid[i]);
+  if (out.size() < n) out.resize(n);   // only the slots listed in idx are read
+  idx.clear();
+  // [lo, hi): the K(n) that can give a fitting key < limit (s(q) saturated: then nothing but the
+  // always-scored nodes can fit)
+  uint64_t sq = (uint64_t)q[0] + ((uint64_t)q[1] >> 20) + ((uint64_t)q[3] >> 24);
+  sq = (uint64_t)q[0] > kScoreMax || (uint64_t)q[2] >= (1ull << 20) || sq >= kScoreMax ? kScoreMax
+                                                                                      : sq + ((uint64_t)q[2] << 20);
+  const uint64_t lo = sq >= kScoreMax ? kNoKey : sq << 24;
+  const uint64_t q2 = sq + 2 >= (1ull << 40) ? kNoKey : (sq + 2) << 24;
+  const uint64_t hi = limit == kNoKey || limit >= kNoKey - q2 ? kNoKey : limit + q2;
+  const uint64_t span = hi > lo ? hi - lo : 0;
+  // the range test k - lo < span (unsigned) or k == ~0, four nodes per AVX2 step (signed compare
+  // of sign-flipped values); the few hits are scored below
+  const uint64_t* kp = kn.data();
+  const __m256i flip = _mm256_set1_epi64x(INT64_MIN), vlo = _mm256_set1_epi64x((int64_t)lo),
+                vspan = _mm256_set1_epi64x((int64_t)(span ^ (1ull << 63))), ones = _mm256_set1_epi64x(-1);
+  size_t i = 0;
+  for (; i + 4 <= n; i += 4) {
+    const __m256i k = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(kp + i));
+    const __m256i d = _mm256_xor_si256(_mm256_sub_epi64(k, vlo), flip);
+    const __m256i hit = _mm256_or_si256(_mm256_cmpgt_epi64(vspan, d), _mm256_cmpeq_epi64(k, ones));
+    for (int m = _mm256_movemask_pd(_mm256_castsi256_pd(hit)); m; m &= m - 1)
+      idx.push_back((int32_t)(i + __builtin_ctz(m)));
+  }
+  for (; i < n; ++i)
+    if (kp[i] - lo < span || kp[i] == kNoKey) idx.push_back((int32_t)i);
+  for (int32_t j : idx) out[j] = key_bf(r0[j], r1[j], r2[j], r3[j], lab[j], q, need, (uint64_t)gid[j]);
 }
 
 uint64_t DirtySet::key_at(int32_t i, const int64_t q[RD], uint32_t need) const {
@@ -108,14 +165,27 @@ uint64_t DirtySet::key_at(int32_t i, const int64_t q[RD], uint32_t need) const {
 
 void merge_shards(const std::vector<const GroupCands*>& parts, GroupCands& out) {
   out.own.clear();
+  out.own_keys.clear();
   out.limit = kNoKey;
   for (const GroupCands* p : parts) out.limit = std::min(out.limit, p->limit);
+  const bool keyed = !parts.empty() && parts[0]->keys;
   for (const GroupCands* p : parts)
-    for (size_t i = 0; i < p->n; ++i)
-      if ((*p)[i].key < out.limit) out.own.push_back((*p)[i]);
-  std::sort(out.own.begin(), out.own.end(), [](const Cand& a, const Cand& b) { return a.key < b.key; });
-  out.data = out.own.data();
-  out.n = out.own.size();
+    for (size_t i = 0; i < p->n; ++i) {
+      if (p->key(i) >= out.limit) continue;
+      if (keyed) out.own_keys.push_back(p->keys[i]);
+      else out.own.push_back(p->data[i]);
+    }
+  if (keyed) {
+    std::sort(out.own_keys.begin(), out.own_keys.end());
+    out.keys = out.own_keys.data();
+    out.data = nullptr;
+    out.n = out.own_keys.size();
+  } else {
+    std::sort(out.own.begin(), out.own.end(), [](const Cand& a, const Cand& b) { return a.key < b.key; });
+    out.data = out.own.data();
+    out.keys = nullptr;
+    out.n = out.own.size();
+  }
 }
 
 void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands,
@@ -136,10 +206,35 @@ void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::v
       gc.limit = limit;
       gc.n = (size_t)std::max(n, 0);
       gc.data = reinterpret_cast<const Cand*>(base + 16);   // 16-B aligned records in the blob
+      gc.keys = nullptr;
       if (copy_blob && n_shards == 1) {
         gc.own.assign(gc.data, gc.data + gc.n);
         gc.data = gc.own.data();
       }
+      pp[r] = &parts[r];
+    }
+    if (n_shards > 1) merge_shards(pp, cands[w]);
+  }
+}
+
+void parse_window_keys(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands) {
+  const size_t gb = 16 + (size_t)K * 8;
+  const size_t shard_bytes = (size_t)n_groups * gb;
+  cands.resize((size_t)n_groups);
+  std::vector<GroupCands> parts((size_t)n_shards);
+  std::vector<const GroupCands*> pp((size_t)n_shards);
+  for (int w = 0; w < n_groups; ++w) {
+    for (int r = 0; r < n_shards; ++r) {
+      const uint8_t* base = blob + (size_t)r * shard_bytes + (size_t)w * gb;
+      int32_t n;
+      uint64_t limit;
+      std::memcpy(&n, base, 4);
+      std::memcpy(&limit, base + 8, 8);
+      GroupCands& gc = n_shards == 1 ? cands[w] : parts[r];
+      gc.limit = limit;
+      gc.n = (size_t)std::max(n, 0);
+      gc.keys = reinterpret_cast<const uint64_t*>(base + 16);
+      gc.data = nullptr;
       pp[r] = &parts[r];
     }
     if (n_shards > 1) merge_shards(pp, cands[w]);
@@ -178,6 +273,12 @@ void Resolver::advance_group() {
   }
 }
 
+NodeState& Resolver::job_node(int64_t gid) {
+  const int32_t i = jslot_.insert(gid, (int32_t)jn_.size());
+  if (i == (int32_t)jn_.size()) jn_.emplace_back(gid, NodeState{});
+  return jn_[i].second;
+}
+
 void Resolver::finish_job(bool ok) {
   const int64_t j = order_[oi_];
   if (ok) {
@@ -190,17 +291,23 @@ void Resolver::finish_job(bool ok) {
       for (int32_t p = 0; p < cnt_[g]; ++p) {
         int32_t& slot = pod_node_[pod_off_[g] + p];
         if (slot < 0) continue;
-        NodeState& st = job_nodes_[slot];
+        NodeState& st = jn_[jslot_.find(slot)].second;
         for (int d = 0; d < RD; ++d) st.res[d] += q[d];
         slot = -1;
         --pods_placed_;
       }
     }
-    for (const auto& kv : job_nodes_) dirty_.mark(dirty_.upsert(kv.first, kv.second));
+    for (const auto& kv : jn_) dirty_.mark(dirty_.upsert(kv.first, kv.second));
     job_status_[j] = 1;
     ++jobs_failed_;
   }
-  job_nodes_.clear();
+  if (!jn_.empty()) {
+    std::vector<int64_t>& ids = jn_ids_;
+    ids.clear();
+    for (const auto& kv : jn_) ids.push_back(kv.first);
+    jslot_.clear(ids.begin(), ids.end());
+  }
+  jn_.clear();
   ++oi_;
   p_ = 0;
   if (!done()) g_ = jgo_[order_[oi_]];
@@ -258,6 +365,7 @@ void Resolver::next_window_from(const Cursor& from, int max_groups, int64_t max_
 bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<GroupCands>& cands,
                        std::vector<Update>& updates, const std::vector<Update>* seed) {
   bool consumed = true;
+  unsigned long long t_ = RP_T();
   if (seed)
     for (const Update& u : *seed) {
       NodeState st;
@@ -265,15 +373,17 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       st.labels = u.labels;
       dirty_.upsert(u.gid, st);   // dirty but untouched: not flushed again unless changed here
     }
+  RP_ADD(seed, t_);
   size_t wi = 0;
   std::vector<uint64_t>& dk = dk_;  // keys of the dirty nodes for the current group
-  auto argmin = [&dk]() -> int32_t {
+  std::vector<int32_t>& dki = dki_;  // the slots among them that can hold a key
+  auto argmin = [&dk, &dki]() -> int32_t {
     int32_t b = -1;
     uint64_t bk = kNoKey;
-    for (size_t i = 0; i < dk.size(); ++i)
+    for (int32_t i : dki)
       if (dk[i] < bk) {
         bk = dk[i];
-        b = (int32_t)i;
+        b = i;
       }
     return b;
   };
@@ -283,13 +393,23 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     const GroupCands& gc = cands[wi];
     const int64_t* q = req_ + (int64_t)g_ * RD;
     const uint32_t need = need_[g_];
-    dirty_.keys(q, need, dk);
+    t_ = RP_T();
+    dirty_.keys(q, need, gc.limit, dk, dki);   // dirty keys >= limit never decide (list head or rescan)
     int32_t best = argmin();
+    RP_ADD(keys, t_);
     size_t ptr = 0;
     bool failed = false;
     while (p_ < cnt_[g_]) {
-      while (ptr < gc.size() && dirty_.find((int64_t)(gc[ptr].key & 0xFFFFFFull)) >= 0) ++ptr;
-      const uint64_t kc = ptr < gc.size() ? gc[ptr].key : kNoKey;
+      t_ = RP_T();
+      while (ptr < gc.size() && dirty_.contains((int64_t)(gc.key(ptr) & 0xFFFFFFull))) {
+        ++ptr;
+#ifdef PE_RES_PROF
+        rp.skips++;
+#endif
+      }
+      RP_ADD(skip, t_);
+      t_ = RP_T();
+      const uint64_t kc = ptr < gc.size() ? gc.key(ptr) : kNoKey;
       const uint64_t kd = best >= 0 ? dk[best] : kNoKey;
       if (ptr == gc.size() && gc.limit != kNoKey && kd >= gc.limit) {
         consumed = false;  // clean nodes beyond the limit could win: rescan from this pod
@@ -307,20 +427,26 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         slot = best;
         st = dirty_.get(slot);
       } else {
-        const Cand& c = gc[ptr];
-        for (int d = 0; d < RD; ++d) st.res[d] = c.res[d];
-        st.labels = c.labels;
+        if (gc.keys) {   // clean: the mirror holds the snapshot state
+          for (int d = 0; d < RD; ++d) st.res[d] = mirror_.res[d * mirror_.n + gid];
+          st.labels = mirror_.labels[gid];
+        } else {
+          const Cand& c = gc.data[ptr];
+          for (int d = 0; d < RD; ++d) st.res[d] = c.res[d];
+          st.labels = c.labels;
+        }
         slot = -1;
       }
       for (int d = 0; d < RD; ++d) st.res[d] -= q[d];
       if (slot < 0) {
         slot = dirty_.upsert(gid, st);
         dk.push_back(kNoKey);
+        dki.push_back(slot);
       } else {
         dirty_.set(slot, st);
       }
       dirty_.mark(slot);
-      job_nodes_[gid] = st;
+      job_node(gid) = st;
       pod_node_[pod_off_[g_] + p_] = (int32_t)gid;
       ++p_;
       ++pods_placed_;
@@ -329,6 +455,10 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       dk[slot] = dirty_.key_at(slot, q, need);
       if (dk[slot] != kNoKey) best = slot;
       else if (best == slot) best = argmin();
+      RP_ADD(place, t_);
+#ifdef PE_RES_PROF
+      rp.pods++;
+#endif
     }
     if (!consumed) break;
     if (failed) {
@@ -341,6 +471,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     }
     ++wi;
   }
+  t_ = RP_T();
   for (size_t i = 0; i < dirty_.size(); ++i) {
     if (!dirty_.touched[i]) continue;
     Update u;
@@ -351,6 +482,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     updates.push_back(u);
   }
   dirty_.clear();
+  RP_ADD(fin, t_);
   if (!consumed) ++rescans_;
   return consumed;
 }

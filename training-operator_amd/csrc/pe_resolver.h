@@ -25,23 +25,35 @@ struct NodeState {
   uint32_t labels;
 };
 
-// One candidate, byte-identical to the device's CandRec (labels in the low half of a u64), so a
-// single-shard window blob is read in place.
+// One candidate record of the pe_resolver_* ABI blob (placement.h): key + the node's residual
+// snapshot, labels in the low half of a u64.
 struct Cand {
   uint64_t key;
   int64_t res[RD];
   uint32_t labels;
   uint32_t pad_;
 };
-static_assert(sizeof(Cand) == 48, "Cand must match the 48-B device record");
+static_assert(sizeof(Cand) == 48, "Cand must match the 48-B ABI record");
 
+// Host copy of the inventory the engine keeps next to the device shard(s): residual SoA
+// res[d * n + gid] and labels[gid] of the GLOBAL inventory, current at the window's snapshot for
+// every clean node.  Key-only candidate lists read their nodes' states here.
+struct Mirror {
+  const int64_t* res = nullptr;
+  int64_t n = 0;
+  const uint32_t* labels = nullptr;
+};
+
+// One group's candidate list: either records (data) or keys whose states come from a Mirror.
 struct GroupCands {
-  const Cand* data = nullptr;  // ascending keys, all clean at the snapshot
+  const Cand* data = nullptr;      // ascending keys, all clean at the snapshot
+  const uint64_t* keys = nullptr;  // key-only form (engine windows)
   size_t n = 0;
-  uint64_t limit = ~0ull;      // every clean node with key < limit is listed
-  std::vector<Cand> own;       // storage when the list is a copy (shard merge, or copy_blob)
+  uint64_t limit = ~0ull;          // every clean node with key < limit is listed
+  std::vector<Cand> own;           // storage when the list is a copy (shard merge, or copy_blob)
+  std::vector<uint64_t> own_keys;
   size_t size() const { return n; }
-  const Cand& operator[](size_t i) const { return data[i]; }
+  uint64_t key(size_t i) const { return keys ? keys[i] : data[i].key; }
 };
 
 struct Update {
@@ -70,27 +82,107 @@ void merge_shards(const std::vector<const GroupCands*>& parts, GroupCands& out);
 // With one shard and copy_blob = false the lists point INTO the blob, which must outlive them.
 void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands,
                   bool copy_blob = false);
+// Key-only window blob (the engine's device format): per shard, per group a 16-B header + K u64
+// keys.  Lists point into the blob when n_shards == 1.
+void parse_window_keys(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands);
+
+// Node id -> small index, open addressing (linear probing) sized to the live entries: the dirty
+// set and a job's nodes hold hundreds of ids out of up to 2^24, so the table stays in L1/L2 where a
+// direct-mapped array over all ids would miss in cache on every lookup.
+class IdMap {
+ public:
+  int32_t find(int64_t id) const {
+    if (n_ == 0) return -1;
+    for (size_t h = hash(id);; h = (h + 1) & mask_) {
+      if (keys_[h] == id) return vals_[h];
+      if (keys_[h] < 0) return -1;
+    }
+  }
+  // value of id, inserting `v` if absent
+  int32_t insert(int64_t id, int32_t v) {
+    if (2 * (n_ + 1) > keys_.size()) grow();
+    for (size_t h = hash(id);; h = (h + 1) & mask_) {
+      if (keys_[h] == id) return vals_[h];
+      if (keys_[h] < 0) {
+        keys_[h] = id;
+        vals_[h] = v;
+        ++n_;
+        return v;
+      }
+    }
+  }
+  // forget every id (the caller lists them: O(entries), not O(table))
+  template <class It>
+  void clear(It b, It e) {
+    if (4 * n_ < keys_.size() / 4 && keys_.size() > 1024) {   // far too big after a burst: shrink
+      keys_.assign(1024, -1);
+      vals_.assign(1024, -1);
+      mask_ = 1023;
+    } else {
+      pos_.clear();
+      for (; b != e; ++b)   // tombstones first, so the remaining ids' probe chains stay intact
+        for (size_t h = hash(*b);; h = (h + 1) & mask_)
+          if (keys_[h] == *b) {
+            keys_[h] = -2;
+            pos_.push_back(h);
+            break;
+          }
+      for (size_t h : pos_) keys_[h] = -1;
+    }
+    n_ = 0;
+  }
+
+ private:
+  size_t hash(int64_t id) const { return (size_t)(((uint64_t)id * 0x9E3779B97F4A7C15ull) >> 40) & mask_; }
+  void grow() {
+    std::vector<int64_t> ok = std::move(keys_);
+    std::vector<int32_t> ov = std::move(vals_);
+    const size_t cap = std::max<size_t>(1024, ok.size() * 2);
+    keys_.assign(cap, -1);
+    vals_.assign(cap, -1);
+    mask_ = cap - 1;
+    n_ = 0;
+    for (size_t i = 0; i < ok.size(); ++i)
+      if (ok[i] >= 0) insert(ok[i], ov[i]);
+  }
+  std::vector<int64_t> keys_;
+  std::vector<int32_t> vals_;
+  std::vector<size_t> pos_;
+  size_t mask_ = 0, n_ = 0;
+};
 
 // Nodes modified since the window's snapshot, as flat struct-of-arrays so the per-group re-score
 // is one branch-free (vectorisable) loop; gid -> slot is a direct-mapped array grown on demand.
 class DirtySet {
  public:
-  int32_t find(int64_t gid) const { return gid < (int64_t)slot_.size() ? slot_[gid] : -1; }
+  int32_t find(int64_t gid) const { return slot_.find(gid); }
+  // membership only: one bit per node id (128 KiB per 1M ids, cache-resident), the candidate
+  // lists' skip test
+  bool contains(int64_t gid) const {
+    const size_t w = (size_t)gid >> 6;
+    return w < bits_.size() && (bits_[w] >> (gid & 63) & 1);
+  }
   int32_t upsert(int64_t gid, const NodeState& st);
   void set(int32_t i, const NodeState& st);
   void mark(int32_t i) { touched[i] = 1; }
   NodeState get(int32_t i) const;
   size_t size() const { return gid.size(); }
   void clear();
-  // keys of every dirty node for request (q, need) -> out (NO_KEY where it does not fit)
-  void keys(const int64_t q[RD], uint32_t need, std::vector<uint64_t>& out) const;
+  // keys of every dirty node for request (q, need) -> out (NO_KEY where it does not fit).  Keys
+  // >= `limit` may be reported as NO_KEY: a node whose node-only key K(n) (below) rules out a key
+  // < limit is not scored (K(n) >= (s(q) << 24) for a fit, key >= K(n) - ((s(q) + 2) << 24)).
+  // `idx` receives the slots that were scored (the rest are NO_KEY in out).
+  void keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
+            std::vector<int32_t>& idx) const;
   uint64_t key_at(int32_t i, const int64_t q[RD], uint32_t need) const;
   std::vector<int64_t> gid, r0, r1, r2, r3;
   std::vector<uint32_t> lab;
+  std::vector<uint64_t> kn;       // K(n) = (S(n) << 24) | gid, or ~0 (saturating / negative: always scored)
   std::vector<uint8_t> touched;   // changed in this window (seeded entries start untouched)
 
  private:
-  std::vector<int32_t> slot_;
+  IdMap slot_;
+  std::vector<uint64_t> bits_;
 };
 
 class Resolver {
@@ -105,6 +197,8 @@ class Resolver {
   void next_window_from(const Cursor& from, int max_groups, int64_t max_pods, std::vector<int32_t>& groups,
                         Cursor* end) const;
   Cursor cursor() const { return Cursor{oi_, g_, p_}; }
+  // states of key-only candidates (must stay valid and current while resolving such lists)
+  void set_mirror(const Mirror& m) { mirror_ = m; }
   // Resolve with candidates for exactly the groups returned by next_window (same order).
   // Appends the residual updates to flush; returns true if the whole window was consumed.
   // seed (pipelined form): nodes changed since the snapshot the candidates were scanned on, with
@@ -130,6 +224,7 @@ class Resolver {
   const int32_t* cnt_;
   const int64_t* req_;
   const uint32_t* need_;
+  Mirror mirror_;
   std::vector<int64_t> order_;
   std::vector<int64_t> pod_off_;
   std::vector<int32_t> pod_node_;
@@ -141,8 +236,13 @@ class Resolver {
   // window state
   DirtySet dirty_;
   std::vector<uint64_t> dk_;
+  std::vector<int32_t> dki_;   // dirty slots with a key for the current group (argmin runs over these)
   // nodes touched by the current job (exact current residuals, survive window flushes)
-  std::unordered_map<int64_t, NodeState> job_nodes_;
+  // gid -> index into jn_ (reset per job): no allocation per pod
+  IdMap jslot_;
+  std::vector<std::pair<int64_t, NodeState>> jn_;
+  std::vector<int64_t> jn_ids_;
+  NodeState& job_node(int64_t gid);
   int64_t jobs_placed_ = 0, jobs_failed_ = 0, pods_placed_ = 0, rescans_ = 0;
 };
 
