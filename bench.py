@@ -126,7 +126,7 @@ def main():
                     help="weak: batch = fit-jobs x n_gpus (fixed per-rank work); strong: batch = fit-jobs")
     ap.add_argument("--fit-path-mask", type=int, default=0, help="pe_config.fit_path_mask (0 = every kernel)")
     ap.add_argument("--greedy-flags", type=int, default=0,
-                    help="pe_config.greedy_flags (bit0: pipelined windows, bit1: full scan instead of the sorted walk)")
+                    help="pe_config.greedy_flags (bit0: sequential windows, bit1: full scan instead of the sorted walk)")
     ap.add_argument("--resort-nodes", type=int, default=0, help="pe_config.resort_nodes (0 = default)")
     args = ap.parse_args()
 
@@ -292,7 +292,9 @@ def main():
                  "100k 8-GPU nodes x 10k gangs of 1-16 pods x 8 GPUs, label-constrained, all-or-nothing")):
             cinv = synth.make_inventory(n_nodes, synth.SEED[cfg], gpu_frac)
             cb = synth.make_jobs(n_jobs, synth.SEED[cfg], mix)
-            ce = Engine(device, rank=rank, world_size=world, comm=new_comm(), exchange=exchange, max_nodes=n_nodes)
+            ce = Engine(device, rank=rank, world_size=world, comm=new_comm(), exchange=exchange, max_nodes=n_nodes,
+                        topk=args.topk, window_groups=args.window_groups, window_pods=args.window_pods,
+                        greedy_flags=args.greedy_flags, resort_nodes=args.resort_nodes)
             ce.load_nodes(cinv.cap, cinv.used, cinv.labels, cinv.island)
             ce.place_batch(cb)                       # warm-up
             ts = []
@@ -309,7 +311,7 @@ def main():
             out["configs"][cfg] = {"workload": what, "nodes": n_nodes, "jobs": n_jobs, "pods": cb.n_pods,
                                    "jobs_placed": int((cst == 0).sum()), "gang_placements_per_s": n_jobs / ct,
                                    "ms_per_batch": ct * 1e3, "windows_per_batch": cs["windows"] / 4.0,
-                                   "group_x_node_evals_per_s": cs["scan_evals"] / 4.0 * world / ct}
+                                   "rescans_per_batch": cs["rescans"] / 4.0}
             ce.close()
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -86,7 +86,7 @@ typedef struct {
   void* exchange_user;
   int64_t max_nodes;             /* global inventory capacity (<= PE_MAX_NODES) */
   const char* gpu_resource_name; /* resource key of dim 2, e.g. "amd.com/gpu" (informational) */
-  int32_t topk;                  /* best-fit candidates kept per group scan (0 = 64) */
+  int32_t topk;                  /* best-fit candidates kept per group and window (0 = 256) */
   int32_t window_groups;         /* groups per scan window (0 = 64) */
   int64_t window_pods;           /* pods per scan window (0 = 1024) */
   int32_t fit_path_mask;         /* allowed fit-mask kernels: bit0 int64 compare, bit1 int32 compare,
@@ -95,12 +95,10 @@ typedef struct {
                                     block-major kernel (PE_MASK_NODE_BLOCKS) instead of the row-major
                                     sweep (PE_MASK_ROWS); no kernel bit set = all kernels (the
                                     int64 path is always allowed) */
-  int32_t greedy_flags;          /* bit0 set = pipelined greedy windows: the GPU scans the next window
-                                    while the host resolves the current one (exact; the current
-                                    window's changes are seeded as dirty).  Off by default: best-fit
-                                    packs consecutive windows onto the same nodes, so the seeded
-                                    nodes shorten the next lists and the extra rescans cost more than
-                                    the overlap saves (profiles/r5_greedy_pipeline.txt).
+  int32_t greedy_flags;          /* bit0 set = sequential greedy windows.  Default (clear): pipelined --
+                                    the GPU scans the next window while the host resolves the current
+                                    one, and the current window's changes are seeded as dirty nodes
+                                    into the next one's resolution (exact either way).
                                     bit1 set = every window scans all nodes of the shard (scan +
                                     merge kernels) instead of the sorted walk */
   int32_t resort_nodes;          /* sorted walk: rebuild the sorted index once this many node updates
