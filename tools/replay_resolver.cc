@@ -29,13 +29,17 @@ int main(int argc, char** argv) {
   size_t ok = std::fread(jgo.data(), 4, J + 1, f) + std::fread(pri.data(), 4, J, f) + std::fread(cnt.data(), 4, G, f) +
               std::fread(req.data(), 8, G * 4, f) + std::fread(need.data(), 4, G, f);
   if (ok != (size_t)(J + 1 + J + G + G * 4 + G)) return 2;
+  int64_t N = 0;
+  if (std::fread(&N, 8, 1, f) != 1) return 2;
+  std::vector<pe::NodeState> mirror0(N);
+  if (std::fread(mirror0.data(), sizeof(pe::NodeState), N, f) != (size_t)N) return 2;
   struct Win {
     std::vector<int32_t> groups;
     std::vector<uint8_t> blob;
     std::vector<pe::Update> seed;
   };
   std::vector<Win> wins;
-  const size_t gb = 16 + (size_t)K * 48;
+  const size_t gb = 16 + (size_t)K * 8;   // key-only lists
   for (;;) {
     int32_t wg;
     if (std::fread(&wg, 4, 1, f) != 1) break;
@@ -56,16 +60,20 @@ int main(int argc, char** argv) {
   for (int r = 0; r < reps; ++r) {
     const auto t0 = std::chrono::steady_clock::now();
     pe::Resolver R(J, jgo.data(), pri.data(), cnt.data(), req.data(), need.data());
+    std::vector<pe::NodeState> mirror = mirror0;
+    R.set_mirror(pe::Mirror{mirror.data(), N});
     std::vector<pe::GroupCands> cands;
     std::vector<pe::Update> upd;
     double t_resolve = 0;
     size_t wi = 0;
     for (; wi < wins.size(); ++wi) {       // the resolve calls of the run, in order
       const Win& w = wins[wi];
-      pe::parse_window(w.blob.data(), 1, (int)w.groups.size(), K, cands);
+      pe::parse_window_keys(w.blob.data(), 1, (int)w.groups.size(), K, cands);
       upd.clear();
       const auto a = std::chrono::steady_clock::now();
       R.resolve(w.groups, cands, upd, w.seed.empty() ? nullptr : &w.seed);
+      for (const pe::Update& u : upd)
+        for (int d = 0; d < 4; ++d) mirror[u.gid].res[d] = u.res[d];
       t_resolve += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
     }
     if (!R.done() && r == 0) std::printf("(partial dump: the batch is not decided after %zu windows)\n", wi);

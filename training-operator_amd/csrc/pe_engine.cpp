@@ -110,10 +110,9 @@ struct pe_ctx {
   // inventory shard
   int64_t n_total = 0, begin = 0, end = 0, Ns = 0, stride = 0;
   bool loaded = false;
-  // host mirror of the GLOBAL inventory (residual SoA [4][n_total], its reset copy, labels): the
-  // greedy windows ship candidate keys only and the resolver reads node states here
-  std::vector<int64_t> m_res, m_res0;
-  std::vector<uint32_t> m_lab;
+  // host mirror of the GLOBAL inventory (node states by id, and the reset copy): the greedy
+  // windows ship candidate keys only and the resolver reads node states here
+  std::vector<pe::NodeState> m_nodes, m_nodes0;
   DevBuf<int64_t> res0, res;
   DevBuf<uint32_t> labels;
   DevBuf<int32_t> island;
@@ -334,14 +333,15 @@ int pe_load_nodes(pe_ctx* ctx, int64_t n, const int64_t* cap, const int64_t* use
       lab[i] = labels ? labels[ctx->begin + i] : 0u;
       isl[i] = island ? island[ctx->begin + i] : -1;
     }
-    ctx->m_res.resize((size_t)pe::D * n);
-    for (int64_t k = 0; k < pe::D * n; ++k) {
-      if (cap[k] < 0 || used[k] < 0) raise(PE_EINVAL, "negative capacity/usage");
-      ctx->m_res[k] = cap[k] - used[k];
-    }
-    ctx->m_res0 = ctx->m_res;
-    ctx->m_lab.assign((size_t)n, 0u);
-    if (labels) std::copy(labels, labels + n, ctx->m_lab.begin());
+    ctx->m_nodes.assign((size_t)n, pe::NodeState{});
+    for (int d = 0; d < pe::D; ++d)
+      for (int64_t g = 0; g < n; ++g) {
+        if (cap[d * n + g] < 0 || used[d * n + g] < 0) raise(PE_EINVAL, "negative capacity/usage");
+        ctx->m_nodes[g].res[d] = cap[d * n + g] - used[d * n + g];
+      }
+    if (labels)
+      for (int64_t g = 0; g < n; ++g) ctx->m_nodes[g].labels = labels[g];
+    ctx->m_nodes0 = ctx->m_nodes;
     hipchk(ctx->res0.ensure(cells), "alloc res0");
     hipchk(ctx->res.ensure(cells), "alloc res");
     hipchk(ctx->labels.ensure((size_t)ctx->stride), "alloc labels");
@@ -382,12 +382,11 @@ int pe_update_nodes(pe_ctx* ctx, int64_t n, const int64_t* slots, const uint8_t*
     // the host mirror takes every entry in order (global inventory)
     for (int64_t i = 0; i < n; ++i) {
       const int64_t g = slots[i];
-      for (int d = 0; d < pe::D; ++d) {
-        const int64_t v = op[i] == PE_NODE_SET ? cap[i * pe::D + d] - used[i * pe::D + d] : pe::NEVER;
-        ctx->m_res[(size_t)d * ctx->n_total + g] = v;
-        ctx->m_res0[(size_t)d * ctx->n_total + g] = v;
-      }
-      ctx->m_lab[g] = op[i] == PE_NODE_SET && labels ? labels[i] : 0u;
+      pe::NodeState& m = ctx->m_nodes[g];
+      for (int d = 0; d < pe::D; ++d)
+        m.res[d] = op[i] == PE_NODE_SET ? cap[i * pe::D + d] - used[i * pe::D + d] : pe::NEVER;
+      m.labels = op[i] == PE_NODE_SET && labels ? labels[i] : 0u;
+      ctx->m_nodes0[g] = m;
     }
     // last entry per slot wins; keep only this shard's slots
     std::unordered_map<int64_t, int64_t> last;
@@ -431,7 +430,7 @@ int pe_reset_residuals(pe_ctx* ctx) {
     hipchk(hipMemcpyAsync(ctx->res.p, ctx->res0.p, (size_t)pe::D * ctx->stride * 8, hipMemcpyDeviceToDevice,
                           ctx->stream),
            "D2D reset");
-    ctx->m_res = ctx->m_res0;
+    ctx->m_nodes = ctx->m_nodes0;
     return PE_OK;
   });
 }
@@ -970,7 +969,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       group_need = no_need.data();
     }
     pe::Resolver R(n_jobs, job_group_off, priority, group_count, group_req, group_need);
-    R.set_mirror(pe::Mirror{ctx->m_res.data(), ctx->n_total, ctx->m_lab.data()});
+    R.set_mirror(pe::Mirror{ctx->m_nodes.data(), ctx->n_total});
     // PE_DUMP_WINDOWS=<file>: record the batch and every window's groups + blob (host resolver
     // replay, tools/replay_resolver.cc); diagnostics only
     FILE* dump = nullptr;
@@ -984,6 +983,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         std::fwrite(group_count, 4, (size_t)G, dump);
         std::fwrite(group_req, 8, (size_t)G * pe::D, dump);
         std::fwrite(group_need, 4, (size_t)G, dump);
+        std::fwrite(&ctx->n_total, 8, 1, dump);   // the host mirror at the batch start
+        std::fwrite(ctx->m_nodes.data(), sizeof(pe::NodeState), ctx->m_nodes.size(), dump);
       }
     }
     struct DumpClose { FILE*& f; ~DumpClose() { if (f) std::fclose(f); } } dump_close{dump};
@@ -1130,7 +1131,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       updates.clear();
       const bool consumed = R.resolve(groups, cands, updates, seed);
       for (const pe::Update& u : updates)          // the mirror follows every placement (all shards)
-        for (int d = 0; d < pe::D; ++d) ctx->m_res[(size_t)d * ctx->n_total + u.gid] = u.res[d];
+        for (int d = 0; d < pe::D; ++d) ctx->m_nodes[u.gid].res[d] = u.res[d];
       ctx->stats.greedy_host_ms +=
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
       return consumed;

@@ -394,6 +394,8 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     const int64_t* q = req_ + (int64_t)g_ * RD;
     const uint32_t need = need_[g_];
     t_ = RP_T();
+    if (gc.keys)   // the first listed nodes' states (the rest are prefetched as the list is consumed)
+      for (size_t i = 0; i < std::min<size_t>(4, gc.size()); ++i) __builtin_prefetch(&mirror_.nodes[gc.keys[i] & 0xFFFFFFull]);
     dirty_.keys(q, need, gc.limit, dk, dki);   // dirty keys >= limit never decide (list head or rescan)
     int32_t best = argmin();
     RP_ADD(keys, t_);
@@ -428,8 +430,8 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         st = dirty_.get(slot);
       } else {
         if (gc.keys) {   // clean: the mirror holds the snapshot state
-          for (int d = 0; d < RD; ++d) st.res[d] = mirror_.res[d * mirror_.n + gid];
-          st.labels = mirror_.labels[gid];
+          st = mirror_.nodes[gid];
+          if (ptr + 4 < gc.size()) __builtin_prefetch(&mirror_.nodes[gc.key(ptr + 4) & 0xFFFFFFull]);
         } else {
           const Cand& c = gc.data[ptr];
           for (int d = 0; d < RD; ++d) st.res[d] = c.res[d];
@@ -437,7 +439,13 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         }
         slot = -1;
       }
-      for (int d = 0; d < RD; ++d) st.res[d] -= q[d];
+      // The chosen node's key only falls while it still fits (its leftovers shrink), so it stays
+      // the minimum for every following pod of the group that still fits on it: place them all
+      // at once, m = min(pods left, min over q_d > 0 of res_d / q_d).
+      int64_t m = cnt_[g_] - p_;
+      for (int d = 0; d < RD; ++d)
+        if (q[d] > 0) m = std::min<int64_t>(m, st.res[d] / q[d]);
+      for (int d = 0; d < RD; ++d) st.res[d] -= m * q[d];
       if (slot < 0) {
         slot = dirty_.upsert(gid, st);
         dk.push_back(kNoKey);
@@ -447,11 +455,10 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       }
       dirty_.mark(slot);
       job_node(gid) = st;
-      pod_node_[pod_off_[g_] + p_] = (int32_t)gid;
-      ++p_;
-      ++pods_placed_;
-      // the chosen node's key only falls while it still fits (its leftovers shrink), so it stays
-      // the minimum; once it no longer fits the next minimum is searched
+      std::fill_n(pod_node_.begin() + pod_off_[g_] + p_, m, (int32_t)gid);
+      p_ += (int32_t)m;
+      pods_placed_ += m;
+      // still fitting only if the group ran out of pods first; then it stays the minimum
       dk[slot] = dirty_.key_at(slot, q, need);
       if (dk[slot] != kNoKey) best = slot;
       else if (best == slot) best = argmin();

@@ -35,13 +35,12 @@ struct Cand {
 };
 static_assert(sizeof(Cand) == 48, "Cand must match the 48-B ABI record");
 
-// Host copy of the inventory the engine keeps next to the device shard(s): residual SoA
-// res[d * n + gid] and labels[gid] of the GLOBAL inventory, current at the window's snapshot for
-// every clean node.  Key-only candidate lists read their nodes' states here.
+// Host copy of the inventory the engine keeps next to the device shard(s): state (residuals +
+// labels) of every node of the GLOBAL inventory by id, current at the window's snapshot for every
+// clean node.  Key-only candidate lists read their nodes' states here (one cache line per node).
 struct Mirror {
-  const int64_t* res = nullptr;
+  const NodeState* nodes = nullptr;
   int64_t n = 0;
-  const uint32_t* labels = nullptr;
 };
 
 // One group's candidate list: either records (data) or keys whose states come from a Mirror.
