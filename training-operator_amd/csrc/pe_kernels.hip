@@ -1027,16 +1027,56 @@ __device__ __forceinline__ void topk_append(TopkShared& s, uint64_t k, bool take
   if (take && base + rank < MG_CAP) s.keys[base + rank] = k;
 }
 
-// Block-wide: sorts (at least) the K + 1 smallest of s.keys[0..T) ascending and returns the array
-// holding them at its front (s.keys or s.sel).  Only the K + 1 smallest matter (K records + the
-// limit), so for T > 2(K+1) a 256-bin histogram of (key - min) >> shift over [min, max] finds the
-// bin holding the (K+1)-th smallest and only the keys up to that bin are bitonic-sorted (typically
-// ~K + a bin instead of all T).  T <= MG_CAP.  Starts and ends with a block barrier.
+// 256-bin histogram cut (block-wide, wave 0 scans): with s.hist filled, the first bin whose
+// inclusive count reaches `need` (255 if none) -> s.sel_bin, and the count of the bins before it
+// -> s.sel_n.  Ends with a barrier.
+__device__ void hist_cut(TopkShared& s, int need) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (tid < 64) {                          // inclusive scan of 256 bins, 4 per lane
+    int h[4], sum = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      h[u] = s.hist[lane * 4 + u];
+      sum += h[u];
+    }
+    int incl = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    int run = incl - sum, cut = 1 << 30, before = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (run + h[u] >= need && cut == (1 << 30)) {
+        cut = lane * 4 + u;
+        before = run;
+      }
+      run += h[u];
+    }
+    const uint64_t bal = __ballot(cut != (1 << 30));   // first lane holding a cut bin
+    const int first = __ffsll((unsigned long long)bal) - 1;
+    const int cb = __shfl(cut, first < 0 ? 0 : first, 64);
+    const int bf = __shfl(before, first < 0 ? 0 : first, 64);
+    if (lane == 0) {
+      s.sel_bin = first < 0 ? 255 : cb;
+      s.sel_n = first < 0 ? incl : bf;   // (no cut: every key counted, the bin is the last)
+    }
+  }
+  __syncthreads();
+}
+
+// Block-wide: the K + 1 smallest of s.keys[0..T) (or all T if fewer), ascending, at the front of
+// the returned array.  Only the K + 1 smallest matter (K records + the limit).  For T > 2(K+1):
+// a 256-bin histogram of (key - min) >> shift over [min, max] finds the bin holding the (K+1)-th
+// smallest, a second 256-bin histogram inside that bin narrows it, and the C keys up to the
+// narrowed cut (C ~ K + 1 + a sub-bin) are placed by rank -- each thread counts the selected keys
+// below its own (keys are unique: the node id is in the low bits) -- instead of a bitonic sort
+// with ~50 block barriers.  Small T, or a cut that still holds > MG_SEL keys, falls back to the
+// bitonic sort of all T.  T <= MG_CAP.  Starts and ends with a block barrier.
 __device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   __syncthreads();
-  uint64_t* sk = s.keys;
-  int C = T;
   if (T > 2 * (K + 1) && K + 1 <= MG_SEL) {
     uint64_t mn = NO_KEY, mx = 0;
     for (int i = tid; i < T; i += MG_THREADS) {
@@ -1050,7 +1090,6 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
       s.red[MG_THREADS / 64 + wave] = mx;
     }
     for (int i = tid; i < 256; i += MG_THREADS) s.hist[i] = 0;
-    if (tid == 0) s.sel_n = 0;
     __syncthreads();
     uint64_t kmin = NO_KEY, kmax = 0;
 #pragma unroll
@@ -1062,48 +1101,56 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
     const int sh = bits > 8 ? bits - 8 : 0;
     for (int i = tid; i < T; i += MG_THREADS) atomicAdd(&s.hist[(int)((s.keys[i] - kmin) >> sh)], 1);
     __syncthreads();
-    if (wave == 0) {                       // inclusive scan of 256 bins, 4 per lane
-      int h[4], sum = 0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        h[u] = s.hist[lane * 4 + u];
-        sum += h[u];
-      }
-      int incl = sum;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += o;
-      }
-      int run = incl - sum, cut = 1 << 30;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        run += h[u];
-        if (run >= K + 1 && cut == (1 << 30)) cut = lane * 4 + u;
-      }
-      const uint64_t bal = __ballot(cut != (1 << 30));   // first lane holding a cut bin
-      const int first = __ffsll((unsigned long long)bal) - 1;
-      const int cb = __shfl(cut, first < 0 ? 0 : first, 64);
-      if (lane == 0) s.sel_bin = first < 0 ? 255 : cb;
-    }
-    __syncthreads();
+    hist_cut(s, K + 1);
     const int cb = s.sel_bin;
+    const int before = s.sel_n;
+    // level 2 inside bin cb: keys in [base, base + 2^sh), 256 sub-bins of 2^sh2
+    const uint64_t base = kmin + ((uint64_t)cb << sh);
+    const int sh2 = sh > 8 ? sh - 8 : 0;
+    int cb2 = 255;
+    if (sh > 0) {
+      __syncthreads();                     // every thread has read sel_bin / sel_n
+      for (int i = tid; i < 256; i += MG_THREADS) s.hist[i] = 0;
+      __syncthreads();
+      for (int i = tid; i < T; i += MG_THREADS) {
+        const uint64_t k = s.keys[i];
+        if ((int)((k - kmin) >> sh) == cb) atomicAdd(&s.hist[(int)((k - base) >> sh2)], 1);
+      }
+      __syncthreads();
+      hist_cut(s, K + 1 - before);
+      cb2 = s.sel_bin;
+    }
+    // selected: below bin cb, or in bin cb up to sub-bin cb2
+    __syncthreads();
+    if (tid == 0) s.sel_n = 0;
+    __syncthreads();
     for (int i = tid; i < T; i += MG_THREADS) {
       const uint64_t k = s.keys[i];
-      if ((int)((k - kmin) >> sh) <= cb) {
+      const int b1 = (int)((k - kmin) >> sh);
+      if (b1 < cb || (b1 == cb && (int)((k - base) >> sh2) <= cb2)) {
         const int pos = atomicAdd(&s.sel_n, 1);
         if (pos < MG_SEL) s.sel[pos] = k;
       }
     }
     __syncthreads();
-    if (s.sel_n <= MG_SEL) {               // else (one bin held too many): sort all T
-      sk = s.sel;
-      C = s.sel_n;
+    const int C = s.sel_n;
+    if (C <= MG_SEL) {
+      // rank placement into s.keys (its old contents are no longer needed)
+      for (int t = tid; t < C; t += MG_THREADS) {
+        const uint64_t k = s.sel[t];
+        int rank = 0;
+        for (int j = 0; j < C; ++j) rank += s.sel[j] < k;
+        if (rank <= K) s.keys[rank] = k;
+      }
+      __syncthreads();
+      return s.keys;
     }
   }
+  // bitonic sort of all T keys
+  uint64_t* sk = s.keys;
   int P = 2;
-  while (P < C) P <<= 1;
-  for (int i = C + tid; i < P; i += MG_THREADS) sk[i] = NO_KEY;
+  while (P < T) P <<= 1;
+  for (int i = T + tid; i < P; i += MG_THREADS) sk[i] = NO_KEY;
   __syncthreads();
   for (int k = 2; k <= P; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
@@ -1307,6 +1354,13 @@ hipError_t launch_walk_build(hipStream_t s, const int64_t* res, int64_t stride, 
   return hipGetLastError();
 }
 
+#ifdef PE_WALK_PROF   // phase timings of walk_kernel (wall clock ticks, summed over blocks), diagnostics build only
+__device__ unsigned long long walk_prof[16];
+#define WPT(i) unsigned long long wpt##i = wall_clock64()
+#else
+#define WPT(i)
+#endif
+
 // One block of WK_ROUND threads per group of the window:
 //  1. per round (all rounds at once): can it hold a fit (q <= max residual per dimension, need in
 //     the OR of labels)?  -> LDS bitmap; and how many rounds start below s(q) << 24 -> the first
@@ -1327,6 +1381,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   __shared__ int start_cnt, below;
   const int g = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
+  WPT(0);
   const ReqRec rq = groups[g];
   const int64_t q0 = rq.q[0], q1 = rq.q[1], q2 = rq.q[2], q3 = rq.q[3];
   const uint32_t need = rq.need;
@@ -1356,6 +1411,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
     for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
     if (lane == 0 && cnt) atomicAdd(&start_cnt, cnt);
   }
+  WPT(1);
   // overlay: every node changed since the sort (and the saturating ones), current values
   const int no = *w.ovl_n;
   for (int i0 = 0; i0 < no; i0 += WK_ROUND) {
@@ -1380,7 +1436,11 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
     }
   }
   __syncthreads();
+  WPT(2);
   bool done = !walk;
+#ifdef PE_WALK_PROF
+  int rounds = 0;
+#endif
   int64_t r = walk ? (start_cnt > 0 ? start_cnt - 1 : 0) : nr;
   auto next_round = [&](int64_t from) -> int64_t {   // first candidate round >= from (uniform)
     int64_t wi = from >> 5;
@@ -1428,10 +1488,30 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
       __syncthreads();
     }
     r = next_round(r + 1);
+#ifdef PE_WALK_PROF
+    ++rounds;
+#endif
   }
+  WPT(3);
   const int T = s.total;
   const uint64_t* sk = topk_sort(s, T, K);
+  WPT(4);
   write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : NO_KEY, K, g, out);
+#ifdef PE_WALK_PROF
+  __syncthreads();
+  WPT(5);
+  if (tid == 0) {
+    atomicAdd(&walk_prof[0], wpt1 - wpt0);
+    atomicAdd(&walk_prof[1], wpt2 - wpt1);
+    atomicAdd(&walk_prof[2], wpt3 - wpt2);
+    atomicAdd(&walk_prof[3], wpt4 - wpt3);
+    atomicAdd(&walk_prof[4], wpt5 - wpt4);
+    atomicAdd(&walk_prof[5], 1ull);
+    atomicAdd(&walk_prof[6], (unsigned long long)no);
+    atomicAdd(&walk_prof[7], (unsigned long long)rounds);
+    atomicAdd(&walk_prof[8], (unsigned long long)T);
+  }
+#endif
 }
 
 hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const WalkIndex& w, const int64_t* res,
@@ -1440,6 +1520,18 @@ hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const
   if (w.nr > WK_MAXR || K + 1 > WK_ROUND) return hipErrorInvalidValue;
   hipLaunchKernelGGL(walk_kernel, dim3((unsigned)Wg), dim3(WK_ROUND), 0, s, groups, K, w, res, stride, labels, Ns,
                      id_base, out);
+#ifdef PE_WALK_PROF
+  static int launches = 0;
+  if (++launches % 500 == 0) {
+    unsigned long long p[16];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(p, HIP_SYMBOL(walk_prof), sizeof(p));
+    const double n = (double)p[5], us = 100.0;   // wall_clock64 runs at 100 MHz: ticks / 100 = us
+    fprintf(stderr, "walk prof over %.0f blocks (us/block): setup+prepass %.2f overlay %.2f walk %.2f sort %.2f write %.2f"
+                    " | overlay %.0f rounds %.2f T %.0f\n", n, p[0] / n / us, p[1] / n / us, p[2] / n / us,
+            p[3] / n / us, p[4] / n / us, p[6] / n, p[7] / n, p[8] / n);
+  }
+#endif
   return hipGetLastError();
 }
 
