@@ -161,7 +161,8 @@ struct pe_ctx {
   int64_t w_est = 0;             // updates applied since the last sort (>= overlay size)
   DevBuf<uint64_t> w_sk, w_kin, w_rmin;
   DevBuf<int64_t> w_sr, w_rmax;
-  DevBuf<uint32_t> w_sl, w_pos, w_ror, w_inovl;
+  DevBuf<uint32_t> w_sl, w_pos, w_ror, w_inovl, w_ovidx, w_ovlab;
+  DevBuf<int64_t> w_ovres;
   DevBuf<int32_t> w_ovl, w_ovln;
   DevBuf<uint8_t> w_temp;
   pe_stats stats{};
@@ -179,6 +180,7 @@ struct pe_ctx {
     g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_out.release(); h_out2.release(); h_own.release(); h_upd.release();
     w_sk.release(); w_kin.release(); w_rmin.release(); w_sr.release(); w_rmax.release(); w_sl.release(); w_pos.release();
     w_ror.release(); w_inovl.release(); w_ovl.release(); w_ovln.release(); w_temp.release();
+    w_ovidx.release(); w_ovlab.release(); w_ovres.release();
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -903,6 +905,9 @@ static pe::WalkIndex walk_index(pe_ctx* ctx) {
   w.ovl = ctx->w_ovl.p;
   w.ovl_n = ctx->w_ovln.p;
   w.in_ovl = ctx->w_inovl.p;
+  w.ovl_idx = ctx->w_ovidx.p;
+  w.ovl_res = ctx->w_ovres.p;
+  w.ovl_lab = ctx->w_ovlab.p;
   w.sstride = ctx->stride;
   w.nr = (ctx->Ns + pe::WK_ROUND - 1) / pe::WK_ROUND;
   return w;
@@ -924,6 +929,9 @@ static void walk_resort(pe_ctx* ctx) {
   hipchk(ctx->w_ovl.ensure(st), "alloc overlay");
   hipchk(ctx->w_ovln.ensure(1), "alloc overlay");
   hipchk(ctx->w_inovl.ensure(st), "alloc overlay");
+  hipchk(ctx->w_ovidx.ensure(st), "alloc overlay");
+  hipchk(ctx->w_ovlab.ensure(st), "alloc overlay");
+  hipchk(ctx->w_ovres.ensure((size_t)pe::D * st), "alloc overlay");
   size_t tb = 0;
   hipchk(pe::sort_keys_u64(nullptr, &tb, ctx->w_kin.p, ctx->w_sk.p, Ns, s), "sort size");
   hipchk(ctx->w_temp.ensure(tb), "alloc sort scratch");
@@ -931,7 +939,8 @@ static void walk_resort(pe_ctx* ctx) {
   hipchk(hipMemsetAsync(ctx->w_ovln.p, 0, sizeof(int32_t), s), "memset overlay");
   hipchk(hipMemsetAsync(ctx->w_inovl.p, 0, (size_t)st * 4, s), "memset overlay");
   hipchk(hipMemsetAsync(ctx->w_pos.p, 0xFF, (size_t)st * 4, s), "memset pos");
-  hipchk(pe::launch_walk_prep(s, ctx->res.p, ctx->stride, Ns, ctx->g_kn.p, ctx->w_kin.p, w), "launch walk_prep");
+  hipchk(pe::launch_walk_prep(s, ctx->res.p, ctx->stride, Ns, ctx->g_kn.p, ctx->labels.p, ctx->w_kin.p, w),
+         "launch walk_prep");
   hipchk(pe::sort_keys_u64(ctx->w_temp.p, &tb, ctx->w_kin.p, ctx->w_sk.p, Ns, s), "sort walk keys");
   hipchk(pe::launch_walk_build(s, ctx->res.p, ctx->stride, ctx->labels.p, Ns, (uint64_t)ctx->begin, w),
          "launch walk_build");
@@ -1108,7 +1117,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (nu > 0) {   // the kernel reads the pinned records directly (no H2D copy)
         const pe::WalkIndex w = walk_index(ctx);
         hipchk(pe::launch_apply(s, ctx->res.p, ctx->stride, ctx->h_upd.dev, nu, (uint64_t)ctx->begin, ctx->g_kn.p,
-                                ctx->g_lo.p, walk ? &w : nullptr),
+                                ctx->g_lo.p, ctx->labels.p, walk ? &w : nullptr),
                "launch apply");
         ctx->w_est += nu;
       }

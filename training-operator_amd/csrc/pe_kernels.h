@@ -170,12 +170,15 @@ struct WalkIndex {
   int32_t* ovl;        // [stride] overlay local node ids
   int32_t* ovl_n;      // overlay size
   uint32_t* in_ovl;    // [stride] 1 = in the overlay
+  uint32_t* ovl_idx;   // [stride] a node's overlay slot (valid while in_ovl)
+  int64_t* ovl_res;    // [4][sstride] residuals by overlay slot (kept current by apply)
+  uint32_t* ovl_lab;   // [stride] labels by overlay slot
   int64_t sstride, nr;
 };
 // kin[n] = K(n) of a walkable node (no negative residual, not saturating), else WK_INVALID; the
 // saturating ones are appended to the overlay (cleared by the caller beforehand).
 hipError_t launch_walk_prep(hipStream_t s, const int64_t* res, int64_t stride, int64_t Ns, const uint64_t* kn,
-                            uint64_t* kin, const WalkIndex& w);
+                            const uint32_t* labels, uint64_t* kin, const WalkIndex& w);
 // hipcub radix sort of n u64 keys (temp == nullptr: *temp_bytes = the scratch size needed).
 hipError_t sort_keys_u64(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n, hipStream_t s);
 // Sorted SoA copy, pos[], round summaries from the sorted keys w.sk.
@@ -189,7 +192,7 @@ hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const
 // (kn, lo nullable: refreshed for the updated nodes when given; w nullable: the updated nodes
 // leave the sorted walk and join its overlay)
 hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n, uint64_t id_base,
-                        uint64_t* kn, uint32_t* lo, const WalkIndex* w);
+                        uint64_t* kn, uint32_t* lo, const uint32_t* labels, const WalkIndex* w);
 
 // Inventory delta for one slot of this shard (pe_update_nodes): residual written to both the
 // live and the reset copy, labels and island replaced.  Slots are unique within a launch.

@@ -1271,30 +1271,41 @@ hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt,
 
 // ------------------------------------------------------------------ sorted walk (greedy default)
 
+// Appends local node n with state (r, lab) to the overlay (slot, state copy, membership).
+__device__ __forceinline__ void overlay_add(const WalkIndex& w, int64_t n, const int64_t (&r)[D], uint32_t lab) {
+  const int32_t i = atomicAdd(w.ovl_n, 1);
+  w.ovl[i] = (int32_t)n;
+  w.ovl_idx[n] = (uint32_t)i;
+#pragma unroll
+  for (int d = 0; d < D; ++d) w.ovl_res[d * w.sstride + i] = r[d];
+  w.ovl_lab[i] = lab;
+}
+
 __global__ __launch_bounds__(256) void walk_prep_kernel(const int64_t* __restrict__ res, int64_t stride, int64_t Ns,
-                                                        const uint64_t* __restrict__ kn, uint64_t* __restrict__ kin,
-                                                        int32_t* __restrict__ ovl, int32_t* __restrict__ ovl_n,
-                                                        uint32_t* __restrict__ in_ovl) {
+                                                        const uint64_t* __restrict__ kn,
+                                                        const uint32_t* __restrict__ labels, uint64_t* __restrict__ kin,
+                                                        WalkIndex w) {
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= Ns) return;
-  const bool neg = (res[n] | res[stride + n] | res[2 * stride + n] | res[3 * stride + n]) < 0;
+  const int64_t r[D] = {res[n], res[stride + n], res[2 * stride + n], res[3 * stride + n]};
+  const bool neg = (r[0] | r[1] | r[2] | r[3]) < 0;
   const uint64_t K = kn[n];
   uint64_t k = K;
   if (neg) {
     k = WK_INVALID;                  // fits nothing
   } else if (K == KEY_SLOW) {
     k = WK_INVALID;                  // saturating terms: evaluated in full through the overlay
-    in_ovl[n] = 1u;
-    ovl[atomicAdd(ovl_n, 1)] = (int32_t)n;
+    w.in_ovl[n] = 1u;
+    overlay_add(w, n, r, labels[n]);
   }
   kin[n] = k;
 }
 
 hipError_t launch_walk_prep(hipStream_t s, const int64_t* res, int64_t stride, int64_t Ns, const uint64_t* kn,
-                            uint64_t* kin, const WalkIndex& w) {
+                            const uint32_t* labels, uint64_t* kin, const WalkIndex& w) {
   if (Ns <= 0) return hipSuccess;
-  hipLaunchKernelGGL(walk_prep_kernel, dim3((unsigned)((Ns + 255) / 256)), dim3(256), 0, s, res, stride, Ns, kn, kin,
-                     w.ovl, w.ovl_n, w.in_ovl);
+  hipLaunchKernelGGL(walk_prep_kernel, dim3((unsigned)((Ns + 255) / 256)), dim3(256), 0, s, res, stride, Ns, kn, labels,
+                     kin, w);
   return hipGetLastError();
 }
 
@@ -1417,11 +1428,9 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   for (int i0 = 0; i0 < no; i0 += WK_ROUND) {
     const int i = i0 + tid;
     uint64_t k = NO_KEY;
-    if (i < no) {
-      const int64_t n = w.ovl[i];
-      k = node_key(res[n], res[stride + n], res[2 * stride + n], res[3 * stride + n], labels[n], q0, q1, q2, q3, need,
-                   id_base + (uint64_t)n);
-    }
+    if (i < no)   // the overlay keeps its own state copy: independent, coalesced loads
+      k = node_key(w.ovl_res[i], w.ovl_res[w.sstride + i], w.ovl_res[2 * w.sstride + i], w.ovl_res[3 * w.sstride + i],
+                   w.ovl_lab[i], q0, q1, q2, q3, need, id_base + (uint64_t)w.ovl[i]);
     topk_append(s, k, k != NO_KEY);
     __syncthreads();
     if (s.total > MG_CAP - WK_ROUND) {     // keep the K + 1 smallest (the rest can never matter)
@@ -1540,7 +1549,7 @@ hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const
 __global__ __launch_bounds__(256) void apply_kernel(int64_t* __restrict__ res, int64_t stride,
                                                     const int64_t* __restrict__ upd, int64_t n, uint64_t id_base,
                                                     uint64_t* __restrict__ kn, uint32_t* __restrict__ lo,
-                                                    WalkIndex w, int walk) {
+                                                    const uint32_t* __restrict__ labels, WalkIndex w, int walk) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t* u = upd + i * (D + 1);
@@ -1561,16 +1570,23 @@ __global__ __launch_bounds__(256) void apply_kernel(int64_t* __restrict__ res, i
       w.sk[p] = WK_INVALID;
       w.pos[node] = ~0u;
     }
-    if (atomicExch(&w.in_ovl[node], 1u) == 0u) w.ovl[atomicAdd(w.ovl_n, 1)] = (int32_t)node;
+    const int64_t r[D] = {u[1], u[2], u[3], u[4]};
+    if (atomicExch(&w.in_ovl[node], 1u) == 0u) {
+      overlay_add(w, node, r, labels[node]);
+    } else {                                  // already there: refresh its state copy
+      const uint32_t i = w.ovl_idx[node];
+#pragma unroll
+      for (int d = 0; d < D; ++d) w.ovl_res[d * w.sstride + i] = r[d];
+    }
   }
 }
 
 hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n, uint64_t id_base,
-                        uint64_t* kn, uint32_t* lo, const WalkIndex* w) {
+                        uint64_t* kn, uint32_t* lo, const uint32_t* labels, const WalkIndex* w) {
   if (n <= 0) return hipSuccess;
   const WalkIndex none{};
   hipLaunchKernelGGL(apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, res, stride, upd, n, id_base,
-                     kn, lo, w ? *w : none, w ? 1 : 0);
+                     kn, lo, labels, w ? *w : none, w ? 1 : 0);
   return hipGetLastError();
 }
 
