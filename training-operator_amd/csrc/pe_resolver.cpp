@@ -165,27 +165,16 @@ uint64_t DirtySet::key_at(int32_t i, const int64_t q[RD], uint32_t need) const {
 
 void merge_shards(const std::vector<const GroupCands*>& parts, GroupCands& out) {
   out.own.clear();
-  out.own_keys.clear();
   out.limit = kNoKey;
   for (const GroupCands* p : parts) out.limit = std::min(out.limit, p->limit);
-  const bool keyed = !parts.empty() && parts[0]->keys;
   for (const GroupCands* p : parts)
-    for (size_t i = 0; i < p->n; ++i) {
-      if (p->key(i) >= out.limit) continue;
-      if (keyed) out.own_keys.push_back(p->keys[i]);
-      else out.own.push_back(p->data[i]);
-    }
-  if (keyed) {
-    std::sort(out.own_keys.begin(), out.own_keys.end());
-    out.keys = out.own_keys.data();
-    out.data = nullptr;
-    out.n = out.own_keys.size();
-  } else {
-    std::sort(out.own.begin(), out.own.end(), [](const Cand& a, const Cand& b) { return a.key < b.key; });
-    out.data = out.own.data();
-    out.keys = nullptr;
-    out.n = out.own.size();
-  }
+    for (size_t i = 0; i < p->n; ++i)
+      if (p->data[i].key < out.limit) out.own.push_back(p->data[i]);
+  std::sort(out.own.begin(), out.own.end(), [](const Cand& a, const Cand& b) { return a.key < b.key; });
+  out.data = out.own.data();
+  out.keys = nullptr;
+  out.keyed = false;
+  out.n = out.own.size();
 }
 
 void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands,
@@ -207,6 +196,7 @@ void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::v
       gc.n = (size_t)std::max(n, 0);
       gc.data = reinterpret_cast<const Cand*>(base + 16);   // 16-B aligned records in the blob
       gc.keys = nullptr;
+      gc.keyed = false;
       if (copy_blob && n_shards == 1) {
         gc.own.assign(gc.data, gc.data + gc.n);
         gc.data = gc.own.data();
@@ -221,23 +211,37 @@ void parse_window_keys(const uint8_t* blob, int n_shards, int n_groups, int K, s
   const size_t gb = 16 + (size_t)K * 8;
   const size_t shard_bytes = (size_t)n_groups * gb;
   cands.resize((size_t)n_groups);
-  std::vector<GroupCands> parts((size_t)n_shards);
-  std::vector<const GroupCands*> pp((size_t)n_shards);
   for (int w = 0; w < n_groups; ++w) {
+    GroupCands& gc = cands[w];
+    gc.keyed = true;
+    gc.data = nullptr;
+    gc.merged.clear();
+    gc.part.clear();
+    gc.part_n.clear();
+    gc.limit = kNoKey;
     for (int r = 0; r < n_shards; ++r) {
       const uint8_t* base = blob + (size_t)r * shard_bytes + (size_t)w * gb;
       int32_t n;
       uint64_t limit;
       std::memcpy(&n, base, 4);
       std::memcpy(&limit, base + 8, 8);
-      GroupCands& gc = n_shards == 1 ? cands[w] : parts[r];
-      gc.limit = limit;
-      gc.n = (size_t)std::max(n, 0);
-      gc.keys = reinterpret_cast<const uint64_t*>(base + 16);
-      gc.data = nullptr;
-      pp[r] = &parts[r];
+      gc.limit = std::min(gc.limit, limit);
+      gc.part.push_back(reinterpret_cast<const uint64_t*>(base + 16));
+      gc.part_n.push_back((size_t)std::max(n, 0));
     }
-    if (n_shards > 1) merge_shards(pp, cands[w]);
+    if (n_shards == 1) {
+      gc.keys = gc.part[0];
+      gc.n = gc.part_n[0];
+      continue;
+    }
+    // global list = every shard's keys below the smallest shard limit
+    gc.keys = nullptr;
+    gc.n = 0;
+    for (int r = 0; r < n_shards; ++r) {
+      gc.part_n[r] = (size_t)(std::lower_bound(gc.part[r], gc.part[r] + gc.part_n[r], gc.limit) - gc.part[r]);
+      gc.n += gc.part_n[r];
+    }
+    gc.head.assign((size_t)n_shards, 0);
   }
 }
 
@@ -394,8 +398,8 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     const int64_t* q = req_ + (int64_t)g_ * RD;
     const uint32_t need = need_[g_];
     t_ = RP_T();
-    if (gc.keys)   // the first listed nodes' states (the rest are prefetched as the list is consumed)
-      for (size_t i = 0; i < std::min<size_t>(4, gc.size()); ++i) __builtin_prefetch(&mirror_.nodes[gc.keys[i] & 0xFFFFFFull]);
+    if (gc.keyed)   // the first listed nodes' states (the rest are prefetched as the list is consumed)
+      for (size_t i = 0; i < std::min<size_t>(4, gc.size()); ++i) __builtin_prefetch(&mirror_.nodes[gc.key(i) & 0xFFFFFFull]);
     dirty_.keys(q, need, gc.limit, dk, dki);   // dirty keys >= limit never decide (list head or rescan)
     int32_t best = argmin();
     RP_ADD(keys, t_);
@@ -429,7 +433,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         slot = best;
         st = dirty_.get(slot);
       } else {
-        if (gc.keys) {   // clean: the mirror holds the snapshot state
+        if (gc.keyed) {   // clean: the mirror holds the snapshot state
           st = mirror_.nodes[gid];
           if (ptr + 4 < gc.size()) __builtin_prefetch(&mirror_.nodes[gc.key(ptr + 4) & 0xFFFFFFull]);
         } else {

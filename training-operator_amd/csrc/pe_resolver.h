@@ -44,15 +44,37 @@ struct Mirror {
 };
 
 // One group's candidate list: either records (data) or keys whose states come from a Mirror.
+// Key lists of several shards are merged lazily: the resolver reads a list from its head and
+// usually stops after a few entries, so only the consumed prefix is ever merged.
 struct GroupCands {
   const Cand* data = nullptr;      // ascending keys, all clean at the snapshot
-  const uint64_t* keys = nullptr;  // key-only form (engine windows)
+  const uint64_t* keys = nullptr;  // key-only form (engine windows), one shard
+  bool keyed = false;              // key-only (keys, or the lazy shard merge below)
   size_t n = 0;
   uint64_t limit = ~0ull;          // every clean node with key < limit is listed
-  std::vector<Cand> own;           // storage when the list is a copy (shard merge, or copy_blob)
-  std::vector<uint64_t> own_keys;
+  std::vector<Cand> own;           // storage when the list is a copy (record shard merge, copy_blob)
+  // lazy k-way merge of per-shard key lists (each ascending, cut at limit)
+  std::vector<const uint64_t*> part;
+  std::vector<size_t> part_n;
+  mutable std::vector<size_t> head;
+  mutable std::vector<uint64_t> merged;
   size_t size() const { return n; }
-  uint64_t key(size_t i) const { return keys ? keys[i] : data[i].key; }
+  uint64_t key(size_t i) const {
+    if (keys) return keys[i];
+    if (!keyed) return data[i].key;
+    while (merged.size() <= i) {
+      size_t best = 0;
+      uint64_t bk = ~0ull;
+      for (size_t r = 0; r < part.size(); ++r)
+        if (head[r] < part_n[r] && part[r][head[r]] < bk) {
+          bk = part[r][head[r]];
+          best = r;
+        }
+      ++head[best];
+      merged.push_back(bk);
+    }
+    return merged[i];
+  }
 };
 
 struct Update {
