@@ -157,7 +157,7 @@ struct pe_ctx {
   HostBuf<int64_t> h_upd;
   // greedy sorted walk (pe_kernels.h WalkIndex; the default window path, greedy_flags bit1 = full scan)
   bool walk = true;
-  int64_t resort_nodes = 4096;   // re-sort once this many applied updates joined the overlay
+  int64_t resort_nodes = 16384;  // re-sort once this many applied updates joined the overlay
   int64_t w_est = 0;             // updates applied since the last sort (>= overlay size)
   DevBuf<uint64_t> w_sk, w_kin, w_rmin;
   DevBuf<int64_t> w_sr, w_rmax;
@@ -277,7 +277,7 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   ctx->pipeline = (cfg->greedy_flags & 1) == 0;
   ctx->walk = (cfg->greedy_flags & 2) == 0;
   if (cfg->resort_nodes < 0) raise(PE_EINVAL, "resort_nodes < 0");
-  ctx->resort_nodes = cfg->resort_nodes > 0 ? cfg->resort_nodes : 4096;
+  ctx->resort_nodes = cfg->resort_nodes > 0 ? cfg->resort_nodes : 16384;
   if (!(ctx->fit_path_mask & PATHS_ALL)) ctx->fit_path_mask |= PATHS_ALL;   // no kernel bits = all kernels
   ctx->fit_path_mask |= PATH_I64;                                           // always available
   int rc = PE_OK;
