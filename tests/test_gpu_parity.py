@@ -441,3 +441,32 @@ def test_greedy_walk_overlay_compaction():
     s = e.stats()
     assert s["resorts"] == 1
     e.close()
+
+
+def test_greedy_unfittable_and_empty_lists():
+    """Requests no node can hold (16 GPUs, more memory than any node, an unknown label) next to
+    normal ones: their walks visit every candidate round and return empty lists with limit
+    NO_KEY, the jobs fail all-or-nothing and roll back, exact vs the oracle."""
+    inv = synth.make_inventory(6000, 101, 0.3)
+    batch = synth.make_jobs(400, 103, "mixed")
+    req = batch.group_req.copy()
+    need = batch.group_need.copy()
+    req[::7, 2] = 16                        # more GPUs than any node has
+    req[3::11, 1] = 1 << 45                 # more memory than any node has
+    need[5::13] |= 1 << 20                  # a label no node carries
+    batch.group_req, batch.group_need = req, need
+    e = Engine(0)
+    st = check_greedy(e, inv, batch)
+    assert (st == 1).sum() > 50 and (st == 0).sum() > 50
+    e.close()
+
+
+def test_greedy_topk_beyond_walk_uses_full_scan():
+    """K + 1 > 1024 does not fit the walk's block: the windows take the full scan + merge."""
+    e = Engine(0, topk=2000, window_groups=16)
+    inv = synth.make_inventory(4000, 107, 0.3)
+    batch = synth.make_jobs(200, 109, "mixed")
+    check_greedy(e, inv, batch)
+    s = e.stats()
+    assert s["scan_evals"] > 0 and s["resorts"] == 0
+    e.close()

@@ -275,7 +275,8 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   ctx->fit_path_mask = cfg->fit_path_mask & (PATHS_ALL | PATH_NO_THERM | PATH_PLANES_BLOCKS);
   ctx->pl_rows = !(ctx->fit_path_mask & PATH_PLANES_BLOCKS);
   ctx->pipeline = (cfg->greedy_flags & 1) == 0;
-  ctx->walk = (cfg->greedy_flags & 2) == 0;
+  // the walk's block holds K + 1 <= WK_ROUND selected keys; larger K takes the full scan + merge
+  ctx->walk = (cfg->greedy_flags & 2) == 0 && ctx->topk + 1 <= pe::WK_ROUND;
   if (cfg->resort_nodes < 0) raise(PE_EINVAL, "resort_nodes < 0");
   ctx->resort_nodes = cfg->resort_nodes > 0 ? cfg->resort_nodes : 16384;
   if (!(ctx->fit_path_mask & PATHS_ALL)) ctx->fit_path_mask |= PATHS_ALL;   // no kernel bits = all kernels
