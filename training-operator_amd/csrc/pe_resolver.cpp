@@ -128,7 +128,7 @@ static inline uint64_t key_bf(int64_t x0, int64_t x1, int64_t x2, int64_t x3, ui
 }
 
 void DirtySet::keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
-                    std::vector<int32_t>& idx) const {
+                    std::vector<int32_t>& idx) const {   // limit: keys >= it may be left out
   const size_t n = gid.size();
   if (out.size() < n) out.resize(n);   // only the slots listed in idx are read
   idx.clear();
@@ -452,7 +452,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       for (int d = 0; d < RD; ++d) st.res[d] -= m * q[d];
       if (slot < 0) {
         slot = dirty_.upsert(gid, st);
-        dk.push_back(kNoKey);
+        if (dk.size() <= (size_t)slot) dk.resize((size_t)slot + 1);
         dki.push_back(slot);
       } else {
         dirty_.set(slot, st);
