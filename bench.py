@@ -73,6 +73,23 @@ def fit_bytes(n_nodes: int, n_jobs: int) -> int:
     return n_nodes * 36 + n_jobs * 36 + n_jobs * ((n_nodes + 63) // 64) * 8 + n_jobs * 8
 
 
+def profiled_counter(kernel: str, n_nodes: int, n_jobs: int, counter: str):
+    """One PMC counter per launch of `kernel` from the committed profile (profiles/LATEST), if it was
+    taken on this same workload; else None."""
+    try:
+        tag = open(os.path.join(PROFILES, "LATEST")).read().strip()
+        summ = json.load(open(os.path.join(PROFILES, tag, "summary.json")))
+    except (OSError, ValueError):
+        return None
+    wl = summ.get("workload", {})
+    if wl.get("nodes") != n_nodes or wl.get("jobs") != n_jobs:
+        return None
+    for k, p in summ.get("pmc", {}).items():
+        if k.startswith(kernel) and counter in p:
+            return p[counter]
+    return None
+
+
 def profiled_traffic(kernel: str, n_nodes: int, n_jobs: int):
     """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/LATEST names the
     directory; FETCH_SIZE doubled per MI355X_MICROARCH.md, + WRITE_SIZE), if they were taken on this
@@ -234,6 +251,10 @@ def main():
     valu_frac = None
     if fit_path == "coded-therm":   # 3 VALU per (job, 64 nodes): or, add_co, addc
         valu_frac = 3.0 * (-(-J // 64) * 64) * (Ns / 64.0) / (kern_ms * 1e-3) / VALU_ISSUE_CEILING
+    else:                           # PMC SQ_INSTS_VALU per launch (committed profile, same workload)
+        insts = profiled_counter(kname, Ns, J, "SQ_INSTS_VALU")
+        if insts is not None:
+            valu_frac = insts / (kern_ms * 1e-3) / VALU_ISSUE_CEILING
 
     out = {
         "metric": METRIC, "value": value, "unit": "job*node fit evals/s", "n_gpus": world, "steps": args.steps,
