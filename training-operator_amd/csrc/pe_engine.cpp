@@ -7,11 +7,18 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <exception>
+#include <functional>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -70,6 +77,54 @@ struct HostBuf {
   }
 };
 constexpr unsigned kZeroCopy = hipHostMallocCoherent | hipHostMallocMapped;
+
+// One helper thread that runs a posted task while the caller does other work (pipelined greedy:
+// the next window's launches are issued while the host resolves the current one).  Spin handoff:
+// the wake-up of a sleeping thread would cost about as much as the launches it hides.
+class SpinWorker {
+ public:
+  explicit SpinWorker(int device) : th_([this, device] {
+    (void)hipSetDevice(device);   // the current device is per thread
+    loop();
+  }) {}
+  ~SpinWorker() {
+    while (state_.load(std::memory_order_acquire) == 1) _mm_pause();   // a posted task finishes first
+    state_.store(3, std::memory_order_release);
+    th_.join();
+  }
+  void post(std::function<void()> f) {
+    task_ = std::move(f);
+    err_ = nullptr;
+    state_.store(1, std::memory_order_release);
+  }
+  void wait() {   // rethrows what the task threw
+    while (state_.load(std::memory_order_acquire) != 2) _mm_pause();
+    state_.store(0, std::memory_order_relaxed);
+    if (err_) std::rethrow_exception(err_);
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      const int st = state_.load(std::memory_order_acquire);
+      if (st == 3) return;
+      if (st != 1) {
+        _mm_pause();
+        continue;
+      }
+      try {
+        task_();
+      } catch (...) {
+        err_ = std::current_exception();
+      }
+      state_.store(2, std::memory_order_release);
+    }
+  }
+  std::atomic<int> state_{0};
+  std::function<void()> task_;
+  std::exception_ptr err_;
+  std::thread th_;   // last: starts after the members above exist
+};
 
 struct PeError {
   int code;
@@ -1031,6 +1086,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     const bool pipelined = ctx->pipeline && !use_exchange;
     // ---- one window on the device: group requests H2D, scan, merge, (RCCL all-gather), blob D2H
     int cb = 0;   // the blob buffer of the window being resolved
+    std::unique_ptr<SpinWorker> worker;
+    if (pipelined) worker.reset(new SpinWorker(ctx->device));
     // blob buffer b (0: h_out, 1: h_out2): the pipelined loop D2Hs the next window's blob while the
     // host still resolves from the current one's
     auto outbuf = [&](int b) { return b ? ctx->h_out2.p : ctx->h_out.p; };
@@ -1169,11 +1226,19 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       // seeds (current state known here).  A window cut short, or a cursor that did not land where
       // the speculation started, discards the speculative scan and rescans from the cursor.
       R.next_window_from(cur_end, Wmax, ctx->window_pods, nxt, &nxt_end);
-      enqueue_apply(pending);                    // device: everything up to the previous window
-      pending.clear();
-      if (!nxt.empty()) enqueue_window(nxt, 1 - cb);   // the other buffer: cur's lists stay valid
+      // the helper thread issues the device work (everything up to the previous window applied,
+      // then nxt scanned into the other blob buffer: cur's lists stay valid) while this thread
+      // resolves cur
+      std::vector<pe::Update> pend;
+      pend.swap(pending);
+      const int nb = 1 - cb;
+      worker->post([&, nb] {
+        enqueue_apply(pend);
+        if (!nxt.empty()) enqueue_window(nxt, nb);
+      });
       std::vector<pe::Update> upd;
       const bool consumed = timed_resolve(cur, upd, &seed);
+      worker->wait();
       if (R.done()) {
         hipchk(hipStreamSynchronize(s), "sync speculative");
         enqueue_apply(upd);
