@@ -232,6 +232,7 @@ void parse_window_keys(const uint8_t* blob, int n_shards, int n_groups, int K, s
     if (n_shards == 1) {
       gc.keys = gc.part[0];
       gc.n = gc.part_n[0];
+      for (int l = 0; l < 4; ++l) __builtin_prefetch(gc.keys + 8 * l);   // list heads, fresh from the device
       continue;
     }
     // global list = every shard's keys below the smallest shard limit
@@ -378,6 +379,12 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       dirty_.upsert(u.gid, st);   // dirty but untouched: not flushed again unless changed here
     }
   RP_ADD(seed, t_);
+  for (int32_t g : groups) {   // the window's group records (scattered over the batch arrays)
+    __builtin_prefetch(req_ + (int64_t)g * RD);
+    __builtin_prefetch(&cnt_[g]);
+    __builtin_prefetch(&need_[g]);
+    __builtin_prefetch(&pod_off_[g]);
+  }
   size_t wi = 0;
   std::vector<uint64_t>& dk = dk_;  // keys of the dirty nodes for the current group
   std::vector<int32_t>& dki = dki_;  // the slots among them that can hold a key
