@@ -273,7 +273,7 @@ def test_greedy_vs_oracle(eng, mix, N, J, gpu_frac):
     assert (st == 0).any()
 
 
-@pytest.mark.parametrize("topk,wg,wp", [(1, 1, 1), (2, 8, 32), (8, 64, 1024), (256, 16, 4096)])
+@pytest.mark.parametrize("topk,wg,wp", [(1, 1, 1), (2, 8, 32), (8, 64, 1024), (256, 16, 4096), (1023, 64, 1024)])
 def test_greedy_window_configs(topk, wg, wp):
     e = Engine(0, topk=topk, window_groups=wg, window_pods=wp)
     inv = synth.make_inventory(1500, 41, 0.3)
