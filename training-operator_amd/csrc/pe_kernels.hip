@@ -1519,6 +1519,13 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
     atomicAdd(&walk_prof[6], (unsigned long long)no);
     atomicAdd(&walk_prof[7], (unsigned long long)rounds);
     atomicAdd(&walk_prof[8], (unsigned long long)T);
+    atomicMax(&walk_prof[9], wpt5 - wpt0);
+    atomicMax(&walk_prof[10], wpt2 - wpt1);
+    atomicMax(&walk_prof[11], wpt3 - wpt2);
+    atomicMax(&walk_prof[12], wpt4 - wpt3);
+    atomicMax(&walk_prof[13], (unsigned long long)rounds);
+    atomicMax(&walk_prof[14], (unsigned long long)T);
+    atomicMax(&walk_prof[15], wpt1 - wpt0);
   }
 #endif
 }
@@ -1539,6 +1546,8 @@ hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const
     fprintf(stderr, "walk prof over %.0f blocks (us/block): setup+prepass %.2f overlay %.2f walk %.2f sort %.2f write %.2f"
                     " | overlay %.0f rounds %.2f T %.0f\n", n, p[0] / n / us, p[1] / n / us, p[2] / n / us,
             p[3] / n / us, p[4] / n / us, p[6] / n, p[7] / n, p[8] / n);
+    fprintf(stderr, "walk prof max: block %.2f us setup %.2f overlay %.2f walk %.2f sort %.2f | rounds %llu T %llu\n",
+            p[9] / us, p[15] / us, p[10] / us, p[11] / us, p[12] / us, p[13], p[14]);
   }
 #endif
   return hipGetLastError();
