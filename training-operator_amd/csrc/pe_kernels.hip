@@ -664,16 +664,17 @@ __device__ __forceinline__ uint32_t reduce64x64(const uint32_t (&p)[64], int lan
 // precomputing 64 row offsets and spilling them); the store is row + lane.
 template <int K>
 __device__ __forceinline__ void rows_batch(uint32_t (&p)[64], uint32_t lo, uint32_t hi, const u32x32& A,
-                                           const u32x32& B, const u32x32& C, const u32x32& Dq, gu32x4* row,
-                                           int64_t step, uint32_t lane_off) {
+                                           const u32x32& B, const u32x32& C, const u32x32& Dq,
+                                           __amdgpu_buffer_rsrc_t rs, uint32_t soff, uint32_t step,
+                                           uint32_t lane_off) {
   u32x4 f;
   plane_job<K>(f, lo, hi, A, B, C, Dq);
-  *(gu32x4*)((__attribute__((address_space(1))) char*)row + lane_off) = f;
+  __builtin_amdgcn_raw_buffer_store_b128(f, rs, lane_off, soff, 0);
   p[K] = __popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w);
   if constexpr (K + 1 < 64) {
-    row += step;
-    asm volatile("" : "+s"(row));
-    rows_batch<K + 1>(p, lo, hi, A, B, C, Dq, row, step, lane_off);
+    soff += step;
+    asm volatile("" : "+s"(soff));
+    rows_batch<K + 1>(p, lo, hi, A, B, C, Dq, rs, soff, step, lane_off);
   }
 }
 
@@ -718,8 +719,11 @@ __global__ __launch_bounds__(256) void fit_mask_planes_rows_kernel(const uint32_
     const uint32_t lo = (uint32_t)cv, hi = (uint32_t)(cv >> 32);
     if (i0 + 128 <= ni) cv = jc[i0 + 64 + lane];   // next batch, in flight during this one
     uint32_t p[64];
-    rows_batch<0>(p, lo, hi, A, B, C, Dq, (gu32x4*)(rows0 + (r + i0 * R) * row_vec), R * row_vec,
-                       (uint32_t)lane * 16u);
+    // buffer stores: batch base in the resource, per-job advance in soffset (SALU), lane offset
+    // in voffset -- no per-job VALU address arithmetic
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(rows0 + (r + i0 * R) * row_vec), 0, -1, 0x00020000);
+    rows_batch<0>(p, lo, hi, A, B, C, Dq, rs, 0u, (uint32_t)(R * row_vec * 16), (uint32_t)lane * 16u);
     const uint32_t F = reduce64x64(p, lane);
     if (F) atomicAdd(&cnt[i0 + sigma], (unsigned long long)F);
   }
