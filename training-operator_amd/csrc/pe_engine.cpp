@@ -1053,6 +1053,27 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
     }
     struct DumpClose { FILE*& f; ~DumpClose() { if (f) std::fclose(f); } } dump_close{dump};
+    // PE_GREEDY_TRACE=1: per-window wait / resolve / post times, summarised on stderr (diagnostics)
+    const bool trace = std::getenv("PE_GREEDY_TRACE") != nullptr;
+    std::vector<double> tr_wait, tr_res, tr_post;
+    struct TraceOut {
+      const bool& on;
+      std::vector<double>& a; std::vector<double>& b; std::vector<double>& c;
+      ~TraceOut() {
+        if (!on || a.empty()) return;
+        auto pr = [](const char* n, std::vector<double>& v) {
+          if (v.empty()) return;
+          std::sort(v.begin(), v.end());
+          double sum = 0;
+          for (double x : v) sum += x;
+          std::fprintf(stderr, "%s n %zu sum %.2f ms mean %.1f us p10 %.1f p50 %.1f p90 %.1f max %.1f\n", n, v.size(),
+                       sum / 1e3, sum / v.size(), v[v.size() / 10], v[v.size() / 2], v[v.size() * 9 / 10], v.back());
+        };
+        pr("wait   ", a);
+        pr("resolve", b);
+        pr("post   ", c);
+      }
+    } trace_out{trace, tr_wait, tr_res, tr_post};
     int64_t dump_left = std::getenv("PE_DUMP_MAX_WINDOWS") ? std::atoll(std::getenv("PE_DUMP_MAX_WINDOWS")) : INT64_MAX;
     const int K = ctx->topk;
     const size_t gb = pe::cand_group_bytes(K);
@@ -1155,6 +1176,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       const auto th = std::chrono::steady_clock::now();
       ctx->stats.greedy_wait_ms += std::chrono::duration<double, std::milli>(th - tw).count();
+      if (trace) tr_wait.push_back(std::chrono::duration<double, std::micro>(th - tw).count());
       pe::parse_window_keys(outbuf(b), ctx->world, Wg, K, cands);   // lists point into the blob
 
       ctx->stats.greedy_host_ms +=
@@ -1197,6 +1219,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       const auto th = std::chrono::steady_clock::now();
       updates.clear();
       const bool consumed = R.resolve(groups, cands, updates, seed);
+      if (trace) tr_res.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - th).count());
       for (const pe::Update& u : updates)          // the mirror follows every placement (all shards)
         for (int d = 0; d < pe::D; ++d) ctx->m_nodes[u.gid].res[d] = u.res[d];
       ctx->stats.greedy_host_ms +=
@@ -1233,8 +1256,10 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       pend.swap(pending);
       const int nb = 1 - cb;
       worker->post([&, nb] {
+        const auto tp = std::chrono::steady_clock::now();
         enqueue_apply(pend);
         if (!nxt.empty()) enqueue_window(nxt, nb);
+        if (trace) tr_post.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
       });
       std::vector<pe::Update> upd;
       const bool consumed = timed_resolve(cur, upd, &seed);
