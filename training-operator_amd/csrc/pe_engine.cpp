@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <immintrin.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1056,7 +1057,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // PE_GREEDY_TRACE=1: per-window wait / resolve / post times, summarised on stderr (diagnostics)
     const bool trace = std::getenv("PE_GREEDY_TRACE") != nullptr;
     std::vector<double> tr_wait, tr_res, tr_post;
+    int helper_cpu = -1;
     struct TraceOut {
+      int& helper_cpu;
       const bool& on;
       std::vector<double>& a; std::vector<double>& b; std::vector<double>& c;
       ~TraceOut() {
@@ -1072,8 +1075,22 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         pr("wait   ", a);
         pr("resolve", b);
         pr("post   ", c);
+        auto sib = [](int cpu) {
+          char path[128], buf[64] = {0};
+          std::snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", cpu);
+          FILE* f = std::fopen(path, "r");
+          if (f) {
+            if (!std::fgets(buf, sizeof buf, f)) buf[0] = 0;
+            std::fclose(f);
+          }
+          buf[std::strcspn(buf, "\n")] = 0;
+          return std::string(buf);
+        };
+        const int mc = sched_getcpu();
+        std::fprintf(stderr, "cpus: main %d (siblings %s) helper %d (siblings %s)\n", mc, sib(mc).c_str(), helper_cpu,
+                     helper_cpu >= 0 ? sib(helper_cpu).c_str() : "-");
       }
-    } trace_out{trace, tr_wait, tr_res, tr_post};
+    } trace_out{helper_cpu, trace, tr_wait, tr_res, tr_post};
     int64_t dump_left = std::getenv("PE_DUMP_MAX_WINDOWS") ? std::atoll(std::getenv("PE_DUMP_MAX_WINDOWS")) : INT64_MAX;
     const int K = ctx->topk;
     const size_t gb = pe::cand_group_bytes(K);
@@ -1257,6 +1274,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       const int nb = 1 - cb;
       worker->post([&, nb] {
         const auto tp = std::chrono::steady_clock::now();
+        if (trace) helper_cpu = sched_getcpu();
         enqueue_apply(pend);
         if (!nxt.empty()) enqueue_window(nxt, nb);
         if (trace) tr_post.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
