@@ -91,7 +91,8 @@ typedef struct {
   int32_t window_groups;         /* groups per scan window (0 = 64) */
   int64_t window_pods;           /* pods per scan window (0 = 1024) */
   int32_t fit_path_mask;         /* allowed fit-mask kernels: bit0 int64 compare, bit1 int32 compare,
-                                    bit2 dictionary-coded, bit4 bit planes; bit3 set = no thermometer
+                                    bit2 dictionary-coded, bit4 bit planes (batches with more than 32
+                                    distinct request values split into plane sets); bit3 set = no thermometer
                                     form of the coded kernel; bit5 set = bit planes through the
                                     block-major kernel (PE_MASK_NODE_BLOCKS) instead of the row-major
                                     sweep (PE_MASK_ROWS); no kernel bit set = all kernels (the

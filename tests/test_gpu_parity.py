@@ -195,9 +195,11 @@ def test_fit_mask_rows_pitch(N, J, pitch_blocks):
     e.close()
 
 
-@pytest.mark.parametrize("case", ["many_values", "odd_bytes", "label_antichain", "many_planes", "extreme_values"])
+@pytest.mark.parametrize("case", ["many_values", "odd_bytes", "label_antichain", "many_planes", "plane_sets",
+                                  "extreme_values"])
 def test_fit_mask_path_fallbacks(eng, case):
-    """Each batch shape lands on the path that can hold it (planes > coded > int32 > int64), exact."""
+    """Each batch shape lands on the path that can hold it (planes > coded > int32 > int64), exact.
+    The compare/coded cases run with the planes path disabled: plane sets hold them otherwise."""
     N, J = 3000, 400
     inv = synth.make_inventory(N, 91, 0.3)
     req, need = synth.make_fit_jobs(J, 93)
@@ -216,18 +218,82 @@ def test_fit_mask_path_fallbacks(eng, case):
     elif case == "many_planes":
         req[:, 0] = 500 + (np.arange(J) % 40) * 7    # 40 distinct cpu values: > 32 planes, SWAR-coded
         want = "fit_runs_coded"
+    elif case == "plane_sets":
+        req[:, 0] = 500 + (np.arange(J) % 40) * 7    # the same batch with planes allowed: plane sets
+        want = "fit_runs_planes"
     else:
         req[0] = [np.iinfo(np.int64).max, 0, 0, 0]   # int64 extremes are just two more planes
         req[1] = [0, np.iinfo(np.int64).max, 0, np.iinfo(np.int64).max]
         inv.used[0, :7] = inv.cap[0, :7] + 5         # over-committed nodes: no request fits them
         want = "fit_runs_planes"
-    eng.reset_stats()
-    eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
-    counts = eng.fit_mask(req, need)
+    e = eng if want == "fit_runs_planes" else Engine(0, fit_path_mask=1 | 2 | 4)   # no planes
+    e.reset_stats()
+    e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    counts = e.fit_mask(req, need)
     o_mask, o_counts = oracle.fit_mask(inv.residual(), inv.labels, req, need)
-    np.testing.assert_array_equal(eng.fit_mask_rows(0, J), o_mask)
+    np.testing.assert_array_equal(e.fit_mask_rows(0, J), o_mask)
     np.testing.assert_array_equal(counts, o_counts)
-    assert eng.stats()[want] == 1
+    assert e.stats()[want] == 1
+    if e is not eng:
+        e.close()
+
+
+@pytest.mark.parametrize("N,J,shape", [(3000, 400, "cpu400"), (20000, 5000, "wide"), (123 * 8192 - 7, 700, "wide"),
+                                       (9000, 2000, "unique_mem"), (70000, 64, "wide"), (3000, 1, "wide")])
+def test_fit_mask_plane_sets(N, J, shape):
+    """Batches with more than 32 distinct (dimension, value) pairs split into plane sets, each
+    encoded and swept by the indexed-row kernel: mask rows and counts exact vs the oracle; the
+    same mask as the compare path."""
+    rng = np.random.default_rng(N + J)
+    inv = synth.make_inventory(N, 31 + N % 89, 0.4)
+    req, need = synth.make_fit_jobs(J, 37 + J)
+    if shape == "cpu400":
+        req[:, 0] = 500 + np.arange(J) * 7                              # 400 distinct cpu values
+    elif shape == "wide":                                               # every dimension many-valued
+        req[:, 0] = rng.integers(1, 120, J) * 250
+        req[:, 1] = rng.integers(1, 60, J) * (1 << 28)
+        req[:, 3] = rng.integers(0, 30, J) * (1 << 30)
+        need[:] = rng.integers(0, 4, J).astype(np.uint32) << 1
+    else:                                                               # unique memory per job
+        req[:, 1] = (1 << 30) + np.arange(J) * 4096
+    e = Engine(0)
+    e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    counts = e.fit_mask(req, need)
+    o_mask, o_counts = oracle.fit_mask(inv.residual(), inv.labels, req, need)
+    np.testing.assert_array_equal(counts, o_counts)
+    np.testing.assert_array_equal(e.fit_mask_rows(0, J), o_mask)
+    s = e.stats()
+    pairs = sum(len(np.unique(req[:, d])) for d in range(4)) + len(np.unique(need))
+    # planes when the sets fit (<= 64: 400 cpu values make ~31 sets; independent random values in
+    # every dimension need hundreds), else a fallback path; exact either way
+    assert s["fit_runs_planes"] + s["fit_runs_coded"] + s["fit_runs_i32"] + s["fit_runs_i64"] == 1
+    if shape == "cpu400" or pairs <= 32:
+        assert s["fit_runs_planes"] == 1 and e.fit_mask_layout() == 3
+    # a second run over the same upload is identical (counts re-zeroed, every set re-encoded)
+    np.testing.assert_array_equal(e.fit_mask(req, need), o_counts)
+    e.close()
+
+
+def test_fit_mask_plane_sets_sharded():
+    """Plane sets on two shard contexts of one inventory: the column blocks concatenate to the
+    unsharded oracle mask, per-job counts sum."""
+    N, J = 30001, 900
+    rng = np.random.default_rng(5)
+    inv = synth.make_inventory(N, 41)
+    req, need = synth.make_fit_jobs(J, 43)
+    req[:, 0] = rng.integers(1, 200, J) * 125
+    o_mask, o_counts = oracle.fit_mask(inv.residual(), inv.labels, req, need)
+    total = np.zeros(J, np.int64)
+    for rank in range(2):
+        e = Engine(0, rank=rank, world_size=2, exchange=lambda b: b + b)
+        e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+        b, en = e.shard_range()
+        total += e.fit_mask(req, need)
+        assert e.stats()["fit_runs_planes"] == 1
+        want, _ = oracle.fit_mask(inv.residual()[:, b:en], inv.labels[b:en], req, need)
+        np.testing.assert_array_equal(e.fit_mask_rows(0, J), want)
+        e.close()
+    np.testing.assert_array_equal(total, o_counts)
 
 
 def test_fit_mask_sharded_columns(eng):

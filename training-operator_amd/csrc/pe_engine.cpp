@@ -187,6 +187,16 @@ struct pe_ctx {
   int64_t pl_nblk = 0;                   // planes path: 8192-node blocks
   bool pl_rows = true;                   // planes path: row-major sweep kernel (else block-major streams)
   int64_t pl_R = 1;                      // row-major kernel: job phases of the uploaded batch
+  // A batch with more than PL_MAX distinct (dimension, value) pairs is split into plane sets of at
+  // most PL_MAX pairs each (row-major layout only); each set is encoded and swept on its own by
+  // the indexed-row kernel, its jobs' codes carrying their mask rows.
+  struct PlaneSet {
+    pe::PlaneSpec spec;
+    int64_t J, R, Jr, off;   // jobs, phases, phase stride, first code / count slot
+  };
+  std::vector<PlaneSet> pl_sets;        // empty: one set (ctx->plane, the rows kernel)
+  std::vector<int64_t> pl_cnt_row;      // multi-set: count slot -> job row (-1: padding)
+  int64_t pl_counts_n = 0;              // count slots of the planes path
   DevBuf<uint32_t> planes;
   DevBuf<uint64_t> plane_jobs;
   pe::CodeSpec code{};
@@ -665,48 +675,137 @@ static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const u
 
 // Bit planes of one batch (pe_kernels.h, PlaneSpec): one plane per distinct request value of each
 // dimension and per distinct label need, each job selecting five.  Any int64 values and any need
-// sets; returns false when the batch needs more than PL_MAX planes.
+// sets.  A batch with more than PL_MAX distinct (dimension, value) pairs is split into plane sets
+// (row-major layout only, at most PL_MAX_SETS); returns false when it cannot be held either way.
+constexpr int PL_MAX_SETS = 64;
+
 static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
   if (n_jobs == 0) return false;
-  pe::PlaneSpec sp{};
-  std::vector<int64_t> vals[pe::D + 1];
-  int off[pe::D + 1];
-  for (int f = 0; f <= pe::D; ++f) {
+  constexpr int F = pe::D + 1;
+  auto value = [&](int64_t j, int f) -> int64_t { return f < pe::D ? req[j * pe::D + f] : (int64_t)(need ? need[j] : 0u); };
+  std::vector<int64_t> vals[F];
+  int64_t off[F], P = 0;
+  for (int f = 0; f < F; ++f) {
     vals[f].resize((size_t)n_jobs);
-    for (int64_t j = 0; j < n_jobs; ++j) vals[f][j] = f < pe::D ? req[j * pe::D + f] : (int64_t)(need ? need[j] : 0u);
+    for (int64_t j = 0; j < n_jobs; ++j) vals[f][j] = value(j, f);
     std::sort(vals[f].begin(), vals[f].end());
     vals[f].erase(std::unique(vals[f].begin(), vals[f].end()), vals[f].end());
-    off[f] = sp.n;
-    if (sp.n + (int64_t)vals[f].size() > pe::PL_MAX) return false;
-    for (int64_t v : vals[f]) {
-      sp.kind[sp.n] = f;
-      sp.val[sp.n] = v;
-      ++sp.n;
-    }
+    off[f] = P;
+    P += (int64_t)vals[f].size();
   }
-  std::vector<uint64_t> jc((size_t)n_jobs);
-  for (int64_t j = 0; j < n_jobs; ++j) {
-    uint64_t c = 0;
-    for (int f = 0; f <= pe::D; ++f) {
-      const int64_t q = f < pe::D ? req[j * pe::D + f] : (int64_t)(need ? need[j] : 0u);
-      const int64_t i = std::lower_bound(vals[f].begin(), vals[f].end(), q) - vals[f].begin();
-      // register offset of the plane (4 words each); dims at bits 0, 7, 14, 21, the need at bit 32
-      c |= (uint64_t)(4 * (off[f] + i)) << (f < pe::D ? 7 * f : 32);
-    }
-    jc[j] = c;
-  }
-  ctx->plane = sp;
+  // pair id (global over the fields) of each job's five selections
+  std::vector<int32_t> pid((size_t)n_jobs * F);
+  for (int64_t j = 0; j < n_jobs; ++j)
+    for (int f = 0; f < F; ++f)
+      pid[(size_t)j * F + f] =
+          (int32_t)(off[f] + (std::lower_bound(vals[f].begin(), vals[f].end(), value(j, f)) - vals[f].begin()));
+  auto pair_spec = [&](int64_t p, int& kind, int64_t& val) {
+    int f = F - 1;
+    while (off[f] > p) --f;
+    kind = f;
+    val = vals[f][(size_t)(p - off[f])];
+  };
+  // field f's plane index sits at bits 0/7/14/21 (dims) and 32 (need) as 4 x index (register offset)
+  auto field_shift = [](int f) { return f < pe::D ? 7 * f : 32; };
   ctx->pl_nblk = (std::max<int64_t>(ctx->Ns, 1) + pe::PL_BLK - 1) / pe::PL_BLK;
-  if (ctx->pl_rows) {
-    // one wave per SIMD (1024 on 256 CUs) = nblk x R job phases; codes phase-major.  (Padding the
-    // row to 1024 / R blocks, i.e. an aligned 1 MiB store window, was measured no faster:
-    // profiles/r5c_row_pitch.txt.)
-    const int64_t R = std::min<int64_t>(n_jobs, std::max<int64_t>(1, 1024 / ctx->pl_nblk));
-    const int64_t Jr = ((n_jobs + R - 1) / R + 3) / 4 * 4;   // = the kernel's phase stride
-    std::vector<uint64_t> perm((size_t)(R * Jr), 0);
-    for (int64_t j = 0; j < n_jobs; ++j) perm[(size_t)((j % R) * Jr + j / R)] = jc[j];
-    jc.swap(perm);
+  // phases of a set of J jobs: one wave per SIMD (1024 on 256 CUs) = nblk x R; codes phase-major.
+  // (Padding the row to 1024 / R blocks, i.e. an aligned 1 MiB store window, was measured no
+  // faster: profiles/r5c_row_pitch.txt.)
+  auto phases = [&](int64_t J, int64_t& R, int64_t& Jr) {
+    R = ctx->pl_rows ? std::min<int64_t>(J, std::max<int64_t>(1, 1024 / ctx->pl_nblk)) : 1;
+    Jr = ctx->pl_rows ? ((J + R - 1) / R + 3) / 4 * 4 : J;   // = the kernel's phase stride
+  };
+  std::vector<uint64_t> jc;
+  ctx->pl_sets.clear();
+  ctx->pl_cnt_row.clear();
+  if (P <= pe::PL_MAX) {   // one set: every pair is a plane
+    pe::PlaneSpec sp{};
+    for (int64_t p = 0; p < P; ++p) {
+      int kind;
+      pair_spec(p, kind, sp.val[sp.n]);
+      sp.kind[sp.n++] = kind;
+    }
+    jc.resize((size_t)n_jobs);
+    for (int64_t j = 0; j < n_jobs; ++j) {
+      uint64_t c = 0;
+      for (int f = 0; f < F; ++f) c |= (uint64_t)(4 * pid[(size_t)j * F + f]) << field_shift(f);
+      jc[j] = c;
+    }
+    ctx->plane = sp;
+    int64_t R, Jr;
+    phases(n_jobs, R, Jr);
+    if (ctx->pl_rows) {
+      std::vector<uint64_t> perm((size_t)(R * Jr), 0);
+      for (int64_t j = 0; j < n_jobs; ++j) perm[(size_t)((j % R) * Jr + j / R)] = jc[j];
+      jc.swap(perm);
+    }
     ctx->pl_R = R;
+    ctx->pl_counts_n = R * Jr;
+  } else {
+    if (!ctx->pl_rows || n_jobs >= (int64_t(1) << 24)) return false;
+    // Sets: jobs ordered by their selections, the field with the most distinct values first, then
+    // swept greedily; a set closes when the next job would take it past PL_MAX planes.
+    int ford[F];
+    for (int f = 0; f < F; ++f) ford[f] = f;
+    std::sort(ford, ford + F, [&](int x, int y) { return vals[x].size() > vals[y].size(); });
+    std::vector<int64_t> order((size_t)n_jobs);
+    for (int64_t j = 0; j < n_jobs; ++j) order[j] = j;
+    std::sort(order.begin(), order.end(), [&](int64_t x, int64_t y) {
+      for (int f : ford)
+        if (pid[(size_t)x * F + f] != pid[(size_t)y * F + f]) return pid[(size_t)x * F + f] < pid[(size_t)y * F + f];
+      return x < y;
+    });
+    std::vector<int32_t> stamp((size_t)P, -1), local((size_t)P, 0);
+    std::vector<std::vector<int64_t>> members;
+    std::vector<std::vector<uint64_t>> codes;
+    std::vector<pe::PlaneSpec> specs;
+    int cur = -1, ncur = 0;
+    for (int64_t j : order) {
+      int add = 0;
+      for (int f = 0; f < F; ++f) add += cur < 0 || stamp[pid[(size_t)j * F + f]] != cur;
+      if (cur < 0 || ncur + add > pe::PL_MAX) {
+        if ((int)specs.size() == PL_MAX_SETS) return false;
+        ++cur;
+        ncur = 0;
+        members.emplace_back();
+        codes.emplace_back();
+        specs.push_back(pe::PlaneSpec{});
+      }
+      uint64_t c = (uint64_t)j << 40;   // the job's mask row
+      for (int f = 0; f < F; ++f) {
+        const int32_t p = pid[(size_t)j * F + f];
+        if (stamp[p] != cur) {
+          stamp[p] = cur;
+          local[p] = ncur++;
+          pe::PlaneSpec& sp = specs[cur];
+          int kind;
+          pair_spec(p, kind, sp.val[sp.n]);
+          sp.kind[sp.n++] = kind;
+        }
+        c |= (uint64_t)(4 * local[p]) << field_shift(f);
+      }
+      members[cur].push_back(j);
+      codes[cur].push_back(c);
+    }
+    int64_t total = 0;
+    for (size_t t = 0; t < specs.size(); ++t) {
+      pe_ctx::PlaneSet st{specs[t], (int64_t)members[t].size(), 0, 0, total};
+      phases(st.J, st.R, st.Jr);
+      total += st.R * st.Jr;
+      ctx->pl_sets.push_back(st);
+    }
+    jc.assign((size_t)total, 0);
+    ctx->pl_cnt_row.assign((size_t)total, -1);
+    for (size_t t = 0; t < specs.size(); ++t) {
+      const pe_ctx::PlaneSet& st = ctx->pl_sets[t];
+      for (int64_t i = 0; i < st.J; ++i) {
+        const size_t k = (size_t)(st.off + (i % st.R) * st.Jr + i / st.R);
+        jc[k] = codes[t][i];
+        ctx->pl_cnt_row[k] = members[t][i];
+      }
+    }
+    ctx->pl_R = 1;
+    ctx->pl_counts_n = total;
   }
   hipchk(ctx->planes.ensure((size_t)ctx->pl_nblk * pe::PL_MAX * 64 * pe::PL_R), "alloc planes");
   hipchk(ctx->plane_jobs.ensure(jc.size()), "alloc plane jobs");
@@ -772,7 +871,7 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
                             : ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
                                                  : (size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4;
   hipchk(ctx->mask.ensure(mask_words), "alloc fit mask");
-  const int64_t n_counts = std::max<int64_t>(Jp, ctx->fit_path == 3 && ctx->pl_rows ? ctx->pl_R * (((n_jobs + ctx->pl_R - 1) / ctx->pl_R + 3) / 4 * 4) : 0);
+  const int64_t n_counts = std::max<int64_t>(Jp, ctx->fit_path == 3 ? ctx->pl_counts_n : 0);
   hipchk(ctx->counts.ensure(n_counts), "alloc fit counts");
   hipchk(ctx->h_counts.ensure(n_counts), "alloc pinned counts");
   hipchk(hipMemcpyAsync(ctx->fit_jobs.p, recs.data(), Jp * sizeof(ReqRec), hipMemcpyHostToDevice, ctx->stream),
@@ -793,6 +892,20 @@ static void fit_run(pe_ctx* ctx) {
   tpw = std::min<int64_t>(16, std::max<int64_t>(1, tpw));
   if (ctx->fit_path == 3) {
     // ~16k waves: every 8192-node block times enough job ranges, at least 64 jobs per wave
+    if (!ctx->pl_sets.empty()) {   // plane sets: encode and sweep each (same planes buffer, stream order)
+      for (const pe_ctx::PlaneSet& st : ctx->pl_sets) {
+        hipchk(pe::launch_encode_planes(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->pl_nblk,
+                                        st.spec, ctx->planes.p),
+               "launch encode_planes");
+        hipchk(pe::launch_fit_mask_planes_rowsidx(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p + st.off,
+                                                  st.J, st.R, st.Jr, reinterpret_cast<uint32_t*>(ctx->mask.p),
+                                                  ctx->counts.p + st.off),
+               "launch fit_mask_planes_rowsidx");
+      }
+      ctx->stats.fit_runs_planes += 1;
+      ctx->stats.fit_evals += J * ctx->Ns;
+      return;
+    }
     hipchk(pe::launch_encode_planes(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->pl_nblk,
                                     ctx->plane, ctx->planes.p),
            "launch encode_planes");
@@ -840,6 +953,15 @@ static void fit_run(pe_ctx* ctx) {
 static void fit_counts(pe_ctx* ctx, int64_t* out) {
   const int64_t J = ctx->fit_J;
   if (J == 0) return;
+  if (ctx->fit_path == 3 && !ctx->pl_sets.empty()) {   // plane sets: slot -> row
+    hipchk(hipMemcpyAsync(ctx->h_counts.p, ctx->counts.p, ctx->pl_counts_n * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, ctx->stream),
+           "D2H counts");
+    hipchk(hipStreamSynchronize(ctx->stream), "sync counts");
+    for (int64_t k = 0; k < ctx->pl_counts_n; ++k)
+      if (ctx->pl_cnt_row[k] >= 0) out[ctx->pl_cnt_row[k]] = (int64_t)ctx->h_counts.p[k];
+    return;
+  }
   const bool phased = ctx->fit_path == 3 && ctx->pl_rows;
   const int64_t R = phased ? ctx->pl_R : 1, Jr = phased ? ((J + R - 1) / R + 3) / 4 * 4 : J;
   hipchk(hipMemcpyAsync(ctx->h_counts.p, ctx->counts.p, R * Jr * sizeof(unsigned long long), hipMemcpyDeviceToHost,

@@ -136,6 +136,12 @@ hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t
 // every wave reads and counts a contiguous run.
 hipError_t launch_fit_mask_planes_rows(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
                                        int64_t J, int64_t R, uint32_t* mask, unsigned long long* counts);
+// Plane-set form (batches with more than PL_MAX distinct request values): the same grid and
+// phase-major codes for the jobs of ONE set, each code carrying its job's mask row in bits 40-63;
+// counts are per code slot (phase-major, stride Jr).
+hipError_t launch_fit_mask_planes_rowsidx(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
+                                          int64_t J, int64_t R, int64_t Jr, uint32_t* mask,
+                                          unsigned long long* counts);
 
 // kn / lo: the node-only score terms of prep_nodes (K(n) = (S(n) << 24) | gid, lo20(r1), lo24(r3)),
 // kept current by apply; see pe_kernels.hip node_prep for the exactness argument.

@@ -753,6 +753,58 @@ hipError_t launch_fit_mask_planes_rows(hipStream_t s, const uint32_t* planes, in
   return hipGetLastError();
 }
 
+// Plane-set variant of the row sweep: the same grid (nblk x R resident waves, wave (blk, r) takes
+// the set's jobs r, r + R, ...), but a job's mask row comes from its code (bits 40-63), so the
+// store address is per job (row * pitch from SGPRs) and the count is a per-job wave sum gathered
+// into one 64-lane atomic per 64 jobs.
+__global__ __launch_bounds__(256) void fit_mask_planes_rowsidx_kernel(const uint32_t* __restrict__ planes,
+                                                                      int64_t nblk, const uint64_t* __restrict__ jcode,
+                                                                      int64_t J, int64_t R, int64_t Jr,
+                                                                      uint32_t* __restrict__ mask,
+                                                                      unsigned long long* __restrict__ counts) {
+  static_assert(PL_MAX == 32 && PL_R == 4, "register map assumes 32 planes x 4 words");
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t blk = wave_id % nblk;
+  const int64_t r = wave_id / nblk;
+  if (r >= R || r >= J) return;
+  const u32x4* pb = reinterpret_cast<const u32x4*>(planes + blk * PL_MAX * (64 * PL_R)) + lane;
+  const u32x32 A = load_planes8(pb), B = load_planes8(pb + 8 * 64), C = load_planes8(pb + 16 * 64),
+               Dq = load_planes8(pb + 24 * 64);
+  const int64_t row_vec = nblk * 64;           // u32x4 per row
+  u32x4* const col = reinterpret_cast<u32x4*>(mask) + blk * 64 + lane;
+  const uint64_t* jc = jcode + r * Jr;
+  unsigned long long* cnt = counts + r * Jr;
+  const int64_t ni = (J - r + R - 1) / R;      // jobs of this phase
+  for (int64_t i0 = 0; i0 < ni; i0 += 64) {
+    const int64_t i1 = min(ni, i0 + 64);
+    uint32_t acc = 0;
+    for (int64_t i = i0; i < i1; ++i) {
+      const uint64_t c = jc[i];
+      u32x4 f;
+      plane_sel(f, (uint32_t)c & 127, A, B, C, Dq);
+      plane_and(f, (uint32_t)(c >> 7) & 127, A, B, C, Dq);
+      plane_and(f, (uint32_t)(c >> 14) & 127, A, B, C, Dq);
+      plane_and(f, (uint32_t)(c >> 21) & 127, A, B, C, Dq);
+      plane_and(f, (uint32_t)(c >> 32) & 127, A, B, C, Dq);
+      *(gu32x4*)(col + (int64_t)(c >> 40) * row_vec) = f;
+      const uint32_t n = wave_sum(__popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w));
+      acc = writelane_s(acc, n, (uint32_t)(i - i0));
+    }
+    if (lane < i1 - i0 && acc) atomicAdd(&cnt[i0 + lane], (unsigned long long)acc);
+  }
+}
+
+hipError_t launch_fit_mask_planes_rowsidx(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
+                                          int64_t J, int64_t R, int64_t Jr, uint32_t* mask,
+                                          unsigned long long* counts) {
+  if (J <= 0 || nblk <= 0 || R <= 0) return hipSuccess;
+  const int64_t waves = nblk * R;
+  hipLaunchKernelGGL(fit_mask_planes_rowsidx_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, planes, nblk,
+                     jcode, J, R, Jr, mask, counts);
+  return hipGetLastError();
+}
+
 hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
                                   int64_t J, int64_t jobs_per_wave, uint32_t* mask, unsigned long long* counts) {
   if (J <= 0 || nblk <= 0) return hipSuccess;
