@@ -264,7 +264,7 @@ def test_fit_mask_plane_sets(N, J, shape):
     np.testing.assert_array_equal(e.fit_mask_rows(0, J), o_mask)
     s = e.stats()
     pairs = sum(len(np.unique(req[:, d])) for d in range(4)) + len(np.unique(need))
-    # planes when the sets fit (<= 64: 400 cpu values make ~31 sets; independent random values in
+    # planes when the sets fit (<= 256: 400 cpu values make ~31 sets; independent random values in
     # every dimension need hundreds), else a fallback path; exact either way
     assert s["fit_runs_planes"] + s["fit_runs_coded"] + s["fit_runs_i32"] + s["fit_runs_i64"] == 1
     if shape == "cpu400" or pairs <= 32:

@@ -195,6 +195,8 @@ struct pe_ctx {
     int64_t J, R, Jr, off;   // jobs, phases, phase stride, first code / count slot
   };
   std::vector<PlaneSet> pl_sets;        // empty: one set (ctx->plane, the rows kernel)
+  DevBuf<pe::PlaneSpec> pl_specs_d;     // multi-set: the sets' specs and {off, J, Jr} on the device
+  DevBuf<int64_t> pl_meta_d;
   std::vector<int64_t> pl_cnt_row;      // multi-set: count slot -> job row (-1: padding)
   int64_t pl_counts_n = 0;              // count slots of the planes path
   DevBuf<uint32_t> planes;
@@ -677,7 +679,8 @@ static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const u
 // dimension and per distinct label need, each job selecting five.  Any int64 values and any need
 // sets.  A batch with more than PL_MAX distinct (dimension, value) pairs is split into plane sets
 // (row-major layout only, at most PL_MAX_SETS); returns false when it cannot be held either way.
-constexpr int PL_MAX_SETS = 64;
+constexpr int PL_MAX_SETS = 256;
+constexpr int64_t PL_SETS_BYTES = int64_t(2) << 30;   // planes of all sets (4 MiB per set at 1M nodes)
 
 static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
   if (n_jobs == 0) return false;
@@ -764,7 +767,9 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const 
       int add = 0;
       for (int f = 0; f < F; ++f) add += cur < 0 || stamp[pid[(size_t)j * F + f]] != cur;
       if (cur < 0 || ncur + add > pe::PL_MAX) {
-        if ((int)specs.size() == PL_MAX_SETS) return false;
+        if ((int)specs.size() == PL_MAX_SETS ||
+            (int64_t)(specs.size() + 1) * ctx->pl_nblk * pe::PL_MAX * 64 * pe::PL_R * 4 > PL_SETS_BYTES)
+          return false;
         ++cur;
         ncur = 0;
         members.emplace_back();
@@ -787,13 +792,40 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const 
       members[cur].push_back(j);
       codes[cur].push_back(c);
     }
-    int64_t total = 0;
-    for (size_t t = 0; t < specs.size(); ++t) {
-      pe_ctx::PlaneSet st{specs[t], (int64_t)members[t].size(), 0, 0, total};
-      phases(st.J, st.R, st.Jr);
-      total += st.R * st.Jr;
-      ctx->pl_sets.push_back(st);
+    // each set's jobs in row order: the sweep's stores in flight then stay in a narrow band of
+    // rows (the partition order scattered them over the whole mask)
+    for (size_t t = 0; t < members.size(); ++t) {
+      std::vector<size_t> ix(members[t].size());
+      for (size_t i = 0; i < ix.size(); ++i) ix[i] = i;
+      std::sort(ix.begin(), ix.end(), [&](size_t x, size_t y) { return members[t][x] < members[t][y]; });
+      std::vector<int64_t> m2(ix.size());
+      std::vector<uint64_t> c2(ix.size());
+      for (size_t i = 0; i < ix.size(); ++i) {
+        m2[i] = members[t][ix[i]];
+        c2[i] = codes[t][ix[i]];
+      }
+      members[t].swap(m2);
+      codes[t].swap(c2);
     }
+    // one launch sweeps every set: the phase count is common (one wave per SIMD over nblk blocks)
+    const int64_t R = std::max<int64_t>(1, 1024 / ctx->pl_nblk);
+    int64_t total = 0;
+    std::vector<int64_t> meta;
+    for (size_t t = 0; t < specs.size(); ++t) {
+      pe_ctx::PlaneSet st{specs[t], (int64_t)members[t].size(), R, 0, total};
+      st.Jr = ((st.J + R - 1) / R + 3) / 4 * 4;
+      total += R * st.Jr;
+      ctx->pl_sets.push_back(st);
+      meta.insert(meta.end(), {st.off, st.J, st.Jr});
+    }
+    hipchk(ctx->pl_specs_d.ensure(specs.size()), "alloc plane specs");
+    hipchk(ctx->pl_meta_d.ensure(meta.size()), "alloc plane set meta");
+    hipchk(hipMemcpyAsync(ctx->pl_specs_d.p, specs.data(), specs.size() * sizeof(pe::PlaneSpec),
+                          hipMemcpyHostToDevice, ctx->stream),
+           "H2D plane specs");
+    hipchk(hipMemcpyAsync(ctx->pl_meta_d.p, meta.data(), meta.size() * 8, hipMemcpyHostToDevice, ctx->stream),
+           "H2D plane set meta");
+    hipchk(hipStreamSynchronize(ctx->stream), "sync plane sets");   // the host vectors die here
     jc.assign((size_t)total, 0);
     ctx->pl_cnt_row.assign((size_t)total, -1);
     for (size_t t = 0; t < specs.size(); ++t) {
@@ -807,7 +839,9 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const 
     ctx->pl_R = 1;
     ctx->pl_counts_n = total;
   }
-  hipchk(ctx->planes.ensure((size_t)ctx->pl_nblk * pe::PL_MAX * 64 * pe::PL_R), "alloc planes");
+  hipchk(ctx->planes.ensure((size_t)std::max<size_t>(ctx->pl_sets.size(), 1) * ctx->pl_nblk * pe::PL_MAX * 64 *
+                            pe::PL_R),
+         "alloc planes");
   hipchk(ctx->plane_jobs.ensure(jc.size()), "alloc plane jobs");
   hipchk(hipMemcpyAsync(ctx->plane_jobs.p, jc.data(), jc.size() * 8, hipMemcpyHostToDevice, ctx->stream),
          "H2D plane jobs");
@@ -892,16 +926,15 @@ static void fit_run(pe_ctx* ctx) {
   tpw = std::min<int64_t>(16, std::max<int64_t>(1, tpw));
   if (ctx->fit_path == 3) {
     // ~16k waves: every 8192-node block times enough job ranges, at least 64 jobs per wave
-    if (!ctx->pl_sets.empty()) {   // plane sets: encode and sweep each (same planes buffer, stream order)
-      for (const pe_ctx::PlaneSet& st : ctx->pl_sets) {
-        hipchk(pe::launch_encode_planes(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->pl_nblk,
-                                        st.spec, ctx->planes.p),
-               "launch encode_planes");
-        hipchk(pe::launch_fit_mask_planes_rowsidx(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p + st.off,
-                                                  st.J, st.R, st.Jr, reinterpret_cast<uint32_t*>(ctx->mask.p),
-                                                  ctx->counts.p + st.off),
-               "launch fit_mask_planes_rowsidx");
-      }
+    if (!ctx->pl_sets.empty()) {   // plane sets: one encode pass and one sweep for all of them
+      const int ns = (int)ctx->pl_sets.size();
+      hipchk(pe::launch_encode_planes_sets(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->pl_nblk,
+                                           ctx->pl_specs_d.p, ns, ctx->planes.p),
+             "launch encode_planes_sets");
+      hipchk(pe::launch_fit_mask_planes_sets(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p,
+                                             ctx->pl_meta_d.p, ns, ctx->pl_sets[0].R,
+                                             reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p),
+             "launch fit_mask_planes_sets");
       ctx->stats.fit_runs_planes += 1;
       ctx->stats.fit_evals += J * ctx->Ns;
       return;

@@ -136,12 +136,15 @@ hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t
 // every wave reads and counts a contiguous run.
 hipError_t launch_fit_mask_planes_rows(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
                                        int64_t J, int64_t R, uint32_t* mask, unsigned long long* counts);
-// Plane-set form (batches with more than PL_MAX distinct request values): the same grid and
-// phase-major codes for the jobs of ONE set, each code carrying its job's mask row in bits 40-63;
-// counts are per code slot (phase-major, stride Jr).
-hipError_t launch_fit_mask_planes_rowsidx(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
-                                          int64_t J, int64_t R, int64_t Jr, uint32_t* mask,
-                                          unsigned long long* counts);
+// Plane-set form (batches with more than PL_MAX distinct request values), all sets in one launch
+// each: encode writes set t's planes at planes + t * nblk * PL_MAX * 256; the sweep has the rows
+// kernel's grid (R phases common to all sets); set t's codes and counts start at meta[3t] (phase-
+// major, stride meta[3t+2], meta[3t+1] jobs), each code carrying its job's mask row in bits 40-63.
+hipError_t launch_encode_planes_sets(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
+                                     int64_t Ns, int64_t nblk, const PlaneSpec* specs, int nsets, uint32_t* planes);
+hipError_t launch_fit_mask_planes_sets(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
+                                       const int64_t* meta, int nsets, int64_t R, uint32_t* mask,
+                                       unsigned long long* counts);
 
 // kn / lo: the node-only score terms of prep_nodes (K(n) = (S(n) << 24) | gid, lo20(r1), lo24(r3)),
 // kept current by apply; see pe_kernels.hip node_prep for the exactness argument.

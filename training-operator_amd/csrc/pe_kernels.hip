@@ -474,6 +474,54 @@ __global__ __launch_bounds__(256) void encode_planes_kernel(const int64_t* __res
   }
 }
 
+// Every plane set of a batch in one pass over the residuals: the encode above per set t (specs
+// from device memory, uniform), planes of set t at planes + t * nblk * PL_MAX * 256.
+__global__ __launch_bounds__(256) void encode_planes_sets_kernel(const int64_t* __restrict__ res, int64_t stride,
+                                                                 const uint32_t* __restrict__ labels, int64_t Ns,
+                                                                 int64_t nblk, const PlaneSpec* __restrict__ specs,
+                                                                 int nsets, uint32_t* __restrict__ planes) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n0 = g * 64;
+  if (n0 >= nblk * PL_BLK) return;
+  const int64_t n = n0 + lane;
+  const bool valid = n < Ns;
+  int64_t r[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) r[d] = valid ? res[d * stride + n] : 0;
+  const uint32_t lab = valid ? labels[n] : 0u;
+  const int64_t blk = n0 / PL_BLK;
+  const int64_t w0 = (n0 % PL_BLK) / 32;
+  for (int t = 0; t < nsets; ++t) {
+    const PlaneSpec& spec = specs[t];
+    uint32_t* out = planes + ((int64_t)t * nblk + blk) * PL_MAX * (64 * PL_R) + w0;
+    const int np = spec.n;
+    for (int p = 0; p < PL_MAX; ++p) {
+      bool pr = false;
+      if (p < np) {
+        const int k = spec.kind[p];
+        const int64_t v = spec.val[p];
+        int64_t rv = r[0];
+        rv = k == 1 ? r[1] : rv;
+        rv = k == 2 ? r[2] : rv;
+        rv = k == 3 ? r[3] : rv;
+        pr = valid && (k == 4 ? (lab & (uint32_t)v) == (uint32_t)v : rv >= v);
+      }
+      const uint64_t b = __builtin_amdgcn_ballot_w64(pr);
+      if (lane < 2) out[p * (64 * PL_R) + lane] = (uint32_t)(lane ? b >> 32 : b);
+    }
+  }
+}
+
+hipError_t launch_encode_planes_sets(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
+                                     int64_t Ns, int64_t nblk, const PlaneSpec* specs, int nsets, uint32_t* planes) {
+  if (nblk <= 0 || nsets <= 0) return hipSuccess;
+  const int64_t waves = nblk * PL_BLK / 64;
+  hipLaunchKernelGGL(encode_planes_sets_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, res, stride,
+                     labels, Ns, nblk, specs, nsets, planes);
+  return hipGetLastError();
+}
+
 hipError_t launch_encode_planes(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
                                 int64_t Ns, int64_t nblk, const PlaneSpec& spec, uint32_t* planes) {
   if (nblk <= 0) return hipSuccess;
@@ -753,55 +801,112 @@ hipError_t launch_fit_mask_planes_rows(hipStream_t s, const uint32_t* planes, in
   return hipGetLastError();
 }
 
-// Plane-set variant of the row sweep: the same grid (nblk x R resident waves, wave (blk, r) takes
-// the set's jobs r, r + R, ...), but a job's mask row comes from its code (bits 40-63), so the
-// store address is per job (row * pitch from SGPRs) and the count is a per-job wave sum gathered
-// into one 64-lane atomic per 64 jobs.
-__global__ __launch_bounds__(256) void fit_mask_planes_rowsidx_kernel(const uint32_t* __restrict__ planes,
-                                                                      int64_t nblk, const uint64_t* __restrict__ jcode,
-                                                                      int64_t J, int64_t R, int64_t Jr,
-                                                                      uint32_t* __restrict__ mask,
-                                                                      unsigned long long* __restrict__ counts) {
+// plane_job with the job's mask row (code bits 40-63 = bits 8-31 of the high half) in an SGPR.
+template <int K>
+__device__ __forceinline__ void plane_job_row(u32x4& f, uint32_t& row, uint32_t lo, uint32_t hi, const u32x32& A,
+                                              const u32x32& B, const u32x32& C, const u32x32& Dq) {
+  uint32_t c, c4, t;
+  asm volatile(
+      "v_readlane_b32 %[c], %[lo], %[k]\n\t"
+      "v_readlane_b32 %[c4], %[hi], %[k]\n\t"
+      "s_and_b32 %[t], %[c], 0x7f\n\t"
+      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      "v_mov_b32_e32 %[f0], v32\n\tv_mov_b32_e32 %[f1], v33\n\tv_mov_b32_e32 %[f2], v34\n\tv_mov_b32_e32 %[f3], v35\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_bfe_u32 %[t], %[c], 0x70007\n\t"
+      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_bfe_u32 %[t], %[c], 0x7000e\n\t"
+      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_bfe_u32 %[t], %[c], 0x70015\n\t"
+      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_and_b32 %[t], %[c4], 0x7f\n\t"
+      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_lshr_b32 %[row], %[c4], 8"
+      : [f0] "=&v"(f.x), [f1] "=&v"(f.y), [f2] "=&v"(f.z), [f3] "=&v"(f.w), [c] "=&s"(c), [c4] "=&s"(c4),
+        [t] "=&s"(t), [row] "=&s"(row)
+      : [lo] "v"(lo), [hi] "v"(hi), [k] "i"(K), "{v[32:63]}"(A), "{v[64:95]}"(B), "{v[96:127]}"(C),
+        "{v[128:159]}"(Dq)
+      : "scc");
+}
+
+// Jobs K .. 63 of a plane-set batch of n (<= 64, uniform) jobs: select, store to the job's own
+// row, per-lane popcount into p[K] (0 past n).
+template <int K>
+__device__ __forceinline__ void sets_batch(uint32_t (&p)[64], uint32_t lo, uint32_t hi, const u32x32& A,
+                                           const u32x32& B, const u32x32& C, const u32x32& Dq, u32x4* col,
+                                           int64_t row_vec, int n) {
+  p[K] = 0;
+  if (K < n) {
+    u32x4 f;
+    uint32_t row;
+    plane_job_row<K>(f, row, lo, hi, A, B, C, Dq);
+    *(gu32x4*)(col + (int64_t)row * row_vec) = f;
+    p[K] = __popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w);
+  }
+  if constexpr (K + 1 < 64) sets_batch<K + 1>(p, lo, hi, A, B, C, Dq, col, row_vec, n);
+}
+
+// Plane-set variant of the row sweep, every set in ONE launch: the rows kernel's grid (nblk x R
+// resident waves, R common to all sets); wave (blk, r) walks the sets in turn, reloading its
+// block's 32 planes of set t into the same registers, and takes set t's jobs r, r + R, ....  A
+// job's mask row comes from its code (bits 40-63), so the store address is per job (row * pitch
+// from SGPRs); counts per 64-job batch by the rows kernel's column sum (reduce64x64), one atomic.
+// meta[t] = {first code / count slot, jobs, phase stride} of set t.
+__global__ __launch_bounds__(256) void fit_mask_planes_sets_kernel(const uint32_t* __restrict__ planes, int64_t nblk,
+                                                                   const uint64_t* __restrict__ jcode,
+                                                                   const int64_t* __restrict__ meta, int nsets,
+                                                                   int64_t R, uint32_t* __restrict__ mask,
+                                                                   unsigned long long* __restrict__ counts) {
   static_assert(PL_MAX == 32 && PL_R == 4, "register map assumes 32 planes x 4 words");
   const int lane = threadIdx.x & 63;
   const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = wave_id % nblk;
   const int64_t r = wave_id / nblk;
-  if (r >= R || r >= J) return;
-  const u32x4* pb = reinterpret_cast<const u32x4*>(planes + blk * PL_MAX * (64 * PL_R)) + lane;
-  const u32x32 A = load_planes8(pb), B = load_planes8(pb + 8 * 64), C = load_planes8(pb + 16 * 64),
-               Dq = load_planes8(pb + 24 * 64);
+  if (r >= R) return;
   const int64_t row_vec = nblk * 64;           // u32x4 per row
   u32x4* const col = reinterpret_cast<u32x4*>(mask) + blk * 64 + lane;
-  const uint64_t* jc = jcode + r * Jr;
-  unsigned long long* cnt = counts + r * Jr;
-  const int64_t ni = (J - r + R - 1) / R;      // jobs of this phase
-  for (int64_t i0 = 0; i0 < ni; i0 += 64) {
-    const int64_t i1 = min(ni, i0 + 64);
-    uint32_t acc = 0;
-    for (int64_t i = i0; i < i1; ++i) {
-      const uint64_t c = jc[i];
-      u32x4 f;
-      plane_sel(f, (uint32_t)c & 127, A, B, C, Dq);
-      plane_and(f, (uint32_t)(c >> 7) & 127, A, B, C, Dq);
-      plane_and(f, (uint32_t)(c >> 14) & 127, A, B, C, Dq);
-      plane_and(f, (uint32_t)(c >> 21) & 127, A, B, C, Dq);
-      plane_and(f, (uint32_t)(c >> 32) & 127, A, B, C, Dq);
-      *(gu32x4*)(col + (int64_t)(c >> 40) * row_vec) = f;
-      const uint32_t n = wave_sum(__popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w));
-      acc = writelane_s(acc, n, (uint32_t)(i - i0));
+  uint32_t sigma;                              // lane l of a batch sum counts batch job sigma
+  {
+    uint32_t probe[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) probe[k] = lane == 0 ? (uint32_t)k : 0u;
+    sigma = reduce64x64(probe, lane);
+  }
+  for (int t = 0; t < nsets; ++t) {
+    const int64_t off = meta[3 * t], J = meta[3 * t + 1], Jr = meta[3 * t + 2];
+    if (r >= J) continue;
+    const u32x4* pb = reinterpret_cast<const u32x4*>(planes + (t * nblk + blk) * PL_MAX * (64 * PL_R)) + lane;
+    const u32x32 A = load_planes8(pb), B = load_planes8(pb + 8 * 64), C = load_planes8(pb + 16 * 64),
+                 Dq = load_planes8(pb + 24 * 64);
+    const uint64_t* jc = jcode + off + r * Jr;
+    unsigned long long* cnt = counts + off + r * Jr;
+    const int64_t ni = (J - r + R - 1) / R;    // jobs of this phase in set t
+    for (int64_t i0 = 0; i0 < ni; i0 += 64) {
+      const int n = (int)min<int64_t>(64, ni - i0);
+      const uint64_t cv = lane < n ? jc[i0 + lane] : 0;   // lane l: code of batch job l
+      uint32_t p[64];
+      sets_batch<0>(p, (uint32_t)cv, (uint32_t)(cv >> 32), A, B, C, Dq, col, row_vec, n);
+      const uint32_t F = reduce64x64(p, lane);
+      if (F) atomicAdd(&cnt[i0 + sigma], (unsigned long long)F);
     }
-    if (lane < i1 - i0 && acc) atomicAdd(&cnt[i0 + lane], (unsigned long long)acc);
   }
 }
 
-hipError_t launch_fit_mask_planes_rowsidx(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
-                                          int64_t J, int64_t R, int64_t Jr, uint32_t* mask,
-                                          unsigned long long* counts) {
-  if (J <= 0 || nblk <= 0 || R <= 0) return hipSuccess;
+hipError_t launch_fit_mask_planes_sets(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
+                                       const int64_t* meta, int nsets, int64_t R, uint32_t* mask,
+                                       unsigned long long* counts) {
+  if (nblk <= 0 || R <= 0 || nsets <= 0) return hipSuccess;
   const int64_t waves = nblk * R;
-  hipLaunchKernelGGL(fit_mask_planes_rowsidx_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, planes, nblk,
-                     jcode, J, R, Jr, mask, counts);
+  hipLaunchKernelGGL(fit_mask_planes_sets_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, planes, nblk,
+                     jcode, meta, nsets, R, mask, counts);
   return hipGetLastError();
 }
 
