@@ -275,6 +275,29 @@ def main():
                              "fit kernel is bound by its mask stores (HBM write)"},
     }
 
+    if not args.no_configs:
+        # the same step on a batch with 400 distinct cpu requests (more than one plane set holds):
+        # plane sets, all swept in one launch; informational, not the headline value
+        mreq = req.copy()
+        mreq[:, 0] = 250 * (1 + np.arange(J) % 400)
+        eng.jobs_upload(mreq, need)
+        eng.fit_mask_run()
+        eng.synchronize()
+        m0, m1 = ev.create(), ev.create()
+        ev.record(m0, stream)
+        for _ in range(args.steps):
+            eng.fit_mask_run()
+        ev.record(m1, stream)
+        eng.synchronize()
+        mms = ev.elapsed_ms(m0, m1) / args.steps
+        out["fit_many_values"] = {"workload": "cfg5 batch with 400 distinct cpu requests (plane sets)",
+                                  "kernel_ms": mms, "evals_per_s_this_rank": float(Ns) * J / (mms * 1e-3),
+                                  "fit_path": "planes" if eng.stats()["fit_runs_planes"] > st0["fit_runs_planes"]
+                                  else "fallback"}
+        eng.jobs_upload(req, need)                  # back to the headline batch (counts for the CPU check)
+        eng.fit_mask_run()
+        eng.synchronize()
+
     if not args.no_greedy:
         batch = synth.make_jobs(args.greedy_jobs, synth.SEED["cfg3"], "mixed")
         eng.reset_residuals()
