@@ -474,30 +474,43 @@ __global__ __launch_bounds__(256) void encode_planes_kernel(const int64_t* __res
   }
 }
 
-// Every plane set of a batch in one pass over the residuals: the encode above per set t (specs
-// from device memory, uniform), planes of set t at planes + t * nblk * PL_MAX * 256.
+// Every plane set of a batch: the same planes as the encode above, set t = blockIdx.y (spec from
+// device memory, uniform), planes of set t at planes + t * nblk * PL_MAX * 256.  One wave owns a
+// segment of ES_G x 64 nodes = 2 ES_G plane words: it ballots the segment's node groups one after
+// the other, parks word 2g / 2g+1 of plane p in lane 2g / 2g+1 of a per-plane VGPR (one select),
+// then stores each plane's words with one contiguous 4 x 2 ES_G-byte store -- instead of a 2-lane
+// 8-byte store per plane and 64 nodes (the per-set cost of that pattern was ~68 us at 1M nodes).
+constexpr int ES_G = 16;                                  // node groups per wave: 32 words, 128 B
+static_assert(PL_BLK % (64 * ES_G) == 0, "segments tile a block");
 __global__ __launch_bounds__(256) void encode_planes_sets_kernel(const int64_t* __restrict__ res, int64_t stride,
                                                                  const uint32_t* __restrict__ labels, int64_t Ns,
                                                                  int64_t nblk, const PlaneSpec* __restrict__ specs,
-                                                                 int nsets, uint32_t* __restrict__ planes) {
+                                                                 uint32_t* __restrict__ planes) {
   const int lane = threadIdx.x & 63;
-  const int64_t g = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t n0 = g * 64;
-  if (n0 >= nblk * PL_BLK) return;
-  const int64_t n = n0 + lane;
-  const bool valid = n < Ns;
-  int64_t r[D];
+  const int64_t seg = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int64_t SEGS_PER_BLK = PL_BLK / (64 * ES_G);
+  if (seg >= nblk * SEGS_PER_BLK) return;
+  const int64_t t = blockIdx.y;
+  const PlaneSpec& spec = specs[t];
+  const int np = spec.n;
+  const int64_t blk = seg / SEGS_PER_BLK;
+  const int64_t wbase = (seg % SEGS_PER_BLK) * (2 * ES_G);   // first plane word of the segment
+  const int64_t nseg = blk * PL_BLK + wbase * 32;            // first node of the segment
+  const uint32_t sh = (lane & 1) * 32;
+  uint32_t w[PL_MAX];
 #pragma unroll
-  for (int d = 0; d < D; ++d) r[d] = valid ? res[d * stride + n] : 0;
-  const uint32_t lab = valid ? labels[n] : 0u;
-  const int64_t blk = n0 / PL_BLK;
-  const int64_t w0 = (n0 % PL_BLK) / 32;
-  for (int t = 0; t < nsets; ++t) {
-    const PlaneSpec& spec = specs[t];
-    uint32_t* out = planes + ((int64_t)t * nblk + blk) * PL_MAX * (64 * PL_R) + w0;
-    const int np = spec.n;
+  for (int p = 0; p < PL_MAX; ++p) w[p] = 0;
+#pragma unroll 2
+  for (int g = 0; g < ES_G; ++g) {
+    const int64_t n = nseg + g * 64 + lane;
+    const bool valid = n < Ns;
+    int64_t r[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) r[d] = valid ? res[d * stride + n] : 0;
+    const uint32_t lab = valid ? labels[n] : 0u;
+    const bool mine = (lane >> 1) == g;                                 // lanes 2g, 2g+1 keep group g
+#pragma unroll
     for (int p = 0; p < PL_MAX; ++p) {
-      bool pr = false;
       if (p < np) {
         const int k = spec.kind[p];
         const int64_t v = spec.val[p];
@@ -505,20 +518,27 @@ __global__ __launch_bounds__(256) void encode_planes_sets_kernel(const int64_t* 
         rv = k == 1 ? r[1] : rv;
         rv = k == 2 ? r[2] : rv;
         rv = k == 3 ? r[3] : rv;
-        pr = valid && (k == 4 ? (lab & (uint32_t)v) == (uint32_t)v : rv >= v);
+        const bool pr = valid && (k == 4 ? (lab & (uint32_t)v) == (uint32_t)v : rv >= v);
+        const uint64_t b = __builtin_amdgcn_ballot_w64(pr);
+        const uint32_t word = (uint32_t)(b >> sh);                  // this lane's half of the ballot
+        w[p] = mine ? word : w[p];
       }
-      const uint64_t b = __builtin_amdgcn_ballot_w64(pr);
-      if (lane < 2) out[p * (64 * PL_R) + lane] = (uint32_t)(lane ? b >> 32 : b);
     }
+  }
+  if (lane < 2 * ES_G) {
+    uint32_t* out = planes + (t * nblk + blk) * PL_MAX * (64 * PL_R) + wbase + lane;
+#pragma unroll
+    for (int p = 0; p < PL_MAX; ++p) out[p * (64 * PL_R)] = w[p];   // planes >= np stay zero
   }
 }
 
 hipError_t launch_encode_planes_sets(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
                                      int64_t Ns, int64_t nblk, const PlaneSpec* specs, int nsets, uint32_t* planes) {
   if (nblk <= 0 || nsets <= 0) return hipSuccess;
-  const int64_t waves = nblk * PL_BLK / 64;
-  hipLaunchKernelGGL(encode_planes_sets_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, res, stride,
-                     labels, Ns, nblk, specs, nsets, planes);
+  if (nsets > 65535) return hipErrorInvalidValue;
+  const int64_t segs = nblk * (PL_BLK / (64 * ES_G));
+  hipLaunchKernelGGL(encode_planes_sets_kernel, dim3((unsigned)((segs + 3) / 4), (unsigned)nsets), dim3(256), 0, s,
+                     res, stride, labels, Ns, nblk, specs, planes);
   return hipGetLastError();
 }
 
