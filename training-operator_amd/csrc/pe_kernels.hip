@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256) void encode_planes_kernel(const int64_t* __res
 // the other, parks word 2g / 2g+1 of plane p in lane 2g / 2g+1 of a per-plane VGPR (one select),
 // then stores each plane's words with one contiguous 4 x 2 ES_G-byte store -- instead of a 2-lane
 // 8-byte store per plane and 64 nodes (the per-set cost of that pattern was ~68 us at 1M nodes).
-constexpr int ES_G = 16;                                  // node groups per wave: 32 words, 128 B
+constexpr int ES_G = 8;                                   // node groups per wave: 16 words, 64 B
 static_assert(PL_BLK % (64 * ES_G) == 0, "segments tile a block");
 __global__ __launch_bounds__(256) void encode_planes_sets_kernel(const int64_t* __restrict__ res, int64_t stride,
                                                                  const uint32_t* __restrict__ labels, int64_t Ns,
@@ -514,12 +514,15 @@ __global__ __launch_bounds__(256) void encode_planes_sets_kernel(const int64_t* 
       if (p < np) {
         const int k = spec.kind[p];
         const int64_t v = spec.val[p];
-        int64_t rv = r[0];
-        rv = k == 1 ? r[1] : rv;
-        rv = k == 2 ? r[2] : rv;
-        rv = k == 3 ? r[3] : rv;
-        const bool pr = valid && (k == 4 ? (lab & (uint32_t)v) == (uint32_t)v : rv >= v);
-        const uint64_t b = __builtin_amdgcn_ballot_w64(pr);
+        bool pr;                                                  // k is wave-uniform: scalar branches
+        switch (k) {
+          case 0: pr = r[0] >= v; break;
+          case 1: pr = r[1] >= v; break;
+          case 2: pr = r[2] >= v; break;
+          case 3: pr = r[3] >= v; break;
+          default: pr = (lab & (uint32_t)v) == (uint32_t)v; break;
+        }
+        const uint64_t b = __builtin_amdgcn_ballot_w64(valid && pr);
         const uint32_t word = (uint32_t)(b >> sh);                  // this lane's half of the ballot
         w[p] = mine ? word : w[p];
       }
