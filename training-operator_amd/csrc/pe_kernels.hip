@@ -497,34 +497,37 @@ __global__ __launch_bounds__(256) void encode_planes_sets_kernel(const int64_t* 
   const int64_t wbase = (seg % SEGS_PER_BLK) * (2 * ES_G);   // first plane word of the segment
   const int64_t nseg = blk * PL_BLK + wbase * 32;            // first node of the segment
   const uint32_t sh = (lane & 1) * 32;
-  uint32_t w[PL_MAX];
+  int64_t r[ES_G][D];                                       // the segment's residuals, loaded once
+  uint32_t lab[ES_G];
+  bool vld[ES_G];
 #pragma unroll
-  for (int p = 0; p < PL_MAX; ++p) w[p] = 0;
-#pragma unroll 2
   for (int g = 0; g < ES_G; ++g) {
     const int64_t n = nseg + g * 64 + lane;
-    const bool valid = n < Ns;
-    int64_t r[D];
+    vld[g] = n < Ns;
 #pragma unroll
-    for (int d = 0; d < D; ++d) r[d] = valid ? res[d * stride + n] : 0;
-    const uint32_t lab = valid ? labels[n] : 0u;
-    const bool mine = (lane >> 1) == g;                                 // lanes 2g, 2g+1 keep group g
+    for (int d = 0; d < D; ++d) r[g][d] = vld[g] ? res[d * stride + n] : 0;
+    lab[g] = vld[g] ? labels[n] : 0u;
+  }
+  uint32_t w[PL_MAX];
 #pragma unroll
-    for (int p = 0; p < PL_MAX; ++p) {
-      if (p < np) {
-        const int k = spec.kind[p];
-        const int64_t v = spec.val[p];
-        bool pr;                                                  // k is wave-uniform: scalar branches
+  for (int p = 0; p < PL_MAX; ++p) {                         // spec read once per plane
+    w[p] = 0;
+    if (p < np) {
+      const int k = spec.kind[p];
+      const int64_t v = spec.val[p];
+#pragma unroll
+      for (int g = 0; g < ES_G; ++g) {
+        bool pr;                                              // k is wave-uniform: scalar branches
         switch (k) {
-          case 0: pr = r[0] >= v; break;
-          case 1: pr = r[1] >= v; break;
-          case 2: pr = r[2] >= v; break;
-          case 3: pr = r[3] >= v; break;
-          default: pr = (lab & (uint32_t)v) == (uint32_t)v; break;
+          case 0: pr = r[g][0] >= v; break;
+          case 1: pr = r[g][1] >= v; break;
+          case 2: pr = r[g][2] >= v; break;
+          case 3: pr = r[g][3] >= v; break;
+          default: pr = (lab[g] & (uint32_t)v) == (uint32_t)v; break;
         }
-        const uint64_t b = __builtin_amdgcn_ballot_w64(valid && pr);
-        const uint32_t word = (uint32_t)(b >> sh);                  // this lane's half of the ballot
-        w[p] = mine ? word : w[p];
+        const uint64_t b = __builtin_amdgcn_ballot_w64(vld[g] && pr);
+        const uint32_t word = (uint32_t)(b >> sh);            // this lane's half of the ballot
+        w[p] = (lane >> 1) == g ? word : w[p];                // lanes 2g, 2g+1 keep group g
       }
     }
   }
