@@ -1,16 +1,20 @@
 #!/usr/bin/env python3
 """Benchmark of the gang-placement hot path (BASELINE.json metric).
 
-A "step" = one fit-mask pass (config 5): every job of the batch evaluated against every node of
-the 1M-node inventory, mask + per-job counts written to HBM, inputs already resident.  The
-inventory is node-sharded over the ranks (north_star); scaling is weak: the batch holds
-100k x n_gpus jobs, so every rank evaluates 100k jobs x 1M nodes worth of pairs (its 1M/N-node
-shard x the whole batch) per step with no collective on the data path.
-`value` = job x node fit evaluations per second for the whole job (all ranks).  The second half
-of the metric, gang placements/s, is measured on the same 1M-node inventory with a 10k-job
-mixed PyTorch/MPI/JAX batch (config 3 mix) and reported in the "greedy" object.
+A "step" = one fit-mask pass (config 5): every job of the 100k-job batch evaluated against every
+node of the 1M-node inventory, mask + per-job counts written to HBM, inputs already resident.  The
+inventory is node-sharded over the ranks (north_star) and the batch is FIXED (strong scaling, the
+BASELINE cfg5 "1M nodes x 100k jobs at 1/2/4/8 GPUs"): every rank evaluates the whole batch against
+its 1M/N-node shard with no collective on the data path.  `value` = job x node fit evaluations per
+second for the whole job (all ranks).  A weak-scaling line (batch 100k x N) is reported beside it
+at N > 1.  The second half of the metric, gang placements/s, is measured on the same 1M-node
+inventory with a 10k-job mixed PyTorch/MPI/JAX batch (config 3 mix) and reported in "greedy".
 
-    python bench.py [--gpus N --steps K --warmup W]          (N>1: one rank per GPU, torchrun)
+    python bench.py [--gpus N --steps K --warmup W]
+
+With --gpus N > 1 and no WORLD_SIZE in the environment this process starts the N ranks itself
+(torch.distributed.run, 127.0.0.1) and exits with their status; it never loads the engine or
+touches a GPU.  Under torchrun (WORLD_SIZE set) --gpus must equal WORLD_SIZE.
 """
 from __future__ import annotations
 
@@ -18,26 +22,79 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-for _p in (ROOT, os.path.join(ROOT, "training-operator_amd")):
-    if _p not in sys.path:
-        sys.path.insert(0, _p)
-
-import numpy as np  # noqa: E402
-
-from placement import Engine, comm_id, synth  # noqa: E402
+PROFILES = os.path.join(ROOT, "profiles")
 
 METRIC = "job×node fit evals/sec + gang placements/sec, 1M-node inventory, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # chip-wide integer VALU issue ceiling, wave-instructions/s: profiles/r1_ubench_valu.txt
 # (v_add_u32 / v_addc_co at 8 waves per SIMD: 4.24 cycles per wave-instruction per SIMD, 256 CUs x 4 SIMDs)
 VALU_ISSUE_CEILING = 5.79e11
-KERNEL_OF_PATH = {"planes": "pe::fit_mask_planes_rows_kernel", "planes-blocks": "pe::fit_mask_planes_kernel", "coded-therm": "pe::fit_mask_coded_kernel", "coded-swar": "pe::fit_mask_coded_kernel",
-                  "i32": "pe::fit_mask_kernel", "i64": "pe::fit_mask_kernel"}
-PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+# per fit path: the kernels of one fit step (the first is the dominant one, the roofline's kernel)
+STEP_KERNELS = {
+    "planes": ("pe::fit_mask_planes_rows_kernel", "pe::encode_planes_kernel"),
+    "planes-sets": ("pe::fit_mask_planes_sets_kernel", "pe::encode_planes_sets_kernel"),
+    "planes-blocks": ("pe::fit_mask_planes_kernel", "pe::encode_planes_kernel"),
+    "lds": ("pe::fit_mask_lds_kernel", "pe::node_ranks_kernel"),
+    "coded-therm": ("pe::fit_mask_coded_kernel", "pe::encode_nodes_kernel"),
+    "coded-swar": ("pe::fit_mask_coded_kernel", "pe::encode_nodes_kernel"),
+    "i32": ("pe::fit_mask_kernel", "pe::compress_res_kernel"),
+    "i64": ("pe::fit_mask_kernel",),
+}
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--nodes", type=int, default=1_000_000)
+    ap.add_argument("--fit-jobs", type=int, default=100_000)
+    ap.add_argument("--greedy-jobs", type=int, default=10_000)
+    ap.add_argument("--greedy-steps", type=int, default=2)
+    ap.add_argument("--topk", type=int, default=0)
+    ap.add_argument("--window-groups", type=int, default=0)
+    ap.add_argument("--window-pods", type=int, default=0)
+    ap.add_argument("--no-greedy", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the cfg2-4 greedy lines and the extra fit lines")
+    ap.add_argument("--cpu-sample-jobs", type=int, default=20000)
+    ap.add_argument("--cpu-greedy-jobs", type=int, default=1000)
+    ap.add_argument("--agg-jobs", type=int, default=1_000_000)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="strong (default): the 100k-job batch is fixed, the nodes are sharded; "
+                         "weak: batch = fit-jobs x n_gpus (fixed per-rank work)")
+    ap.add_argument("--fit-path-mask", type=int, default=0, help="pe_config.fit_path_mask (0 = every kernel)")
+    ap.add_argument("--greedy-flags", type=int, default=0,
+                    help="pe_config.greedy_flags (bit0: sequential windows, bit1: full scan instead of the sorted walk)")
+    ap.add_argument("--resort-nodes", type=int, default=0, help="pe_config.resort_nodes (0 = default)")
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(args, argv):
+    """The torchrun command line of the N-rank run (one rank per GPU, 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_launch(args, argv, run=subprocess.call):
+    """Parent side of `--gpus N` without torchrun: start the N ranks as a child process and return
+    its exit status; None when this process is a rank itself (or N == 1).  Imports nothing that
+    loads the engine or initialises a GPU."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    return run(launch_cmd(args, argv))
 
 
 class HipEvents:
@@ -73,39 +130,52 @@ def fit_bytes(n_nodes: int, n_jobs: int) -> int:
     return n_nodes * 36 + n_jobs * 36 + n_jobs * ((n_nodes + 63) // 64) * 8 + n_jobs * 8
 
 
-def profiled_counter(kernel: str, n_nodes: int, n_jobs: int, counter: str):
-    """One PMC counter per launch of `kernel` from the committed profile (profiles/LATEST), if it was
-    taken on this same workload; else None."""
-    try:
-        tag = open(os.path.join(PROFILES, "LATEST")).read().strip()
-        summ = json.load(open(os.path.join(PROFILES, tag, "summary.json")))
-    except (OSError, ValueError):
-        return None
-    wl = summ.get("workload", {})
-    if wl.get("nodes") != n_nodes or wl.get("jobs") != n_jobs:
-        return None
-    for k, p in summ.get("pmc", {}).items():
-        if k.startswith(kernel) and counter in p:
-            return p[counter]
-    return None
+def agg_bytes(job_group_off, group_cont_off) -> int:
+    """SURVEY.md 8(d) aggregation bytes: per job G*(4 + 32 + 1) + 32 + 4 + 1 + 1, with the
+    container records (32 + 1 B each) counted as they are read."""
+    J = len(job_group_off) - 1
+    G = int(job_group_off[-1])
+    C = int(group_cont_off[-1])
+    return G * (4 + 4) + C * (32 + 1) + J * (4 + 4 + 32 + 1 + 4 + 1)
 
 
-def profiled_traffic(kernel: str, n_nodes: int, n_jobs: int):
-    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/LATEST names the
-    directory; FETCH_SIZE doubled per MI355X_MICROARCH.md, + WRITE_SIZE), if they were taken on this
-    same workload.  None when no matching profile exists."""
+def profile_summary():
+    """The committed profile profiles/LATEST names (summary.json), or None."""
     try:
         tag = open(os.path.join(PROFILES, "LATEST")).read().strip()
-        summ = json.load(open(os.path.join(PROFILES, tag, "summary.json")))
+        return tag, json.load(open(os.path.join(PROFILES, tag, "summary.json")))
     except (OSError, ValueError):
         return None, None
+
+
+def profile_check(path: str, n_nodes: int, n_jobs: int, kern_ms: float, src_hash: str):
+    """Compare the committed profile with this run: same engine sources, same workload, and a fit
+    step (sum of the step kernels' average durations) within 5 % of this run's hipEvent time.
+    Returns the roofline fields taken from it (traffic and counters are null unless all hold)."""
+    tag, summ = profile_summary()
+    out = {"profile": None, "profile_kernel_ms": None, "profile_step_ms": None, "profile_matches": False,
+           "traffic": None, "traffic_source": None, "pmc": {}}
+    if summ is None:
+        return out
+    out["profile"] = f"profiles/{tag}/summary.json"
+    kernels = summ.get("kernels", {})
+    names = STEP_KERNELS[path]
+    if names[0] not in kernels:
+        return out
+    out["profile_kernel_ms"] = kernels[names[0]]["avg_ns"] / 1e6
+    out["profile_step_ms"] = sum(kernels[k]["avg_ns"] for k in names if k in kernels) / 1e6
     wl = summ.get("workload", {})
-    if wl.get("nodes") != n_nodes or wl.get("jobs") != n_jobs:
-        return None, None
-    for k, p in summ.get("pmc", {}).items():
-        if k.startswith(kernel) and "hbm_traffic_bytes" in p:
-            return p["hbm_traffic_bytes"], f"profiles/{tag}/summary.json (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)"
-    return None, None
+    same = (summ.get("source_hash") == src_hash and wl.get("nodes") == n_nodes and wl.get("jobs") == n_jobs
+            and abs(out["profile_step_ms"] - kern_ms) <= 0.05 * kern_ms)
+    out["profile_matches"] = bool(same)
+    if same:
+        p = summ.get("pmc", {}).get(names[0], {})
+        out["pmc"] = p
+        if "hbm_traffic_bytes" in p:
+            out["traffic"] = p["hbm_traffic_bytes"]
+            out["traffic_source"] = (f"profiles/{tag}/summary.json (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, "
+                                     f"per launch of {names[0]})")
+    return out
 
 
 def _count(n: int) -> str:
@@ -123,33 +193,45 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--nodes", type=int, default=1_000_000)
-    ap.add_argument("--fit-jobs", type=int, default=100_000)
-    ap.add_argument("--greedy-jobs", type=int, default=10_000)
-    ap.add_argument("--greedy-steps", type=int, default=2)
-    ap.add_argument("--topk", type=int, default=0)
-    ap.add_argument("--window-groups", type=int, default=0)
-    ap.add_argument("--window-pods", type=int, default=0)
-    ap.add_argument("--no-greedy", action="store_true")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-configs", action="store_true", help="skip the cfg2-4 greedy lines")
-    ap.add_argument("--cpu-sample-jobs", type=int, default=20000)
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="weak: batch = fit-jobs x n_gpus (fixed per-rank work); strong: batch = fit-jobs")
-    ap.add_argument("--fit-path-mask", type=int, default=0, help="pe_config.fit_path_mask (0 = every kernel)")
-    ap.add_argument("--greedy-flags", type=int, default=0,
-                    help="pe_config.greedy_flags (bit0: sequential windows, bit1: full scan instead of the sorted walk)")
-    ap.add_argument("--resort-nodes", type=int, default=0, help="pe_config.resort_nodes (0 = default)")
-    args = ap.parse_args()
+def cpu_share() -> int:
+    """Host threads this process may use: the box's stated CPU share (OMP_NUM_THREADS, 16 per GPU
+    on the GPU pool), else the affinity mask.  os.cpu_count() shows the whole machine there."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def fit_path_of(stats: dict, before: dict, blocks: bool) -> str:
+    d = {k: stats[k] - before.get(k, 0) for k in stats if isinstance(stats[k], int)}
+    if d.get("fit_runs_lds", 0):
+        return "lds"
+    if d.get("fit_runs_planes", 0):
+        return "planes-blocks" if blocks else ("planes-sets" if d.get("fit_runs_sets", 0) else "planes")
+    if d.get("fit_runs_coded", 0):
+        return "coded-therm" if d.get("fit_runs_therm", 0) else "coded-swar"
+    return "i32" if d.get("fit_runs_i32", 0) else "i64"
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    rc = maybe_launch(args, argv)
+    if rc is not None:
+        sys.exit(rc)
+
+    sys.path[:0] = [p for p in (ROOT, os.path.join(ROOT, "training-operator_amd"), PROFILES) if p not in sys.path]
+    import numpy as np
+
+    from placement import Engine, comm_id, synth
+    from provenance import source_hash
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     dist = None
     cid, exchange, device = None, None, local
     host_exchange = os.environ.get("PE_BENCH_EXCHANGE", "rccl") == "host"
@@ -194,6 +276,11 @@ def main():
             t = torch.tensor([x], dtype=torch.int64, device=tdev)
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
             return int(t.item())
+
+        def allgather(x):
+            parts = [None] * world
+            dist.all_gather_object(parts, x)
+            return parts
     else:
         def new_comm():
             return None
@@ -207,6 +294,9 @@ def main():
         def allsum(x):
             return x
 
+        def allgather(x):
+            return [x]
+
     N = args.nodes
     J = args.fit_jobs * (world if args.scaling == "weak" else 1)
     inv = synth.make_inventory(N, synth.SEED["cfg5"], gpu_frac=0.2)
@@ -217,44 +307,44 @@ def main():
     b, e = eng.shard_range()
     Ns = e - b
     req, need = synth.make_fit_jobs(J, synth.SEED["cfg5"])
-    eng.jobs_upload(req, need)
     stream = eng.stream()
     ev = HipEvents()
+    blocks = bool(args.fit_path_mask & 32)
 
-    for _ in range(args.warmup):
-        eng.fit_mask_run()
-    eng.synchronize()
-    feasible = allsum(int(eng.fit_counts().sum()))
+    def time_fit(rq, nd, steps, warmup, label):
+        """Upload a batch, warm up, time `steps` fit steps (barrier + sync on both sides, max over
+        ranks).  Returns (wall seconds, hipEvent ms per step on this rank, fit path, feasible pairs)."""
+        st0 = eng.stats()
+        eng.jobs_upload(rq, nd)
+        for _ in range(warmup):
+            eng.fit_mask_run()
+        eng.synchronize()
+        feas = allsum(int(eng.fit_counts().sum()))
+        e0, e1 = ev.create(), ev.create()
+        barrier()
+        eng.synchronize()
+        t0 = time.perf_counter()
+        ev.record(e0, stream)
+        for _ in range(steps):
+            eng.fit_mask_run()
+        ev.record(e1, stream)
+        eng.synchronize()
+        barrier()
+        wall = allmax(time.perf_counter() - t0)
+        return wall, ev.elapsed_ms(e0, e1) / steps, fit_path_of(eng.stats(), st0, blocks), feas
 
-    e0, e1 = ev.create(), ev.create()
-    barrier()
-    eng.synchronize()
-    t0 = time.perf_counter()
-    ev.record(e0, stream)
-    for _ in range(args.steps):
-        eng.fit_mask_run()
-    ev.record(e1, stream)
-    eng.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = allmax(t1 - t0)
-    kern_ms = ev.elapsed_ms(e0, e1) / args.steps
+    elapsed, kern_ms, fit_path, feasible = time_fit(req, need, args.steps, args.warmup, "headline")
     value = float(N) * J * args.steps / elapsed
-    st0 = eng.stats()
-    fit_path = (("planes-blocks" if args.fit_path_mask & 32 else "planes") if st0["fit_runs_planes"] else
-                (("coded-therm" if st0["fit_runs_therm"] else "coded-swar") if st0["fit_runs_coded"] else
-                 ("i32" if st0["fit_runs_i32"] else "i64")))
     alg = fit_bytes(Ns, J)
     achieved = alg / (kern_ms * 1e-3) / 1e9
-    kname = KERNEL_OF_PATH[fit_path]
-    traffic, tsrc = profiled_traffic(kname, Ns, J)
+    kname = STEP_KERNELS[fit_path][0]
+    src_hash = source_hash(ROOT)
+    prof = profile_check(fit_path, Ns, J, kern_ms, src_hash)
     valu_frac = None
-    if fit_path == "coded-therm":   # 3 VALU per (job, 64 nodes): or, add_co, addc
-        valu_frac = 3.0 * (-(-J // 64) * 64) * (Ns / 64.0) / (kern_ms * 1e-3) / VALU_ISSUE_CEILING
-    else:                           # PMC SQ_INSTS_VALU per launch (committed profile, same workload)
-        insts = profiled_counter(kname, Ns, J, "SQ_INSTS_VALU")
-        if insts is not None:
-            valu_frac = insts / (kern_ms * 1e-3) / VALU_ISSUE_CEILING
+    if "SQ_INSTS_VALU" in prof["pmc"]:   # PMC SQ_INSTS_VALU per launch (committed profile, same build)
+        valu_frac = prof["pmc"]["SQ_INSTS_VALU"] / (kern_ms * 1e-3) / VALU_ISSUE_CEILING
+    shards = allgather(Ns)
+    rccl = eng.comm_ranks()
 
     out = {
         "metric": METRIC, "value": value, "unit": "job*node fit evals/s", "n_gpus": world, "steps": args.steps,
@@ -263,45 +353,97 @@ def main():
         "config": {"workload": f"cfg5: fit bitmask, {_count(N)}-node inventory x {_count(args.fit_jobs)} jobs"
                                f"{' per GPU' if args.scaling == 'weak' else ''} ({J} jobs in all), device-resident",
                    "nodes": N, "jobs": J, "jobs_per_gpu": J // world if args.scaling == "weak" else J,
-                   "shard_nodes": Ns,
-                   "parallelism": f"node-shard x{world}" + (" (host exchange rehearsal)" if host_exchange and world > 1 else ""), "feasible_pairs": feasible},
+                   "shard_nodes": Ns, "shard_nodes_per_rank": shards, "rccl_ranks": rccl,
+                   "parallelism": f"node-shard x{world}" + (" (host exchange rehearsal)" if host_exchange and world > 1
+                                                            else ""),
+                   "feasible_pairs": feasible},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": tsrc, "kernel_ms": kern_ms, "alg_bytes_per_launch": alg,
-                     "fit_path": fit_path, "valu_issue_frac": valu_frac,
-                     "note": "kernel_ms = hipEvent time on the engine stream / fit_mask_run (one count memset, "
-                             "the node encode and the fit kernel) on this rank's shard; achieved = algorithmic "
-                             "bytes (shard nodes x 36 + jobs x 44 + jobs x ceil(shard/64) x 8) / kernel_ms; the "
-                             "fit kernel is bound by its mask stores (HBM write)"},
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": prof["traffic"],
+                     "traffic_source": prof["traffic_source"], "kernel_ms": kern_ms,
+                     "profile_kernel_ms": prof["profile_kernel_ms"], "profile_step_ms": prof["profile_step_ms"],
+                     "profile": prof["profile"], "profile_matches": prof["profile_matches"],
+                     "source_hash": src_hash, "alg_bytes_per_launch": alg, "fit_path": fit_path,
+                     "valu_issue_frac": valu_frac,
+                     "note": "kernel_ms = hipEvent time on the engine stream / fit step (count memset, node encode, fit "
+                             "kernel) on this rank's shard; achieved = algorithmic bytes (shard nodes x 36 + jobs x 44 + "
+                             "jobs x ceil(shard/64) x 8) / kernel_ms; traffic / valu_issue_frac come from the committed "
+                             "profile only when it was taken on the same engine sources and workload and its step time "
+                             "agrees with kernel_ms within 5 % (profile_matches)"},
     }
 
+    if world > 1:
+        # weak scaling beside the strong headline: batch 100k x N, every rank the whole batch
+        Jw = args.fit_jobs * world
+        wreq, wneed = synth.make_fit_jobs(Jw, synth.SEED["cfg5"])
+        wt, wms, wpath, _ = time_fit(wreq, wneed, args.steps, 1, "weak")
+        out["fit_weak_scaling"] = {"workload": f"cfg5 batch of {Jw} jobs (100k per GPU) x {_count(N)} nodes",
+                                   "jobs": Jw, "value": float(N) * Jw * args.steps / wt,
+                                   "ms_per_step": wt / args.steps * 1e3, "kernel_ms": wms, "fit_path": wpath}
+
     if not args.no_configs:
-        # the same step on a batch with 400 distinct cpu requests (more than one plane set holds):
-        # plane sets, all swept in one launch; informational, not the headline value
+        # end-to-end fit batch: host planning + H2D (pe_jobs_upload) + fit step + counts D2H
+        reps = []
+        for _ in range(3):
+            eng.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            eng.jobs_upload(req, need)
+            eng.fit_mask_run()
+            eng.fit_counts()
+            barrier()
+            reps.append(allmax(time.perf_counter() - t0))
+        t_up = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            eng.jobs_upload(req, need)
+            t_up.append(time.perf_counter() - t0)
+        e2e = float(np.median(reps))
+        out["fit_end_to_end"] = {"workload": "headline batch incl. pe_jobs_upload (host planning + H2D), the fit step "
+                                             "and the per-job counts D2H", "ms_per_batch": e2e * 1e3,
+                                 "upload_ms": float(np.median(t_up)) * 1e3,
+                                 "evals_per_s": float(N) * J / e2e}
+        # high-cardinality batches (not the headline): 400 distinct cpu values; unique memory per job
+        # with 1000 cpu and 100 ephemeral values; unique cpu, memory and ephemeral per job
         mreq = req.copy()
         mreq[:, 0] = 250 * (1 + np.arange(J) % 400)
-        eng.jobs_upload(mreq, need)
-        eng.fit_mask_run()
-        eng.synchronize()
-        m0, m1 = ev.create(), ev.create()
-        ev.record(m0, stream)
-        for _ in range(args.steps):
-            eng.fit_mask_run()
-        ev.record(m1, stream)
-        eng.synchronize()
-        mms = ev.elapsed_ms(m0, m1) / args.steps
-        out["fit_many_values"] = {"workload": "cfg5 batch with 400 distinct cpu requests (plane sets)",
-                                  "kernel_ms": mms, "evals_per_s_this_rank": float(Ns) * J / (mms * 1e-3),
-                                  "fit_path": "planes" if eng.stats()["fit_runs_planes"] > st0["fit_runs_planes"]
-                                  else "fallback"}
+        cases = [("fit_many_values", "cfg5 batch with 400 distinct cpu requests", mreq, need)]
+        wreq, wneed = synth.make_fit_jobs_worst(J, synth.SEED["cfg5"], (1,))
+        cases.append(("fit_worst_case", "cfg5 batch, memory unique per job, cpu over 1000 and ephemeral over 100 "
+                                        "values", wreq, wneed))
+        areq, aneed = synth.make_fit_jobs_worst(J, synth.SEED["cfg5"], (0, 1, 3))
+        cases.append(("fit_adversarial", "cfg5 batch, cpu, memory and ephemeral each unique per job", areq, aneed))
+        for key, what, rq, nd in cases:
+            wt, wms, wpath, wfeas = time_fit(rq, nd, max(2, args.steps // 2), 1, key)
+            pairs = {f"distinct_{n}": int(len(np.unique(rq[:, d]))) for d, n in enumerate(("cpu", "mem", "gpu", "eph"))}
+            out[key] = {"workload": what, **pairs, "kernel_ms": wms, "ms_per_step": wt / max(2, args.steps // 2) * 1e3,
+                        "vs_headline_step": wms / kern_ms, "fit_path": wpath, "kernel": STEP_KERNELS[wpath][0],
+                        "frac": fit_bytes(Ns, J) / (wms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "evals_per_s": float(N) * J / wt * max(2, args.steps // 2), "feasible_pairs": wfeas}
         eng.jobs_upload(req, need)                  # back to the headline batch (counts for the CPU check)
         eng.fit_mask_run()
         eng.synchronize()
+
+        # PodGroup MinResources aggregation (v1 CalcPGMinResources over a batch), end to end per call
+        agg = synth.make_pg_batch(args.agg_jobs, synth.SEED["cfg3"])
+        eng.pg_min_resources(1, *agg)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            eng.pg_min_resources(1, *agg)
+            ts.append(time.perf_counter() - t0)
+        at = float(np.median(ts))
+        ab = agg_bytes(agg[0], agg[3])
+        out["aggregation"] = {"workload": f"{args.agg_jobs} v1 PyTorchJob-like jobs (Master 1 + Worker 0-63, 1-2 "
+                                          "containers), CalcPGMinResources on the GPU incl. H2D/D2H",
+                              "jobs_per_s": args.agg_jobs / at, "ms_per_call": at * 1e3, "alg_bytes": ab,
+                              "achieved_gbs": ab / at / 1e9,
+                              "note": "PCIe-inclusive (the ABI hands over host buffers): bound by the H2D/D2H copies"}
 
     if not args.no_greedy:
         batch = synth.make_jobs(args.greedy_jobs, synth.SEED["cfg3"], "mixed")
         eng.reset_residuals()
         eng.place_batch(batch)                      # warm-up pass (allocations, code paths)
+        eng.reset_stats()
         times = []
         placed = 0
         for _ in range(args.greedy_steps):
@@ -315,15 +457,38 @@ def main():
             placed = int((st == 0).sum())
         s = eng.stats()
         gt = float(np.median(times))
+        gs = args.greedy_steps
         out["greedy"] = {"workload": "cfg3 mix on the 1M-node inventory: 10k jobs (50% PyTorch, 25% MPI, 25% JAX)",
                          "jobs": args.greedy_jobs, "pods": batch.n_pods, "jobs_placed": placed,
                          "gang_placements_per_s": args.greedy_jobs / gt, "ms_per_batch": gt * 1e3,
-                         "windows_per_batch": s["windows"] / (args.greedy_steps + 1),
-                         "rescans_per_batch": s["rescans"] / (args.greedy_steps + 1),
-                         "scan_evals_per_s": s["scan_evals"] / (args.greedy_steps + 1) * world / gt,
-                         "device_wait_ms_per_batch": s["greedy_wait_ms"] / (args.greedy_steps + 1),
-                         "host_resolve_ms_per_batch": s["greedy_host_ms"] / (args.greedy_steps + 1),
+                         "windows_per_batch": s["windows"] / gs, "rescans_per_batch": s["rescans"] / gs,
+                         "device_wait_ms_per_batch": s["greedy_wait_ms"] / gs,
+                         "host_resolve_ms_per_batch": s["greedy_host_ms"] / gs,
                          "naive_pod_x_node_evals_per_s": batch.n_pods * float(N) / gt}
+        if s["walk_groups"] > 0:
+            # greedy roofline: one more (untimed) pass with hipEvents around every walk launch; bytes the
+            # walk kernel reads: per group the round summaries (first key 8 B, max residual 32 B, label OR
+            # 4 B per round), the overlay entries (state 32 + 4 B, id 4 B) and the visited sorted entries
+            # (key 8 B, residuals 32 B, labels 4 B)
+            eng.reset_residuals()
+            eng.reset_stats()
+            os.environ["PE_WALK_EVENTS"] = "1"
+            try:
+                eng.place_batch(batch)
+            finally:
+                del os.environ["PE_WALK_EVENTS"]
+            w = eng.stats()
+            walked = w["walk_prepass"] * 44 + w["walk_overlay"] * 40 + w["walk_rounds"] * 1024 * 44
+            wms = w["walk_ms"]
+            out["greedy"]["roofline"] = {
+                "bound": "hbm", "kernel": "pe::walk_kernel", "bytes_per_batch": walked, "walk_ms_per_batch": wms,
+                "walk_launches": w["windows"], "rounds_per_group": w["walk_rounds"] / max(1, w["walk_groups"]),
+                "overlay_per_group": w["walk_overlay"] / max(1, w["walk_groups"]),
+                "achieved": walked / (wms * 1e-3) / 1e9 if wms > 0 else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": walked / (wms * 1e-3) / 1e9 / HBM_PEAK_GBS if wms > 0 else None,
+                "host_ms_per_batch": w["greedy_host_ms"], "device_wait_ms_per_batch": w["greedy_wait_ms"],
+                "note": "latency-bound, not bandwidth-bound: one 1024-thread block per group walks 1-7 rounds of "
+                        "1024 sorted nodes; walk time = hipEvents around every walk launch (PE_WALK_EVENTS pass)"}
 
     if not args.no_configs:
         # BASELINE.json configs 2-4 at their own sizes (greedy best-fit, all-or-nothing); every rank
@@ -341,6 +506,7 @@ def main():
                         greedy_flags=args.greedy_flags, resort_nodes=args.resort_nodes)
             ce.load_nodes(cinv.cap, cinv.used, cinv.labels, cinv.island)
             ce.place_batch(cb)                       # warm-up
+            ce.reset_stats()
             ts = []
             for _ in range(3):
                 ce.reset_residuals()
@@ -354,13 +520,16 @@ def main():
             cs = ce.stats()
             out["configs"][cfg] = {"workload": what, "nodes": n_nodes, "jobs": n_jobs, "pods": cb.n_pods,
                                    "jobs_placed": int((cst == 0).sum()), "gang_placements_per_s": n_jobs / ct,
-                                   "ms_per_batch": ct * 1e3, "windows_per_batch": cs["windows"] / 4.0,
-                                   "rescans_per_batch": cs["rescans"] / 4.0}
+                                   "ms_per_batch": ct * 1e3, "windows_per_batch": cs["windows"] / 3.0,
+                                   "rescans_per_batch": cs["rescans"] / 3.0,
+                                   "host_resolve_ms_per_batch": cs["greedy_host_ms"] / 3.0,
+                                   "device_wait_ms_per_batch": cs["greedy_wait_ms"] / 3.0}
             ce.close()
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle
-        nthreads = max(1, min(16, os.cpu_count() or 1))
+        from placement import Resolver
+        nthreads = cpu_share()
         js = min(args.cpu_sample_jobs, J)
         res = inv.residual()
         oracle.fit_mask(res, inv.labels, req[:16], need[:16], want_mask=False, nthreads=nthreads)  # warm-up
@@ -370,20 +539,40 @@ def main():
             _, ocounts = oracle.fit_mask(res, inv.labels, req[:js], need[:js], want_mask=True, nthreads=nthreads)
             reps.append(time.perf_counter() - c0)
         ct = float(np.median(reps))
-        gpu_counts = eng.fit_counts()[:js] if world == 1 else None
+        c0 = time.perf_counter()
+        oracle.fit_mask(res, inv.labels, req[:200], need[:200], want_mask=True, nthreads=1)
+        c1 = time.perf_counter() - c0
+        gpu_counts = eng.fit_counts()[:js]
         out["cpu_baseline"] = {"value": js * float(N) / ct, "unit": "job*node fit evals/s", "cores": nthreads,
                                "kind": "port", "sample": f"C oracle (oracle/oracle.c, OpenMP x{nthreads}, "
-                               f"{cpu_model()}) on the first {js} jobs x all {N} nodes, median of 3; "
+                               f"{cpu_model()}) on the first {js} jobs x all {N} nodes, mask written, median of 3; "
                                "the Go reference cannot be timed (no Go toolchain, SURVEY.md 0.3)",
+                               "single_thread_value": 200 * float(N) / c1, "nproc": os.cpu_count(),
+                               "affinity_cpus": len(os.sched_getaffinity(0)),
+                               "threads_note": "threads = this box's CPU share (OMP_NUM_THREADS, else the affinity "
+                                               "mask); nproc counts the whole machine, shared with other GPUs' jobs",
                                "counts_match_gpu": bool(np.array_equal(ocounts, gpu_counts))}
         if "greedy" in out:
-            gb = synth.make_jobs(40, synth.SEED["cfg3"], "mixed")
+            # the same algorithm on the CPU: windowed protocol (K = 256, 64 groups / 1024 pods per window),
+            # each window's candidate lists built by the C oracle over all 1M nodes (OpenMP over groups),
+            # resolved by the product's host resolver -- on the first jobs of the same batch
+            gj = args.cpu_greedy_jobs
+            full = synth.make_jobs(args.greedy_jobs, synth.SEED["cfg3"], "mixed")
+            gb = synth.make_jobs(gj, synth.SEED["cfg3"], "mixed")
             c0 = time.perf_counter()
-            oracle.place_greedy(res, inv.labels, gb.job_group_off, gb.priority, gb.group_count, gb.group_req,
-                                gb.group_need, nthreads=nthreads)
+            _, gst, _, gw = oracle.place_greedy_windowed(Resolver, res, inv.labels, gb, K=256, nthreads=nthreads)
             ct = time.perf_counter() - c0
-            out["cpu_baseline"]["greedy"] = {"gang_placements_per_s": 40 / ct, "cores": nthreads,
-                                             "sample": "naive per-pod argmin oracle, first 40 jobs of the batch"}
+            c0 = time.perf_counter()
+            oracle.place_greedy(res, inv.labels, gb.job_group_off[:41], gb.priority[:40], gb.group_count,
+                                gb.group_req, gb.group_need, nthreads=nthreads)
+            cn = time.perf_counter() - c0
+            out["cpu_baseline"]["greedy"] = {
+                "gang_placements_per_s": gj / ct, "cores": nthreads, "windows": gw,
+                "sample": f"windowed protocol on the CPU (oracle window scan x{nthreads} threads + the host resolver), "
+                          f"first {gj} jobs of the cfg3-mix batch ({full.n_jobs} in the GPU line) on the 1M-node "
+                          "inventory", "jobs_placed": int((gst == 0).sum()),
+                "naive_gang_placements_per_s": 40 / cn,
+                "naive_sample": "naive per-pod argmin over all nodes (oracle.c orc_place_greedy), first 40 jobs"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

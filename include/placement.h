@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 2
+#define PE_ABI_VERSION 3
 #define PE_DIMS 4
 #define PE_COMM_ID_BYTES 128
 #define PE_MAX_NODES (1LL << 24) /* node ids live in the low 24 bits of the best-fit key */
@@ -125,6 +125,13 @@ typedef struct {
   int64_t fit_runs_therm; /* ... of which used the thermometer code (3 VALU per 64 evaluations) */
   int64_t fit_runs_planes; /* fit-mask launches on the bit-plane path (5-way AND per 32 nodes) */
   int64_t resorts;       /* sorted-walk index builds (greedy) */
+  int64_t fit_runs_lds;  /* fit-mask launches on the LDS digit-plane path (any cardinality) */
+  int64_t fit_runs_sets; /* ... bit-plane launches that swept more than one plane set */
+  int64_t walk_rounds;   /* greedy sorted walk: 1024-entry rounds walked, summed over groups */
+  int64_t walk_overlay;  /* greedy sorted walk: overlay entries evaluated, summed over groups */
+  int64_t walk_groups;   /* greedy sorted walk: group blocks launched */
+  int64_t walk_prepass;  /* greedy sorted walk: round summaries read (rounds x groups) */
+  double walk_ms;        /* walk kernel time by hipEvents, only when PE_WALK_EVENTS=1 in the environment */
 } pe_stats;
 
 int pe_abi_version(void);
@@ -155,6 +162,9 @@ enum { PE_NODE_SET = 0, PE_NODE_REMOVE = 1 };
 int pe_update_nodes(pe_ctx* ctx, int64_t n, const int64_t* slots, const uint8_t* op, const int64_t* cap /*[n][4]*/,
                     const int64_t* used /*[n][4]*/, const uint32_t* labels, const int32_t* island);
 int pe_shard_range(const pe_ctx* ctx, int64_t* begin, int64_t* end);
+/* Ranks of the context's RCCL communicator (ncclCommCount); 0 when the shards exchange through the
+ * host callback, or an unsharded context was created without a comm_id. */
+int pe_comm_ranks(const pe_ctx* ctx, int32_t* nranks);
 int pe_read_residuals(pe_ctx* ctx, int64_t* res_out /* [4][end-begin] of this shard */);
 
 /* Batched PodGroup MinResources (one job per lane on the GPU).

@@ -47,6 +47,8 @@ def lib():
         L.orc_key.argtypes = [P, ctypes.c_uint32, P, ctypes.c_uint32, ctypes.c_uint64]
         L.orc_key.restype = ctypes.c_uint64
         L.orc_num_threads.restype = ctypes.c_int
+        L.orc_window_cands.argtypes = [i64, P, P, i32, P, P, i32, P, ctypes.c_int]
+        L.orc_window_cands.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -110,6 +112,36 @@ def key(res4, labels, req4, need, gid):
     r = _c(res4, np.int64)
     q = _c(req4, np.int64)
     return int(lib().orc_key(_p(r), int(labels), _p(q), int(need), int(gid)))
+
+
+def window_cands(res, labels, group_req, group_need, K: int, nthreads=0) -> bytes:
+    """One scan window on the CPU: per group the K best keys + limit, pe_resolver_* blob layout."""
+    res = _c(res, np.int64)
+    req = _c(group_req, np.int64).reshape(-1, 4)
+    G = req.shape[0]
+    blob = np.zeros(G * (16 + 48 * K), dtype=np.uint8)
+    rc = lib().orc_window_cands(res.shape[1], _p(res), _p(_c(labels, np.uint32)), G, _p(req),
+                                _p(_c(group_need, np.uint32)), int(K), _p(blob), int(nthreads))
+    assert rc == 0
+    return blob.tobytes()
+
+
+def place_greedy_windowed(Resolver, res, labels, batch, K=256, max_groups=64, max_pods=1024, nthreads=0):
+    """The engine's windowed greedy protocol with the scan done by window_cands on the CPU and the
+    resolution by the product's host resolver (pe_resolver_*): the same algorithm as
+    pe_place_greedy, no device.  Returns (pods, status, residual_after, windows)."""
+    res = np.array(res, dtype=np.int64, copy=True)
+    R = Resolver(batch.job_group_off, batch.priority, batch.group_count, batch.group_req, batch.group_need)
+    windows = 0
+    while not R.done():
+        groups = R.next_window(max_groups, max_pods)
+        blob = window_cands(res, labels, batch.group_req[groups], batch.group_need[groups], K, nthreads)
+        upd, _ = R.resolve(groups, blob, 1, K)
+        for row in upd:
+            res[:, int(row[0])] = row[1:]
+        windows += 1
+    pods, st = R.results()
+    return pods, st, res, windows
 
 
 def num_threads() -> int:

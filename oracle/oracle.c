@@ -293,6 +293,76 @@ int64_t orc_place_greedy(int64_t N, int64_t* res, const uint32_t* labels, int64_
   return placed;
 }
 
+/* One greedy scan window restated on the CPU (the windowed protocol's device half, SURVEY.md sec. 7
+ * step 7): for each of the n_groups requests, the K smallest keys over all N nodes and the limit
+ * (the (K+1)-th smallest key, UINT64_MAX when at most K nodes fit), written in the pe_resolver_*
+ * blob layout of include/placement.h (16-B header {i32 n, i32 flags, u64 limit} + K 48-B records
+ * {u64 key, i64 res[4], u64 labels}).  Used by bench.py's same-algorithm CPU greedy baseline and by
+ * tests; groups run in parallel, each a bounded max-heap pass over the nodes. */
+static void heap_sift_down(uint64_t* h, int n, int i) {
+  for (;;) {
+    int l = 2 * i + 1, r = l + 1, m = i;
+    if (l < n && h[l] > h[m]) m = l;
+    if (r < n && h[r] > h[m]) m = r;
+    if (m == i) return;
+    uint64_t t = h[i];
+    h[i] = h[m];
+    h[m] = t;
+    i = m;
+  }
+}
+
+static int cmp_u64(const void* a, const void* b) {
+  const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+  return x < y ? -1 : x > y;
+}
+
+int orc_window_cands(int64_t N, const int64_t* res, const uint32_t* labels, int32_t n_groups,
+                     const int64_t* group_req, const uint32_t* group_need, int32_t K, uint8_t* blob,
+                     int nthreads) {
+  if (K < 1) return -1;
+  const size_t gbytes = 16 + (size_t)K * 48;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int32_t g = 0; g < n_groups; ++g) {
+    const int64_t* q = group_req + (int64_t)g * ORC_D;
+    const int cap = K + 1;
+    uint64_t* h = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)cap);
+    int n = 0;
+    for (int64_t i = 0; i < N; ++i) {
+      const uint64_t k = node_key(res, N, i, (uint64_t)i, labels[i], q, group_need[g]);
+      if (k == UINT64_MAX) continue;
+      if (n < cap) {
+        h[n++] = k;
+        if (n == cap)
+          for (int s = cap / 2 - 1; s >= 0; --s) heap_sift_down(h, cap, s);
+      } else if (k < h[0]) {
+        h[0] = k;
+        heap_sift_down(h, cap, 0);
+      }
+    }
+    qsort(h, (size_t)n, sizeof(uint64_t), cmp_u64);
+    uint8_t* out = blob + (size_t)g * gbytes;
+    memset(out, 0, gbytes);
+    const int32_t listed = n > K ? K : n;
+    const uint64_t limit = n > K ? h[K] : UINT64_MAX;
+    memcpy(out, &listed, 4);
+    memcpy(out + 8, &limit, 8);
+    for (int32_t i = 0; i < listed; ++i) {
+      uint8_t* rec = out + 16 + (size_t)i * 48;
+      const int64_t node = (int64_t)(h[i] & 0xFFFFFFull);
+      uint64_t lab = labels[node];
+      memcpy(rec, &h[i], 8);
+      for (int d = 0; d < ORC_D; ++d) memcpy(rec + 8 + 8 * d, &res[(int64_t)d * N + node], 8);
+      memcpy(rec + 40, &lab, 8);
+    }
+    free(h);
+  }
+  return 0;
+}
+
 int orc_num_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

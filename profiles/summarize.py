@@ -10,9 +10,13 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from provenance import source_hash  # noqa: E402
+
 
 def main(d):
-    out = {"kernels": {}, "pmc": collections.defaultdict(dict)}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {"source_hash": source_hash(root), "kernels": {}, "pmc": collections.defaultdict(dict)}
     for f in glob.glob(os.path.join(d, "trace", "*kernel_stats.csv")):
         for r in csv.DictReader(open(f)):
             out["kernels"][r["Name"].split("(")[0]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),

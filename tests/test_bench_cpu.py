@@ -1,0 +1,84 @@
+"""bench.py's launcher and bookkeeping on CPU (no GPU): `--gpus N` starts N ranks through
+torch.distributed.run without the parent loading the engine or any GPU runtime; a world size that
+contradicts --gpus is refused; the profile cross-check only trusts a profile of the same build."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    return env
+
+
+def test_launcher_starts_ranks_without_loading_the_engine():
+    code = (
+        "import sys, json; sys.path.insert(0, %r); import bench\n"
+        "argv = ['--gpus', '4', '--steps', '3']\n"
+        "calls = []\n"
+        "rc = bench.maybe_launch(bench.parse_args(argv), argv, run=lambda c: calls.append(c) or 7)\n"
+        "heavy = [m for m in ('placement', 'torch', 'oracle', 'numpy') if m in sys.modules]\n"
+        "print(json.dumps({'rc': rc, 'cmd': calls[0], 'heavy': heavy}))\n" % ROOT)
+    out = subprocess.run([sys.executable, "-c", code], env=_env(), capture_output=True, text=True, check=True)
+    got = json.loads(out.stdout.strip().splitlines()[-1])
+    assert got["rc"] == 7                      # the parent exits with the children's status
+    assert got["heavy"] == []                  # nothing that loads the engine / a GPU runtime
+    cmd = got["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]           # the ranks get the same arguments
+    assert os.path.basename(cmd[-5]) == "bench.py"
+
+
+def test_single_gpu_and_ranks_do_not_relaunch():
+    sys.path.insert(0, ROOT)
+    import bench
+    called = []
+    env_ws = os.environ.pop("WORLD_SIZE", None)
+    try:
+        assert bench.maybe_launch(bench.parse_args([]), [], run=called.append) is None
+        os.environ["WORLD_SIZE"] = "2"
+        assert bench.maybe_launch(bench.parse_args(["--gpus", "2"]), ["--gpus", "2"], run=called.append) is None
+    finally:
+        os.environ.pop("WORLD_SIZE", None)
+        if env_ws is not None:
+            os.environ["WORLD_SIZE"] = env_ws
+    assert called == []
+
+
+def test_world_size_must_match_gpus():
+    env = _env()
+    env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], env=env,
+                         capture_output=True, text=True)
+    assert out.returncode == 2 and "WORLD_SIZE=2" in out.stderr
+
+
+def test_default_is_strong_scaling():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.parse_args([]).scaling == "strong"
+
+
+def test_profile_check_requires_same_build(tmp_path, monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    prof = tmp_path / "p"
+    prof.mkdir()
+    (tmp_path / "LATEST").write_text("p\n")
+    summ = {"source_hash": "abc", "workload": {"nodes": 100, "jobs": 10},
+            "kernels": {"pe::fit_mask_planes_rows_kernel": {"avg_ns": 1.0e6, "calls": 5, "total_ns": 5e6},
+                        "pe::encode_planes_kernel": {"avg_ns": 0.02e6, "calls": 5, "total_ns": 1e5}},
+            "pmc": {"pe::fit_mask_planes_rows_kernel": {"hbm_traffic_bytes": 123.0, "SQ_INSTS_VALU": 5.0}}}
+    (prof / "summary.json").write_text(json.dumps(summ))
+    monkeypatch.setattr(bench, "PROFILES", str(tmp_path))
+    ok = bench.profile_check("planes", 100, 10, 1.03, "abc")
+    assert ok["profile_matches"] and ok["traffic"] == 123.0 and abs(ok["profile_step_ms"] - 1.02) < 1e-9
+    assert not bench.profile_check("planes", 100, 10, 1.03, "other")["profile_matches"]     # other build
+    assert bench.profile_check("planes", 100, 10, 1.20, "abc")["traffic"] is None          # > 5 % apart
+    assert bench.profile_check("planes", 100, 11, 1.03, "abc")["traffic"] is None          # other workload

@@ -91,3 +91,16 @@ def test_resolver_rejects_bad_input():
     with pytest.raises(PlacementError):
         Resolver(np.array([0, 1], np.int32), np.array([0], np.int32), np.array([1], np.int32),
                  -np.ones((1, 4), np.int64))
+
+
+@pytest.mark.parametrize("K", [1, 4, 256])
+def test_windowed_cpu_greedy_matches_naive_oracle(K):
+    """bench.py's same-algorithm CPU greedy baseline (C window scan + the host resolver) is exact."""
+    inv, batch = small_world(900, 80, 21, "mixed", 0.3)
+    want = oracle_run(inv, batch)
+    pods, st, res, windows = oracle.place_greedy_windowed(Resolver, inv.residual(), inv.labels, batch, K=K,
+                                                          max_groups=16, max_pods=64, nthreads=2)
+    np.testing.assert_array_equal(st, want[1])
+    np.testing.assert_array_equal(pods, want[0])
+    np.testing.assert_array_equal(res, want[2])
+    assert windows > 1

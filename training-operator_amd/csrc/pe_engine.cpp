@@ -233,6 +233,7 @@ struct pe_ctx {
   DevBuf<int64_t> w_ovres;
   DevBuf<int32_t> w_ovl, w_ovln;
   DevBuf<uint8_t> w_temp;
+  DevBuf<unsigned long long> w_stat;   // walk counters of the current pe_place_greedy (rounds, overlay)
   pe_stats stats{};
 
   ~pe_ctx() {
@@ -248,7 +249,7 @@ struct pe_ctx {
     g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_out.release(); h_out2.release(); h_own.release(); h_upd.release();
     w_sk.release(); w_kin.release(); w_rmin.release(); w_sr.release(); w_rmax.release(); w_sl.release(); w_pos.release();
     w_ror.release(); w_inovl.release(); w_ovl.release(); w_ovln.release(); w_temp.release();
-    w_ovidx.release(); w_ovlab.release(); w_ovres.release();
+    w_ovidx.release(); w_ovlab.release(); w_ovres.release(); w_stat.release();
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -510,6 +511,16 @@ int pe_shard_range(const pe_ctx* ctx, int64_t* begin, int64_t* end) {
   if (!ctx || !begin || !end) return PE_EINVAL;
   *begin = ctx->begin;
   *end = ctx->end;
+  return PE_OK;
+}
+
+int pe_comm_ranks(const pe_ctx* ctx, int32_t* nranks) {
+  if (!ctx || !nranks) return PE_EINVAL;
+  *nranks = 0;
+  if (!ctx->comm) return PE_OK;
+  int n = 0;
+  if (ncclCommCount(ctx->comm, &n) != ncclSuccess) return PE_ERCCL;
+  *nranks = n;
   return PE_OK;
 }
 
@@ -936,6 +947,7 @@ static void fit_run(pe_ctx* ctx) {
                                              reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p),
              "launch fit_mask_planes_sets");
       ctx->stats.fit_runs_planes += 1;
+      ctx->stats.fit_runs_sets += 1;
       ctx->stats.fit_evals += J * ctx->Ns;
       return;
     }
@@ -1120,6 +1132,7 @@ static pe::WalkIndex walk_index(pe_ctx* ctx) {
   w.ovl_idx = ctx->w_ovidx.p;
   w.ovl_res = ctx->w_ovres.p;
   w.ovl_lab = ctx->w_ovlab.p;
+  w.stat = ctx->w_stat.p;
   w.sstride = ctx->stride;
   w.nr = (ctx->Ns + pe::WK_ROUND - 1) / pe::WK_ROUND;
   return w;
@@ -1271,7 +1284,23 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
                                  ctx->g_lo.p),
            "launch prep_nodes");
     const bool walk = ctx->walk && ctx->Ns > 0;
+    hipchk(ctx->w_stat.ensure(2), "alloc walk counters");
+    hipchk(hipMemsetAsync(ctx->w_stat.p, 0, 2 * sizeof(unsigned long long), ctx->stream), "memset walk counters");
     if (walk) walk_resort(ctx);
+    // PE_WALK_EVENTS=1: hipEvents around every walk launch, summed into stats.walk_ms (diagnostics:
+    // the greedy roofline of bench.py; the events cost a few us of host time per window)
+    const bool wev = walk && std::getenv("PE_WALK_EVENTS") != nullptr;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> walk_events;
+    struct EventsFree {
+      std::vector<std::pair<hipEvent_t, hipEvent_t>>& v;
+      ~EventsFree() {
+        for (auto& p : v) {
+          (void)hipEventDestroy(p.first);
+          (void)hipEventDestroy(p.second);
+        }
+      }
+    } events_free{walk_events};
+    int64_t walk_launch_groups = 0;
     std::vector<pe::GroupCands> cands;
     hipStream_t s = ctx->stream;
     const bool use_exchange = ctx->exchange && !(ctx->world == 1 && !ctx->comm);
@@ -1297,9 +1326,18 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       uint8_t* const dst = direct_out ? outbufdev(b) : ctx->g_out.p;
       if (walk) {   // one 64-B request per block: read from pinned host memory, no H2D copy
         if (ctx->w_est > ctx->resort_nodes) walk_resort(ctx);
+        std::pair<hipEvent_t, hipEvent_t> evp{nullptr, nullptr};
+        if (wev) {
+          hipchk(hipEventCreate(&evp.first), "event");
+          hipchk(hipEventCreate(&evp.second), "event");
+          walk_events.push_back(evp);
+          hipchk(hipEventRecord(evp.first, s), "event record");
+        }
         hipchk(pe::launch_walk(s, ctx->h_groups.dev, Wg, K, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p,
                                ctx->Ns, (uint64_t)ctx->begin, dst),
                "launch walk");
+        if (wev) hipchk(hipEventRecord(evp.second, s), "event record");
+        walk_launch_groups += Wg;
       } else if (ctx->Ns > 0) {
         hipchk(hipMemcpyAsync(ctx->g_groups.p, ctx->h_groups.p, Wgp * sizeof(ReqRec), hipMemcpyHostToDevice, s),
                "H2D window");
@@ -1457,6 +1495,19 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (!cur.empty()) enqueue_window(cur, cb);
     }
     hipchk(hipStreamSynchronize(s), "sync greedy");
+    if (walk) {
+      unsigned long long wc[2] = {0, 0};
+      hipchk(hipMemcpy(wc, ctx->w_stat.p, sizeof(wc), hipMemcpyDeviceToHost), "D2H walk counters");
+      ctx->stats.walk_rounds += (int64_t)wc[0];
+      ctx->stats.walk_overlay += (int64_t)wc[1];
+      ctx->stats.walk_groups += walk_launch_groups;
+      ctx->stats.walk_prepass += walk_launch_groups * ((ctx->Ns + pe::WK_ROUND - 1) / pe::WK_ROUND);
+      for (auto& p : walk_events) {
+        float ms = 0.f;
+        hipchk(hipEventElapsedTime(&ms, p.first, p.second), "event elapsed");
+        ctx->stats.walk_ms += ms;
+      }
+    }
     if (P > 0) std::memcpy(out_pod_node, R.pod_node().data(), (size_t)P * 4);
     std::memcpy(out_job_status, R.job_status().data(), (size_t)n_jobs * 4);
     ctx->stats.rescans += R.rescans();

@@ -182,6 +182,7 @@ struct WalkIndex {
   uint32_t* ovl_idx;   // [stride] a node's overlay slot (valid while in_ovl)
   int64_t* ovl_res;    // [4][sstride] residuals by overlay slot (kept current by apply)
   uint32_t* ovl_lab;   // [stride] labels by overlay slot
+  unsigned long long* stat;   // nullable: [0] += rounds walked, [1] += overlay entries, per group
   int64_t sstride, nr;
 };
 // kin[n] = K(n) of a walkable node (no negative residual, not saturating), else WK_INVALID; the

@@ -1634,9 +1634,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   __syncthreads();
   WPT(2);
   bool done = !walk;
-#ifdef PE_WALK_PROF
   int rounds = 0;
-#endif
   int64_t r = walk ? (start_cnt > 0 ? start_cnt - 1 : 0) : nr;
   auto next_round = [&](int64_t from) -> int64_t {   // first candidate round >= from (uniform)
     int64_t wi = from >> 5;
@@ -1684,15 +1682,17 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
       __syncthreads();
     }
     r = next_round(r + 1);
-#ifdef PE_WALK_PROF
     ++rounds;
-#endif
   }
   WPT(3);
   const int T = s.total;
   const uint64_t* sk = topk_sort(s, T, K);
   WPT(4);
   write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : NO_KEY, K, g, out);
+  if (tid == 0 && w.stat) {
+    atomicAdd(&w.stat[0], (unsigned long long)rounds);
+    atomicAdd(&w.stat[1], (unsigned long long)no);
+  }
 #ifdef PE_WALK_PROF
   __syncthreads();
   WPT(5);

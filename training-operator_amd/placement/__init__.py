@@ -142,6 +142,12 @@ class Engine:
         self._chk(self.lib.pe_shard_range(self.h, ctypes.byref(b), ctypes.byref(e)), "pe_shard_range")
         return b.value, e.value
 
+    def comm_ranks(self) -> int:
+        """ncclCommCount of the context's RCCL communicator (0 = host exchange / none)."""
+        v = ctypes.c_int32()
+        self._chk(self.lib.pe_comm_ranks(self.h, ctypes.byref(v)), "pe_comm_ranks")
+        return v.value
+
     def read_residuals(self) -> np.ndarray:
         b, e = self.shard_range()
         out = np.zeros((4, e - b), dtype=np.int64)

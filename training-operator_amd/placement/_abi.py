@@ -43,7 +43,10 @@ class PeStats(ctypes.Structure):
                 ("jobs_placed", ctypes.c_int64), ("jobs_failed", ctypes.c_int64), ("last_greedy_ms", ctypes.c_double),
                 ("greedy_wait_ms", ctypes.c_double), ("greedy_host_ms", ctypes.c_double),
                 ("fit_runs_i32", ctypes.c_int64), ("fit_runs_i64", ctypes.c_int64), ("fit_runs_coded", ctypes.c_int64),
-                ("fit_runs_therm", ctypes.c_int64), ("fit_runs_planes", ctypes.c_int64), ("resorts", ctypes.c_int64)]
+                ("fit_runs_therm", ctypes.c_int64), ("fit_runs_planes", ctypes.c_int64), ("resorts", ctypes.c_int64),
+                ("fit_runs_lds", ctypes.c_int64), ("fit_runs_sets", ctypes.c_int64), ("walk_rounds", ctypes.c_int64),
+                ("walk_overlay", ctypes.c_int64), ("walk_groups", ctypes.c_int64), ("walk_prepass", ctypes.c_int64),
+                ("walk_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -63,6 +66,7 @@ SIGNATURES = {
     "pe_reset_residuals": (ctypes.c_int, [P]),
     "pe_update_nodes": (ctypes.c_int, [P, i64, P, P, P, P, P, P]),
     "pe_shard_range": (ctypes.c_int, [P, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
+    "pe_comm_ranks": (ctypes.c_int, [P, ctypes.POINTER(i32)]),
     "pe_read_residuals": (ctypes.c_int, [P, P]),
     "pe_pg_min_resources": (ctypes.c_int, [P, i32, i64, P, P, P, P, P, P, P, P, P, P]),
     "pe_fit_mask": (ctypes.c_int, [P, i64, P, P, P, ctypes.POINTER(P), ctypes.POINTER(i64)]),

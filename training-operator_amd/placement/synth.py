@@ -168,3 +168,61 @@ def make_jobs(n_jobs: int, seed: int, mix: str = "pytorch") -> JobBatch:
 def make_fit_jobs(n_jobs: int, seed: int):
     """cfg5: one request vector (the trainer pod) per job."""
     return pod_requests(seed, 500, n_jobs)
+
+
+MiB = 1 << 20
+
+
+def make_fit_jobs_worst(n_jobs: int, seed: int, unique_dims=(1,)):
+    """cfg5-sized batch with high-cardinality requests (the fit mask's hard case): every dimension in
+    `unique_dims` gets a value unique to each job (memory: distinct MiB counts in [0.5, 256) GiB;
+    cpu: distinct milli counts; ephemeral: distinct MiB counts), cpu and ephemeral-storage that are
+    not unique are uniform over 1000 / 100 values (100m steps up to 100 cores, 1 GiB steps), gpu and
+    the label need as in cfg5."""
+    req, need = pod_requests(seed, 500, n_jobs)
+    J = n_jobs
+    perm = (stream(seed, 520, J) % np.uint64(1 << 62)).argsort(kind="stable").astype(np.int64)  # a permutation
+    req[:, 0] = 100 * (1 + (stream(seed, 521, J) % np.uint64(1000)).astype(np.int64))
+    req[:, 3] = GiB * (stream(seed, 523, J) % np.uint64(100)).astype(np.int64)
+    if 0 in unique_dims:
+        req[:, 0] = 100 + perm                               # J distinct milli values
+    if 1 in unique_dims:
+        req[:, 1] = (512 + perm * ((256 * 1024 - 512) // max(J, 1))) * MiB
+    if 3 in unique_dims:
+        req[:, 3] = perm * 7 * MiB
+    return req, need
+
+
+def make_pg_batch(n_jobs: int, seed: int):
+    """Aggregation batch (pe_pg_min_resources CSR, v1): PyTorchJob-like jobs, Master 1 + Worker W
+    (W in [0, 63]), one or two containers per pod (a trainer + an optional sidecar-style helper),
+    cpu/memory always present, gpu on GPU jobs, minMember = total replicas or a random smaller
+    MinAvailable.  Returns (job_group_off, min_member, group_replicas, group_cont_off, cont_req,
+    cont_flags)."""
+    J = n_jobs
+    w = (stream(seed, 600, J) % np.uint64(64)).astype(np.int32)
+    two_ctr = (stream(seed, 601, J) % np.uint64(2)).astype(bool)
+    req, _ = pod_requests(seed, 610, J)
+    total = 1 + w
+    mm = np.where(stream(seed, 602, J) % np.uint64(4) == 0,
+                  1 + (stream(seed, 603, J) % total.astype(np.uint64)).astype(np.int32), total).astype(np.int32)
+    jgo = (2 * np.arange(J + 1)).astype(np.int32)
+    rep = np.empty(2 * J, np.int32)
+    rep[0::2] = 1
+    rep[1::2] = w
+    nct = np.where(two_ctr, 2, 1).astype(np.int32)
+    per_group = np.repeat(nct, 2)
+    gco = np.zeros(2 * J + 1, np.int32)
+    np.cumsum(per_group, out=gco[1:])
+    C = int(gco[-1])
+    cont = np.zeros((C, 4), np.int64)
+    flags = np.zeros(C, np.uint8)
+    first = gco[:-1]
+    g_req = np.repeat(req, 2, axis=0)
+    cont[first] = g_req
+    gpu = g_req[:, 2] > 0
+    flags[first] = np.where(gpu, 0b1111, 0b1011)
+    helper = first[per_group == 2] + 1
+    cont[helper] = [250, 256 * MiB, 0, 0]
+    flags[helper] = 0b0011
+    return jgo, mm, rep, gco, cont, flags
