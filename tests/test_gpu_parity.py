@@ -196,10 +196,11 @@ def test_fit_mask_rows_pitch(N, J, pitch_blocks):
 
 
 @pytest.mark.parametrize("case", ["many_values", "odd_bytes", "label_antichain", "many_planes", "plane_sets",
-                                  "extreme_values"])
+                                  "lds", "extreme_values"])
 def test_fit_mask_path_fallbacks(eng, case):
-    """Each batch shape lands on the path that can hold it (planes > coded > int32 > int64), exact.
-    The compare/coded cases run with the planes path disabled: plane sets hold them otherwise."""
+    """Each batch shape lands on the path that can hold it (one plane set > LDS digit planes > plane
+    sets > coded > int32 > int64), exact.  The compare/coded cases run with the plane paths disabled:
+    the LDS digit planes hold them otherwise."""
     N, J = 3000, 400
     inv = synth.make_inventory(N, 91, 0.3)
     req, need = synth.make_fit_jobs(J, 93)
@@ -219,14 +220,22 @@ def test_fit_mask_path_fallbacks(eng, case):
         req[:, 0] = 500 + (np.arange(J) % 40) * 7    # 40 distinct cpu values: > 32 planes, SWAR-coded
         want = "fit_runs_coded"
     elif case == "plane_sets":
-        req[:, 0] = 500 + (np.arange(J) % 40) * 7    # the same batch with planes allowed: plane sets
+        req[:, 0] = 500 + (np.arange(J) % 40) * 7    # the same batch with planes but not LDS: plane sets
         want = "fit_runs_planes"
+    elif case == "lds":
+        req[:, 0] = 500 + (np.arange(J) % 40) * 7    # the same batch with every path: LDS digit planes
+        want = "fit_runs_lds"
     else:
         req[0] = [np.iinfo(np.int64).max, 0, 0, 0]   # int64 extremes are just two more planes
         req[1] = [0, np.iinfo(np.int64).max, 0, np.iinfo(np.int64).max]
         inv.used[0, :7] = inv.cap[0, :7] + 5         # over-committed nodes: no request fits them
         want = "fit_runs_planes"
-    e = eng if want == "fit_runs_planes" else Engine(0, fit_path_mask=1 | 2 | 4)   # no planes
+    if case == "plane_sets":
+        e = Engine(0, fit_path_mask=16)                   # bit planes (sets), no LDS digit planes
+    elif want in ("fit_runs_planes", "fit_runs_lds"):
+        e = eng
+    else:
+        e = Engine(0, fit_path_mask=1 | 2 | 4)            # no planes
     e.reset_stats()
     e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     counts = e.fit_mask(req, need)
@@ -256,7 +265,7 @@ def test_fit_mask_plane_sets(N, J, shape):
         need[:] = rng.integers(0, 4, J).astype(np.uint32) << 1
     else:                                                               # unique memory per job
         req[:, 1] = (1 << 30) + np.arange(J) * 4096
-    e = Engine(0)
+    e = Engine(0, fit_path_mask=16)                       # bit planes (+ the int64 fallback), no LDS
     e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     counts = e.fit_mask(req, need)
     o_mask, o_counts = oracle.fit_mask(inv.residual(), inv.labels, req, need)
@@ -285,7 +294,7 @@ def test_fit_mask_plane_sets_sharded():
     o_mask, o_counts = oracle.fit_mask(inv.residual(), inv.labels, req, need)
     total = np.zeros(J, np.int64)
     for rank in range(2):
-        e = Engine(0, rank=rank, world_size=2, exchange=lambda b: b + b)
+        e = Engine(0, rank=rank, world_size=2, exchange=lambda b: b + b, fit_path_mask=16)
         e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
         b, en = e.shard_range()
         total += e.fit_mask(req, need)

@@ -145,8 +145,9 @@ void ncclchk(ncclResult_t r, const char* what) {
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // pe_config.fit_path_mask bits
-constexpr int PATH_I64 = 1, PATH_I32 = 2, PATH_CODED = 4, PATH_NO_THERM = 8, PATH_PLANES = 16, PATH_PLANES_BLOCKS = 32;
-constexpr int PATHS_ALL = PATH_I64 | PATH_I32 | PATH_CODED | PATH_PLANES;
+constexpr int PATH_I64 = 1, PATH_I32 = 2, PATH_CODED = 4, PATH_NO_THERM = 8, PATH_PLANES = 16, PATH_PLANES_BLOCKS = 32,
+              PATH_LDS = 64;
+constexpr int PATHS_ALL = PATH_I64 | PATH_I32 | PATH_CODED | PATH_PLANES | PATH_LDS;
 
 }  // namespace
 
@@ -181,7 +182,16 @@ struct pe_ctx {
   DevBuf<int32_t> res32;
   bool fit32 = false;      // batch is exactly representable in 32 bits (see ReqRec32)
   int fit_shift[pe::D] = {0, 0, 0, 0};
-  int fit_path = 0;        // 0 int64 compare, 1 int32 compare, 2 dictionary-coded, 3 bit planes
+  int fit_path = 0;        // 0 int64 compare, 1 int32 compare, 2 dictionary-coded, 3 bit planes, 4 LDS digit planes
+  // LDS digit-plane path (pe_kernels.h LdsSpec): spec, node-block geometry, codes, ranks
+  pe::LdsSpec lds{};
+  int lds_W = 4;                          // u32 words per lane per plane: block = 2048 W nodes
+  int64_t lds_nblk = 0, lds_R = 1, lds_Tpad = 0, lds_npad = 0, lds_pitch = 0;   // pitch in u64 words
+  DevBuf<pe::LdsSpec> lds_spec_d;
+  DevBuf<int64_t> lds_vals;
+  DevBuf<uint16_t> lds_codes;
+  DevBuf<uint32_t> lds_ranks, lds_aux;
+  int num_cu = 256;
   int fit_path_mask = PATHS_ALL;   // allowed paths (pe_config.fit_path_mask)
   pe::PlaneSpec plane{};
   int64_t pl_nblk = 0;                   // planes path: 8192-node blocks
@@ -243,6 +253,7 @@ struct pe_ctx {
     fit_jobs.release(); fit_jobs32.release(); res32.release(); mask.release();
     code_vals.release(); code_needs.release(); code_jobs.release(); code_x.release(); counts.release(); h_counts.release();
     planes.release(); plane_jobs.release();
+    lds_spec_d.release(); lds_vals.release(); lds_codes.release(); lds_ranks.release(); lds_aux.release();
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
@@ -354,6 +365,9 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   try {
     hipchk(hipSetDevice(dev), "hipSetDevice");
     hipchk(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "hipStreamCreate");
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+      ctx->num_cu = ncu;
     // RCCL whenever shards exchange without a host callback; a comm_id at world_size 1 also
     // builds a 1-rank communicator (exercises the RCCL window path on a single GPU)
     if (!ctx->exchange && (ctx->world > 1 || cfg->comm_id)) {
@@ -693,7 +707,7 @@ static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const u
 constexpr int PL_MAX_SETS = 256;
 constexpr int64_t PL_SETS_BYTES = int64_t(2) << 30;   // planes of all sets (4 MiB per set at 1M nodes)
 
-static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
+static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need, bool allow_sets) {
   if (n_jobs == 0) return false;
   constexpr int F = pe::D + 1;
   auto value = [&](int64_t j, int f) -> int64_t { return f < pe::D ? req[j * pe::D + f] : (int64_t)(need ? need[j] : 0u); };
@@ -756,7 +770,7 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const 
     ctx->pl_R = R;
     ctx->pl_counts_n = R * Jr;
   } else {
-    if (!ctx->pl_rows || n_jobs >= (int64_t(1) << 24)) return false;
+    if (!allow_sets || !ctx->pl_rows || n_jobs >= (int64_t(1) << 24)) return false;
     // Sets: jobs ordered by their selections, the field with the most distinct values first, then
     // swept greedily; a set closes when the next job would take it past PL_MAX planes.
     int ford[F];
@@ -859,6 +873,201 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const 
   return true;
 }
 
+// LDS digit planes of one batch (pe_kernels.h LdsSpec): per dimension with >= 2 distinct values a
+// digit field of L levels (chosen with the node-block size W to minimise plane reads per job within
+// the LDS budget), dimensions with one value folded into the need planes, one plane per distinct
+// need.  Returns false when no configuration fits 160 KiB of LDS (the other paths take the batch).
+// PE_LDS_W=1|2|4 forces the block size, PE_LDS_MAXL=1..3 caps the levels (tuning / tests).
+static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
+  if (n_jobs == 0 || ctx->Ns == 0) return false;
+  std::vector<int64_t> vals[pe::D];
+  for (int d = 0; d < pe::D; ++d) {
+    vals[d].resize((size_t)n_jobs);
+    for (int64_t j = 0; j < n_jobs; ++j) vals[d][j] = req[j * pe::D + d];
+    std::sort(vals[d].begin(), vals[d].end());
+    vals[d].erase(std::unique(vals[d].begin(), vals[d].end()), vals[d].end());
+  }
+  std::vector<uint32_t> needs((size_t)n_jobs);
+  for (int64_t j = 0; j < n_jobs; ++j) needs[j] = need ? need[j] : 0u;
+  std::sort(needs.begin(), needs.end());
+  needs.erase(std::unique(needs.begin(), needs.end()), needs.end());
+  if ((int)needs.size() > pe::LD_MAXNEED) return false;
+  pe::LdsSpec sp{};
+  int fdim[pe::LD_MAXF];
+  for (int d = 0; d < pe::D; ++d) {
+    if (vals[d].size() == 1) {
+      sp.fold_dim[sp.nfold] = d;
+      sp.fold_val[sp.nfold++] = vals[d][0];
+    } else {
+      fdim[sp.nf++] = d;
+    }
+  }
+  // planes of a field with m values at L levels (lower levels base B, top level whatever is left)
+  auto plan = [](int64_t m, int L, int64_t& B) -> int64_t {
+    if (L == 1) {
+      B = m;
+      return m;
+    }
+    int64_t best = INT64_MAX;
+    for (int64_t b = 2; b <= m; ++b) {
+      const int64_t low = L == 2 ? b : b * b;
+      if (L == 3 && b * b > 4 * m + 4) break;
+      const int64_t T = m / low + 1;
+      const int64_t p = (T + 1) + (L == 3 ? (b + 1) : 0) + b;
+      if (p < best) {
+        best = p;
+        B = b;
+      }
+      if (L == 2 && b * b > 4 * m + 4) break;
+    }
+    return best;
+  };
+  int maxl = 3;
+  if (const char* e = std::getenv("PE_LDS_MAXL")) maxl = std::max(1, std::min(3, std::atoi(e)));
+  int forced_w = 0;
+  if (const char* e = std::getenv("PE_LDS_W")) forced_w = std::atoi(e);
+  const int64_t nneed = (int64_t)needs.size();
+  int bestW = 0, bestL[pe::LD_MAXF] = {1, 1, 1, 1};
+  int64_t bestB[pe::LD_MAXF] = {0, 0, 0, 0};
+  double bestCost = 1e300;
+  for (int W : {4, 2, 1}) {
+    if (forced_w && W != forced_w) continue;
+    const int64_t budget = 163840 / (256 * W);
+    int combos = 1;
+    for (int i = 0; i < sp.nf; ++i) combos *= maxl;
+    for (int cix = 0; cix < combos; ++cix) {
+      int L[pe::LD_MAXF];
+      int64_t B[pe::LD_MAXF];
+      int64_t planes = nneed, reads = 1;
+      for (int i = 0, x = cix; i < sp.nf; ++i, x /= maxl) {
+        L[i] = 1 + x % maxl;
+        const int64_t m = (int64_t)vals[fdim[i]].size();
+        if (L[i] > 1 && m < 4) L[i] = 1;
+        planes += plan(m, L[i], B[i]);
+        reads += 2 * L[i] - 1;
+      }
+      if (planes > budget || planes > 65535) continue;
+      // LDS cycles per KiB of plane reads (b128 / b64: 4, b32: 8) plus ~60 VALU cycles of fixed work
+      // per job and wave, both per 8192 nodes
+      const double cost = reads * (W == 1 ? 8.0 : 4.0) + 60.0 * 4 / W;
+      if (cost < bestCost - 1e-9) {
+        bestCost = cost;
+        bestW = W;
+        for (int i = 0; i < sp.nf; ++i) {
+          bestL[i] = L[i];
+          bestB[i] = B[i];
+        }
+      }
+    }
+  }
+  if (!bestW) return false;
+  // level specs, plane bases
+  int32_t p = 0;
+  int64_t voff = 0;
+  std::vector<int64_t> allv;
+  for (int i = 0; i < sp.nf; ++i) {
+    const int64_t m = (int64_t)vals[fdim[i]].size(), B = bestB[i];
+    const int L = bestL[i];
+    sp.dim[i] = fdim[i];
+    sp.L[i] = L;
+    sp.voff[i] = voff;
+    sp.m[i] = m;
+    allv.insert(allv.end(), vals[fdim[i]].begin(), vals[fdim[i]].end());
+    voff += m;
+    for (int k = 0; k < L; ++k) {
+      const bool top = k == L - 1;
+      int64_t dv = 1;
+      for (int t = 0; t < k; ++t) dv *= B;
+      sp.div[i][k] = (uint32_t)dv;
+      sp.mod[i][k] = top ? 0u : (uint32_t)B;
+      if (L == 1) {
+        sp.vlo[i][k] = 1;
+        sp.nv[i][k] = (int32_t)m;
+      } else {
+        sp.vlo[i][k] = 0;
+        sp.nv[i][k] = (int32_t)(top ? m / dv + 2 : (k == 0 ? B : B + 1));
+      }
+      sp.pbase[i][k] = p;
+      p += sp.nv[i][k];
+    }
+  }
+  sp.need_pbase = p;
+  sp.nneed = (int32_t)nneed;
+  for (int64_t i = 0; i < nneed; ++i) sp.needs[i] = needs[i];
+  sp.nplanes = p + (int32_t)nneed;
+  // geometry: W words per lane, blocks of 2048 W nodes, R job phases for an even spread over the CUs
+  const int W = bestW;
+  const int64_t S = 2048 * W;
+  const int64_t nblk = (ctx->Ns + S - 1) / S;
+  const int64_t lds_bytes = (int64_t)sp.nplanes * S / 8;
+  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(2, 163840 / std::max<int64_t>(lds_bytes, 1)));
+  const int64_t slots = (int64_t)ctx->num_cu * per_cu;
+  int64_t R = 1;
+  double best_eff = 0;
+  for (int64_t r = 1; r <= 64 && (r == 1 || 16 * r <= n_jobs); ++r) {
+    const int64_t wg = nblk * r;
+    const double eff = (double)wg / (double)(((wg + slots - 1) / slots) * slots);
+    if (eff > best_eff + 1e-9) {
+      best_eff = eff;
+      R = r;
+    }
+    if (eff > 0.97) break;
+  }
+  const int64_t Tmax = ((n_jobs + R - 1) / R + 15) / 16;
+  const int64_t Tpad = round_up(std::max<int64_t>(Tmax, 1), 16);
+  // job codes: u16 plane indices at the kernel's slots, stored in the kernel's consumption order
+  std::vector<uint16_t> codes((size_t)(R * 16 * Tpad * pe::LD_CODE), 0);
+  for (int64_t j = 0; j < n_jobs; ++j) {
+    const int64_t r = j % R, q = j / R, w = q % 16, t = q / 16;
+    uint16_t* c = codes.data() + (size_t)(((r * 16 + w) * Tpad + t) * pe::LD_CODE);
+    for (int i = 0; i < sp.nf; ++i) {
+      const std::vector<int64_t>& v = vals[fdim[i]];
+      const int64_t rank = (int64_t)(std::lower_bound(v.begin(), v.end(), req[j * pe::D + fdim[i]]) - v.begin()) + 1;
+      if (sp.L[i] == 1) {
+        c[3 * i] = (uint16_t)(sp.pbase[i][0] + rank - 1);
+      } else {
+        int64_t x = rank;
+        for (int k = 0; k < sp.L[i]; ++k) {
+          const int64_t digit = sp.mod[i][k] ? x % sp.mod[i][k] : x;
+          x = sp.mod[i][k] ? x / sp.mod[i][k] : 0;
+          c[3 * i + k] = (uint16_t)(sp.pbase[i][k] + digit);
+        }
+      }
+    }
+    const uint32_t nd = need ? need[j] : 0u;
+    c[pe::LD_NEED_SLOT] =
+        (uint16_t)(sp.need_pbase + (std::lower_bound(needs.begin(), needs.end(), nd) - needs.begin()));
+  }
+  if (std::getenv("PE_LDS_DEBUG")) {   // diagnostics: the chosen configuration
+    std::fprintf(stderr, "lds: W %d nblk %lld R %lld planes %d need %d fold %d |", W, (long long)nblk, (long long)R,
+                 sp.nplanes, sp.nneed, sp.nfold);
+    for (int i = 0; i < sp.nf; ++i)
+      std::fprintf(stderr, " dim %d m %lld L %d B %u", sp.dim[i], (long long)sp.m[i], sp.L[i], sp.mod[i][0]);
+    std::fprintf(stderr, "\n");
+  }
+  ctx->lds = sp;
+  ctx->lds_W = W;
+  ctx->lds_nblk = nblk;
+  ctx->lds_R = R;
+  ctx->lds_Tpad = Tpad;
+  ctx->lds_npad = nblk * S;
+  ctx->lds_pitch = nblk * S / 64;
+  hipchk(ctx->lds_spec_d.ensure(1), "alloc lds spec");
+  hipchk(ctx->lds_vals.ensure(std::max<size_t>(allv.size(), 1)), "alloc lds vals");
+  hipchk(ctx->lds_codes.ensure(codes.size()), "alloc lds codes");
+  hipchk(ctx->lds_ranks.ensure((size_t)std::max(sp.nf, 1) * ctx->lds_npad), "alloc lds ranks");
+  hipchk(ctx->lds_aux.ensure((size_t)2 * ctx->lds_npad), "alloc lds aux");
+  hipchk(hipMemcpyAsync(ctx->lds_spec_d.p, &ctx->lds, sizeof(pe::LdsSpec), hipMemcpyHostToDevice, ctx->stream),
+         "H2D lds spec");
+  if (!allv.empty())
+    hipchk(hipMemcpyAsync(ctx->lds_vals.p, allv.data(), allv.size() * 8, hipMemcpyHostToDevice, ctx->stream),
+           "H2D lds vals");
+  hipchk(hipMemcpyAsync(ctx->lds_codes.p, codes.data(), codes.size() * 2, hipMemcpyHostToDevice, ctx->stream),
+         "H2D lds codes");
+  hipchk(hipStreamSynchronize(ctx->stream), "sync lds upload");   // the host vectors die here
+  return true;
+}
+
 static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
   if (n_jobs < 0) raise(PE_EINVAL, "n_jobs < 0");
   if (!ctx->loaded) raise(PE_ESTATE, "no inventory loaded");
@@ -909,10 +1118,15 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
   ctx->Wn = (ctx->Ns + 63) / 64;
   ctx->Wt = (ctx->Wn + 3) / 4;
   ctx->fit_path = ctx->fit32 ? 1 : 0;
-  if ((ctx->fit_path_mask & PATH_PLANES) && build_planes(ctx, n_jobs, req, need)) ctx->fit_path = 3;
+  // one bit-plane set (register planes) > LDS digit planes > bit-plane sets > coded > int32 > int64
+  const bool planes_ok = ctx->fit_path_mask & PATH_PLANES;
+  if (planes_ok && build_planes(ctx, n_jobs, req, need, false)) ctx->fit_path = 3;
+  else if ((ctx->fit_path_mask & PATH_LDS) && build_lds(ctx, n_jobs, req, need)) ctx->fit_path = 4;
+  else if (planes_ok && build_planes(ctx, n_jobs, req, need, true)) ctx->fit_path = 3;
   else if ((ctx->fit_path_mask & PATH_CODED) && build_codes(ctx, n_jobs, req, need)) ctx->fit_path = 2;
   hipchk(ctx->fit_jobs.ensure(Jp), "alloc fit jobs");
-  const size_t mask_words = ctx->fit_path == 3   ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->pl_nblk * 128
+  const size_t mask_words = ctx->fit_path == 4   ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->lds_pitch
+                            : ctx->fit_path == 3 ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->pl_nblk * 128
                             : ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
                                                  : (size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4;
   hipchk(ctx->mask.ensure(mask_words), "alloc fit mask");
@@ -935,7 +1149,17 @@ static void fit_run(pe_ctx* ctx) {
   const int64_t want_x = std::max<int64_t>(1, (16384 + waves_y - 1) / waves_y);
   int64_t tpw = (ctx->Ns + 256 * want_x - 1) / (256 * want_x);
   tpw = std::min<int64_t>(16, std::max<int64_t>(1, tpw));
-  if (ctx->fit_path == 3) {
+  if (ctx->fit_path == 4) {
+    hipchk(pe::launch_node_ranks(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->lds_npad,
+                                 ctx->lds_spec_d.p, ctx->lds_vals.p, ctx->lds_ranks.p, ctx->lds_aux.p),
+           "launch node_ranks");
+    hipchk(pe::launch_fit_mask_lds(ctx->stream, ctx->lds_W, ctx->lds_spec_d.p, ctx->lds.nplanes, ctx->lds_ranks.p,
+                                   ctx->lds_npad, ctx->lds_aux.p, ctx->lds_nblk, ctx->lds_codes.p, J,
+                                   ctx->lds_R, ctx->lds_Tpad, ctx->lds_pitch * 8,
+                                   reinterpret_cast<uint8_t*>(ctx->mask.p), ctx->counts.p),
+           "launch fit_mask_lds");
+    ctx->stats.fit_runs_lds += 1;
+  } else if (ctx->fit_path == 3) {
     // ~16k waves: every 8192-node block times enough job ranges, at least 64 jobs per wave
     if (!ctx->pl_sets.empty()) {   // plane sets: one encode pass and one sweep for all of them
       const int ns = (int)ctx->pl_sets.size();
@@ -1045,10 +1269,10 @@ int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out) {
     if (row0 < 0 || n_rows < 0 || row0 + n_rows > ctx->fit_J) raise(PE_EINVAL, "row range");
     if (n_rows == 0 || ctx->Wn == 0) return PE_OK;
     need_ptr(out, "out");
-    if (ctx->fit_path == 3 && ctx->pl_rows) {   // row-major, row pitch pl_nblk 8192-node blocks
-      hipchk(hipMemcpy2DAsync(out, (size_t)ctx->Wn * 8, ctx->mask.p + (size_t)row0 * ctx->pl_nblk * 128,
-                              (size_t)ctx->pl_nblk * 128 * 8, (size_t)ctx->Wn * 8, (size_t)n_rows,
-                              hipMemcpyDeviceToHost, ctx->stream),
+    if ((ctx->fit_path == 3 && ctx->pl_rows) || ctx->fit_path == 4) {   // row-major
+      const int64_t pitch = ctx->fit_path == 4 ? ctx->lds_pitch : ctx->pl_nblk * 128;
+      hipchk(hipMemcpy2DAsync(out, (size_t)ctx->Wn * 8, ctx->mask.p + (size_t)row0 * pitch, (size_t)pitch * 8,
+                              (size_t)ctx->Wn * 8, (size_t)n_rows, hipMemcpyDeviceToHost, ctx->stream),
              "D2H mask rows");
       hipchk(hipStreamSynchronize(ctx->stream), "sync mask");
       return PE_OK;
@@ -1522,13 +1746,16 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
 
 int pe_fit_mask_layout(const pe_ctx* ctx, int32_t* layout) {
   if (!ctx || !layout) return PE_EINVAL;
-  *layout = ctx->fit_path == 3 ? (ctx->pl_rows ? PE_MASK_ROWS : PE_MASK_NODE_BLOCKS) : ctx->fit_path == 2 ? PE_MASK_JOB_BITS : PE_MASK_NODE_TILES;
+  *layout = ctx->fit_path == 4   ? PE_MASK_ROWS
+            : ctx->fit_path == 3 ? (ctx->pl_rows ? PE_MASK_ROWS : PE_MASK_NODE_BLOCKS)
+            : ctx->fit_path == 2 ? PE_MASK_JOB_BITS
+                                 : PE_MASK_NODE_TILES;
   return PE_OK;
 }
 
 int pe_fit_mask_row_pitch(const pe_ctx* ctx, int64_t* words) {
   if (!ctx || !words) return PE_EINVAL;
-  *words = ctx->fit_path == 3 && ctx->pl_rows ? ctx->pl_nblk * 128 : 0;
+  *words = ctx->fit_path == 4 ? ctx->lds_pitch : ctx->fit_path == 3 && ctx->pl_rows ? ctx->pl_nblk * 128 : 0;
   return PE_OK;
 }
 

@@ -146,6 +146,56 @@ hipError_t launch_fit_mask_planes_sets(hipStream_t s, const uint32_t* planes, in
                                        const int64_t* meta, int nsets, int64_t R, uint32_t* mask,
                                        unsigned long long* counts);
 
+// ---- LDS digit-plane path (fit mask, any number of distinct request values).  Per dimension the
+// host ranks the batch's distinct request values v_1 < ... < v_m; a job asks rank c (v_c = its
+// request), a node has rank R = #{v_i <= residual}, and  q <= res  <=>  c <= R  exactly.  R >= c is
+// decided digit by digit (mixed radix, most significant first): with threshold planes
+// GE_k(v) = [digit_k(R) >= v],
+//     [R >= c] = GE_top(c_top + 1) | (GE_top(c_top) & ( ... GE_0(c_0) ... ))
+// so a field of m values costs L digit levels (m^(1/L)-ish planes each) and 2L - 1 plane reads per
+// job; a single-level field is one plane per value.  Label needs are one plane each, and
+// dimensions with a single requested value are folded into those.  The workgroup builds its node
+// block's planes in LDS (scatter of the equality bits + suffix OR), then streams the jobs: per job
+// a handful of LDS reads, AND/AND-OR combines, one store of the block's slice of the mask row.
+constexpr int LD_MAXF = 4;        // digit fields (dimensions with >= 2 distinct values)
+constexpr int LD_MAXL = 3;        // digit levels per field
+constexpr int LD_MAXNEED = 64;    // distinct label needs
+constexpr int LD_CODE = 16;       // u16 plane indices per job: field f, level slot k at 3f + k; need at 12
+constexpr int LD_NEED_SLOT = 12;
+constexpr int LD_THREADS = 1024;  // 16 waves per workgroup, one node block per workgroup
+struct LdsSpec {
+  int32_t nf;                       // digit fields
+  int32_t dim[LD_MAXF];             // resource dimension of field f
+  int32_t L[LD_MAXF];               // digit levels of field f
+  // level slot k (0 = least significant): digit = (R / div) % mod (mod 0 = no modulus); threshold
+  // planes GE(v) for v in [vlo, vlo + nv) at planes pbase + v - vlo
+  uint32_t div[LD_MAXF][LD_MAXL];
+  uint32_t mod[LD_MAXF][LD_MAXL];
+  int32_t pbase[LD_MAXF][LD_MAXL];
+  int32_t vlo[LD_MAXF][LD_MAXL];
+  int32_t nv[LD_MAXF][LD_MAXL];
+  int32_t nneed, need_pbase, nplanes, nfold;
+  uint32_t needs[LD_MAXNEED];
+  int32_t fold_dim[D];              // single-valued dimensions folded into the need planes:
+  int64_t fold_val[D];              // a node passes them iff res[fold_dim] >= fold_val
+  int64_t voff[LD_MAXF];            // field f's sorted distinct values at vals[voff[f] .. voff[f] + m[f])
+  int64_t m[LD_MAXF];
+};
+// ranks: [nf][npad] u32 (npad = node blocks x S, padding nodes 0); aux: [2][npad] u32, row 0 = 1 for
+// a shard node passing the folded dimensions (else 0), row 1 = its labels (0 for padding).
+// spec: device copy.
+hipError_t launch_node_ranks(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
+                             int64_t npad, const LdsSpec* spec, const int64_t* vals, uint32_t* ranks, uint32_t* aux);
+// S = 2048 * W nodes per workgroup block (W u32 words per lane per plane); grid = nblk x R
+// workgroups, wave w of workgroup (blk, r) takes jobs j = r + R (w + 16 t).  codes: LD_CODE u16 per
+// job, job j's at position (r * 16 + w) * Tpad + t (Tpad >= the longest run, a multiple of 16).
+// Mask row-major (PE_MASK_ROWS): row j at mask + j * pitch_bytes, block blk's S/8 bytes at + blk * S/8.
+// counts: [J], per job (zeroed by the caller).  spec: device copy; nplanes = spec->nplanes.
+hipError_t launch_fit_mask_lds(hipStream_t s, int W, const LdsSpec* spec, int nplanes, const uint32_t* ranks,
+                               int64_t npad, const uint32_t* aux, int64_t nblk,
+                               const uint16_t* codes, int64_t J, int64_t R, int64_t Tpad, int64_t pitch_bytes,
+                               uint8_t* mask, unsigned long long* counts);
+
 // kn / lo: the node-only score terms of prep_nodes (K(n) = (S(n) << 24) | gid, lo20(r1), lo24(r3)),
 // kept current by apply; see pe_kernels.hip node_prep for the exactness argument.
 hipError_t launch_prep_nodes(hipStream_t s, const int64_t* res, int64_t stride, int64_t Ns, uint64_t id_base,

@@ -12,6 +12,7 @@
 //
 // Integer compare/reduce only: no MFMA (nothing is a contraction).  Roofline = HBM / VALU issue.
 #include "pe_kernels.h"
+#include "pe_wave.h"
 
 namespace pe {
 
@@ -696,41 +697,6 @@ __device__ __forceinline__ void plane_job(u32x4& f, uint32_t lo, uint32_t hi, co
       : [lo] "v"(lo), [hi] "v"(hi), [k] "i"(K), "{v[32:63]}"(A), "{v[64:95]}"(B), "{v[96:127]}"(C),
         "{v[128:159]}"(Dq)
       : "scc");
-}
-
-// Column sums of a 64 x 64 block: p[k] holds, per lane, a partial count of job k; returns F with
-// F[l] = sum over all 64 lanes of p[sigma(l)] for a fixed permutation sigma of 0..63 (find it by
-// reducing a probe, p[k] = (lane == 0) ? k : 0).  Six halving levels, each pairing two registers
-// into one that carries both jobs on half the lanes: permlane32_swap (halves), permlane16_swap
-// (rows), then DPP row_ror:8, row_half_mirror, quad_perm [2,3,0,1], [1,0,3,2] with a lane select.
-// 141 VALU per 64 jobs, no dependent chains: 2.2 per job where a per-job wave sum costs ~12.
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_pair(uint32_t x, uint32_t y, bool take_y) {
-  const uint32_t tx = x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
-  const uint32_t ty = y + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)y, CTRL, 0xf, 0xf, false);
-  return take_y ? ty : tx;
-}
-
-__device__ __forceinline__ uint32_t reduce64x64(const uint32_t (&p)[64], int lane) {
-  uint32_t s1[32], s2[16], s3[8], s4[4], s5[2];
-#pragma unroll
-  for (int m = 0; m < 32; ++m) {
-    const auto r = __builtin_amdgcn_permlane32_swap(p[2 * m], p[2 * m + 1], false, false);
-    s1[m] = r[0] + r[1];
-  }
-#pragma unroll
-  for (int m = 0; m < 16; ++m) {
-    const auto r = __builtin_amdgcn_permlane16_swap(s1[2 * m], s1[2 * m + 1], false, false);
-    s2[m] = r[0] + r[1];
-  }
-  const bool b8 = lane & 8, b4 = lane & 4, b2 = lane & 2, b1 = lane & 1;
-#pragma unroll
-  for (int m = 0; m < 8; ++m) s3[m] = dpp_pair<0x128>(s2[2 * m], s2[2 * m + 1], b8);   // row_ror:8
-#pragma unroll
-  for (int m = 0; m < 4; ++m) s4[m] = dpp_pair<0x141>(s3[2 * m], s3[2 * m + 1], b4);   // row_half_mirror
-#pragma unroll
-  for (int m = 0; m < 2; ++m) s5[m] = dpp_pair<0x4e>(s4[2 * m], s4[2 * m + 1], b2);   // quad_perm [2,3,0,1]
-  return dpp_pair<0xb1>(s5[0], s5[1], b1);                                          // quad_perm [1,0,3,2]
 }
 
 // Jobs K .. 63 of a batch: select, store (row stride `step` u32x4), per-lane popcount into p[K].
