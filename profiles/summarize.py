@@ -14,17 +14,26 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from provenance import source_hash  # noqa: E402
 
 
+def kname(name: str) -> str:
+    """Kernel key: the demangled name without arguments, return type or template arguments
+    ("void pe::fit_mask_lds_kernel<2, 1, 1, 2>(...)" -> "pe::fit_mask_lds_kernel")."""
+    n = name.split("(")[0]
+    if n.startswith("void "):
+        n = n[5:]
+    return n.split("<")[0].strip()
+
+
 def main(d):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = {"source_hash": source_hash(root), "kernels": {}, "pmc": collections.defaultdict(dict)}
     for f in glob.glob(os.path.join(d, "trace", "*kernel_stats.csv")):
         for r in csv.DictReader(open(f)):
-            out["kernels"][r["Name"].split("(")[0]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+            out["kernels"][kname(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                                        "total_ns": float(r["TotalDurationNs"])}
     for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
         acc = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
-            acc[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append(float(r["Counter_Value"]))
+            acc[(kname(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
         for (k, c), v in acc.items():
             out["pmc"][k][c] = sum(v) / len(v)
     for k, p in out["pmc"].items():

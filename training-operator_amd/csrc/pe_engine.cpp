@@ -186,6 +186,7 @@ struct pe_ctx {
   // LDS digit-plane path (pe_kernels.h LdsSpec): spec, node-block geometry, codes, ranks
   pe::LdsSpec lds{};
   int lds_W = 4;                          // u32 words per lane per plane: block = 2048 W nodes
+  int lds_shape[3] = {0, 0, 0};           // fields with 3 / 2 / 1 digit levels (kernel template)
   int64_t lds_nblk = 0, lds_R = 1, lds_Tpad = 0, lds_npad = 0, lds_pitch = 0;   // pitch in u64 words
   DevBuf<pe::LdsSpec> lds_spec_d;
   DevBuf<int64_t> lds_vals;
@@ -961,6 +962,25 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uin
     }
   }
   if (!bestW) return false;
+  // fields in the kernel's order: three-level first, then two-level, then single-level
+  {
+    int ord[pe::LD_MAXF] = {0, 1, 2, 3};
+    std::stable_sort(ord, ord + sp.nf, [&](int x, int y) { return bestL[x] > bestL[y]; });
+    int d2[pe::LD_MAXF], L2[pe::LD_MAXF];
+    int64_t B2[pe::LD_MAXF];
+    for (int i = 0; i < sp.nf; ++i) {
+      d2[i] = fdim[ord[i]];
+      L2[i] = bestL[ord[i]];
+      B2[i] = bestB[ord[i]];
+    }
+    for (int i = 0; i < sp.nf; ++i) {
+      fdim[i] = d2[i];
+      bestL[i] = L2[i];
+      bestB[i] = B2[i];
+    }
+  }
+  int shape[3] = {0, 0, 0};
+  for (int i = 0; i < sp.nf; ++i) ++shape[3 - bestL[i]];
   // level specs, plane bases
   int32_t p = 0;
   int64_t voff = 0;
@@ -1002,17 +1022,19 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uin
   const int64_t lds_bytes = (int64_t)sp.nplanes * S / 8;
   const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(2, 163840 / std::max<int64_t>(lds_bytes, 1)));
   const int64_t slots = (int64_t)ctx->num_cu * per_cu;
+  // job phases R: every workgroup builds its block's planes before its share (1/R) of the jobs, so
+  // minimise rounds(R) x (prologue + 1/R) -- the prologue being ~2 % of one block's full job sweep
   int64_t R = 1;
-  double best_eff = 0;
+  double best_t = 1e300;
   for (int64_t r = 1; r <= 64 && (r == 1 || 16 * r <= n_jobs); ++r) {
-    const int64_t wg = nblk * r;
-    const double eff = (double)wg / (double)(((wg + slots - 1) / slots) * slots);
-    if (eff > best_eff + 1e-9) {
-      best_eff = eff;
+    const int64_t rounds = (nblk * r + slots - 1) / slots;
+    const double t = (double)rounds * (0.02 + 1.0 / (double)r);
+    if (t < best_t - 1e-9) {
+      best_t = t;
       R = r;
     }
-    if (eff > 0.97) break;
   }
+  if (const char* ev = std::getenv("PE_LDS_R")) R = std::max<int64_t>(1, std::atoll(ev));
   const int64_t Tmax = ((n_jobs + R - 1) / R + 15) / 16;
   const int64_t Tpad = round_up(std::max<int64_t>(Tmax, 1), 16);
   // job codes: u16 plane indices at the kernel's slots, stored in the kernel's consumption order
@@ -1047,6 +1069,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uin
   }
   ctx->lds = sp;
   ctx->lds_W = W;
+  for (int i = 0; i < 3; ++i) ctx->lds_shape[i] = shape[i];
   ctx->lds_nblk = nblk;
   ctx->lds_R = R;
   ctx->lds_Tpad = Tpad;
@@ -1125,7 +1148,7 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
   else if (planes_ok && build_planes(ctx, n_jobs, req, need, true)) ctx->fit_path = 3;
   else if ((ctx->fit_path_mask & PATH_CODED) && build_codes(ctx, n_jobs, req, need)) ctx->fit_path = 2;
   hipchk(ctx->fit_jobs.ensure(Jp), "alloc fit jobs");
-  const size_t mask_words = ctx->fit_path == 4   ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->lds_pitch
+  const size_t mask_words = ctx->fit_path == 4   ? (size_t)(n_jobs + 1) * ctx->lds_pitch   // + the scratch row
                             : ctx->fit_path == 3 ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->pl_nblk * 128
                             : ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
                                                  : (size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4;
@@ -1153,7 +1176,8 @@ static void fit_run(pe_ctx* ctx) {
     hipchk(pe::launch_node_ranks(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->lds_npad,
                                  ctx->lds_spec_d.p, ctx->lds_vals.p, ctx->lds_ranks.p, ctx->lds_aux.p),
            "launch node_ranks");
-    hipchk(pe::launch_fit_mask_lds(ctx->stream, ctx->lds_W, ctx->lds_spec_d.p, ctx->lds.nplanes, ctx->lds_ranks.p,
+    hipchk(pe::launch_fit_mask_lds(ctx->stream, ctx->lds_W, ctx->lds_shape, ctx->lds_spec_d.p, ctx->lds.nplanes,
+                                   ctx->lds_ranks.p,
                                    ctx->lds_npad, ctx->lds_aux.p, ctx->lds_nblk, ctx->lds_codes.p, J,
                                    ctx->lds_R, ctx->lds_Tpad, ctx->lds_pitch * 8,
                                    reinterpret_cast<uint8_t*>(ctx->mask.p), ctx->counts.p),

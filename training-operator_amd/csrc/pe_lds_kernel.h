@@ -1,0 +1,181 @@
+// The LDS digit-plane fit kernel (pe_kernels.h LdsSpec), templated on the block size W and on the
+// batch's field shape: N3 fields of three digit levels, then N2 of two, then N1 of one (the host
+// orders the fields that way).  With the shape fixed at compile time a job's body is straight-line
+// code -- every plane read issued first, one AND-OR per level, no branches -- so the scheduler can
+// overlap consecutive jobs of the 16-job batch.  Included by pe_lds_w{1,2,4}.hip, one W each.
+#pragma once
+#include "pe_kernels.h"
+#include "pe_wave.h"
+
+namespace pe {
+
+template <int W> struct LdVec;
+template <> struct LdVec<1> { typedef uint32_t T; };
+template <> struct LdVec<2> { typedef uint32_t T __attribute__((ext_vector_type(2))); };
+template <> struct LdVec<4> { typedef uint32_t T __attribute__((ext_vector_type(4))); };
+
+template <int W>
+__device__ __forceinline__ uint32_t popc_vec(typename LdVec<W>::T v) {
+  if constexpr (W == 1) return __popc(v);
+  else if constexpr (W == 2) return __popc(v.x) + __popc(v.y);
+  else return __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+}
+
+// Plane p's slice of lane `lane` (W u32 words: nodes 32 W lane .. +32 W - 1 of the block).
+template <int W>
+__device__ __forceinline__ typename LdVec<W>::T plane_rd(const uint32_t* lds, uint32_t p, int lane) {
+  return *reinterpret_cast<const typename LdVec<W>::T*>(lds + p * (64u * W) + (uint32_t)lane * W);
+}
+
+// One workgroup = node block blk (S = 2048 W nodes) x job phase r.
+//  1. zero the digit planes; scatter one equality bit per (node, field, level) into the plane of its
+//     digit -- work items are (field, level, u32 word column), so no two threads write one word;
+//  2. suffix OR per (field, level): GE(v) = E(v) | GE(v + 1), turning equality into threshold planes;
+//     need planes by wave ballots (label test AND the folded dimensions);
+//  3. waves stream jobs r + R (w + 16 t): per job the need plane AND, per field, the last level's
+//     plane, then GE_k(c + 1) | (GE_k(c) & acc) per higher level; the slice is stored, its popcount
+//     joins a 16-job batch that one column sum (reduce16x64) turns into 16 per-job atomics.  A batch
+//     is always 16 jobs: past the wave's last job the slices go to the scratch row J.
+template <int W, int N3, int N2, int N1>
+__global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec* __restrict__ spp,
+                                                                  const uint32_t* __restrict__ ranks, int64_t npad,
+                                                                  const uint32_t* __restrict__ aux, int64_t nblk,
+                                                                  const uint2* __restrict__ codes, int64_t J,
+                                                                  int64_t R, int64_t Tpad, int64_t pitch_bytes,
+                                                                  uint8_t* __restrict__ mask,
+                                                                  unsigned long long* __restrict__ counts) {
+  typedef typename LdVec<W>::T V;
+  constexpr int S = 2048 * W;                 // nodes per block
+  constexpr int WPP = S / 32;                 // u32 words per plane
+  extern __shared__ uint32_t lds[];
+  const LdsSpec& sp = *spp;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t blk = blockIdx.x % nblk, r = blockIdx.x / nblk;
+  const int64_t n0 = blk * S;
+
+  // 1. equality bits
+  const int ndig = sp.need_pbase * WPP;       // digit planes occupy planes [0, need_pbase)
+  for (int i = tid; i < ndig; i += LD_THREADS) lds[i] = 0u;
+  __syncthreads();
+  int cols = 0;                               // (field, level, word column) items
+  for (int f = 0; f < sp.nf; ++f) cols += sp.L[f] * WPP;
+  for (int c = tid; c < cols; c += LD_THREADS) {
+    int f = 0, rest = c;
+    while (rest >= sp.L[f] * WPP) rest -= sp.L[f++] * WPP;
+    const int k = rest / WPP, w = rest % WPP;
+    const uint32_t* rk = ranks + f * npad + n0 + 32 * w;
+    const uint32_t dv = sp.div[f][k], md = sp.mod[f][k];
+    const int vlo = sp.vlo[f][k], nv = sp.nv[f][k];
+    uint32_t* const base = lds + sp.pbase[f][k] * WPP + w;
+    for (int b = 0; b < 32; ++b) {
+      uint32_t d = rk[b] / dv;
+      if (md) d %= md;
+      const int v = (int)d - vlo;
+      if (v >= 0 && v < nv) base[v * WPP] |= 1u << b;
+    }
+  }
+  __syncthreads();
+  // 2. threshold planes, one (field, level, word) column per thread; need planes by ballots
+  for (int c = tid; c < cols; c += LD_THREADS) {
+    int f = 0, rest = c;
+    while (rest >= sp.L[f] * WPP) rest -= sp.L[f++] * WPP;
+    const int k = rest / WPP, w = rest % WPP;
+    uint32_t* const base = lds + sp.pbase[f][k] * WPP + w;
+    uint32_t acc = 0u;
+    for (int v = sp.nv[f][k] - 1; v >= 0; --v) {
+      acc |= base[v * WPP];
+      base[v * WPP] = acc;
+    }
+  }
+  for (int g = wave; g < S / 64; g += LD_THREADS / 64) {
+    const int64_t n = n0 + 64 * g + lane;
+    const bool ok = aux[n] != 0u;
+    const uint32_t lab = aux[npad + n];
+    for (int i = 0; i < sp.nneed; ++i) {
+      const uint64_t b = __ballot(ok && (lab & sp.needs[i]) == sp.needs[i]);
+      if (lane == 0) *reinterpret_cast<uint64_t*>(lds + (sp.need_pbase + i) * WPP + 2 * g) = b;
+    }
+  }
+  __syncthreads();
+
+  // 3. the jobs of this wave: j = r + R (wave + 16 t), t < T.  Their codes are contiguous (the t-major
+  //    run of wave (r, wave), padded to 16 jobs): a 16-job batch is 512 B, one 8-B load per lane
+  //    issued a batch ahead; lane 4K + i holds dwords 2i, 2i + 1 of batch job K (v_readlane).
+  const int64_t j0 = r + R * wave, step = 16 * R;
+  const int64_t T = j0 < J ? (J - j0 + step - 1) / step : 0;
+  uint8_t* const col = mask + blk * (S / 8) + lane * (4 * W);
+  const uint2* const cb = codes + (r * 16 + wave) * Tpad * (LD_CODE / 4);
+  uint32_t sigma;
+  {
+    uint32_t probe[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) probe[k] = lane == 0 ? (uint32_t)k : 0u;
+    sigma = reduce16x64(probe, lane);
+  }
+  uint2 cv = T > 0 ? cb[lane] : make_uint2(0u, 0u);
+  for (int64_t t0 = 0; t0 < T; t0 += 16) {
+    const int n = (int)min<int64_t>(16, T - t0);
+    const uint2 cur = cv;
+    if (t0 + 16 < T) cv = cb[(t0 + 16) * (LD_CODE / 4) + lane];   // next batch, in flight meanwhile
+    uint32_t p[16];
+#pragma unroll
+    for (int K = 0; K < 16; ++K) {
+      const int64_t j = K < n ? j0 + step * (t0 + K) : J;           // past the run: the scratch row
+      auto entry = [&](int e) -> uint32_t {                           // u16 entry e of job K
+        const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)((e & 2) ? cur.y : cur.x), 4 * K + e / 4);
+        return (e & 1) ? d >> 16 : d & 0xFFFFu;
+      };
+      V f = plane_rd<W>(lds, entry(LD_NEED_SLOT), lane);
+#pragma unroll
+      for (int fi = 0; fi < N3; ++fi) {
+        const uint32_t p1 = entry(3 * fi + 1), p2 = entry(3 * fi + 2);
+        V a = plane_rd<W>(lds, entry(3 * fi), lane);
+        const V g1 = plane_rd<W>(lds, p1, lane), h1 = plane_rd<W>(lds, p1 + 1, lane);
+        const V g2 = plane_rd<W>(lds, p2, lane), h2 = plane_rd<W>(lds, p2 + 1, lane);
+        a = h1 | (g1 & a);
+        a = h2 | (g2 & a);
+        f &= a;
+      }
+#pragma unroll
+      for (int fi = N3; fi < N3 + N2; ++fi) {
+        const uint32_t p1 = entry(3 * fi + 1);
+        V a = plane_rd<W>(lds, entry(3 * fi), lane);
+        const V g1 = plane_rd<W>(lds, p1, lane), h1 = plane_rd<W>(lds, p1 + 1, lane);
+        a = h1 | (g1 & a);
+        f &= a;
+      }
+#pragma unroll
+      for (int fi = N3 + N2; fi < N3 + N2 + N1; ++fi) f &= plane_rd<W>(lds, entry(3 * fi), lane);
+      *reinterpret_cast<V*>(col + j * pitch_bytes) = f;
+      p[K] = popc_vec<W>(f);
+    }
+    const uint32_t F = reduce16x64(p, lane);
+    if ((lane & 3) == 0 && sigma < (uint32_t)n && F)
+      atomicAdd(&counts[j0 + step * (t0 + sigma)], (unsigned long long)F);
+  }
+}
+
+// Every field shape (N3, N2, N1) with N3 + N2 + N1 <= LD_MAXF.
+#define PE_LDS_SHAPES(X, W)                                                                               \
+  X(W, 0, 0, 0) X(W, 0, 0, 1) X(W, 0, 1, 0) X(W, 1, 0, 0) X(W, 0, 0, 2) X(W, 0, 1, 1) X(W, 0, 2, 0)         \
+  X(W, 1, 0, 1) X(W, 1, 1, 0) X(W, 2, 0, 0) X(W, 0, 0, 3) X(W, 0, 1, 2) X(W, 0, 2, 1) X(W, 0, 3, 0)         \
+  X(W, 1, 0, 2) X(W, 1, 1, 1) X(W, 1, 2, 0) X(W, 2, 0, 1) X(W, 2, 1, 0) X(W, 3, 0, 0) X(W, 0, 0, 4)         \
+  X(W, 0, 1, 3) X(W, 0, 2, 2) X(W, 0, 3, 1) X(W, 0, 4, 0) X(W, 1, 0, 3) X(W, 1, 1, 2) X(W, 1, 2, 1)         \
+  X(W, 1, 3, 0) X(W, 2, 0, 2) X(W, 2, 1, 1) X(W, 2, 2, 0) X(W, 3, 0, 1) X(W, 3, 1, 0) X(W, 4, 0, 0)
+
+// The kernel of block size W for shape (n3, n2, n1); nullptr for a shape outside the table.
+template <int W>
+const void* lds_kernel_for(int n3, int n2, int n1) {
+#define PE_LDS_PICK(W_, a, b, c) \
+  if (n3 == a && n2 == b && n1 == c) return (const void*)fit_mask_lds_kernel<W_, a, b, c>;
+  PE_LDS_SHAPES(PE_LDS_PICK, W)
+#undef PE_LDS_PICK
+  return nullptr;
+}
+
+const void* lds_kernel_w1(int n3, int n2, int n1);
+const void* lds_kernel_w2(int n3, int n2, int n1);
+const void* lds_kernel_w4(int n3, int n2, int n1);
+
+}  // namespace pe

@@ -1,0 +1,8 @@
+// LDS digit-plane fit kernels of block size 2048 nodes (W = 1), every field shape.
+#include "pe_lds_kernel.h"
+
+namespace pe {
+
+const void* lds_kernel_w1(int n3, int n2, int n1) { return lds_kernel_for<1>(n3, n2, n1); }
+
+}  // namespace pe
