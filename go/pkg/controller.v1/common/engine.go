@@ -1,0 +1,88 @@
+/*
+Engine-backed CalcPGMinResources: a drop-in for pkg/controller.v1/common/util.go:108 with the same
+signature, wired in at job.go:455-457:
+
+	func (jc *JobController) calcPGMinResources(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpec) *corev1.ResourceList {
+		return jc.calcPGMinResourcesFn(minMember, replicas, jc.PriorityClassLister.Get)
+	}
+	// jc.calcPGMinResourcesFn = CalcPGMinResourcesEngine(engine, "nvidia.com/gpu") (or CalcPGMinResources)
+
+The flattening restates util.go:108-145: one group per replica type in ReplicasPriority order
+(priority desc; the reference breaks equal priorities by Go map order, which is random -- here by
+type name, one of the orders the reference can produce), Replicas nil -> -1 (the type is skipped,
+util.go:129), and per container the effective list AddResourceList adds (util.go:79-104): Requests,
+or Limits only when the Requests map is nil (an empty non-nil map does not fall back).  Init
+containers and pod overhead are not counted (util.go:138).  The engine counts pods up to minMember
+exactly as the per-pod loop.  Inputs the tensor path does not hold exactly go to the reference's
+CalcPGMinResources unchanged, so the answer is the reference's for every input.
+*/
+package common
+
+import (
+	"sort"
+
+	apiv1 "github.com/kubeflow/training-operator/pkg/apis/kubeflow.org/v1"
+	"github.com/kubeflow/training-operator/pkg/placement/hip"
+	v1 "k8s.io/api/core/v1"
+)
+
+// flattenV1 builds the one-job v1 CSR of CalcPGMinResources(minMember, replicas, pcGetFunc).
+func flattenV1(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpec, pcGetFunc PriorityClassGetFunc,
+	gpuName string) (*hip.CSR, error) {
+	type typed struct {
+		name     string
+		priority int32
+		spec     *apiv1.ReplicaSpec
+	}
+	order := make([]typed, 0, len(replicas))
+	for t, replica := range replicas {
+		rp := typed{name: string(t), spec: replica}
+		if pc, err := pcGetFunc(replica.Template.Spec.PriorityClassName); err == nil && pc != nil {
+			rp.priority = pc.Value // util.go:114-119: a failed lookup counts as priority 0
+		}
+		order = append(order, rp)
+	}
+	sort.SliceStable(order, func(i, j int) bool {
+		if order[i].priority != order[j].priority {
+			return order[i].priority > order[j].priority // ReplicasPriority.Less, util.go:42-44
+		}
+		return order[i].name < order[j].name
+	})
+	b := &hip.CSR{}
+	for _, t := range order {
+		for _, c := range t.spec.Template.Spec.Containers {
+			rl := c.Resources.Requests
+			if rl == nil { // AddResourceList: Limits only when Requests is nil (util.go:90-92)
+				rl = c.Resources.Limits
+			}
+			if err := b.AddContainer(rl, hip.KindContainer, gpuName); err != nil {
+				return nil, err
+			}
+		}
+		replicasOrNil := int32(-1)
+		if t.spec.Replicas != nil {
+			replicasOrNil = *t.spec.Replicas
+		}
+		b.EndGroup(replicasOrNil)
+	}
+	b.EndJob(minMember)
+	return b, nil
+}
+
+// CalcPGMinResourcesEngine returns a CalcPGMinResources with the pod counting and the resource sums
+// on the GPU.  Like the reference it never returns nil.
+func CalcPGMinResourcesEngine(eng *hip.Engine, gpuName string) func(int32, map[apiv1.ReplicaType]*apiv1.ReplicaSpec,
+	PriorityClassGetFunc) *v1.ResourceList {
+	return func(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpec, pcGetFunc PriorityClassGetFunc) *v1.ResourceList {
+		csr, err := flattenV1(minMember, replicas, pcGetFunc, gpuName)
+		if err != nil {
+			return CalcPGMinResources(minMember, replicas, pcGetFunc) // exact reference path
+		}
+		agg, err := eng.PGMinResources(hip.ModeV1, csr)
+		if err != nil || agg.Overflow[0] != 0 {
+			return CalcPGMinResources(minMember, replicas, pcGetFunc)
+		}
+		rl := agg.Unflatten(0, gpuName, nil)
+		return &rl
+	}
+}

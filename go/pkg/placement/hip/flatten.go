@@ -1,0 +1,120 @@
+package hip
+
+// Object graph <-> engine CSR conversion shared by the v1 and v2 adapters (pure Go, no cgo).
+// Canonical units (SURVEY.md Appendix A): cpu in milli-cores (exact iff the Quantity has no finer
+// scale), memory / ephemeral-storage in bytes and the accelerator in units (exact iff integral).
+// Anything else -- another resource key, an inexact or negative value -- is refused, and the
+// adapters answer those objects with the reference's own arbitrary-precision code.
+
+import (
+	"fmt"
+
+	corev1 "k8s.io/api/core/v1"
+	"k8s.io/apimachinery/pkg/api/resource"
+)
+
+// DimNames are the resource keys of the four engine dimensions.
+func DimNames(gpuName string) [4]corev1.ResourceName {
+	return [4]corev1.ResourceName{corev1.ResourceCPU, corev1.ResourceMemory, corev1.ResourceName(gpuName),
+		corev1.ResourceEphemeralStorage}
+}
+
+// ErrNotTensor: an input the int64 tensor path does not represent exactly.
+type ErrNotTensor struct{ Reason string }
+
+func (e *ErrNotTensor) Error() string { return "placement: not representable: " + e.Reason }
+
+// Canonical is the engine's int64 for quantity q of dimension d.
+func Canonical(d int, q resource.Quantity) (int64, error) {
+	if q.Sign() < 0 {
+		return 0, &ErrNotTensor{fmt.Sprintf("negative quantity %s", q.String())}
+	}
+	if d == 0 { // cpu: milli-cores, exact only if q has no finer scale than 1m
+		m := q.MilliValue()
+		if resource.NewMilliQuantity(m, q.Format).Cmp(q) != 0 {
+			return 0, &ErrNotTensor{fmt.Sprintf("cpu %s is finer than 1m", q.String())}
+		}
+		return m, nil
+	}
+	v, ok := q.AsInt64()
+	if !ok {
+		return 0, &ErrNotTensor{fmt.Sprintf("%s is not an exact int64", q.String())}
+	}
+	return v, nil
+}
+
+// AddContainer appends one container record: its ResourceList's keys (present even when zero) and
+// canonical values, with the record kind.  rl == nil is a record with no keys.
+func (b *CSR) AddContainer(rl corev1.ResourceList, kind uint8, gpuName string) error {
+	names := DimNames(gpuName)
+	var vec [4]int64
+	var present uint8
+	for key, q := range rl {
+		d := -1
+		for i, n := range names {
+			if n == key {
+				d = i
+			}
+		}
+		if d < 0 {
+			return &ErrNotTensor{fmt.Sprintf("resource %q is not an engine dimension", key)}
+		}
+		v, err := Canonical(d, q)
+		if err != nil {
+			return err
+		}
+		vec[d] = v
+		present |= 1 << uint(d)
+	}
+	b.ContReq = append(b.ContReq, vec[:]...)
+	b.ContFlags = append(b.ContFlags, present|kind<<KindShift)
+	return nil
+}
+
+// EndGroup closes the current group (replicas: -1 = nil, v1) and EndJob the current job.
+func (b *CSR) EndGroup(replicas int32) {
+	if len(b.GroupContOff) == 0 {
+		b.GroupContOff = append(b.GroupContOff, 0)
+	}
+	b.GroupReplicas = append(b.GroupReplicas, replicas)
+	b.GroupContOff = append(b.GroupContOff, int32(len(b.ContFlags)))
+}
+
+func (b *CSR) EndJob(minMember int32) {
+	if len(b.JobGroupOff) == 0 {
+		b.JobGroupOff = append(b.JobGroupOff, 0)
+	}
+	if len(b.GroupContOff) == 0 {
+		b.GroupContOff = append(b.GroupContOff, 0)
+	}
+	b.MinMember = append(b.MinMember, minMember)
+	b.JobGroupOff = append(b.JobGroupOff, int32(len(b.GroupReplicas)))
+}
+
+// Unflatten turns job j's result back into a ResourceList: one entry per present key (zero values
+// included, as the reference's maps hold them).  formats, when given, is the Quantity format per
+// dimension the reference's Add would have kept (the first contributing quantity's), so that
+// String() prints identically; equality (Cmp) never depends on it.
+func (a *Agg) Unflatten(j int, gpuName string, formats *[4]resource.Format) corev1.ResourceList {
+	names := DimNames(gpuName)
+	out := corev1.ResourceList{}
+	for d := 0; d < Dims; d++ {
+		if a.Present[j]&(1<<uint(d)) == 0 {
+			continue
+		}
+		v := a.MinRes[j*Dims+d]
+		f := resource.DecimalSI
+		if d == 1 || d == 3 {
+			f = resource.BinarySI
+		}
+		if formats != nil {
+			f = formats[d]
+		}
+		if d == 0 {
+			out[names[d]] = *resource.NewMilliQuantity(v, f)
+		} else {
+			out[names[d]] = *resource.NewQuantity(v, f)
+		}
+	}
+	return out
+}

@@ -1,0 +1,135 @@
+/*
+Engine-backed CoScheduling plugin: a drop-in for coscheduling.New in the v2 plugin registry.
+
+The reference plugin is pkg/runtime.v2/framework/plugins/coscheduling/coscheduling.go.  This file is
+added next to it (same package) and keeps everything but the aggregation: EnforcePodGroupPolicy,
+the watch extension (ReconcilerBuilders, coscheduling.go:298-320), the indexers set up by New
+(:71-85) and needsCreateOrUpdate (:150-153) are the reference's own.  Build (:103-148) computes
+MinMember / MinResources (:108-118) with one pe_pg_min_resources(PE_MODE_V2) call on the GPU
+instead of the Quantity loop; objects the int64 tensor path does not hold exactly (another resource
+key, an inexact value, an int64 overflow) go through the reference's Build unchanged.
+
+Registration (registry.go:32-42) -- the same name, so the framework's type assertions
+(framework.go:53-77) see the same capabilities:
+
+	func NewRegistryWithEngine(eng *hip.Engine, gpuName string) Registry {
+		r := NewRegistry()
+		r[coscheduling.Name] = coscheduling.NewWithEngine(eng, gpuName)
+		return r
+	}
+*/
+package coscheduling
+
+import (
+	"context"
+	"sort"
+
+	corev1 "k8s.io/api/core/v1"
+	apierrors "k8s.io/apimachinery/pkg/api/errors"
+	metav1 "k8s.io/apimachinery/pkg/apis/meta/v1"
+	"k8s.io/utils/ptr"
+	"sigs.k8s.io/controller-runtime/pkg/client"
+	ctrlutil "sigs.k8s.io/controller-runtime/pkg/controller/controllerutil"
+	schedulerpluginsv1alpha1 "sigs.k8s.io/scheduler-plugins/apis/scheduling/v1alpha1"
+
+	kubeflowv2 "github.com/kubeflow/training-operator/pkg/apis/kubeflow.org/v2alpha1"
+	"github.com/kubeflow/training-operator/pkg/constants"
+	"github.com/kubeflow/training-operator/pkg/placement/hip"
+	runtime "github.com/kubeflow/training-operator/pkg/runtime.v2"
+	"github.com/kubeflow/training-operator/pkg/runtime.v2/framework"
+)
+
+// EngineCoScheduling is CoScheduling with Build's aggregation on the GPU.
+type EngineCoScheduling struct {
+	*CoScheduling
+	eng     *hip.Engine
+	gpuName string
+}
+
+var _ framework.EnforcePodGroupPolicyPlugin = (*EngineCoScheduling)(nil)
+var _ framework.WatchExtensionPlugin = (*EngineCoScheduling)(nil)
+var _ framework.ComponentBuilderPlugin = (*EngineCoScheduling)(nil)
+
+// NewWithEngine returns the plugin factory (registry.go:32's signature) of the engine-backed plugin.
+func NewWithEngine(eng *hip.Engine, gpuName string) func(ctx context.Context, c client.Client,
+	indexer client.FieldIndexer) (framework.Plugin, error) {
+	return func(ctx context.Context, c client.Client, indexer client.FieldIndexer) (framework.Plugin, error) {
+		p, err := New(ctx, c, indexer) // indexers + client exactly as the reference (coscheduling.go:71-85)
+		if err != nil {
+			return nil, err
+		}
+		return &EngineCoScheduling{CoScheduling: p.(*CoScheduling), eng: eng, gpuName: gpuName}, nil
+	}
+}
+
+// flattenInfo turns info.TotalRequests into the engine's v2 CSR: one job, one group per entry
+// (Replicas, and its PodRequests as one container record -- NewInfo has already applied kueue's
+// TotalRequests, runtime.go:130-136).  Entries in name order (the sum does not depend on it).
+func flattenInfo(info *runtime.Info, gpuName string) (*hip.CSR, error) {
+	names := make([]string, 0, len(info.TotalRequests))
+	for name := range info.TotalRequests {
+		names = append(names, name)
+	}
+	sort.Strings(names)
+	b := &hip.CSR{}
+	for _, name := range names {
+		trr := info.TotalRequests[name]
+		if err := b.AddContainer(trr.PodRequests, hip.KindContainer, gpuName); err != nil {
+			return nil, err
+		}
+		b.EndGroup(trr.Replicas)
+	}
+	b.EndJob(0)
+	return b, nil
+}
+
+// unflatten is job 0's ResourceList.
+func unflatten(agg *hip.Agg, gpuName string) corev1.ResourceList { return agg.Unflatten(0, gpuName, nil) }
+
+// Build is coscheduling.go:103-148 with the aggregation (:108-118) on the engine.
+func (c *EngineCoScheduling) Build(ctx context.Context, obj client.Object, info *runtime.Info,
+	trainJob *kubeflowv2.TrainJob) (client.Object, error) {
+	if info == nil || info.RuntimePolicy.PodGroupPolicy == nil || info.RuntimePolicy.PodGroupPolicy.Coscheduling == nil || trainJob == nil {
+		return nil, nil
+	}
+	csr, err := flattenInfo(info, c.gpuName)
+	if err != nil {
+		return c.CoScheduling.Build(ctx, obj, info, trainJob) // exact reference path (inf.Dec, other keys)
+	}
+	agg, err := c.eng.PGMinResources(hip.ModeV2, csr)
+	if err != nil {
+		return nil, err
+	}
+	if agg.Overflow[0] != 0 {
+		return c.CoScheduling.Build(ctx, obj, info, trainJob)
+	}
+	newPG := &schedulerpluginsv1alpha1.PodGroup{
+		TypeMeta: metav1.TypeMeta{
+			APIVersion: schedulerpluginsv1alpha1.SchemeGroupVersion.String(),
+			Kind:       constants.PodGroupKind,
+		},
+		ObjectMeta: metav1.ObjectMeta{
+			Name:      trainJob.Name,
+			Namespace: trainJob.Namespace,
+		},
+		Spec: schedulerpluginsv1alpha1.PodGroupSpec{
+			ScheduleTimeoutSeconds: info.RuntimePolicy.PodGroupPolicy.Coscheduling.ScheduleTimeoutSeconds,
+			MinMember:              agg.Members[0],
+			MinResources:           unflatten(agg, c.gpuName),
+		},
+	}
+	if err := ctrlutil.SetControllerReference(trainJob, newPG, c.scheme); err != nil {
+		return nil, err
+	}
+	oldPG := &schedulerpluginsv1alpha1.PodGroup{}
+	if err := c.client.Get(ctx, client.ObjectKeyFromObject(newPG), oldPG); err != nil {
+		if !apierrors.IsNotFound(err) {
+			return nil, err
+		}
+		oldPG = nil
+	}
+	if needsCreateOrUpdate(oldPG, newPG, ptr.Deref(trainJob.Spec.Suspend, false)) {
+		return newPG, nil
+	}
+	return nil, nil
+}
