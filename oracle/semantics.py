@@ -103,8 +103,8 @@ def add_resource_list(lst: ResourceList, req: Optional[ResourceList], limit: Opt
 
 
 def get_total_replicas(replicas: Dict[str, dict]) -> int:
-    """k8sutil.go:126-137: nil Replicas counts as 1."""
-    return sum(1 if r.get("replicas") is None else int(r["replicas"]) for r in replicas.values())
+    """k8sutil.go:126-137: nil Replicas counts as 1; the int32 sum wraps like Go's."""
+    return _wrap_int32(sum(1 if r.get("replicas") is None else int(r["replicas"]) for r in replicas.values()))
 
 
 def _v1_order(replicas: Dict[str, dict], pc_get: Callable[[str], Optional[int]]) -> List[Tuple[int, str]]:
@@ -252,3 +252,65 @@ def needs_create_or_update(old: Optional[dict], new: dict, suspended: bool) -> b
 def same_resource_list(a: ResourceList, b: ResourceList) -> bool:
     """Reference equality: same key set, each value equal under Quantity.Cmp."""
     return set(a) == set(b) and all(Fraction(a[k]) == Fraction(b[k]) for k in a)
+
+
+# --------------------------------------------------------------------------- placement (Appendix B)
+
+SCORE_MAX = (1 << 40) - 1
+
+
+def appendix_b_key(res4, labels: int, q4, need: int, node: int) -> Optional[int]:
+    """SURVEY.md Appendix B, restated independently of oracle.c: None when the node does not fit,
+    else (score << 24) | node with score = sat40(sat40(l0) + sat40(l1 >> 20) + sat40(l2 << 20) +
+    sat40(l3 >> 24)), l = residual - request (all non-negative for a fitting node)."""
+    if (labels & need) != need:
+        return None
+    left = [int(r) - int(q) for r, q in zip(res4, q4)]
+    if any(v < 0 for v in left):
+        return None
+    terms = [left[0], left[1] >> 20, left[2] << 20, left[3] >> 24]
+    score = min(SCORE_MAX, sum(min(SCORE_MAX, t) for t in terms))
+    return (score << 24) | node
+
+
+def place_greedy_appendix_b(res, labels, job_group_off, priority, group_count, group_req, group_need):
+    """The sequential greedy rule in plain Python (small inputs only): jobs by (priority desc, index
+    asc), groups in order, each pod on the argmin-key node, all-or-nothing per job with rollback.
+    Returns (pod_node list, job_status list, residual [4][N] as lists of ints)."""
+    R = [[int(x) for x in row] for row in res]
+    N = len(R[0]) if R else 0
+    J = len(priority)
+    pod_off = [0]
+    for c in group_count:
+        pod_off.append(pod_off[-1] + max(0, int(c)))
+    pods = [-1] * pod_off[-1]
+    status = [0] * J
+    order = sorted(range(J), key=lambda j: (-int(priority[j]), j))
+    for j in order:
+        placed = []
+        ok = True
+        for g in range(int(job_group_off[j]), int(job_group_off[j + 1])):
+            q = [int(x) for x in group_req[g]]
+            for p in range(int(group_count[g])):
+                best = None
+                for n in range(N):
+                    k = appendix_b_key([R[d][n] for d in range(4)], int(labels[n]), q, int(group_need[g]), n)
+                    if k is not None and (best is None or k < best):
+                        best = k
+                if best is None:
+                    ok = False
+                    break
+                n = best & 0xFFFFFF
+                for d in range(4):
+                    R[d][n] -= q[d]
+                pods[pod_off[g] + p] = n
+                placed.append((g, p, n))
+            if not ok:
+                break
+        if not ok:
+            for g, p, n in placed:
+                for d in range(4):
+                    R[d][n] += int(group_req[g][d])
+                pods[pod_off[g] + p] = -1
+            status[j] = 1
+    return pods, status, R

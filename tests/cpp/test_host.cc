@@ -264,6 +264,11 @@ TEST_CPU(TestGetTotalReplicas) {
   auto r = mnist(3);
   r["Worker"].replicas.reset();                   // nil counts as 1 (k8sutil.go:131-133)
   CHECK(GetTotalReplicas(r) == 2);
+  // Go's int32 sum wraps: INT32_MAX + 1 (the nil Worker) is INT32_MIN
+  r["Master"].replicas = INT32_MAX;
+  CHECK(GetTotalReplicas(r) == INT32_MIN);
+  r["Worker"].replicas = INT32_MAX;
+  CHECK(GetTotalReplicas(r) == -2);
 }
 
 // framework_test.go:154-253 TestRunEnforceMLPolicyPlugins

@@ -248,7 +248,8 @@ def test_fit_mask_path_fallbacks(eng, case):
 
 
 @pytest.mark.parametrize("N,J,shape", [(3000, 400, "cpu400"), (20000, 5000, "wide"), (123 * 8192 - 7, 700, "wide"),
-                                       (9000, 2000, "unique_mem"), (70000, 64, "wide"), (3000, 1, "wide")])
+                                       (9000, 2000, "unique_mem"), (70000, 64, "wide"), (3000, 1, "wide"),
+                                       (3 * 8192 + 777, 1200, "needs_sets")])
 def test_fit_mask_plane_sets(N, J, shape):
     """Batches with more than 32 distinct (dimension, value) pairs split into plane sets, each
     encoded and swept by the indexed-row kernel: mask rows and counts exact vs the oracle; the
@@ -263,6 +264,12 @@ def test_fit_mask_plane_sets(N, J, shape):
         req[:, 1] = rng.integers(1, 60, J) * (1 << 28)
         req[:, 3] = rng.integers(0, 30, J) * (1 << 30)
         need[:] = rng.integers(0, 4, J).astype(np.uint32) << 1
+    elif shape == "needs_sets":
+        # label-need planes (kind 4) in every set, at least 3 sets, and a last 512-node encode
+        # segment that is partial: the per-set offsets and the valid-node masking of the encode meet
+        req[:, 0] = 100 * (1 + np.arange(J) % 90)
+        need[:] = (np.arange(J) % 6).astype(np.uint32) << 1
+        inv.labels[:] |= (np.arange(N, dtype=np.uint32) % 7).astype(np.uint32) << 1
     else:                                                               # unique memory per job
         req[:, 1] = (1 << 30) + np.arange(J) * 4096
     e = Engine(0, fit_path_mask=16)                       # bit planes (+ the int64 fallback), no LDS
@@ -276,8 +283,10 @@ def test_fit_mask_plane_sets(N, J, shape):
     # planes when the sets fit (<= 256: 400 cpu values make ~31 sets; independent random values in
     # every dimension need hundreds), else a fallback path; exact either way
     assert s["fit_runs_planes"] + s["fit_runs_coded"] + s["fit_runs_i32"] + s["fit_runs_i64"] == 1
-    if shape == "cpu400" or pairs <= 32:
+    if shape in ("cpu400", "needs_sets") or pairs <= 32:
         assert s["fit_runs_planes"] == 1 and e.fit_mask_layout() == 3
+    if shape == "needs_sets":
+        assert s["fit_runs_sets"] == 1 and pairs > 3 * 32      # more pairs than 3 sets hold
     # a second run over the same upload is identical (counts re-zeroed, every set re-encoded)
     np.testing.assert_array_equal(e.fit_mask(req, need), o_counts)
     e.close()

@@ -1721,7 +1721,18 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         if (trace) tr_post.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
       });
       std::vector<pe::Update> upd;
-      const bool consumed = timed_resolve(cur, upd, &seed);
+      bool consumed = false;
+      try {
+        consumed = timed_resolve(cur, upd, &seed);
+      } catch (...) {
+        // the helper task still reads pend / nxt (locals of this loop): let it finish before the
+        // unwinding frees them, then report the resolver's error (the helper's is secondary)
+        try {
+          worker->wait();
+        } catch (...) {
+        }
+        throw;
+      }
       worker->wait();
       if (R.done()) {
         hipchk(hipStreamSynchronize(s), "sync speculative");

@@ -216,9 +216,9 @@ struct FormatAcc {
 // ------------------------------------------------------------------ v1
 
 int32_t GetTotalReplicas(const std::map<ReplicaType, ReplicaSpec>& replicas) {
-  int32_t total = 0;
-  for (const auto& kv : replicas) total += kv.second.replicas ? *kv.second.replicas : 1;  // k8sutil.go:131-133
-  return total;
+  uint32_t total = 0;   // Go int32 addition wraps; signed overflow would be UB here, so add unsigned
+  for (const auto& kv : replicas) total += (uint32_t)(kv.second.replicas ? *kv.second.replicas : 1);  // k8sutil.go:131-133
+  return (int32_t)total;
 }
 
 std::map<std::string, Format> MinResourcesFormatsV1(int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
