@@ -1,0 +1,50 @@
+"""One rank of tests/test_gpu_multiproc.py: a separate process holding one inventory shard context of
+the engine on device 0, exchanging the per-window candidate blobs with the other ranks over gloo
+(the pe_config.exchange hook -- RCCL's role on a multi-GPU node).  Writes its results to out_dir.
+
+    python tests/mp_shard_worker.py <rank> <world> <port> <mix> <n_nodes> <n_jobs> <out_dir>
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "training-operator_amd")):
+    sys.path.insert(0, p)
+
+
+def main():
+    rank, world, port = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    mix, n_nodes, n_jobs, out_dir = sys.argv[4], int(sys.argv[5]), int(sys.argv[6]), sys.argv[7]
+    import numpy as np
+    import torch.distributed as dist
+
+    from placement import Engine, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def exchange(blob: bytes) -> bytes:
+        parts = [None] * world
+        dist.all_gather_object(parts, blob)
+        return b"".join(parts)
+
+    inv = synth.make_inventory(n_nodes, 3, 0.2 if mix != "gang8" else 1.0)
+    batch = synth.make_jobs(n_jobs, 3, mix)
+    e = Engine(0, rank=rank, world_size=world, exchange=exchange, max_nodes=n_nodes)
+    e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    b, en = e.shard_range()
+    pods, st = e.place_batch(batch)
+    res = e.read_residuals()
+    # a second batch on the updated inventory: every rank's device shard and host mirror stay in step
+    batch2 = synth.make_jobs(n_jobs // 2, 4, mix)
+    pods2, st2 = e.place_batch(batch2)
+    res2 = e.read_residuals()
+    s = e.stats()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), pods=pods, st=st, res=res, pods2=pods2, st2=st2, res2=res2,
+             b=b, e=en, windows=s["windows"])
+    e.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

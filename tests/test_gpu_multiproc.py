@@ -1,0 +1,73 @@
+"""The sharded greedy across PROCESSES on the GPU box: 2 (and 3) separate rank processes, each with its
+own engine context holding one node shard on device 0, exchanging candidate blobs over gloo through
+the pe_config.exchange hook.  Every rank must return the unsharded oracle's placements, and the
+concatenated shard residuals must equal the oracle's -- for two consecutive batches (the second on
+the inventory the first left).  This is the cross-process protocol of the multi-GPU runs, with gloo
+standing in for RCCL on a one-GPU box."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+from placement import synth
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world,mix,n_nodes,n_jobs", [(2, "mixed", 20000, 600), (3, "gang8", 9000, 300)])
+def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs):
+    port = free_port()
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "mp_shard_worker.py"), str(r), str(world), str(port),
+                               mix, str(n_nodes), str(n_jobs), str(tmp_path)], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=100)
+            outs.append(out)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{outs[r][-3000:]}"
+    inv = synth.make_inventory(n_nodes, 3, 0.2 if mix != "gang8" else 1.0)
+    batch = synth.make_jobs(n_jobs, 3, mix)
+    w_pods, w_st, w_res = oracle.place_greedy(inv.residual(), inv.labels, batch.job_group_off, batch.priority,
+                                              batch.group_count, batch.group_req, batch.group_need)
+    batch2 = synth.make_jobs(n_jobs // 2, 4, mix)
+    w_pods2, w_st2, w_res2 = oracle.place_greedy(w_res, inv.labels, batch2.job_group_off, batch2.priority,
+                                                 batch2.group_count, batch2.group_req, batch2.group_need)
+    full, full2 = np.zeros_like(w_res), np.zeros_like(w_res2)
+    covered = 0
+    for r in range(world):
+        d = np.load(tmp_path / f"rank{r}.npz")
+        np.testing.assert_array_equal(d["st"], w_st)
+        np.testing.assert_array_equal(d["pods"], w_pods)
+        np.testing.assert_array_equal(d["st2"], w_st2)
+        np.testing.assert_array_equal(d["pods2"], w_pods2)
+        b, e = int(d["b"]), int(d["e"])
+        full[:, b:e] = d["res"]
+        full2[:, b:e] = d["res2"]
+        covered += e - b
+        assert int(d["windows"]) > 1
+    assert covered == n_nodes
+    np.testing.assert_array_equal(full, w_res)
+    np.testing.assert_array_equal(full2, w_res2)
+    assert 0 < (w_st == 0).sum() <= n_jobs
