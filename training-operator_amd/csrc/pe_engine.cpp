@@ -620,25 +620,76 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
 
 // ------------------------------------------------------------------ fit mask
 
+// The batch's dictionary, built once per upload and shared by every fit path's planning: per field
+// (dims 0-3, field 4 = label need) the distinct values ascending and each job's index into them.
+// One hashing pass per field (first-seen ids), then only the distinct values are sorted -- O(J)
+// for the usual few-valued batches instead of five O(J log J) sorts.
+struct BatchDict {
+  static constexpr int F = pe::D + 1;
+  std::vector<int64_t> vals[F];
+  std::vector<uint32_t> rank[F];
+};
+
+static void dict_field(int64_t n, const std::function<int64_t(int64_t)>& value, std::vector<int64_t>& vals,
+                       std::vector<uint32_t>& rank) {
+  size_t cap = 64;
+  while (cap < 2 * (size_t)n) cap *= 2;
+  std::vector<int64_t> keys(cap);
+  std::vector<uint32_t> ids(cap, UINT32_MAX);
+  const size_t mask = cap - 1;
+  vals.clear();
+  rank.resize((size_t)n);
+  for (int64_t j = 0; j < n; ++j) {
+    const int64_t v = value(j);
+    size_t h = (size_t)(((uint64_t)v * 0x9E3779B97F4A7C15ull) >> 32) & mask;
+    while (ids[h] != UINT32_MAX && keys[h] != v) h = (h + 1) & mask;
+    if (ids[h] == UINT32_MAX) {
+      keys[h] = v;
+      ids[h] = (uint32_t)vals.size();
+      vals.push_back(v);
+    }
+    rank[j] = ids[h];
+  }
+  std::vector<uint32_t> ord(vals.size());
+  for (size_t i = 0; i < ord.size(); ++i) ord[i] = (uint32_t)i;
+  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return vals[a] < vals[b]; });
+  std::vector<uint32_t> pos(vals.size());
+  std::vector<int64_t> sorted(vals.size());
+  for (size_t i = 0; i < ord.size(); ++i) {
+    pos[ord[i]] = (uint32_t)i;
+    sorted[i] = vals[ord[i]];
+  }
+  vals.swap(sorted);
+  for (int64_t j = 0; j < n; ++j) rank[j] = pos[rank[j]];
+}
+
+static void build_dict(BatchDict& bd, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
+  for (int f = 0; f < BatchDict::F; ++f) {
+    if (f < pe::D)
+      dict_field(n_jobs, [&](int64_t j) { return req[j * pe::D + f]; }, bd.vals[f], bd.rank[f]);
+    else
+      dict_field(n_jobs, [&](int64_t j) { return (int64_t)(need ? need[j] : 0u); }, bd.vals[f], bd.rank[f]);
+  }
+}
+
 // Dictionary codes of one batch (pe_kernels.h, CodeSpec): per dimension the sorted distinct request
 // values, per job their ranks packed with guard bits; label needs must form an inclusion chain.
 // Returns false when the batch does not fit the 32-bit code word (the compare paths take it).
-static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
+static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   if (n_jobs == 0) return false;
-  std::vector<int64_t> vals[pe::D];
-  for (int d = 0; d < pe::D; ++d) {
-    vals[d].resize((size_t)n_jobs);
-    for (int64_t j = 0; j < n_jobs; ++j) vals[d][j] = req[j * pe::D + d];
-    std::sort(vals[d].begin(), vals[d].end());
-    vals[d].erase(std::unique(vals[d].begin(), vals[d].end()), vals[d].end());
+  const std::vector<int64_t>* vals = bd.vals;
+  for (int d = 0; d < pe::D; ++d)
     if ((int)vals[d].size() >= pe::CODE_MAXV) return false;
-  }
+  if ((int)bd.vals[4].size() >= pe::CODE_MAXV) return false;
   std::vector<uint32_t> needs;
-  for (int64_t j = 0; j < n_jobs; ++j) needs.push_back(need ? need[j] : 0u);
+  for (int64_t v : bd.vals[4]) needs.push_back((uint32_t)v);
   std::sort(needs.begin(), needs.end(), [](uint32_t a, uint32_t b) {
     return __builtin_popcount(a) != __builtin_popcount(b) ? __builtin_popcount(a) < __builtin_popcount(b) : a < b;
   });
-  needs.erase(std::unique(needs.begin(), needs.end()), needs.end());
+  // need dictionary index -> position in the inclusion chain
+  std::vector<uint32_t> need_pos(bd.vals[4].size());
+  for (size_t i = 0; i < bd.vals[4].size(); ++i)
+    need_pos[i] = (uint32_t)(std::find(needs.begin(), needs.end(), (uint32_t)bd.vals[4][i]) - needs.begin());
   if ((int)needs.size() >= pe::CODE_MAXV) return false;
   for (size_t i = 0; i + 1 < needs.size(); ++i)
     if ((needs[i] & needs[i + 1]) != needs[i]) return false;   // not a chain under inclusion
@@ -666,14 +717,8 @@ static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const u
   std::vector<uint32_t> jc((size_t)Jp, sp.therm ? ~(1u << 31) : sp.guard);
   for (int64_t j = 0; j < n_jobs; ++j) {
     uint32_t c = 0;
-    for (int d = 0; d < pe::D; ++d) {
-      const int64_t q = req[j * pe::D + d];
-      const uint32_t rank = (uint32_t)(std::lower_bound(vals[d].begin(), vals[d].end(), q) - vals[d].begin()) + 1;
-      c |= rank << sp.off[d];
-    }
-    const uint32_t nd = need ? need[j] : 0u;
-    const uint32_t rank = (uint32_t)(std::find(needs.begin(), needs.end(), nd) - needs.begin()) + 1;
-    c |= rank << sp.off[4];
+    for (int d = 0; d < pe::D; ++d) c |= (bd.rank[d][j] + 1) << sp.off[d];
+    c |= (need_pos[bd.rank[4][j]] + 1) << sp.off[4];
     if (sp.therm) {
       uint32_t y = 0;   // one bit per field: rank c <=> bit c-1
       for (int f = 0; f < pe::CODE_FIELDS; ++f) {
@@ -708,26 +753,20 @@ static bool build_codes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const u
 constexpr int PL_MAX_SETS = 256;
 constexpr int64_t PL_SETS_BYTES = int64_t(2) << 30;   // planes of all sets (4 MiB per set at 1M nodes)
 
-static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need, bool allow_sets) {
+static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd, bool allow_sets) {
   if (n_jobs == 0) return false;
   constexpr int F = pe::D + 1;
-  auto value = [&](int64_t j, int f) -> int64_t { return f < pe::D ? req[j * pe::D + f] : (int64_t)(need ? need[j] : 0u); };
-  std::vector<int64_t> vals[F];
+  const std::vector<int64_t>* vals = bd.vals;
   int64_t off[F], P = 0;
   for (int f = 0; f < F; ++f) {
-    vals[f].resize((size_t)n_jobs);
-    for (int64_t j = 0; j < n_jobs; ++j) vals[f][j] = value(j, f);
-    std::sort(vals[f].begin(), vals[f].end());
-    vals[f].erase(std::unique(vals[f].begin(), vals[f].end()), vals[f].end());
     off[f] = P;
     P += (int64_t)vals[f].size();
   }
+  if (P > pe::PL_MAX && !allow_sets) return false;
   // pair id (global over the fields) of each job's five selections
   std::vector<int32_t> pid((size_t)n_jobs * F);
   for (int64_t j = 0; j < n_jobs; ++j)
-    for (int f = 0; f < F; ++f)
-      pid[(size_t)j * F + f] =
-          (int32_t)(off[f] + (std::lower_bound(vals[f].begin(), vals[f].end(), value(j, f)) - vals[f].begin()));
+    for (int f = 0; f < F; ++f) pid[(size_t)j * F + f] = (int32_t)(off[f] + bd.rank[f][j]);
   auto pair_spec = [&](int64_t p, int& kind, int64_t& val) {
     int f = F - 1;
     while (off[f] > p) --f;
@@ -879,19 +918,11 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const 
 // the LDS budget), dimensions with one value folded into the need planes, one plane per distinct
 // need.  Returns false when no configuration fits 160 KiB of LDS (the other paths take the batch).
 // PE_LDS_W=1|2|4 forces the block size, PE_LDS_MAXL=1..3 caps the levels (tuning / tests).
-static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
+static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   if (n_jobs == 0 || ctx->Ns == 0) return false;
-  std::vector<int64_t> vals[pe::D];
-  for (int d = 0; d < pe::D; ++d) {
-    vals[d].resize((size_t)n_jobs);
-    for (int64_t j = 0; j < n_jobs; ++j) vals[d][j] = req[j * pe::D + d];
-    std::sort(vals[d].begin(), vals[d].end());
-    vals[d].erase(std::unique(vals[d].begin(), vals[d].end()), vals[d].end());
-  }
-  std::vector<uint32_t> needs((size_t)n_jobs);
-  for (int64_t j = 0; j < n_jobs; ++j) needs[j] = need ? need[j] : 0u;
-  std::sort(needs.begin(), needs.end());
-  needs.erase(std::unique(needs.begin(), needs.end()), needs.end());
+  const std::vector<int64_t>* vals = bd.vals;
+  std::vector<uint32_t> needs;
+  for (int64_t v : bd.vals[4]) needs.push_back((uint32_t)v);   // ascending
   if ((int)needs.size() > pe::LD_MAXNEED) return false;
   pe::LdsSpec sp{};
   int fdim[pe::LD_MAXF];
@@ -1043,8 +1074,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uin
     const int64_t r = j % R, q = j / R, w = q % 16, t = q / 16;
     uint16_t* c = codes.data() + (size_t)(((r * 16 + w) * Tpad + t) * pe::LD_CODE);
     for (int i = 0; i < sp.nf; ++i) {
-      const std::vector<int64_t>& v = vals[fdim[i]];
-      const int64_t rank = (int64_t)(std::lower_bound(v.begin(), v.end(), req[j * pe::D + fdim[i]]) - v.begin()) + 1;
+      const int64_t rank = (int64_t)bd.rank[fdim[i]][j] + 1;
       if (sp.L[i] == 1) {
         c[3 * i] = (uint16_t)(sp.pbase[i][0] + rank - 1);
       } else {
@@ -1056,9 +1086,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uin
         }
       }
     }
-    const uint32_t nd = need ? need[j] : 0u;
-    c[pe::LD_NEED_SLOT] =
-        (uint16_t)(sp.need_pbase + (std::lower_bound(needs.begin(), needs.end(), nd) - needs.begin()));
+    c[pe::LD_NEED_SLOT] = (uint16_t)(sp.need_pbase + bd.rank[4][j]);
   }
   if (std::getenv("PE_LDS_DEBUG")) {   // diagnostics: the chosen configuration
     std::fprintf(stderr, "lds: W %d nblk %lld R %lld planes %d need %d fold %d |", W, (long long)nblk, (long long)R,
@@ -1099,55 +1127,67 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
     check_req(req, n_jobs, "req");
   }
   const int64_t Jp = round_up(std::max<int64_t>(n_jobs, 1), pe::FM_JT);
-  std::vector<ReqRec> recs((size_t)Jp);
-  for (int64_t j = 0; j < Jp; ++j) {
-    if (j < n_jobs) fill_req(recs[j], req + j * pe::D, need ? need[j] : 0u);
-    else {
-      const int64_t never[pe::D] = {INT64_MAX, INT64_MAX, INT64_MAX, INT64_MAX};
-      fill_req(recs[j], never, 0xFFFFFFFFu);
-    }
-  }
-  // exact 32-bit form: per dim the shift that brings the largest request below 2^31, valid only
-  // if 2^shift divides every request of the batch in that dim
-  bool use32 = true;
-  for (int d = 0; d < pe::D && use32; ++d) {
-    int64_t mx = 0, orv = 0;
-    for (int64_t j = 0; j < n_jobs; ++j) {
-      mx = std::max(mx, req[j * pe::D + d]);
-      orv |= req[j * pe::D + d];
-    }
-    int sh = 0;
-    while (sh < 62 && (mx >> sh) > (int64_t)INT32_MAX) ++sh;
-    if (orv & ((int64_t(1) << sh) - 1)) use32 = false;
-    ctx->fit_shift[d] = sh;
-  }
-  ctx->fit32 = use32 && (ctx->fit_path_mask & PATH_I32);
-  if (ctx->fit32) {
-    std::vector<pe::ReqRec32> r32((size_t)Jp);
-    for (int64_t j = 0; j < Jp; ++j) {
-      std::memset(&r32[j], 0, sizeof(pe::ReqRec32));
-      for (int d = 0; d < pe::D; ++d)
-        r32[j].q[d] = j < n_jobs ? (int32_t)(req[j * pe::D + d] >> ctx->fit_shift[d]) : INT32_MAX;
-      r32[j].need = j < n_jobs ? (need ? need[j] : 0u) : 0xFFFFFFFFu;
-    }
-    hipchk(ctx->fit_jobs32.ensure(Jp), "alloc fit jobs32");
-    hipchk(ctx->res32.ensure((size_t)pe::D * ctx->stride), "alloc res32");
-    hipchk(hipMemcpyAsync(ctx->fit_jobs32.p, r32.data(), Jp * sizeof(pe::ReqRec32), hipMemcpyHostToDevice,
-                          ctx->stream),
-           "H2D fit jobs32");
-  }
   ctx->fit_J = n_jobs;
   ctx->fit_Jp = Jp;
   ctx->Wn = (ctx->Ns + 63) / 64;
   ctx->Wt = (ctx->Wn + 3) / 4;
-  ctx->fit_path = ctx->fit32 ? 1 : 0;
   // one bit-plane set (register planes) > LDS digit planes > bit-plane sets > coded > int32 > int64
   const bool planes_ok = ctx->fit_path_mask & PATH_PLANES;
-  if (planes_ok && build_planes(ctx, n_jobs, req, need, false)) ctx->fit_path = 3;
-  else if ((ctx->fit_path_mask & PATH_LDS) && build_lds(ctx, n_jobs, req, need)) ctx->fit_path = 4;
-  else if (planes_ok && build_planes(ctx, n_jobs, req, need, true)) ctx->fit_path = 3;
-  else if ((ctx->fit_path_mask & PATH_CODED) && build_codes(ctx, n_jobs, req, need)) ctx->fit_path = 2;
-  hipchk(ctx->fit_jobs.ensure(Jp), "alloc fit jobs");
+  ctx->fit_path = -1;
+  if (n_jobs > 0 && (ctx->fit_path_mask & (PATH_PLANES | PATH_LDS | PATH_CODED))) {
+    BatchDict bd;
+    build_dict(bd, n_jobs, req, need);
+    if (planes_ok && build_planes(ctx, n_jobs, bd, false)) ctx->fit_path = 3;
+    else if ((ctx->fit_path_mask & PATH_LDS) && build_lds(ctx, n_jobs, bd)) ctx->fit_path = 4;
+    else if (planes_ok && build_planes(ctx, n_jobs, bd, true)) ctx->fit_path = 3;
+    else if ((ctx->fit_path_mask & PATH_CODED) && build_codes(ctx, n_jobs, bd)) ctx->fit_path = 2;
+  }
+  if (ctx->fit_path < 0) {
+    // compare paths.  Exact 32-bit form: per dim the shift that brings the largest request below
+    // 2^31, valid only if 2^shift divides every request of the batch in that dim
+    bool use32 = true;
+    for (int d = 0; d < pe::D && use32; ++d) {
+      int64_t mx = 0, orv = 0;
+      for (int64_t j = 0; j < n_jobs; ++j) {
+        mx = std::max(mx, req[j * pe::D + d]);
+        orv |= req[j * pe::D + d];
+      }
+      int sh = 0;
+      while (sh < 62 && (mx >> sh) > (int64_t)INT32_MAX) ++sh;
+      if (orv & ((int64_t(1) << sh) - 1)) use32 = false;
+      ctx->fit_shift[d] = sh;
+    }
+    ctx->fit32 = use32 && (ctx->fit_path_mask & PATH_I32);
+    ctx->fit_path = ctx->fit32 ? 1 : 0;
+    if (ctx->fit32) {
+      std::vector<pe::ReqRec32> r32((size_t)Jp);
+      for (int64_t j = 0; j < Jp; ++j) {
+        std::memset(&r32[j], 0, sizeof(pe::ReqRec32));
+        for (int d = 0; d < pe::D; ++d)
+          r32[j].q[d] = j < n_jobs ? (int32_t)(req[j * pe::D + d] >> ctx->fit_shift[d]) : INT32_MAX;
+        r32[j].need = j < n_jobs ? (need ? need[j] : 0u) : 0xFFFFFFFFu;
+      }
+      hipchk(ctx->fit_jobs32.ensure(Jp), "alloc fit jobs32");
+      hipchk(ctx->res32.ensure((size_t)pe::D * ctx->stride), "alloc res32");
+      hipchk(hipMemcpyAsync(ctx->fit_jobs32.p, r32.data(), Jp * sizeof(pe::ReqRec32), hipMemcpyHostToDevice,
+                            ctx->stream),
+             "H2D fit jobs32");
+      hipchk(hipStreamSynchronize(ctx->stream), "sync fit jobs32");   // the host vector dies here
+    } else {
+      std::vector<ReqRec> recs((size_t)Jp);
+      for (int64_t j = 0; j < Jp; ++j) {
+        if (j < n_jobs) fill_req(recs[j], req + j * pe::D, need ? need[j] : 0u);
+        else {
+          const int64_t never[pe::D] = {INT64_MAX, INT64_MAX, INT64_MAX, INT64_MAX};
+          fill_req(recs[j], never, 0xFFFFFFFFu);
+        }
+      }
+      hipchk(ctx->fit_jobs.ensure(Jp), "alloc fit jobs");
+      hipchk(hipMemcpyAsync(ctx->fit_jobs.p, recs.data(), Jp * sizeof(ReqRec), hipMemcpyHostToDevice, ctx->stream),
+             "H2D fit jobs");
+      hipchk(hipStreamSynchronize(ctx->stream), "sync fit jobs");
+    }
+  }
   const size_t mask_words = ctx->fit_path == 4   ? (size_t)(n_jobs + 1) * ctx->lds_pitch   // + the scratch row
                             : ctx->fit_path == 3 ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->pl_nblk * 128
                             : ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
@@ -1156,8 +1196,6 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
   const int64_t n_counts = std::max<int64_t>(Jp, ctx->fit_path == 3 ? ctx->pl_counts_n : 0);
   hipchk(ctx->counts.ensure(n_counts), "alloc fit counts");
   hipchk(ctx->h_counts.ensure(n_counts), "alloc pinned counts");
-  hipchk(hipMemcpyAsync(ctx->fit_jobs.p, recs.data(), Jp * sizeof(ReqRec), hipMemcpyHostToDevice, ctx->stream),
-         "H2D fit jobs");
   hipchk(hipStreamSynchronize(ctx->stream), "sync fit upload");
   ctx->fit_uploaded = true;
 }
