@@ -79,8 +79,11 @@ int main(int argc, char** argv) {
     if (!R.done() && r == 0) std::printf("(partial dump: the batch is not decided after %zu windows)\n", wi);
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     best = ms < best ? ms : best;
-    std::printf("rep %d: %.3f ms total, %.3f ms in resolve, %zu windows, %lld pods placed, %lld rescans\n", r, ms,
-                t_resolve, wi, (long long)R.pods_placed(), (long long)R.rescans());
+    uint64_t h = 1469598103934665603ull;   // FNV-1a over the placements and job states (A/B exactness)
+    for (int32_t v : R.pod_node()) h = (h ^ (uint32_t)v) * 1099511628211ull;
+    for (int32_t v : R.job_status()) h = (h ^ (uint32_t)v) * 1099511628211ull;
+    std::printf("rep %d: %.3f ms total, %.3f ms in resolve, %zu windows, %lld pods placed, %lld rescans, result %016llx\n",
+                r, ms, t_resolve, wi, (long long)R.pods_placed(), (long long)R.rescans(), (unsigned long long)h);
   }
   std::printf("best %.3f ms\n", best);
   return 0;

@@ -6,6 +6,7 @@
 #include <numeric>
 #include <utility>
 #include <cstdio>
+#include <cstdlib>
 
 #include <immintrin.h>
 #ifdef PE_RES_PROF
@@ -14,8 +15,8 @@
 
 namespace pe {
 #ifdef PE_RES_PROF   // section cycle counts for tools/replay_resolver (-DPE_RES_PROF)
-struct ResProf { unsigned long long seed = 0, keys = 0, skip = 0, place = 0, fin = 0, other = 0; long skips = 0, pods = 0;
-  ~ResProf() { std::fprintf(stderr, "cycles seed %.1fM keys %.1fM skip %.1fM place %.1fM fin %.1fM | skips %ld pods %ld\n", seed / 1e6, keys / 1e6, skip / 1e6, place / 1e6, fin / 1e6, skips, pods); } };
+struct ResProf { unsigned long long seed = 0, keys = 0, skip = 0, place = 0, fin = 0, other = 0; long skips = 0, pods = 0, groups = 0, dirty = 0, scored = 0;
+  ~ResProf() { std::fprintf(stderr, "cycles seed %.1fM keys %.1fM skip %.1fM place %.1fM fin %.1fM | skips %ld pods %ld | per group: dirty %.0f scored %.1f\n", seed / 1e6, keys / 1e6, skip / 1e6, place / 1e6, fin / 1e6, skips, pods, (double)dirty / groups, (double)scored / groups); } };
 static ResProf rp;
 #define RP_T() __rdtsc()
 #define RP_ADD(f, t) (rp.f += __rdtsc() - (t))
@@ -159,6 +160,88 @@ void DirtySet::keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vec
   for (int32_t j : idx) out[j] = key_bf(r0[j], r1[j], r2[j], r3[j], lab[j], q, need, (uint64_t)gid[j]);
 }
 
+// keys_all, 8 dirty nodes per AVX-512 step: the K(n) range test, the Appendix-B fit and key (the
+// arithmetic of key_bf), the fitting slots compressed into idx and the running minimum.
+__attribute__((target("avx512f,avx512dq,avx512vl,avx512bw"))) static uint64_t keys_avx512(
+    size_t n, const uint64_t* kn, const int64_t* x0p, const int64_t* x1p, const int64_t* x2p, const int64_t* x3p,
+    const uint32_t* lab, const int64_t* gid, const int64_t q[RD], uint32_t need, uint64_t lo, uint64_t span,
+    uint64_t* out, int32_t* idx, size_t* n_idx) {
+  const __m512i ones = _mm512_set1_epi64(-1), vlo = _mm512_set1_epi64((int64_t)lo),
+                vspan = _mm512_set1_epi64((int64_t)span), vneed = _mm512_set1_epi64(need),
+                q0 = _mm512_set1_epi64(q[0]), q1 = _mm512_set1_epi64(q[1]), q2 = _mm512_set1_epi64(q[2]),
+                q3 = _mm512_set1_epi64(q[3]), smax = _mm512_set1_epi64((int64_t)kScoreMax),
+                c20 = _mm512_set1_epi64(1ll << 20);
+  const __m256i lane = _mm256_set_epi32(7, 6, 5, 4, 3, 2, 1, 0);
+  __m512i vmin = ones;
+  size_t ni = 0;
+  for (size_t i = 0; i < n; i += 8) {
+    const __mmask8 m = n - i >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << (n - i)) - 1);
+    const __m512i k = _mm512_maskz_loadu_epi64(m, kn + i);
+    __mmask8 fit = m & (_mm512_cmplt_epu64_mask(_mm512_sub_epi64(k, vlo), vspan) | _mm512_cmpeq_epi64_mask(k, ones));
+    if (!fit) {
+      _mm512_mask_storeu_epi64(out + i, m, ones);
+      continue;
+    }
+    const __m512i x0 = _mm512_maskz_loadu_epi64(m, x0p + i), x1 = _mm512_maskz_loadu_epi64(m, x1p + i),
+                  x2 = _mm512_maskz_loadu_epi64(m, x2p + i), x3 = _mm512_maskz_loadu_epi64(m, x3p + i);
+    const __m512i l = _mm512_cvtepu32_epi64(_mm256_maskz_loadu_epi32(m, lab + i));
+    fit &= _mm512_cmpeq_epi64_mask(_mm512_and_si512(l, vneed), vneed) & _mm512_cmple_epi64_mask(q0, x0) &
+           _mm512_cmple_epi64_mask(q1, x1) & _mm512_cmple_epi64_mask(q2, x2) & _mm512_cmple_epi64_mask(q3, x3);
+    const __m512i a = _mm512_sub_epi64(x0, q0), b = _mm512_srli_epi64(_mm512_sub_epi64(x1, q1), 20),
+                  c = _mm512_sub_epi64(x2, q2), d = _mm512_srli_epi64(_mm512_sub_epi64(x3, q3), 24);
+    const __m512i sum = _mm512_add_epi64(_mm512_add_epi64(a, b), _mm512_add_epi64(_mm512_slli_epi64(c, 20), d));
+    const __mmask8 big = _mm512_cmpgt_epu64_mask(a, smax) | _mm512_cmpgt_epu64_mask(b, smax) |
+                         _mm512_cmpge_epu64_mask(c, c20) | _mm512_cmpgt_epu64_mask(d, smax) |
+                         _mm512_cmpgt_epu64_mask(sum, smax);
+    const __m512i score = _mm512_mask_mov_epi64(sum, big, smax);
+    const __m512i key = _mm512_mask_mov_epi64(
+        ones, fit, _mm512_or_si512(_mm512_slli_epi64(score, 24), _mm512_maskz_loadu_epi64(m, gid + i)));
+    _mm512_mask_storeu_epi64(out + i, m, key);
+    vmin = _mm512_min_epu64(vmin, key);
+    _mm256_mask_compressstoreu_epi32(idx + ni, fit, _mm256_add_epi32(lane, _mm256_set1_epi32((int32_t)i)));
+    ni += (size_t)__builtin_popcount(fit);
+  }
+  *n_idx = ni;
+  return (uint64_t)_mm512_reduce_min_epu64(vmin);
+}
+
+uint64_t DirtySet::keys_all(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
+                            std::vector<int32_t>& idx) const {
+  // PE_NO_AVX512=1 forces the AVX2 path (tests cover both)
+  static const bool avx512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") &&
+                             __builtin_cpu_supports("avx512vl") && __builtin_cpu_supports("avx512bw") &&
+                             !std::getenv("PE_NO_AVX512");
+  const size_t n = gid.size();
+  if (out.size() < n) out.resize(n);
+  if (!avx512) {
+    keys(q, need, limit, out, idx);
+    uint64_t mk = kNoKey;
+    std::vector<int32_t> fit;
+    for (int32_t j : idx)
+      if (out[j] != kNoKey) fit.push_back(j);
+    std::vector<uint8_t> seen(n, 0);
+    for (int32_t j : idx) seen[j] = 1;
+    for (size_t j = 0; j < n; ++j)
+      if (!seen[j]) out[j] = kNoKey;
+    for (int32_t j : fit) mk = std::min(mk, out[j]);
+    idx.swap(fit);
+    return mk;
+  }
+  uint64_t sq = (uint64_t)q[0] + ((uint64_t)q[1] >> 20) + ((uint64_t)q[3] >> 24);
+  sq = (uint64_t)q[0] > kScoreMax || (uint64_t)q[2] >= (1ull << 20) || sq >= kScoreMax ? kScoreMax
+                                                                                      : sq + ((uint64_t)q[2] << 20);
+  const uint64_t lo = sq >= kScoreMax ? kNoKey : sq << 24;
+  const uint64_t q2 = sq + 2 >= (1ull << 40) ? kNoKey : (sq + 2) << 24;
+  const uint64_t hi = limit == kNoKey || limit >= kNoKey - q2 ? kNoKey : limit + q2;
+  const uint64_t span = hi > lo ? hi - lo : 0;
+  if (idx.size() < n + 16) idx.resize(n + 16);
+  size_t ni = 0;
+  const uint64_t mk = keys_avx512(n, kn.data(), r0.data(), r1.data(), r2.data(), r3.data(), lab.data(), gid.data(),
+                                  q, need, lo, span, out.data(), idx.data(), &ni);
+  idx.resize(ni);
+  return mk;
+}
+
 uint64_t DirtySet::key_at(int32_t i, const int64_t q[RD], uint32_t need) const {
   return key_bf(r0[i], r1[i], r2[i], r3[i], lab[i], q, need, (uint64_t)gid[i]);
 }
@@ -278,9 +361,27 @@ void Resolver::advance_group() {
   }
 }
 
+// The current job's nodes: a linear search over the few ids (a job touches at most its pod count
+// of nodes, usually < 20), the hash map only past kJobLinear of them.
+int32_t Resolver::job_find(int64_t gid) const {
+  if (jn_.size() > kJobLinear) return jslot_.find(gid);
+  const int64_t* ids = jn_ids_.data();
+  for (size_t i = 0; i < jn_ids_.size(); ++i)
+    if (ids[i] == gid) return (int32_t)i;
+  return -1;
+}
+
 NodeState& Resolver::job_node(int64_t gid) {
-  const int32_t i = jslot_.insert(gid, (int32_t)jn_.size());
-  if (i == (int32_t)jn_.size()) jn_.emplace_back(gid, NodeState{});
+  int32_t i = job_find(gid);
+  if (i < 0) {
+    i = (int32_t)jn_.size();
+    jn_.emplace_back(gid, NodeState{});
+    jn_ids_.push_back(gid);
+    if (jn_.size() == kJobLinear + 1)   // switch to the map: enter every id so far
+      for (size_t k = 0; k < jn_ids_.size(); ++k) jslot_.insert(jn_ids_[k], (int32_t)k);
+    else if (jn_.size() > kJobLinear + 1)
+      jslot_.insert(gid, i);
+  }
   return jn_[i].second;
 }
 
@@ -296,7 +397,7 @@ void Resolver::finish_job(bool ok) {
       for (int32_t p = 0; p < cnt_[g]; ++p) {
         int32_t& slot = pod_node_[pod_off_[g] + p];
         if (slot < 0) continue;
-        NodeState& st = jn_[jslot_.find(slot)].second;
+        NodeState& st = jn_[job_find(slot)].second;
         for (int d = 0; d < RD; ++d) st.res[d] += q[d];
         slot = -1;
         --pods_placed_;
@@ -306,12 +407,8 @@ void Resolver::finish_job(bool ok) {
     job_status_[j] = 1;
     ++jobs_failed_;
   }
-  if (!jn_.empty()) {
-    std::vector<int64_t>& ids = jn_ids_;
-    ids.clear();
-    for (const auto& kv : jn_) ids.push_back(kv.first);
-    jslot_.clear(ids.begin(), ids.end());
-  }
+  if (jn_.size() > kJobLinear) jslot_.clear(jn_ids_.begin(), jn_ids_.end());
+  jn_ids_.clear();
   jn_.clear();
   ++oi_;
   p_ = 0;
@@ -385,6 +482,10 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     __builtin_prefetch(&need_[g]);
     __builtin_prefetch(&pod_off_[g]);
   }
+  head_.assign(groups.size(), 0);
+  if (!groups.empty() && !cands.empty() && cands[0].keyed)   // the first group's list head
+    for (size_t i = 0; i < std::min<size_t>(4, cands[0].size()); ++i)
+      __builtin_prefetch(&mirror_.nodes[cands[0].key(i) & 0xFFFFFFull]);
   size_t wi = 0;
   std::vector<uint64_t>& dk = dk_;  // keys of the dirty nodes for the current group
   std::vector<int32_t>& dki = dki_;  // the slots among them that can hold a key
@@ -405,12 +506,30 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     const int64_t* q = req_ + (int64_t)g_ * RD;
     const uint32_t need = need_[g_];
     t_ = RP_T();
-    if (gc.keyed)   // the first listed nodes' states (the rest are prefetched as the list is consumed)
-      for (size_t i = 0; i < std::min<size_t>(4, gc.size()); ++i) __builtin_prefetch(&mirror_.nodes[gc.key(i) & 0xFFFFFFull]);
-    dirty_.keys(q, need, gc.limit, dk, dki);   // dirty keys >= limit never decide (list head or rescan)
+    // Look ahead one group: the next list's first clean entries (their mirror states prefetched, the
+    // dirty entries before them skipped for good -- the dirty set only grows during a resolve).
+    if (wi + 1 < groups.size() && cands[wi + 1].keyed) {
+      const GroupCands& gn = cands[wi + 1];
+      size_t p = 0;
+      int c = 0;
+      while (p < gn.size() && dirty_.contains((int64_t)(gn.key(p) & 0xFFFFFFull))) ++p;
+      head_[wi + 1] = p;
+      for (; p < gn.size() && c < 3; ++p)
+        if (!dirty_.contains((int64_t)(gn.key(p) & 0xFFFFFFull))) {
+          __builtin_prefetch(&mirror_.nodes[gn.key(p) & 0xFFFFFFull]);
+          ++c;
+        }
+    }
+    dirty_.keys_all(q, need, gc.limit, dk, dki);   // dirty keys >= limit never decide (list head or rescan)
     int32_t best = argmin();
     RP_ADD(keys, t_);
-    size_t ptr = 0;
+#ifdef PE_RES_PROF
+    rp.groups++;
+    rp.dirty += (long)dirty_.size();
+    rp.scored += (long)dki.size();
+#endif
+    size_t ptr = head_[wi];
+    size_t pf = ptr;   // clean entries up to pf have been prefetched
     bool failed = false;
     while (p_ < cnt_[g_]) {
       t_ = RP_T();
@@ -442,7 +561,12 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       } else {
         if (gc.keyed) {   // clean: the mirror holds the snapshot state
           st = mirror_.nodes[gid];
-          if (ptr + 4 < gc.size()) __builtin_prefetch(&mirror_.nodes[gc.key(ptr + 4) & 0xFFFFFFull]);
+          // keep the next two clean entries' states on their way
+          for (int c = 0; pf < gc.size() && c < 2; ++pf)
+            if (pf > ptr && !dirty_.contains((int64_t)(gc.key(pf) & 0xFFFFFFull))) {
+              __builtin_prefetch(&mirror_.nodes[gc.key(pf) & 0xFFFFFFull]);
+              ++c;
+            }
         } else {
           const Cand& c = gc.data[ptr];
           for (int d = 0; d < RD; ++d) st.res[d] = c.res[d];
@@ -454,8 +578,16 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       // the minimum for every following pod of the group that still fits on it: place them all
       // at once, m = min(pods left, min over q_d > 0 of res_d / q_d).
       int64_t m = cnt_[g_] - p_;
-      for (int d = 0; d < RD; ++d)
-        if (q[d] > 0) m = std::min<int64_t>(m, st.res[d] / q[d]);
+      if (m > 1) {   // (the chosen node fits one pod; divide only when the rest may not fit)
+        bool all = true;
+        for (int d = 0; d < RD; ++d) {
+          int64_t need_d;
+          all &= q[d] == 0 || (!__builtin_mul_overflow(q[d], m, &need_d) && need_d <= st.res[d]);
+        }
+        if (!all)
+          for (int d = 0; d < RD; ++d)
+            if (q[d] > 0) m = std::min<int64_t>(m, st.res[d] / q[d]);
+      }
       for (int d = 0; d < RD; ++d) st.res[d] -= m * q[d];
       if (slot < 0) {
         slot = dirty_.upsert(gid, st);

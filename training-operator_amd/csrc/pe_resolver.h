@@ -195,6 +195,11 @@ class DirtySet {
   // `idx` receives the slots that were scored (the rest are NO_KEY in out).
   void keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
             std::vector<int32_t>& idx) const;
+  // every slot's key for (q, need) -> out[0..size()) (NO_KEY where it does not fit or where the
+  // K(n) range test above rules out a key < limit); returns the smallest.  AVX-512 where the CPU
+  // has it (8 nodes per step, no index list), else keys() + a scalar pass.
+  uint64_t keys_all(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
+                    std::vector<int32_t>& idx) const;
   uint64_t key_at(int32_t i, const int64_t q[RD], uint32_t need) const;
   std::vector<int64_t> gid, r0, r1, r2, r3;
   std::vector<uint32_t> lab;
@@ -258,12 +263,15 @@ class Resolver {
   DirtySet dirty_;
   std::vector<uint64_t> dk_;
   std::vector<int32_t> dki_;   // dirty slots with a key for the current group (argmin runs over these)
+  std::vector<size_t> head_;   // per window group: its list's first entry not known to be dirty
   // nodes touched by the current job (exact current residuals, survive window flushes)
   // gid -> index into jn_ (reset per job): no allocation per pod
-  IdMap jslot_;
+  static constexpr size_t kJobLinear = 32;
+  IdMap jslot_;                    // gid -> index into jn_, only for jobs with > kJobLinear nodes
   std::vector<std::pair<int64_t, NodeState>> jn_;
-  std::vector<int64_t> jn_ids_;
+  std::vector<int64_t> jn_ids_;    // the ids of jn_, in order
   NodeState& job_node(int64_t gid);
+  int32_t job_find(int64_t gid) const;
   int64_t jobs_placed_ = 0, jobs_failed_ = 0, pods_placed_ = 0, rescans_ = 0;
 };
 
