@@ -139,6 +139,15 @@ def agg_bytes(job_group_off, group_cont_off) -> int:
     return G * (4 + 4) + C * (32 + 1) + J * (4 + 4 + 32 + 1 + 4 + 1)
 
 
+def pg_slice(agg, a: int, b: int):
+    """Jobs [a, b) of a pe_pg_min_resources CSR batch (job_group_off, min_member, group_replicas,
+    group_cont_off, cont_req, cont_flags), offsets rebased."""
+    jgo, mm, rep, gco, cont, flags = agg
+    g0, g1 = int(jgo[a]), int(jgo[b])
+    c0, c1 = int(gco[g0]), int(gco[g1])
+    return (jgo[a:b + 1] - g0, mm[a:b], rep[g0:g1], gco[g0:g1 + 1] - c0, cont[c0:c1], flags[c0:c1])
+
+
 def profile_summary():
     """The committed profile profiles/LATEST names (summary.json), or None."""
     try:
@@ -423,21 +432,28 @@ def main(argv=None):
         eng.fit_mask_run()
         eng.synchronize()
 
-        # PodGroup MinResources aggregation (v1 CalcPGMinResources over a batch), end to end per call
+        # PodGroup MinResources aggregation (v1 CalcPGMinResources over a batch), end to end per call; jobs
+        # are independent, so at N > 1 every rank aggregates its contiguous slice of the batch
         agg = synth.make_pg_batch(args.agg_jobs, synth.SEED["cfg3"])
-        eng.pg_min_resources(1, *agg)
+        lo_j, hi_j = rank * args.agg_jobs // world, (rank + 1) * args.agg_jobs // world
+        mine = pg_slice(agg, lo_j, hi_j)
+        eng.pg_min_resources(1, *mine)
         ts = []
         for _ in range(3):
+            barrier()
             t0 = time.perf_counter()
-            eng.pg_min_resources(1, *agg)
-            ts.append(time.perf_counter() - t0)
+            eng.pg_min_resources(1, *mine)
+            ts.append(allmax(time.perf_counter() - t0))
         at = float(np.median(ts))
         ab = agg_bytes(agg[0], agg[3])
         out["aggregation"] = {"workload": f"{args.agg_jobs} v1 PyTorchJob-like jobs (Master 1 + Worker 0-63, 1-2 "
-                                          "containers), CalcPGMinResources on the GPU incl. H2D/D2H",
+                                          "containers), CalcPGMinResources on the GPU incl. H2D/D2H"
+                                          + (f", split over {world} ranks ({hi_j - lo_j} jobs on rank {rank})"
+                                             if world > 1 else ""),
                               "jobs_per_s": args.agg_jobs / at, "ms_per_call": at * 1e3, "alg_bytes": ab,
                               "achieved_gbs": ab / at / 1e9,
-                              "note": "PCIe-inclusive (the ABI hands over host buffers): bound by the H2D/D2H copies"}
+                              "note": "PCIe-inclusive (the ABI hands over host buffers): bound by the H2D/D2H copies; "
+                                      "time = max over ranks"}
 
     if not args.no_greedy:
         batch = synth.make_jobs(args.greedy_jobs, synth.SEED["cfg3"], "mixed")

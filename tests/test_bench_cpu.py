@@ -82,3 +82,21 @@ def test_profile_check_requires_same_build(tmp_path, monkeypatch):
     assert not bench.profile_check("planes", 100, 10, 1.03, "other")["profile_matches"]     # other build
     assert bench.profile_check("planes", 100, 10, 1.20, "abc")["traffic"] is None          # > 5 % apart
     assert bench.profile_check("planes", 100, 11, 1.03, "abc")["traffic"] is None          # other workload
+
+
+def test_aggregation_slices_partition_the_batch():
+    """bench.py splits the aggregation batch over ranks by contiguous job slices: the slices'
+    CalcPGMinResources results (C oracle) concatenate to the whole batch's."""
+    sys.path.insert(0, ROOT)
+    import numpy as np
+
+    import bench
+    import oracle
+    from placement import synth
+    agg = synth.make_pg_batch(2001, 3)
+    want = oracle.pg_min_resources(1, *agg)
+    for world in (2, 3, 8):
+        parts = [oracle.pg_min_resources(1, *bench.pg_slice(agg, r * 2001 // world, (r + 1) * 2001 // world))
+                 for r in range(world)]
+        for k in range(len(want)):
+            np.testing.assert_array_equal(np.concatenate([p[k] for p in parts]), want[k])
