@@ -513,10 +513,13 @@ def main(argv=None):
         for cfg, mix, n_nodes, n_jobs, gpu_frac, what in (
                 ("cfg2", "pytorch", 10_000, 1_000, 0.2, "10k nodes x 1k PyTorchJobs (Master 1 + Worker 0-15)"),
                 ("cfg3", "mixed", 100_000, 10_000, 0.2, "100k nodes x 10k jobs, 50% PyTorch / 25% MPI / 25% JAX"),
-                ("cfg4", "gang8", 100_000, 10_000, 1.0,
-                 "100k 8-GPU nodes x 10k gangs of 1-16 pods x 8 GPUs, label-constrained, all-or-nothing")):
-            cinv = synth.make_inventory(n_nodes, synth.SEED[cfg], gpu_frac)
-            cb = synth.make_jobs(n_jobs, synth.SEED[cfg], mix)
+                ("cfg4", "island8", 100_000, 10_000, 1.0,
+                 "100k 8-GPU nodes x 10k 8-GPU gang jobs on single-node xGMI islands (island groups of 1-8 pods "
+                 "x 8/M GPUs co-located on one node; 1/4 multi-node gangs of 2-4 whole-node pods), all-or-nothing"),
+                ("cfg4_gang8", "gang8", 100_000, 10_000, 1.0,
+                 "100k 8-GPU nodes x 10k gangs of 1-16 whole-node pods x 8 GPUs, label-constrained, all-or-nothing")):
+            cinv = synth.make_inventory(n_nodes, synth.SEED[cfg[:4]], gpu_frac)
+            cb = synth.make_jobs(n_jobs, synth.SEED[cfg[:4]], mix)
             ce = Engine(device, rank=rank, world_size=world, comm=new_comm(), exchange=exchange, max_nodes=n_nodes,
                         topk=args.topk, window_groups=args.window_groups, window_pods=args.window_pods,
                         greedy_flags=args.greedy_flags, resort_nodes=args.resort_nodes)

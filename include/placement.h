@@ -64,6 +64,15 @@ enum {
 
 enum { PE_MODE_V1 = 1, PE_MODE_V2 = 2 };
 enum { PE_JOB_PLACED = 0, PE_JOB_UNSCHEDULABLE = 1 };
+/* xGMI islands (SURVEY.md Appendix B extension; BASELINE config 4).  Label bit 31 of every node is
+ * the engine's: set iff the node has an island (island >= 0 at pe_load_nodes / pe_update_nodes;
+ * the caller's bit 31 is replaced).  A greedy group whose need has bit 31 is an ISLAND GROUP: its
+ * group_count pods are co-located on ONE node with an island, chosen as a unit -- the node with
+ * the smallest Appendix-B key for the summed request count x request (exact int64; a sum that
+ * overflows fits nowhere) -- and all of them land on it, or the job fails (all-or-nothing).
+ * Islands are single nodes in this model (one 8-GPU node = one xGMI island). */
+#define PE_LABEL_ISLAND 0x80000000u
+#define PE_NEED_ISLAND PE_LABEL_ISLAND
 
 /* container record flags for pe_pg_min_resources: bits 0-3 = which dims are present in the
  * container's ResourceList (keys with value 0 are present), bits 4-5 = kind */
@@ -219,7 +228,8 @@ int pe_fit_mask_row_pitch(const pe_ctx* ctx, int64_t* words);
  * out_pod_node[sum(group_count)]: GLOBAL node id per pod slot (groups in input order), -1 = none.
  * out_job_status[J]: PE_JOB_PLACED / PE_JOB_UNSCHEDULABLE.  Residuals are updated in place
  * (successful placements stay; failed jobs are rolled back).  Every rank of a sharded context
- * must make the same call; all ranks return the same placements. */
+ * must make the same call; all ranks return the same placements.  group_need bit 31
+ * (PE_NEED_ISLAND) makes the group an island group (see PE_LABEL_ISLAND). */
 int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority,
                     const int32_t* group_count, const int64_t* group_req, const uint32_t* group_need,
                     int32_t* out_pod_node, int32_t* out_job_status);
@@ -230,7 +240,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
  * Window blob layout (what the device merge kernel writes, per shard, per window group):
  *   16-B header {int32 n; int32 flags; uint64 limit} + K records of 48 B
  *   {uint64 key; int64 res[4]; uint64 labels}; shards are concatenated.
- * Updates are returned as [n][5] int64 {global node id, res[0..3]} (absolute residuals). */
+ * Updates are returned as [n][5] int64 {global node id, res[0..3]} (absolute residuals).
+ * An island group's (PE_NEED_ISLAND) lists must be scanned for group_count x request. */
 typedef struct pe_resolver pe_resolver;
 int pe_resolver_create(int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority,
                        const int32_t* group_count, const int64_t* group_req, const uint32_t* group_need,

@@ -132,10 +132,16 @@ def place_greedy_windowed(Resolver, res, labels, batch, K=256, max_groups=96, ma
     pe_place_greedy, no device.  Returns (pods, status, residual_after, windows)."""
     res = np.array(res, dtype=np.int64, copy=True)
     R = Resolver(batch.job_group_off, batch.priority, batch.group_count, batch.group_req, batch.group_need)
+    # island groups (need bit 31) are scanned for count x request (placement.h PE_NEED_ISLAND)
+    isl = (np.asarray(batch.group_need, dtype=np.uint32) >> 31) != 0
+    scan_req = np.array(batch.group_req, dtype=np.int64, copy=True)
+    for g in np.nonzero(isl)[0]:
+        c = max(int(batch.group_count[g]), 0)
+        scan_req[g] = [min(int(v) * c, (1 << 63) - 1) for v in batch.group_req[g]]
     windows = 0
     while not R.done():
         groups = R.next_window(max_groups, max_pods)
-        blob = window_cands(res, labels, batch.group_req[groups], batch.group_need[groups], K, nthreads)
+        blob = window_cands(res, labels, scan_req[groups], batch.group_need[groups], K, nthreads)
         upd, _ = R.resolve(groups, blob, 1, K)
         for row in upd:
             res[:, int(row[0])] = row[1:]

@@ -31,6 +31,9 @@
  *      key  = fit ? (score << 24) | node : UINT64_MAX     (argmin => ties to lowest node id)
  *      greedy: jobs by (priority desc, index asc); groups in given order; one argmin per pod;
  *              a pod with no fitting node fails the job -> roll back all its pods.
+ *              Island groups (need bit 31, Appendix B extension for BASELINE config 4): the
+ *              group's pods as one unit, argmin over the key of count x request, all on that
+ *              node (node label bit 31 = the node has an xGMI island).
  *      => the greedy/fit oracle is "parity unpinned" against the reference (nothing to pin to);
  *         the aggregation oracle is pinned by the reference's own test known answers
  *         (tests/golden/ fixtures, tests/test_oracle_golden.py).
@@ -46,6 +49,7 @@
 #define ORC_V1 1
 #define ORC_V2 2
 #define SCORE_MAX ((uint64_t)0xFFFFFFFFFFull) /* 2^40 - 1 */
+#define ORC_NEED_ISLAND 0x80000000u /* island group: pods co-located as one unit (placement.h) */
 
 /* ------------------------------------------------------------------ aggregation */
 
@@ -264,6 +268,20 @@ int64_t orc_place_greedy(int64_t N, int64_t* res, const uint32_t* labels, int64_
     int ok = 1;
     for (int32_t g = job_group_off[j]; g < job_group_off[j + 1] && ok; ++g) {
       const int64_t* q = group_req + (int64_t)g * ORC_D;
+      if (group_need[g] & ORC_NEED_ISLAND) {
+        /* island group (placement.h PE_NEED_ISLAND): all group_count pods as one unit on the node
+         * with the smallest key for count x request; a sum that overflows fits nowhere */
+        int64_t qe[ORC_D];
+        int ovf = 0;
+        for (int d = 0; d < ORC_D; ++d) ovf |= mul_ovf(q[d], (int64_t)(group_count[g] > 0 ? group_count[g] : 0), &qe[d]);
+        if (group_count[g] <= 0) continue;
+        uint64_t k = ovf ? UINT64_MAX : argmin_key(N, res, labels, qe, group_need[g], 0);
+        if (k == UINT64_MAX) { ok = 0; break; }
+        int64_t n = (int64_t)(k & 0xFFFFFFull);
+        for (int d = 0; d < ORC_D; ++d) res[(int64_t)d * N + n] -= qe[d];
+        for (int32_t p = 0; p < group_count[g]; ++p) out_pod_node[pod_off[g] + p] = (int32_t)n;
+        continue;
+      }
       for (int32_t p = 0; p < group_count[g]; ++p) {
         uint64_t k = argmin_key(N, res, labels, q, group_need[g], 0);
         if (k == UINT64_MAX) { ok = 0; break; }

@@ -257,6 +257,8 @@ def same_resource_list(a: ResourceList, b: ResourceList) -> bool:
 # --------------------------------------------------------------------------- placement (Appendix B)
 
 SCORE_MAX = (1 << 40) - 1
+INT64_MAX = (1 << 63) - 1
+NEED_ISLAND = 1 << 31   # placement.h PE_NEED_ISLAND: the group's pods as one unit on one island node
 
 
 def appendix_b_key(res4, labels: int, q4, need: int, node: int) -> Optional[int]:
@@ -275,7 +277,8 @@ def appendix_b_key(res4, labels: int, q4, need: int, node: int) -> Optional[int]
 
 def place_greedy_appendix_b(res, labels, job_group_off, priority, group_count, group_req, group_need):
     """The sequential greedy rule in plain Python (small inputs only): jobs by (priority desc, index
-    asc), groups in order, each pod on the argmin-key node, all-or-nothing per job with rollback.
+    asc), groups in order, each pod on the argmin-key node (an island group, need bit 31: all its pods
+    on the one node with the smallest key for count x request), all-or-nothing per job with rollback.
     Returns (pod_node list, job_status list, residual [4][N] as lists of ints)."""
     R = [[int(x) for x in row] for row in res]
     N = len(R[0]) if R else 0
@@ -291,6 +294,26 @@ def place_greedy_appendix_b(res, labels, job_group_off, priority, group_count, g
         ok = True
         for g in range(int(job_group_off[j]), int(job_group_off[j + 1])):
             q = [int(x) for x in group_req[g]]
+            if int(group_need[g]) & NEED_ISLAND and int(group_count[g]) > 0:
+                # island group: every pod on one node, chosen for the summed request
+                c = int(group_count[g])
+                qe = [x * c for x in q]
+                best = None
+                if all(v <= INT64_MAX for v in qe):
+                    for n in range(N):
+                        k = appendix_b_key([R[d][n] for d in range(4)], int(labels[n]), qe, int(group_need[g]), n)
+                        if k is not None and (best is None or k < best):
+                            best = k
+                if best is None:
+                    ok = False
+                    break
+                n = best & 0xFFFFFF
+                for p in range(c):
+                    for d in range(4):
+                        R[d][n] -= q[d]
+                    pods[pod_off[g] + p] = n
+                    placed.append((g, p, n))
+                continue
             for p in range(int(group_count[g])):
                 best = None
                 for n in range(N):

@@ -11,6 +11,8 @@ import struct
 
 import numpy as np
 
+from placement import synth
+
 NO_KEY = np.uint64(0xFFFFFFFFFFFFFFFF)
 SMAX = np.uint64((1 << 40) - 1)
 
@@ -63,12 +65,13 @@ def run_resolver(Resolver, inv_res, labels, batch, K=8, shards=1, max_groups=16,
     N = res.shape[1]
     bounds = [(N * r // shards, N * (r + 1) // shards) for r in range(shards)]
     R = Resolver(batch.job_group_off, batch.priority, batch.group_count, batch.group_req, batch.group_need)
+    scan_req = synth.scan_requests(batch)   # island groups are scanned for count x request
     rng = np.random.default_rng(seed)
     windows = 0
     while not R.done():
         groups = R.next_window(max_groups, max_pods)
         assert len(groups) > 0
-        blob = b"".join(shard_blob(res[:, b:e], labels[b:e], b, batch.group_req[groups], batch.group_need[groups], K,
+        blob = b"".join(shard_blob(res[:, b:e], labels[b:e], b, scan_req[groups], batch.group_need[groups], K,
                                    rng, weak) for b, e in bounds)
         upd, _ = R.resolve(groups, blob, shards, K)
         for row in upd:

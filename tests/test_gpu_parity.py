@@ -349,7 +349,7 @@ def check_greedy(e, inv, batch):
 
 
 @pytest.mark.parametrize("mix,N,J,gpu_frac", [("pytorch", 2000, 200, 0.2), ("mixed", 3000, 300, 0.3),
-                                               ("gang8", 600, 120, 1.0)])
+                                               ("gang8", 600, 120, 1.0), ("island8", 800, 300, 0.8)])
 def test_greedy_vs_oracle(eng, mix, N, J, gpu_frac):
     inv = synth.make_inventory(N, 31 + N, gpu_frac)
     batch = synth.make_jobs(J, 37 + J, mix)
@@ -480,7 +480,8 @@ def test_greedy_score_corner_nodes(eng, case):
 
 
 @pytest.mark.parametrize("mix,N,J,topk,wg", [("mixed", 3000, 400, 64, 64), ("mixed", 1500, 300, 2, 8),
-                                             ("gang8", 500, 150, 4, 16), ("pytorch", 2000, 300, 1, 1)])
+                                             ("gang8", 500, 150, 4, 16), ("pytorch", 2000, 300, 1, 1),
+                                             ("island8", 600, 250, 2, 8)])
 def test_greedy_pipelined_vs_sequential(mix, N, J, topk, wg):
     """The pipelined window loop (next window scanned while the host resolves the current one,
     the current window's changes seeded as dirty) against the sequential loop and the oracle --
@@ -497,7 +498,8 @@ def test_greedy_pipelined_vs_sequential(mix, N, J, topk, wg):
 
 @pytest.mark.parametrize("flags,resort", [(2, 0), (0, 1), (0, 64), (1, 16), (3, 0)])
 @pytest.mark.parametrize("mix,N,J,gpu_frac,topk,wg", [("mixed", 3000, 300, 0.3, 64, 64), ("pytorch", 2500, 300, 0.2, 2, 8),
-                                                       ("gang8", 700, 150, 1.0, 4, 16), ("mixed", 5000, 200, 0.5, 1, 1)])
+                                                       ("gang8", 700, 150, 1.0, 4, 16), ("mixed", 5000, 200, 0.5, 1, 1),
+                                                       ("island8", 900, 300, 0.7, 4, 16)])
 def test_greedy_walk_and_full_scan(flags, resort, mix, N, J, gpu_frac, topk, wg):
     """Both window paths against the oracle: the sorted walk (default; resort_nodes 1 rebuilds the
     sorted index after every applied window, 64 / 16 let the overlay grow across many windows) and
@@ -554,3 +556,36 @@ def test_greedy_topk_beyond_walk_uses_full_scan():
     s = e.stats()
     assert s["scan_evals"] > 0 and s["resorts"] == 0
     e.close()
+
+
+def test_greedy_island_groups(eng):
+    """Island groups (need bit 31): every pod of the group on one node that has an xGMI island,
+    chosen for count x request; island-less nodes (CPU nodes, island -1) never take them even when
+    they would fit; a summed request that overflows int64 fails the job; mixed with ordinary
+    groups and multi-node gangs in one batch, bit-exact vs the oracle and the independent Python
+    restatement."""
+    from oracle import semantics as S
+    inv = synth.make_inventory(400, 83, 0.5)
+    batch = synth.make_jobs(160, 89, "island8")
+    # a cpu-only island group (fits CPU nodes too, but only island nodes may take it) and an overflow
+    g0 = int(batch.job_group_off[3])
+    batch.group_req[g0] = [1000, 1 << 30, 0, 0]
+    batch.group_count[g0] = 3
+    batch.group_need[g0] = np.uint32(1 << 31)
+    g1 = int(batch.job_group_off[5])
+    batch.group_req[g1] = [1, 1 << 61, 0, 0]
+    batch.group_count[g1] = 8
+    batch.group_need[g1] = np.uint32(1 << 31)
+    st = check_greedy(eng, inv, batch)
+    py_pods, py_st, _ = S.place_greedy_appendix_b(inv.residual(), inv.labels, batch.job_group_off, batch.priority,
+                                                  batch.group_count, batch.group_req, batch.group_need)
+    np.testing.assert_array_equal(st, py_st)
+    assert st[5] == 1                                   # the overflowing island group fits nowhere
+    eng.reset_residuals()
+    got_pods, got_st = eng.place_batch(batch)
+    np.testing.assert_array_equal(got_pods, py_pods)
+    off = np.concatenate([[0], np.cumsum(batch.group_count)])
+    for g in np.nonzero(batch.group_need >> 31)[0]:
+        nodes = got_pods[off[g]:off[g + 1]]
+        if len(nodes) and nodes[0] >= 0:
+            assert (nodes == nodes[0]).all() and inv.island[nodes[0]] >= 0   # one island node

@@ -59,7 +59,8 @@ def test_cfg5_fit_mask_full(cfg5):
 
 
 @pytest.mark.parametrize("cfg,mix,n_nodes,n_jobs,gpu_frac", [("cfg3", "mixed", 100_000, 10_000, 0.2),
-                                                            ("cfg4", "gang8", 100_000, 10_000, 1.0)])
+                                                            ("cfg4", "gang8", 100_000, 10_000, 1.0),
+                                                            ("cfg4", "island8", 100_000, 10_000, 1.0)])
 def test_greedy_full_size_bit_exact(cfg, mix, n_nodes, n_jobs, gpu_frac):
     inv = synth.make_inventory(n_nodes, synth.SEED[cfg], gpu_frac)
     batch = synth.make_jobs(n_jobs, synth.SEED[cfg], mix)

@@ -20,7 +20,7 @@ def corner_inventory(N, seed):
     return inv
 
 
-@pytest.mark.parametrize("mix,gpu_frac", [("pytorch", 0.2), ("mixed", 0.3), ("gang8", 1.0)])
+@pytest.mark.parametrize("mix,gpu_frac", [("pytorch", 0.2), ("mixed", 0.3), ("gang8", 1.0), ("island8", 0.7)])
 @pytest.mark.parametrize("seed", [1, 2])
 def test_python_greedy_matches_c_oracle(mix, gpu_frac, seed):
     N, J = 120, 30

@@ -2,6 +2,10 @@
 
 The device scan is replaced by tests/scan_emulator.py (exact per-shard top-K lists); what is
 under test is the product's windowed, sharded, exact resolution protocol and its rollback."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
@@ -31,7 +35,7 @@ def test_emulator_keys_match_c_oracle():
             assert int(k[n]) == oracle.key(res[:, n], inv.labels[n], req[j], need[j], n)
 
 
-@pytest.mark.parametrize("mix,gpu_frac", [("pytorch", 0.2), ("mixed", 0.3), ("gang8", 1.0)])
+@pytest.mark.parametrize("mix,gpu_frac", [("pytorch", 0.2), ("mixed", 0.3), ("gang8", 1.0), ("island8", 0.7)])
 @pytest.mark.parametrize("shards", [1, 2, 3])
 def test_resolver_matches_oracle(mix, gpu_frac, shards):
     inv, batch = small_world(700, 60, 5, mix, gpu_frac)
@@ -40,7 +44,7 @@ def test_resolver_matches_oracle(mix, gpu_frac, shards):
     np.testing.assert_array_equal(st, want_st)
     np.testing.assert_array_equal(pods, want_pods)
     np.testing.assert_array_equal(res, want_res)
-    assert 0 < (st == 0).sum() < len(st) or mix == "gang8"   # exercises placement AND rollback
+    assert 0 < (st == 0).sum() < len(st) or mix in ("gang8", "island8")   # placement AND rollback
 
 
 @pytest.mark.parametrize("K,max_groups,max_pods", [(1, 1, 1), (1, 8, 64), (2, 4, 16), (32, 64, 1024)])
@@ -104,3 +108,14 @@ def test_windowed_cpu_greedy_matches_naive_oracle(K):
     np.testing.assert_array_equal(pods, want[0])
     np.testing.assert_array_equal(res, want[2])
     assert windows > 1
+
+
+def test_resolver_avx2_path_matches_oracle():
+    """The dirty-node scoring has an AVX-512 path and an AVX2 one (CPUs without AVX-512): run the
+    resolver tests again in a process that forces the AVX2 path."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PE_NO_AVX512="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", os.path.join(here, "test_resolver_cpu.py"),
+                        "-k", "matches_oracle and not avx2 or window_shapes or weak_limits or edge_cases"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

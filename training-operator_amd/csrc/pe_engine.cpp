@@ -392,6 +392,14 @@ void pe_destroy(pe_ctx* ctx) { delete ctx; }
 
 const char* pe_last_error(const pe_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+// A node's device / mirror labels: the caller's bits 0-30, bit 31 = the node has an xGMI island
+// (PE_LABEL_ISLAND, what an island group's need requires).
+static uint32_t node_labels(const uint32_t* labels, const int32_t* island, int64_t i) {
+  const uint32_t l = labels ? labels[i] : 0u;
+  const bool has = island && island[i] >= 0;
+  return (l & ~PE_LABEL_ISLAND) | (has ? PE_LABEL_ISLAND : 0u);
+}
+
 int pe_load_nodes(pe_ctx* ctx, int64_t n, const int64_t* cap, const int64_t* used, const uint32_t* labels,
                   const int32_t* island) {
   return guarded(ctx, [&]() -> int {
@@ -417,7 +425,7 @@ int pe_load_nodes(pe_ctx* ctx, int64_t n, const int64_t* cap, const int64_t* use
         r[(size_t)d * ctx->stride + i] = c - u;
       }
     for (int64_t i = 0; i < ctx->Ns; ++i) {
-      lab[i] = labels ? labels[ctx->begin + i] : 0u;
+      lab[i] = node_labels(labels, island, ctx->begin + i);
       isl[i] = island ? island[ctx->begin + i] : -1;
     }
     ctx->m_nodes.assign((size_t)n, pe::NodeState{});
@@ -426,8 +434,7 @@ int pe_load_nodes(pe_ctx* ctx, int64_t n, const int64_t* cap, const int64_t* use
         if (cap[d * n + g] < 0 || used[d * n + g] < 0) raise(PE_EINVAL, "negative capacity/usage");
         ctx->m_nodes[g].res[d] = cap[d * n + g] - used[d * n + g];
       }
-    if (labels)
-      for (int64_t g = 0; g < n; ++g) ctx->m_nodes[g].labels = labels[g];
+    for (int64_t g = 0; g < n; ++g) ctx->m_nodes[g].labels = node_labels(labels, island, g);
     ctx->m_nodes0 = ctx->m_nodes;
     hipchk(ctx->res0.ensure(cells), "alloc res0");
     hipchk(ctx->res.ensure(cells), "alloc res");
@@ -472,7 +479,7 @@ int pe_update_nodes(pe_ctx* ctx, int64_t n, const int64_t* slots, const uint8_t*
       pe::NodeState& m = ctx->m_nodes[g];
       for (int d = 0; d < pe::D; ++d)
         m.res[d] = op[i] == PE_NODE_SET ? cap[i * pe::D + d] - used[i * pe::D + d] : pe::NEVER;
-      m.labels = op[i] == PE_NODE_SET && labels ? labels[i] : 0u;
+      m.labels = op[i] == PE_NODE_SET ? node_labels(labels, island, i) : 0u;
       ctx->m_nodes0[g] = m;
     }
     // last entry per slot wins; keep only this shard's slots
@@ -489,7 +496,7 @@ int pe_update_nodes(pe_ctx* ctx, int64_t n, const int64_t* slots, const uint8_t*
       u.local = slots[i] - ctx->begin;
       if (op[i] == PE_NODE_SET) {
         for (int d = 0; d < pe::D; ++d) u.res[d] = cap[i * pe::D + d] - used[i * pe::D + d];
-        u.labels = labels ? labels[i] : 0u;
+        u.labels = node_labels(labels, island, i);
         u.island = island ? island[i] : -1;
       } else {
         for (int d = 0; d < pe::D; ++d) u.res[d] = pe::NEVER;
@@ -1606,7 +1613,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       const int Wgp = (int)round_up(Wg, pe::SC_GT);
       for (int w = 0; w < Wgp; ++w) {
         const int g = groups[std::min(w, Wg - 1)];
-        fill_req(ctx->h_groups.p[w], group_req + (int64_t)g * pe::D, group_need[g]);
+        fill_req(ctx->h_groups.p[w], R.scan_req(g), group_need[g]);   // island groups: count x request
       }
       // unsharded: the kernel writes the blob straight into pinned host memory (no D2H copy)
       uint8_t* const dst = direct_out ? outbufdev(b) : ctx->g_out.p;

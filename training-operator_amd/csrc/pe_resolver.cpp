@@ -26,6 +26,7 @@ static ResProf rp;
 #endif
 
 static constexpr uint64_t kNoKey = ~0ull;
+static constexpr uint32_t kNeedIsland = 0x80000000u;   // placement.h PE_NEED_ISLAND
 static constexpr uint64_t kScoreMax = (1ull << 40) - 1;
 
 uint64_t score_of(const int64_t left[RD]) {
@@ -340,6 +341,17 @@ Resolver::Resolver(int64_t n_jobs, const int32_t* job_group_off, const int32_t* 
   for (int64_t g = 0; g < G; ++g) pod_off_[g + 1] = pod_off_[g] + std::max<int32_t>(cnt_[g], 0);
   pod_node_.assign((size_t)pod_off_[G], -1);
   job_status_.assign((size_t)J_, 0);
+  qeff_.assign(req_, req_ + (size_t)G * RD);
+  unit_.assign((size_t)G, 0);
+  for (int64_t g = 0; g < G; ++g)
+    if (need_[g] & kNeedIsland) {
+      unit_[g] = 1;
+      for (int d = 0; d < RD; ++d)
+        if (__builtin_mul_overflow(req_[g * RD + d], (int64_t)std::max<int32_t>(cnt_[g], 0), &qeff_[g * RD + d])) {
+          unit_[g] = 2;   // fits nowhere; the scan request saturates
+          qeff_[g * RD + d] = INT64_MAX;
+        }
+    }
   if (!done()) g_ = jgo_[order_[0]];
   advance_group();
 }
@@ -503,8 +515,9 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     while (wi < groups.size() && groups[wi] != g_) ++wi;  // groups of failed jobs are skipped
     if (wi == groups.size()) break;
     const GroupCands& gc = cands[wi];
-    const int64_t* q = req_ + (int64_t)g_ * RD;
+    const int64_t* q = scan_req(g_);   // an island group is one unit of count x request
     const uint32_t need = need_[g_];
+    const uint8_t unit = unit_[g_];
     t_ = RP_T();
     // Look ahead one group: the next list's first clean entries (their mirror states prefetched, the
     // dirty entries before them skipped for good -- the dirty set only grows during a resolve).
@@ -531,7 +544,8 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     size_t ptr = head_[wi];
     size_t pf = ptr;   // clean entries up to pf have been prefetched
     bool failed = false;
-    while (p_ < cnt_[g_]) {
+    if (unit == 2) failed = true;   // an island group whose summed request overflows fits nowhere
+    while (!failed && p_ < cnt_[g_]) {
       t_ = RP_T();
       while (ptr < gc.size() && dirty_.contains((int64_t)(gc.key(ptr) & 0xFFFFFFull))) {
         ++ptr;
@@ -578,7 +592,9 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       // the minimum for every following pod of the group that still fits on it: place them all
       // at once, m = min(pods left, min over q_d > 0 of res_d / q_d).
       int64_t m = cnt_[g_] - p_;
-      if (m > 1) {   // (the chosen node fits one pod; divide only when the rest may not fit)
+      if (unit) {             // the whole island group on this node (it fits count x request)
+        for (int d = 0; d < RD; ++d) st.res[d] -= q[d];
+      } else if (m > 1) {   // (the chosen node fits one pod; divide only when the rest may not fit)
         bool all = true;
         for (int d = 0; d < RD; ++d) {
           int64_t need_d;
@@ -588,7 +604,8 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
           for (int d = 0; d < RD; ++d)
             if (q[d] > 0) m = std::min<int64_t>(m, st.res[d] / q[d]);
       }
-      for (int d = 0; d < RD; ++d) st.res[d] -= m * q[d];
+      if (!unit)
+        for (int d = 0; d < RD; ++d) st.res[d] -= m * q[d];
       if (slot < 0) {
         slot = dirty_.upsert(gid, st);
         if (dk.size() <= (size_t)slot) dk.resize((size_t)slot + 1);

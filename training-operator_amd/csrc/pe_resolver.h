@@ -233,6 +233,9 @@ class Resolver {
   bool resolve(const std::vector<int32_t>& groups, const std::vector<GroupCands>& cands,
                std::vector<Update>& updates, const std::vector<Update>* seed = nullptr);
 
+  // The request a group's candidate lists are scanned for: the pod request, or count x request
+  // for an island group (need bit 31: its pods are placed as one unit on one node).
+  const int64_t* scan_req(int64_t g) const { return &qeff_[(size_t)g * RD]; }
   const std::vector<int32_t>& pod_node() const { return pod_node_; }
   const std::vector<int32_t>& job_status() const { return job_status_; }
   int64_t jobs_placed() const { return jobs_placed_; }
@@ -250,6 +253,8 @@ class Resolver {
   const int32_t* cnt_;
   const int64_t* req_;
   const uint32_t* need_;
+  std::vector<int64_t> qeff_;    // [G][4] scan request (island groups: count x request)
+  std::vector<uint8_t> unit_;    // [G] 1 = island group, 2 = island group whose summed request overflows
   Mirror mirror_;
   std::vector<int64_t> order_;
   std::vector<int64_t> pod_off_;

@@ -73,6 +73,7 @@ def make_inventory(n: int, seed: int, gpu_frac: float = 0.2) -> Inventory:
     zone = (stream(seed, 14, n) % np.uint64(3)).astype(np.uint32)
     labels = (is_gpu.astype(np.uint32) | (np.uint32(1) << (np.uint32(1) + zone))).astype(np.uint32)
     island = np.where(is_gpu, np.arange(n, dtype=np.int32), -1).astype(np.int32)
+    labels = island_labels(labels, island)
     return Inventory(cap, used, labels, island)
 
 
@@ -80,6 +81,27 @@ CPU_REQ = [500, 1000, 2000, 4000, 8000, 16000]
 MEM_REQ = [g * GiB for g in (1, 2, 4, 8, 16, 32, 64, 128)]
 GPU_REQ = [0, 0, 0, 0, 1, 2, 4, 8]
 EPH_REQ = [0, 10 * GiB, 50 * GiB, 100 * GiB]
+
+
+LABEL_ISLAND = np.uint32(1 << 31)   # placement.h PE_LABEL_ISLAND / PE_NEED_ISLAND
+
+
+def island_labels(labels, island):
+    """Node labels as the engine keeps them: bit 31 = the node has an xGMI island (island >= 0)."""
+    lab = np.asarray(labels, dtype=np.uint32) & ~LABEL_ISLAND
+    return np.where(np.asarray(island) >= 0, lab | LABEL_ISLAND, lab).astype(np.uint32)
+
+
+def scan_requests(batch: "JobBatch") -> np.ndarray:
+    """[G][4] the request each group's candidate lists are scanned for (the resolver's scan_req):
+    the pod request, or count x request for an island group (saturated at INT64_MAX on overflow,
+    which fits nowhere)."""
+    req = np.array(batch.group_req, dtype=np.int64, copy=True)
+    isl = (np.asarray(batch.group_need, dtype=np.uint32) & LABEL_ISLAND) != 0
+    for g in np.nonzero(isl)[0]:
+        c = max(int(batch.group_count[g]), 0)
+        req[g] = [min(int(v) * c, (1 << 63) - 1) for v in batch.group_req[g]]
+    return req
 
 
 def pod_requests(seed: int, sid: int, n: int):
@@ -115,7 +137,10 @@ class JobBatch:
 def make_jobs(n_jobs: int, seed: int, mix: str = "pytorch") -> JobBatch:
     """mix: 'pytorch' (cfg2: Master 1 + Worker W in [0,15]),
             'mixed'   (cfg3: 50% PyTorch, 25% MPI {Launcher 1 (1 cpu, 2Gi), Worker W}, 25% JAX {Worker W+1}),
-            'gang8'   (cfg4: one group of M in {1,2,4,8,16} pods x 8 GPUs, requires label bit0)."""
+            'gang8'   (cfg4: one group of M in {1,2,4,8,16} pods x 8 GPUs, requires label bit0),
+            'island8' (cfg4: 8-GPU gang jobs on single-node xGMI islands: one island group of M in
+                       {1,2,4,8} pods x 8/M GPUs, all on one island node; with probability 1/4 a
+                       multi-node gang of M in {2,4} whole-node pods instead)."""
     J = n_jobs
     pri = (stream(seed, 100, J) % np.uint64(1000)).astype(np.int32)
     w = (stream(seed, 101, J) % np.uint64(16)).astype(np.int32)
@@ -124,7 +149,7 @@ def make_jobs(n_jobs: int, seed: int, mix: str = "pytorch") -> JobBatch:
     elif mix == "mixed":
         k = (stream(seed, 102, J) % np.uint64(4)).astype(np.int64)
         kind = np.select([k < 2, k == 2], [0, 1], 2).astype(np.int8)
-    elif mix == "gang8":
+    elif mix in ("gang8", "island8"):
         kind = np.full(J, 3, dtype=np.int8)
     else:
         raise ValueError(mix)
@@ -158,6 +183,19 @@ def make_jobs(n_jobs: int, seed: int, mix: str = "pytorch") -> JobBatch:
         req[first, 2] = 8
         req[first, 3] = 100 * GiB
         need[first] = 1
+    elif mix == "island8":
+        m = pick([1, 2, 4, 8], stream(seed, 103, J)).astype(np.int64)
+        multi = (stream(seed, 106, J) % np.uint64(4)) == 0
+        count[first] = np.where(multi, pick([2, 4], stream(seed, 107, J)), m)
+        # an island job's totals are a gang8 pod's (8 GPUs, 32-96 cores, 256/512 GiB, 100 GiB eph)
+        # split evenly over its M pods; a multi-node gang's pods each take a whole node's GPUs
+        cpu = pick([32_000, 64_000, 96_000], stream(seed, 104, J))
+        mem = pick([256 * GiB, 512 * GiB], stream(seed, 105, J))
+        req[first, 0] = np.where(multi, cpu, cpu // m)
+        req[first, 1] = np.where(multi, mem, mem // m)
+        req[first, 2] = np.where(multi, 8, 8 // m)
+        req[first, 3] = np.where(multi, 100 * GiB, 100 * GiB // m)
+        need[first] = np.where(multi, 1, 1 | (1 << 31)).astype(np.uint32)
     else:
         count[first[one]] = w[one] + 1      # JAX Worker W+1
         req[first[one]] = b_req[one]
