@@ -51,6 +51,10 @@ const (
 const (
 	JobPlaced        = int32(C.PE_JOB_PLACED)
 	JobUnschedulable = int32(C.PE_JOB_UNSCHEDULABLE)
+	// LabelIsland is node label bit 31 (set by the engine when island >= 0); a greedy group whose
+	// need carries NeedIsland is placed as one unit on one island node (placement.h).
+	LabelIsland = uint32(C.PE_LABEL_ISLAND)
+	NeedIsland  = uint32(C.PE_NEED_ISLAND)
 )
 
 // Node inventory update ops.
