@@ -9,14 +9,16 @@
 #include <cstdlib>
 
 #include <immintrin.h>
+#include <pthread.h>
+#include <sched.h>
 #ifdef PE_RES_PROF
 #include <x86intrin.h>
 #endif
 
 namespace pe {
 #ifdef PE_RES_PROF   // section cycle counts for tools/replay_resolver (-DPE_RES_PROF)
-struct ResProf { unsigned long long seed = 0, keys = 0, skip = 0, place = 0, fin = 0, other = 0; long skips = 0, pods = 0, groups = 0, dirty = 0, scored = 0;
-  ~ResProf() { std::fprintf(stderr, "cycles seed %.1fM keys %.1fM skip %.1fM place %.1fM fin %.1fM | skips %ld pods %ld | per group: dirty %.0f scored %.1f\n", seed / 1e6, keys / 1e6, skip / 1e6, place / 1e6, fin / 1e6, skips, pods, (double)dirty / groups, (double)scored / groups); } };
+struct ResProf { unsigned long long seed = 0, keys = 0, skip = 0, place = 0, fin = 0, other = 0; long skips = 0, pods = 0, groups = 0, dirty = 0, scored = 0, sready = 0, slocal = 0, sfull = 0;
+  ~ResProf() { std::fprintf(stderr, "cycles seed %.1fM keys %.1fM skip %.1fM place %.1fM fin %.1fM | skips %ld pods %ld | per group: dirty %.0f scored %.1f\n", seed / 1e6, keys / 1e6, skip / 1e6, place / 1e6, fin / 1e6, skips, pods, (double)dirty / groups, (double)scored / groups); std::fprintf(stderr, "seed tops: helper %ld local %ld full %ld\n", sready, slocal, sfull); } };
 static ResProf rp;
 #define RP_T() __rdtsc()
 #define RP_ADD(f, t) (rp.f += __rdtsc() - (t))
@@ -27,6 +29,10 @@ static ResProf rp;
 
 static constexpr uint64_t kNoKey = ~0ull;
 static constexpr uint32_t kNeedIsland = 0x80000000u;   // placement.h PE_NEED_ISLAND
+#ifndef PE_LOOK_STATES
+#define PE_LOOK_STATES 2
+#endif
+static constexpr size_t kLookStates = PE_LOOK_STATES, kLookLines = PE_LOOK_STATES + 2;   // groups ahead
 static constexpr uint64_t kScoreMax = (1ull << 40) - 1;
 
 uint64_t score_of(const int64_t left[RD]) {
@@ -330,6 +336,130 @@ void parse_window_keys(const uint8_t* blob, int n_shards, int n_groups, int K, s
   }
 }
 
+// ------------------------------------------------------------------ SeedScorer
+
+// CPUs sharing cpu's last-level cache (sysfs cache/index3/shared_cpu_list, e.g. "0-7,128-135").
+bool l3_cpus(int cpu, cpu_set_t* set) {
+  if (cpu < 0) return false;
+  char path[96];
+  std::snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return false;
+  char buf[512] = {0};
+  const bool ok = std::fgets(buf, sizeof(buf), f) != nullptr;
+  std::fclose(f);
+  if (!ok) return false;
+  CPU_ZERO(set);
+  int n = 0;
+  for (char* p = buf; *p && *p != '\n';) {
+    char* e;
+    const long a = std::strtol(p, &e, 10);
+    if (e == p) break;
+    long b = a;
+    if (*e == '-') b = std::strtol(e + 1, &e, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c, ++n) CPU_SET((int)c, set);
+    p = *e == ',' ? e + 1 : e;
+  }
+  return n > 0;
+}
+
+void SeedScorer::compute(const DirtySet& seeds, const GroupCands& gc, const int64_t q[RD], uint32_t need,
+                         SeedTop& top, std::vector<uint64_t>& out, std::vector<int32_t>& idx) {
+  size_t h = 0;   // (plain key arrays only: a lazily merged shard list is the resolver's to read)
+  if (gc.keys)
+    while (h < gc.size() && seeds.contains((int64_t)(gc.keys[h] & 0xFFFFFFull))) ++h;
+  top.head = h;
+  seeds.keys_all(q, need, gc.limit, out, idx);
+  int n = 0;
+  bool trunc = false;
+  for (int32_t i : idx) {   // insertion into the ascending top (few fit below the limit)
+    const uint64_t k = out[(size_t)i];
+    if (k >= gc.limit) continue;
+    if (n == SeedTop::kTop) {
+      trunc = true;
+      if (k >= top.key[n - 1]) continue;
+      --n;
+    }
+    int j = n++;
+    for (; j > 0 && top.key[j - 1] > k; --j) top.key[j] = top.key[j - 1];
+    top.key[j] = k;
+  }
+  top.n = n;
+  top.truncated = trunc;
+}
+
+SeedScorer::~SeedScorer() {
+  if (!th_) return;
+  stop();
+  state_.store(3, std::memory_order_release);
+  th_->join();
+}
+
+void SeedScorer::start(const DirtySet* seeds, const std::vector<int32_t>* groups,
+                       const std::vector<GroupCands>* cands, const int64_t* scan_req, const uint32_t* need) {
+  seeds_ = seeds;
+  groups_ = groups;
+  cands_ = cands;
+  req_ = scan_req;
+  need_ = need;
+  if (tops_.size() < groups->size()) tops_.resize(groups->size());
+  if (cap_ < groups->size()) {
+    cap_ = std::max<size_t>(groups->size(), 2 * cap_);
+    ready_.reset(new std::atomic<uint32_t>[cap_]);
+    for (size_t i = 0; i < cap_; ++i) ready_[i].store(0, std::memory_order_relaxed);
+    gen_ = 0;
+  }
+  if (++gen_ == 0) {   // generation wrap-around: clear the flags
+    for (size_t i = 0; i < cap_; ++i) ready_[i].store(0, std::memory_order_relaxed);
+    gen_ = 1;
+  }
+  main_wi_.store(0, std::memory_order_relaxed);
+  busy_.store(true, std::memory_order_relaxed);
+  if (!th_) {
+    th_.reset(new std::thread([this] { loop(); }));
+    // The resolver and the helper exchange a few cache lines per group (flags, tops): keep the
+    // helper on the CPUs that share the resolver thread's L3 (one CCD), not across the machine.
+    cpu_set_t set;
+    if (l3_cpus(sched_getcpu(), &set)) (void)pthread_setaffinity_np(th_->native_handle(), sizeof(set), &set);
+  }
+  state_.store(1, std::memory_order_release);
+}
+
+void SeedScorer::stop() {
+  if (!th_) return;
+  int posted = 1;
+  state_.compare_exchange_strong(posted, 2, std::memory_order_acq_rel);
+  for (int spin = 0; busy_.load(std::memory_order_acquire); ++spin)   // at most one group's work
+    if (spin < 4096) _mm_pause();
+    else std::this_thread::yield();   // the helper is not running (oversubscribed host)
+  state_.store(0, std::memory_order_release);
+}
+
+void SeedScorer::loop() {
+  for (;;) {
+    const int st = state_.load(std::memory_order_acquire);
+    if (st == 3) return;
+    if (st != 1) {
+      if (busy_.load(std::memory_order_relaxed) && st == 2) busy_.store(false, std::memory_order_release);
+      _mm_pause();
+      continue;
+    }
+    const size_t W = groups_->size();
+    const uint32_t gen = gen_;
+    for (size_t wi = 0; wi < W; ++wi) {
+      if (state_.load(std::memory_order_acquire) != 1) break;   // cancelled: the resolver moved on
+      wi = std::max(wi, main_wi_.load(std::memory_order_relaxed) + 1);   // leapfrog a resolver ahead
+      if (wi >= W) break;
+      const int32_t g = (*groups_)[wi];
+      compute(*seeds_, (*cands_)[wi], req_ + (int64_t)g * RD, need_[g], tops_[wi], out_, idx_);
+      ready_[wi].store(gen, std::memory_order_release);
+    }
+    // done with the window: wait for stop() (state 2) before going idle
+    while (state_.load(std::memory_order_acquire) == 1) _mm_pause();
+    busy_.store(false, std::memory_order_release);
+  }
+}
+
 Resolver::Resolver(int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority, const int32_t* group_count,
                    const int64_t* group_req, const uint32_t* group_need)
     : J_(n_jobs), jgo_(job_group_off), cnt_(group_count), req_(group_req), need_(group_need) {
@@ -480,13 +610,25 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
                        std::vector<Update>& updates, const std::vector<Update>* seed) {
   bool consumed = true;
   unsigned long long t_ = RP_T();
-  if (seed)
+  // Pipelined windows: the seeds (dirty for the whole window, their state known) are kept apart
+  // from the window's own changes (dirty_); the helper thread scores them for every group ahead of
+  // this thread.  A seed this window changes moves to dirty_ and is scored here from then on.
+  const bool useS = seed && !seed->empty();
+  struct ScorerStop {   // the helper never outlives this call (it reads groups / cands / seeds_)
+    SeedScorer& s;
+    ~ScorerStop() { s.stop(); }
+  } scorer_stop{scorer_};
+  if (useS) {
+    seeds_.clear();
     for (const Update& u : *seed) {
       NodeState st;
       for (int d = 0; d < RD; ++d) st.res[d] = u.res[d];
       st.labels = u.labels;
-      dirty_.upsert(u.gid, st);   // dirty but untouched: not flushed again unless changed here
+      seeds_.upsert(u.gid, st);
     }
+    scorer_.start(&seeds_, &groups, &cands, qeff_.data(), need_);
+  }
+  auto is_dirty = [&](int64_t gid) { return dirty_.contains(gid) || (useS && seeds_.contains(gid)); };
   RP_ADD(seed, t_);
   for (int32_t g : groups) {   // the window's group records (scattered over the batch arrays)
     __builtin_prefetch(req_ + (int64_t)g * RD);
@@ -495,9 +637,10 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     __builtin_prefetch(&pod_off_[g]);
   }
   head_.assign(groups.size(), 0);
-  if (!groups.empty() && !cands.empty() && cands[0].keyed)   // the first group's list head
-    for (size_t i = 0; i < std::min<size_t>(4, cands[0].size()); ++i)
-      __builtin_prefetch(&mirror_.nodes[cands[0].key(i) & 0xFFFFFFull]);
+  for (size_t w = 0; w < std::min<size_t>(kLookStates, groups.size()); ++w)   // the first groups' list heads
+    if (cands[w].keyed)
+      for (size_t i = 0; i < std::min<size_t>(4, cands[w].size()); ++i)
+        __builtin_prefetch(&mirror_.nodes[cands[w].key(i) & 0xFFFFFFull]);
   size_t wi = 0;
   std::vector<uint64_t>& dk = dk_;  // keys of the dirty nodes for the current group
   std::vector<int32_t>& dki = dki_;  // the slots among them that can hold a key
@@ -519,35 +662,79 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     const uint32_t need = need_[g_];
     const uint8_t unit = unit_[g_];
     t_ = RP_T();
-    // Look ahead one group: the next list's first clean entries (their mirror states prefetched, the
-    // dirty entries before them skipped for good -- the dirty set only grows during a resolve).
-    if (wi + 1 < groups.size() && cands[wi + 1].keyed) {
-      const GroupCands& gn = cands[wi + 1];
-      size_t p = 0;
+    // Look ahead: the list lines of the group kLookLines ahead on their way; the first clean entries
+    // of the group kLookStates ahead found (the dirty entries before them skipped for good -- the
+    // dirty set only grows during a resolve) and their mirror states prefetched.
+    if (wi + kLookLines < groups.size() && cands[wi + kLookLines].keys)
+      for (int l = 0; l < 2; ++l) __builtin_prefetch(cands[wi + kLookLines].keys + 8 * l);
+    if (wi + kLookStates < groups.size() && cands[wi + kLookStates].keyed) {
+      const size_t wn = wi + kLookStates;
+      const GroupCands& gn = cands[wn];
+      size_t p = useS && scorer_.ready(wn) ? scorer_.top(wn).head : 0;   // (the helper skipped the seeds)
       int c = 0;
-      while (p < gn.size() && dirty_.contains((int64_t)(gn.key(p) & 0xFFFFFFull))) ++p;
-      head_[wi + 1] = p;
+      while (p < gn.size() && is_dirty((int64_t)(gn.key(p) & 0xFFFFFFull))) ++p;
+      head_[wn] = p;
       for (; p < gn.size() && c < 3; ++p)
-        if (!dirty_.contains((int64_t)(gn.key(p) & 0xFFFFFFull))) {
+        if (!is_dirty((int64_t)(gn.key(p) & 0xFFFFFFull))) {
           __builtin_prefetch(&mirror_.nodes[gn.key(p) & 0xFFFFFFull]);
           ++c;
         }
     }
     dirty_.keys_all(q, need, gc.limit, dk, dki);   // dirty keys >= limit never decide (list head or rescan)
     int32_t best = argmin();
+    // the seeds' keys: the helper's top (or computed here when it is not ready yet)
+    SeedTop local;
+    const SeedTop* top = nullptr;
+    if (useS) {
+      scorer_.at(wi);
+      if (scorer_.ready(wi)) {
+        top = &scorer_.top(wi);
+#ifdef PE_RES_PROF
+        rp.sready++;
+#endif
+      } else {
+#ifdef PE_RES_PROF
+        rp.slocal++;
+#endif
+        SeedScorer::compute(seeds_, gc, q, need, local, sk_out_, sk_idx_);
+        top = &local;
+      }
+    }
+    size_t sp = 0;        // next candidate of the seed top
+    bool sfull = false;   // the top ran out (truncated): every seed key below the limit in sfull_
+    auto seed_key = [&]() -> uint64_t {   // smallest key of a seed this window has not changed
+      if (!useS) return kNoKey;
+      for (;;) {
+        const uint64_t* ks = sfull ? sfull_.data() : top->key;
+        const size_t n = sfull ? sfull_.size() : (size_t)top->n;
+        while (sp < n && dirty_.contains((int64_t)(ks[sp] & 0xFFFFFFull))) ++sp;
+        if (sp < n) return ks[sp];
+        if (sfull || !top->truncated) return kNoKey;
+        seeds_.keys_all(q, need, gc.limit, sk_out_, sk_idx_);
+        sfull_.clear();
+        for (int32_t i : sk_idx_)
+          if (sk_out_[(size_t)i] < gc.limit) sfull_.push_back(sk_out_[(size_t)i]);
+        std::sort(sfull_.begin(), sfull_.end());
+#ifdef PE_RES_PROF
+        rp.sfull++;
+#endif
+        sfull = true;
+        sp = 0;
+      }
+    };
     RP_ADD(keys, t_);
 #ifdef PE_RES_PROF
     rp.groups++;
     rp.dirty += (long)dirty_.size();
     rp.scored += (long)dki.size();
 #endif
-    size_t ptr = head_[wi];
+    size_t ptr = useS ? std::max(top->head, head_[wi]) : head_[wi];
     size_t pf = ptr;   // clean entries up to pf have been prefetched
     bool failed = false;
     if (unit == 2) failed = true;   // an island group whose summed request overflows fits nowhere
     while (!failed && p_ < cnt_[g_]) {
       t_ = RP_T();
-      while (ptr < gc.size() && dirty_.contains((int64_t)(gc.key(ptr) & 0xFFFFFFull))) {
+      while (ptr < gc.size() && is_dirty((int64_t)(gc.key(ptr) & 0xFFFFFFull))) {
         ++ptr;
 #ifdef PE_RES_PROF
         rp.skips++;
@@ -556,7 +743,9 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       RP_ADD(skip, t_);
       t_ = RP_T();
       const uint64_t kc = ptr < gc.size() ? gc.key(ptr) : kNoKey;
-      const uint64_t kd = best >= 0 ? dk[best] : kNoKey;
+      const uint64_t kdT = best >= 0 ? dk[best] : kNoKey;
+      const uint64_t kdS = seed_key();
+      const uint64_t kd = std::min(kdT, kdS);
       if (ptr == gc.size() && gc.limit != kNoKey && kd >= gc.limit) {
         consumed = false;  // clean nodes beyond the limit could win: rescan from this pod
         break;
@@ -569,15 +758,18 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       const int64_t gid = (int64_t)(bkey & 0xFFFFFFull);
       NodeState st;
       int32_t slot;
-      if (bkey == kd) {
+      if (bkey == kdT) {
         slot = best;
         st = dirty_.get(slot);
+      } else if (bkey == kdS) {   // an unchanged seed: its window-start state is current
+        st = seeds_.get(seeds_.find(gid));
+        slot = -1;
       } else {
         if (gc.keyed) {   // clean: the mirror holds the snapshot state
           st = mirror_.nodes[gid];
           // keep the next two clean entries' states on their way
           for (int c = 0; pf < gc.size() && c < 2; ++pf)
-            if (pf > ptr && !dirty_.contains((int64_t)(gc.key(pf) & 0xFFFFFFull))) {
+            if (pf > ptr && !is_dirty((int64_t)(gc.key(pf) & 0xFFFFFFull))) {
               __builtin_prefetch(&mirror_.nodes[gc.key(pf) & 0xFFFFFFull]);
               ++c;
             }

@@ -10,9 +10,13 @@
 // the device and the next window rescans from the current pod.  Pure C++, no HIP: the same code
 // runs behind every shard (all ranks resolve identically) and under the CPU tests.
 #pragma once
+#include <sched.h>
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <memory>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -211,6 +215,62 @@ class DirtySet {
   std::vector<uint64_t> bits_;
 };
 
+// CPUs that share cpu's L3 (Linux sysfs); false if unknown.
+bool l3_cpus(int cpu, cpu_set_t* set);
+
+// Per window group: the smallest keys over the window's SEEDS (nodes changed since the lists'
+// snapshot, their current state known at the window start), below the group's limit.
+struct SeedTop {
+  static constexpr int kTop = 32;
+  int n = 0;                 // keys in key[], ascending
+  bool truncated = false;    // more seed keys lie below the limit than kTop
+  size_t head = 0;           // the group list's first entry that is not a seed
+  uint64_t key[kTop];
+};
+
+// Scores the seeds of a pipelined window for every group of the window, in group order, on a
+// helper thread that runs ahead of the resolver: the seeds stay untouched until the resolver
+// changes them, so a seed's key computed from its window-start state is current until then
+// (the resolver skips the entries of seeds it has changed and scores those itself).  The
+// resolver never waits: a group whose top is not ready yet is scored on the resolver's thread.
+class SeedScorer {
+ public:
+  SeedScorer() = default;
+  ~SeedScorer();
+  SeedScorer(const SeedScorer&) = delete;
+  SeedScorer& operator=(const SeedScorer&) = delete;
+  // Main thread: start scoring a window (seeds, cands and the request arrays must stay unchanged
+  // until stop()).
+  void start(const DirtySet* seeds, const std::vector<int32_t>* groups, const std::vector<GroupCands>* cands,
+             const int64_t* scan_req, const uint32_t* need);
+  bool ready(size_t wi) const { return ready_[wi].load(std::memory_order_acquire) == gen_; }
+  const SeedTop& top(size_t wi) const { return tops_[wi]; }
+  // the resolver is at group wi: the helper skips what it would finish too late
+  void at(size_t wi) { main_wi_.store(wi, std::memory_order_relaxed); }
+  void stop();   // cancel the window and wait until the helper is idle
+  // one group's top (any thread; out / idx are the caller's scratch)
+  static void compute(const DirtySet& seeds, const GroupCands& gc, const int64_t q[RD], uint32_t need, SeedTop& top,
+                      std::vector<uint64_t>& out, std::vector<int32_t>& idx);
+
+ private:
+  void loop();
+  std::unique_ptr<std::thread> th_;
+  std::atomic<int> state_{0};            // 0 idle, 1 window posted, 2 cancel, 3 exit
+  std::unique_ptr<std::atomic<uint32_t>[]> ready_;   // ready_[wi] == gen_: tops_[wi] is final
+  size_t cap_ = 0;
+  uint32_t gen_ = 0;                                  // window generation (written before posting)
+  std::atomic<size_t> main_wi_{0};
+  std::atomic<bool> busy_{false};
+  const DirtySet* seeds_ = nullptr;
+  const std::vector<int32_t>* groups_ = nullptr;
+  const std::vector<GroupCands>* cands_ = nullptr;
+  const int64_t* req_ = nullptr;
+  const uint32_t* need_ = nullptr;
+  std::vector<SeedTop> tops_;
+  std::vector<uint64_t> out_;
+  std::vector<int32_t> idx_;
+};
+
 class Resolver {
  public:
   Resolver(int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority, const int32_t* group_count,
@@ -269,6 +329,13 @@ class Resolver {
   std::vector<uint64_t> dk_;
   std::vector<int32_t> dki_;   // dirty slots with a key for the current group (argmin runs over these)
   std::vector<size_t> head_;   // per window group: its list's first entry not known to be dirty
+  // pipelined windows: the seeds live here (not in dirty_, which then holds the window's own
+  // changes only); their per-group keys come from the scorer's helper thread
+  DirtySet seeds_;
+  std::vector<uint64_t> sk_out_;
+  std::vector<int32_t> sk_idx_;
+  std::vector<uint64_t> sfull_;      // a group's every seed key below the limit (truncated top)
+  SeedScorer scorer_;                // declared after what its thread reads: stopped first
   // nodes touched by the current job (exact current residuals, survive window flushes)
   // gid -> index into jn_ (reset per job): no allocation per pod
   static constexpr size_t kJobLinear = 32;
