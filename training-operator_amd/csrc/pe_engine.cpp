@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <immintrin.h>
+#include <pthread.h>
 #include <sched.h>
 
 #include <algorithm>
@@ -93,6 +94,7 @@ class SpinWorker {
     state_.store(3, std::memory_order_release);
     th_.join();
   }
+  void pin(const cpu_set_t& set) { (void)pthread_setaffinity_np(th_.native_handle(), sizeof(set), &set); }
   void post(std::function<void()> f) {
     task_ = std::move(f);
     err_ = nullptr;
@@ -1602,7 +1604,27 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // ---- one window on the device: group requests H2D, scan, merge, (RCCL all-gather), blob D2H
     int cb = 0;   // the blob buffer of the window being resolved
     std::unique_ptr<SpinWorker> worker;
-    if (pipelined) worker.reset(new SpinWorker(ctx->device));
+    // The resolver, the seed scorer (pe_resolver.cpp) and the launch helper hand cache lines to each
+    // other every window / group: keep the three on the CPUs that share this thread's L3 (one CCD)
+    // for the call -- intersected with the caller's affinity, restored on return; PE_NO_PIN=1 skips.
+    struct Pin {
+      cpu_set_t old_set, l3;
+      bool on = false;
+      Pin() {
+        if (std::getenv("PE_NO_PIN") || pthread_getaffinity_np(pthread_self(), sizeof(old_set), &old_set) != 0 ||
+            !pe::l3_cpus(sched_getcpu(), &l3))
+          return;
+        CPU_AND(&l3, &l3, &old_set);
+        on = CPU_COUNT(&l3) >= 3 && pthread_setaffinity_np(pthread_self(), sizeof(l3), &l3) == 0;
+      }
+      ~Pin() {
+        if (on) (void)pthread_setaffinity_np(pthread_self(), sizeof(old_set), &old_set);
+      }
+    } pin;
+    if (pipelined) {
+      worker.reset(new SpinWorker(ctx->device));
+      if (pin.on) worker->pin(pin.l3);
+    }
     // blob buffer b (0: h_out, 1: h_out2): the pipelined loop D2Hs the next window's blob while the
     // host still resolves from the current one's
     auto outbuf = [&](int b) { return b ? ctx->h_out2.p : ctx->h_out.p; };
