@@ -572,7 +572,7 @@ def main(argv=None):
                                                "mask); nproc counts the whole machine, shared with other GPUs' jobs",
                                "counts_match_gpu": bool(np.array_equal(ocounts, gpu_counts))}
         if "greedy" in out:
-            # the same algorithm on the CPU: windowed protocol (K = 256, 96 groups / 1024 pods per window, the engine defaults),
+            # the same algorithm on the CPU: windowed protocol (K = 256, 128 groups / 1024 pods per window, the engine defaults),
             # each window's candidate lists built by the C oracle over all 1M nodes (OpenMP over groups),
             # resolved by the product's host resolver -- on the first jobs of the same batch
             gj = args.cpu_greedy_jobs

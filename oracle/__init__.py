@@ -126,7 +126,7 @@ def window_cands(res, labels, group_req, group_need, K: int, nthreads=0) -> byte
     return blob.tobytes()
 
 
-def place_greedy_windowed(Resolver, res, labels, batch, K=256, max_groups=96, max_pods=1024, nthreads=0):
+def place_greedy_windowed(Resolver, res, labels, batch, K=256, max_groups=128, max_pods=1024, nthreads=0):
     """The engine's windowed greedy protocol with the scan done by window_cands on the CPU and the
     resolution by the product's host resolver (pe_resolver_*): the same algorithm as
     pe_place_greedy, no device.  Returns (pods, status, residual_after, windows)."""

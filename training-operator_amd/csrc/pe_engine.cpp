@@ -160,7 +160,7 @@ struct pe_ctx {
   ncclComm_t comm = nullptr;
   pe_allgather_fn exchange = nullptr;
   void* exchange_user = nullptr;
-  int topk = 256, window_groups = 96;
+  int topk = 256, window_groups = 128;
   bool pipeline = true;   // greedy: scan window w+1 while the host resolves window w (greedy_flags bit0 = off)
   int64_t window_pods = 1024;
   int64_t max_nodes = 0;
@@ -352,7 +352,7 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   ctx->exchange_user = cfg->exchange_user;
   ctx->max_nodes = cfg->max_nodes > 0 ? cfg->max_nodes : PE_MAX_NODES;
   ctx->topk = cfg->topk > 0 ? std::min(cfg->topk, pe::MG_CAP) : 256;
-  ctx->window_groups = cfg->window_groups > 0 ? cfg->window_groups : 96;
+  ctx->window_groups = cfg->window_groups > 0 ? cfg->window_groups : 128;
   ctx->window_pods = cfg->window_pods > 0 ? cfg->window_pods : 1024;
   ctx->gpu_name = cfg->gpu_resource_name ? cfg->gpu_resource_name : "amd.com/gpu";
   ctx->fit_path_mask = cfg->fit_path_mask & (PATHS_ALL | PATH_NO_THERM | PATH_PLANES_BLOCKS);
