@@ -444,6 +444,24 @@ func (r *Resolver) Resolve(groups []int32, blob []byte, nShards, topK int32) ([]
 	return upd[:5*int64(nu)], consumed != 0, nil
 }
 
+// ResolveSeeded is Resolve for the pipelined protocol: seeds ([n][6] int64: node id, res[0..3],
+// labels) are the nodes changed since the snapshot the blob was scanned on, with current state.
+func (r *Resolver) ResolveSeeded(groups []int32, blob []byte, nShards, topK int32, seeds []int64) ([]int64, bool, error) {
+	if len(seeds)%6 != 0 {
+		return nil, false, fmt.Errorf("placement: seeds must be [n][6]")
+	}
+	maxUpd := int64(2*r.pods + 64)
+	upd := make([]int64, 5*maxUpd)
+	var nu C.int64_t
+	var consumed C.int32_t
+	rc := C.pe_resolver_resolve_seeded(r.r, C.int32_t(len(groups)), ptr32(groups), ptr8(blob), C.int32_t(nShards),
+		C.int32_t(topK), C.int64_t(len(seeds)/6), ptr64(seeds), ptr64(upd), C.int64_t(maxUpd), &nu, &consumed)
+	if rc != C.PE_OK {
+		return nil, false, fmt.Errorf("placement: pe_resolver_resolve_seeded: %d", int(rc))
+	}
+	return upd[:5*int64(nu)], consumed != 0, nil
+}
+
 // Results: the node of every pod slot (-1 = none) and every job's status.
 func (r *Resolver) Results() (podNode, jobStatus []int32, err error) {
 	podNode = make([]int32, r.pods)

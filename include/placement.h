@@ -253,6 +253,15 @@ int pe_resolver_next_window(pe_resolver* r, int32_t max_groups, int64_t max_pods
 int pe_resolver_resolve(pe_resolver* r, int32_t n_groups, const int32_t* groups, const uint8_t* blob,
                         int32_t n_shards, int32_t topk, int64_t* out_updates, int64_t max_updates,
                         int64_t* out_n_updates, int32_t* out_consumed);
+/* Pipelined form (what pe_place_greedy does internally): the blob's lists were scanned on a
+ * snapshot that misses some changes; seeds [n_seeds][6] = {global node id, res[0..3], labels} are
+ * every node changed since that snapshot, with its CURRENT state (e.g. the previous window's
+ * updates).  They count as dirty for the whole window and are scored by a helper thread ahead of
+ * the resolution.  Updates returned as by pe_resolver_resolve (nodes this window changed). */
+int pe_resolver_resolve_seeded(pe_resolver* r, int32_t n_groups, const int32_t* groups, const uint8_t* blob,
+                               int32_t n_shards, int32_t topk, int64_t n_seeds, const int64_t* seeds,
+                               int64_t* out_updates, int64_t max_updates, int64_t* out_n_updates,
+                               int32_t* out_consumed);
 int pe_resolver_results(const pe_resolver* r, int32_t* out_pod_node, int32_t* out_job_status);
 
 int pe_synchronize(pe_ctx* ctx);

@@ -11,7 +11,7 @@ import pytest
 
 import oracle
 from placement import Resolver, synth
-from scan_emulator import keys, run_resolver
+from scan_emulator import keys, run_resolver, shard_blob
 
 
 def small_world(n_nodes, n_jobs, seed, mix="pytorch", gpu_frac=0.2):
@@ -119,3 +119,68 @@ def test_resolver_avx2_path_matches_oracle():
                         "-k", "matches_oracle and not avx2 or window_shapes or weak_limits or edge_cases"],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def run_resolver_pipelined(inv, batch, K, max_groups, max_pods, shards=1):
+    """The engine's pipelined protocol driven from Python: every window's lists are scanned on a
+    snapshot that lags one window behind (the previous window's changes not applied yet), and
+    those changes, with their current states, are the resolution's seeds
+    (pe_resolver_resolve_seeded).  A window cut short drops the lag: its successor is scanned on
+    the current state without seeds, as the engine's rescan does."""
+    res = inv.residual().copy()           # current state (every resolved window applied)
+    snap = res.copy()                     # what the "device" scans: one window behind
+    labels = inv.labels
+    N = res.shape[1]
+    bounds = [(N * r // shards, N * (r + 1) // shards) for r in range(shards)]
+    scan_req = synth.scan_requests(batch)
+    R = Resolver(batch.job_group_off, batch.priority, batch.group_count, batch.group_req, batch.group_need)
+    pending = np.zeros((0, 5), np.int64)  # the previous window's updates (not in snap yet)
+    n_seeded = 0
+    while not R.done():
+        groups = R.next_window(max_groups, max_pods)
+        blob = b"".join(shard_blob(snap[:, b:e], labels[b:e], b, scan_req[groups], batch.group_need[groups], K)
+                        for b, e in bounds)
+        seeds = None
+        if len(pending):
+            seeds = np.concatenate([pending, labels[pending[:, 0]].astype(np.int64)[:, None]], axis=1)
+            n_seeded += 1
+        upd, consumed = R.resolve(groups, blob, shards, K, seeds=seeds)
+        for row in pending:               # the device catches up by one window
+            snap[:, int(row[0])] = row[1:]
+        for row in upd:
+            res[:, int(row[0])] = row[1:]
+        if consumed:
+            pending = upd
+        else:
+            for row in upd:
+                snap[:, int(row[0])] = row[1:]
+            pending = np.zeros((0, 5), np.int64)
+    pods, st = R.results()
+    return pods, st, res, n_seeded
+
+
+@pytest.mark.parametrize("mix,gpu_frac,K,wg,wp", [("mixed", 0.3, 32, 16, 64), ("mixed", 0.3, 256, 48, 1024),
+                                                  ("pytorch", 0.2, 8, 8, 32), ("island8", 0.7, 32, 16, 64),
+                                                  ("gang8", 1.0, 32, 8, 64)])
+@pytest.mark.parametrize("shards", [1, 2])
+def test_resolver_pipelined_seeds_match_oracle(mix, gpu_frac, K, wg, wp, shards):
+    """Seeds (nodes changed since the lists' snapshot) are scored by the resolver's helper thread
+    and skipped in the lists: the pipelined protocol stays bit-exact to the sequential oracle,
+    including dense seed sets (more than the helper's 32-key top below a limit) and rescans."""
+    inv, batch = small_world(3000, 400, 7, mix, gpu_frac)
+    want = oracle_run(inv, batch)
+    pods, st, res, n_seeded = run_resolver_pipelined(inv, batch, K, wg, wp, shards)
+    np.testing.assert_array_equal(st, want[1])
+    np.testing.assert_array_equal(pods, want[0])
+    np.testing.assert_array_equal(res, want[2])
+    assert n_seeded > 0
+
+
+def test_resolver_seeded_rejects_bad_seeds():
+    from placement import PlacementError
+    inv, batch = small_world(100, 5, 3)
+    R = Resolver(batch.job_group_off, batch.priority, batch.group_count, batch.group_req, batch.group_need)
+    groups = R.next_window(4, 64)
+    blob = shard_blob(inv.residual(), inv.labels, 0, batch.group_req[groups], batch.group_need[groups], 4)
+    with pytest.raises(PlacementError):
+        R.resolve(groups, blob, 1, 4, seeds=np.array([[-1, 0, 0, 0, 0, 0]], np.int64))

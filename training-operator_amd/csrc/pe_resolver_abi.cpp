@@ -78,13 +78,33 @@ int pe_resolver_next_window(pe_resolver* r, int32_t max_groups, int64_t max_pods
 int pe_resolver_resolve(pe_resolver* r, int32_t n_groups, const int32_t* groups, const uint8_t* blob,
                         int32_t n_shards, int32_t topk, int64_t* out_updates, int64_t max_updates,
                         int64_t* out_n_updates, int32_t* out_consumed) {
+  return pe_resolver_resolve_seeded(r, n_groups, groups, blob, n_shards, topk, 0, nullptr, out_updates, max_updates,
+                                    out_n_updates, out_consumed);
+}
+
+int pe_resolver_resolve_seeded(pe_resolver* r, int32_t n_groups, const int32_t* groups, const uint8_t* blob,
+                               int32_t n_shards, int32_t topk, int64_t n_seeds, const int64_t* seeds,
+                               int64_t* out_updates, int64_t max_updates, int64_t* out_n_updates,
+                               int32_t* out_consumed) {
   if (!r || n_groups < 0 || n_shards < 1 || topk < 1 || !out_n_updates || !out_consumed) return PE_EINVAL;
   if (n_groups > 0 && (!groups || !blob)) return PE_EINVAL;
+  if (n_seeds < 0 || (n_seeds > 0 && !seeds)) return PE_EINVAL;
+  for (int64_t i = 0; i < n_seeds; ++i)
+    if (seeds[i * 6] < 0 || seeds[i * 6] >= PE_MAX_NODES || seeds[i * 6 + 5] < 0 || seeds[i * 6 + 5] > 0xFFFFFFFFll)
+      return PE_EINVAL;
   try {
     std::vector<int32_t> g(groups, groups + n_groups);
+    for (int32_t x : g)
+      if (x < 0 || x >= (int32_t)r->cnt.size()) return PE_EINVAL;
     pe::parse_window(blob, n_shards, n_groups, topk, r->cands);
+    std::vector<pe::Update> seed((size_t)n_seeds);
+    for (int64_t i = 0; i < n_seeds; ++i) {
+      seed[i].gid = seeds[i * 6];
+      for (int d = 0; d < 4; ++d) seed[i].res[d] = seeds[i * 6 + 1 + d];
+      seed[i].labels = (uint32_t)seeds[i * 6 + 5];
+    }
     r->updates.clear();
-    const bool consumed = r->r->resolve(g, r->cands, r->updates);
+    const bool consumed = r->r->resolve(g, r->cands, r->updates, n_seeds > 0 ? &seed : nullptr);
     if ((int64_t)r->updates.size() > max_updates || (!out_updates && !r->updates.empty())) return PE_EINVAL;
     for (size_t i = 0; i < r->updates.size(); ++i) {
       out_updates[i * 5] = r->updates[i].gid;

@@ -285,14 +285,21 @@ class Resolver:
             raise PlacementError(rc, "pe_resolver_next_window")
         return out[:n.value].copy()
 
-    def resolve(self, groups: np.ndarray, blob: bytes, n_shards: int, topk: int):
+    def resolve(self, groups: np.ndarray, blob: bytes, n_shards: int, topk: int, seeds=None):
+        """seeds: [n][6] int64 {node id, res[0..3], labels} -- nodes changed since the snapshot the
+        blob was scanned on, current state (pipelined form, pe_resolver_resolve_seeded)."""
         g = _c(groups, np.int32)
         buf = np.frombuffer(blob, dtype=np.uint8)
         cap = max(64, 2 * self.P + 64)
         upd = np.zeros((cap, 5), dtype=np.int64)
         nu, cons = ctypes.c_int64(), ctypes.c_int32()
-        rc = self.lib.pe_resolver_resolve(self.h, len(g), _p(g), _p(buf), n_shards, topk, _p(upd), cap,
-                                          ctypes.byref(nu), ctypes.byref(cons))
+        if seeds is not None and len(seeds):
+            sd = _c(seeds, np.int64).reshape(-1, 6)
+            rc = self.lib.pe_resolver_resolve_seeded(self.h, len(g), _p(g), _p(buf), n_shards, topk, sd.shape[0],
+                                                     _p(sd), _p(upd), cap, ctypes.byref(nu), ctypes.byref(cons))
+        else:
+            rc = self.lib.pe_resolver_resolve(self.h, len(g), _p(g), _p(buf), n_shards, topk, _p(upd), cap,
+                                              ctypes.byref(nu), ctypes.byref(cons))
         if rc != 0:
             raise PlacementError(rc, "pe_resolver_resolve")
         return upd[:nu.value].copy(), bool(cons.value)

@@ -83,6 +83,8 @@ SIGNATURES = {
     "pe_resolver_next_window": (ctypes.c_int, [P, i32, i64, P, ctypes.POINTER(i32)]),
     "pe_resolver_resolve": (ctypes.c_int, [P, i32, P, P, i32, i32, P, i64, ctypes.POINTER(i64),
                                            ctypes.POINTER(i32)]),
+    "pe_resolver_resolve_seeded": (ctypes.c_int, [P, i32, P, P, i32, i32, i64, P, P, i64, ctypes.POINTER(i64),
+                                                  ctypes.POINTER(i32)]),
     "pe_resolver_results": (ctypes.c_int, [P, P, P]),
     "pe_synchronize": (ctypes.c_int, [P]),
     "pe_stream": (P, [P]),
