@@ -451,7 +451,11 @@ void SeedScorer::loop() {
       wi = std::max(wi, main_wi_.load(std::memory_order_relaxed) + 1);   // leapfrog a resolver ahead
       if (wi >= W) break;
       const int32_t g = (*groups_)[wi];
-      compute(*seeds_, (*cands_)[wi], req_ + (int64_t)g * RD, need_[g], tops_[wi], out_, idx_);
+      try {
+        compute(*seeds_, (*cands_)[wi], req_ + (int64_t)g * RD, need_[g], tops_[wi], out_, idx_);
+      } catch (...) {   // (bad_alloc) the resolver scores the remaining groups itself
+        break;
+      }
       ready_[wi].store(gen, std::memory_order_release);
     }
     // done with the window: wait for stop() (state 2) before going idle
