@@ -788,8 +788,12 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd, bool 
   // phases of a set of J jobs: one wave per SIMD (1024 on 256 CUs) = nblk x R; codes phase-major.
   // (Padding the row to 1024 / R blocks, i.e. an aligned 1 MiB store window, was measured no
   // faster: profiles/r5c_row_pitch.txt.)
+  // PE_PL_WAVES / PE_PL_JPW (A/B studies): a fixed wave count, or R from a jobs-per-wave target
+  static const int64_t pl_waves = std::getenv("PE_PL_WAVES") ? std::max(1ll, std::atoll(std::getenv("PE_PL_WAVES"))) : 1024;
+  static const int64_t pl_jpw = std::getenv("PE_PL_JPW") ? std::max(1ll, std::atoll(std::getenv("PE_PL_JPW"))) : 0;
   auto phases = [&](int64_t J, int64_t& R, int64_t& Jr) {
-    R = ctx->pl_rows ? std::min<int64_t>(J, std::max<int64_t>(1, 1024 / ctx->pl_nblk)) : 1;
+    R = ctx->pl_rows ? std::min<int64_t>(J, std::max<int64_t>(1, pl_waves / ctx->pl_nblk)) : 1;
+    if (ctx->pl_rows && pl_jpw) R = std::min<int64_t>(J, std::max<int64_t>(R, (J + pl_jpw - 1) / pl_jpw));
     Jr = ctx->pl_rows ? ((J + R - 1) / R + 3) / 4 * 4 : J;   // = the kernel's phase stride
   };
   std::vector<uint64_t> jc;

@@ -580,6 +580,14 @@ __device__ __forceinline__ uint32_t writelane_s(uint32_t v, uint32_t x, uint32_t
   return v;
 }
 
+// Switching the indexed plane inside one gpr_idx region: PE_GPRIDX_CHAIN keeps the mode on and
+// moves the index with s_set_gpr_idx_idx (one SALU instead of an off / on pair).
+#ifdef PE_GPRIDX_CHAIN
+#define PE_IDX_SWITCH(sel) sel "s_set_gpr_idx_idx %[t]\n\t"
+#else
+#define PE_IDX_SWITCH(sel) "s_set_gpr_idx_off\n\t" sel "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+#endif
+
 // Plane registers.  Plane p = 8q + s lives in tuple q (pinned to v[32+32q : 63+32q]) at elements
 // 4s..4s+3 = its 4 node words, i.e. word r of plane p is v(32 + 4p + r): one dwordx4 load per plane
 // lands in place, and ONE gpr_idx region with index 4p addresses all four words (src0 = v32..v35
@@ -675,21 +683,13 @@ __device__ __forceinline__ void plane_job(u32x4& f, uint32_t lo, uint32_t hi, co
       "s_and_b32 %[t], %[c], 0x7f\n\t"
       "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
       "v_mov_b32_e32 %[f0], v32\n\tv_mov_b32_e32 %[f1], v33\n\tv_mov_b32_e32 %[f2], v34\n\tv_mov_b32_e32 %[f3], v35\n\t"
-      "s_set_gpr_idx_off\n\t"
-      "s_bfe_u32 %[t], %[c], 0x70007\n\t"
-      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      PE_IDX_SWITCH("s_bfe_u32 %[t], %[c], 0x70007\n\t")
       "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
-      "s_set_gpr_idx_off\n\t"
-      "s_bfe_u32 %[t], %[c], 0x7000e\n\t"
-      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      PE_IDX_SWITCH("s_bfe_u32 %[t], %[c], 0x7000e\n\t")
       "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
-      "s_set_gpr_idx_off\n\t"
-      "s_bfe_u32 %[t], %[c], 0x70015\n\t"
-      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      PE_IDX_SWITCH("s_bfe_u32 %[t], %[c], 0x70015\n\t")
       "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
-      "s_set_gpr_idx_off\n\t"
-      "s_and_b32 %[t], %[c4], 0x7f\n\t"
-      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      PE_IDX_SWITCH("s_and_b32 %[t], %[c4], 0x7f\n\t")
       "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
       "s_set_gpr_idx_off"
       : [f0] "=&v"(f.x), [f1] "=&v"(f.y), [f2] "=&v"(f.z), [f3] "=&v"(f.w), [c] "=&s"(c), [c4] "=&s"(c4),
@@ -804,21 +804,13 @@ __device__ __forceinline__ void plane_job_row(u32x4& f, uint32_t& row, uint32_t 
       "s_and_b32 %[t], %[c], 0x7f\n\t"
       "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
       "v_mov_b32_e32 %[f0], v32\n\tv_mov_b32_e32 %[f1], v33\n\tv_mov_b32_e32 %[f2], v34\n\tv_mov_b32_e32 %[f3], v35\n\t"
-      "s_set_gpr_idx_off\n\t"
-      "s_bfe_u32 %[t], %[c], 0x70007\n\t"
-      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      PE_IDX_SWITCH("s_bfe_u32 %[t], %[c], 0x70007\n\t")
       "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
-      "s_set_gpr_idx_off\n\t"
-      "s_bfe_u32 %[t], %[c], 0x7000e\n\t"
-      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      PE_IDX_SWITCH("s_bfe_u32 %[t], %[c], 0x7000e\n\t")
       "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
-      "s_set_gpr_idx_off\n\t"
-      "s_bfe_u32 %[t], %[c], 0x70015\n\t"
-      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      PE_IDX_SWITCH("s_bfe_u32 %[t], %[c], 0x70015\n\t")
       "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
-      "s_set_gpr_idx_off\n\t"
-      "s_and_b32 %[t], %[c4], 0x7f\n\t"
-      "s_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+      PE_IDX_SWITCH("s_and_b32 %[t], %[c4], 0x7f\n\t")
       "v_and_b32_e32 %[f0], v32, %[f0]\n\tv_and_b32_e32 %[f1], v33, %[f1]\n\tv_and_b32_e32 %[f2], v34, %[f2]\n\tv_and_b32_e32 %[f3], v35, %[f3]\n\t"
       "s_set_gpr_idx_off\n\t"
       "s_lshr_b32 %[row], %[c4], 8"
