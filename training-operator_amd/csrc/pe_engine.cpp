@@ -101,20 +101,25 @@ class SpinWorker {
     state_.store(1, std::memory_order_release);
   }
   void wait() {   // rethrows what the task threw
-    while (state_.load(std::memory_order_acquire) != 2) _mm_pause();
+    for (int spin = 0; state_.load(std::memory_order_acquire) != 2; ++spin)
+      if (spin < 4096) _mm_pause();
+      else std::this_thread::yield();   // the helper is not running (oversubscribed host)
     state_.store(0, std::memory_order_relaxed);
     if (err_) std::rethrow_exception(err_);
   }
 
  private:
   void loop() {
+    int idle = 0;
     for (;;) {
       const int st = state_.load(std::memory_order_acquire);
       if (st == 3) return;
       if (st != 1) {
-        _mm_pause();
+        if (++idle < 4096) _mm_pause();
+        else std::this_thread::yield();   // long idle (host resolving): let others run
         continue;
       }
+      idle = 0;
       try {
         task_();
       } catch (...) {

@@ -436,14 +436,17 @@ void SeedScorer::stop() {
 }
 
 void SeedScorer::loop() {
+  int idle = 0;
   for (;;) {
     const int st = state_.load(std::memory_order_acquire);
     if (st == 3) return;
     if (st != 1) {
       if (busy_.load(std::memory_order_relaxed) && st == 2) busy_.store(false, std::memory_order_release);
-      _mm_pause();
+      if (++idle < 4096) _mm_pause();
+      else std::this_thread::yield();   // long idle: let others run
       continue;
     }
+    idle = 0;
     const size_t W = groups_->size();
     const uint32_t gen = gen_;
     for (size_t wi = 0; wi < W; ++wi) {
@@ -459,7 +462,9 @@ void SeedScorer::loop() {
       ready_[wi].store(gen, std::memory_order_release);
     }
     // done with the window: wait for stop() (state 2) before going idle
-    while (state_.load(std::memory_order_acquire) == 1) _mm_pause();
+    for (int spin = 0; state_.load(std::memory_order_acquire) == 1; ++spin)
+      if (spin < 4096) _mm_pause();
+      else std::this_thread::yield();
     busy_.store(false, std::memory_order_release);
   }
 }
