@@ -634,6 +634,37 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
 
 // ------------------------------------------------------------------ fit mask
 
+// body(j0, j1) over [0, n) in contiguous chunks: on up to 8 threads for large batches (the batch
+// planning is on the upload's path), inline for small ones.  Exceptions are rethrown here.
+extern "C++" {
+template <class Body>
+static void parallel_for(int64_t n, Body body) {
+  const int64_t nt = n < 32768 ? 1 : std::min<int64_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+  if (nt <= 1) {
+    body(0, n);
+    return;
+  }
+  std::vector<std::exception_ptr> err((size_t)nt);
+  std::vector<std::thread> th;
+  for (int64_t t = 1; t < nt; ++t)
+    th.emplace_back([&, t] {
+      try {
+        body(n * t / nt, n * (t + 1) / nt);
+      } catch (...) {
+        err[(size_t)t] = std::current_exception();
+      }
+    });
+  try {
+    body(0, n / nt);
+  } catch (...) {
+    err[0] = std::current_exception();
+  }
+  for (auto& x : th) x.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+}
+}  // extern "C++"
+
 // The batch's dictionary, built once per upload and shared by every fit path's planning: per field
 // (dims 0-3, field 4 = label need) the distinct values ascending and each job's index into them.
 // One hashing pass per field (first-seen ids), then only the distinct values are sorted -- O(J)
@@ -644,8 +675,9 @@ struct BatchDict {
   std::vector<uint32_t> rank[F];
 };
 
-static void dict_field(int64_t n, const std::function<int64_t(int64_t)>& value, std::vector<int64_t>& vals,
-                       std::vector<uint32_t>& rank) {
+extern "C++" {   // (this part of the file sits in the ABI's extern "C" block)
+template <class V>
+static void dict_field(int64_t n, V value, std::vector<int64_t>& vals, std::vector<uint32_t>& rank) {
   size_t cap = 64;
   while (cap < 2 * (size_t)n) cap *= 2;
   std::vector<int64_t> keys(cap);
@@ -664,26 +696,68 @@ static void dict_field(int64_t n, const std::function<int64_t(int64_t)>& value, 
     }
     rank[j] = ids[h];
   }
-  std::vector<uint32_t> ord(vals.size());
-  for (size_t i = 0; i < ord.size(); ++i) ord[i] = (uint32_t)i;
-  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return vals[a] < vals[b]; });
-  std::vector<uint32_t> pos(vals.size());
-  std::vector<int64_t> sorted(vals.size());
-  for (size_t i = 0; i < ord.size(); ++i) {
-    pos[ord[i]] = (uint32_t)i;
-    sorted[i] = vals[ord[i]];
+  // order the distinct values: (value, first-seen id) pairs, LSD radix (11-bit digits, passes whose
+  // digit is constant skipped) for many values, a comparison sort for few
+  const size_t m = vals.size();
+  std::vector<std::pair<uint64_t, uint32_t>> pr(m), tmp;
+  for (size_t i = 0; i < m; ++i) pr[i] = {(uint64_t)vals[i] ^ (1ull << 63), (uint32_t)i};   // signed order
+  if (m < 4096) {
+    std::sort(pr.begin(), pr.end());
+  } else {
+    tmp.resize(m);
+    uint64_t orv = 0, andv = ~0ull;
+    for (const auto& e : pr) {
+      orv |= e.first;
+      andv &= e.first;
+    }
+    for (int sh = 0; sh < 64; sh += 11) {
+      if ((((orv ^ andv) >> sh) & 0x7FF) == 0) continue;   // every value has the same digit here
+      size_t cnt[2049] = {0};
+      for (const auto& e : pr) ++cnt[((e.first >> sh) & 0x7FF) + 1];
+      for (int b = 0; b < 2048; ++b) cnt[b + 1] += cnt[b];
+      for (const auto& e : pr) tmp[cnt[(e.first >> sh) & 0x7FF]++] = e;
+      pr.swap(tmp);
+    }
   }
-  vals.swap(sorted);
+  std::vector<uint32_t> pos(m);
+  for (size_t i = 0; i < m; ++i) {
+    pos[pr[i].second] = (uint32_t)i;
+    vals[i] = (int64_t)(pr[i].first ^ (1ull << 63));
+  }
   for (int64_t j = 0; j < n; ++j) rank[j] = pos[rank[j]];
 }
+}  // extern "C++"
 
 static void build_dict(BatchDict& bd, int64_t n_jobs, const int64_t* req, const uint32_t* need) {
-  for (int f = 0; f < BatchDict::F; ++f) {
+  auto field = [&](int f) {
     if (f < pe::D)
       dict_field(n_jobs, [&](int64_t j) { return req[j * pe::D + f]; }, bd.vals[f], bd.rank[f]);
     else
       dict_field(n_jobs, [&](int64_t j) { return (int64_t)(need ? need[j] : 0u); }, bd.vals[f], bd.rank[f]);
+  };
+  if (n_jobs < 16384) {
+    for (int f = 0; f < BatchDict::F; ++f) field(f);
+    return;
   }
+  // large batches: the five independent fields on five threads (the upload is on the batch's path)
+  std::exception_ptr err[BatchDict::F];
+  std::vector<std::thread> th;
+  for (int f = 1; f < BatchDict::F; ++f)
+    th.emplace_back([&, f] {
+      try {
+        field(f);
+      } catch (...) {
+        err[f] = std::current_exception();
+      }
+    });
+  try {
+    field(0);
+  } catch (...) {
+    err[0] = std::current_exception();
+  }
+  for (auto& t : th) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
 }
 
 // Dictionary codes of one batch (pe_kernels.h, CodeSpec): per dimension the sorted distinct request
@@ -777,10 +851,15 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd, bool 
     P += (int64_t)vals[f].size();
   }
   if (P > pe::PL_MAX && !allow_sets) return false;
-  // pair id (global over the fields) of each job's five selections
-  std::vector<int32_t> pid((size_t)n_jobs * F);
-  for (int64_t j = 0; j < n_jobs; ++j)
-    for (int f = 0; f < F; ++f) pid[(size_t)j * F + f] = (int32_t)(off[f] + bd.rank[f][j]);
+  // pair id (global over the fields) of each job's five selections (the plane-set path)
+  std::vector<int32_t> pid;
+  if (P > pe::PL_MAX) {
+    pid.resize((size_t)n_jobs * F);
+    parallel_for(n_jobs, [&](int64_t j0, int64_t j1) {
+      for (int64_t j = j0; j < j1; ++j)
+        for (int f = 0; f < F; ++f) pid[(size_t)j * F + f] = (int32_t)(off[f] + bd.rank[f][j]);
+    });
+  }
   auto pair_spec = [&](int64_t p, int& kind, int64_t& val) {
     int f = F - 1;
     while (off[f] > p) --f;
@@ -811,20 +890,18 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd, bool 
       pair_spec(p, kind, sp.val[sp.n]);
       sp.kind[sp.n++] = kind;
     }
-    jc.resize((size_t)n_jobs);
-    for (int64_t j = 0; j < n_jobs; ++j) {
-      uint64_t c = 0;
-      for (int f = 0; f < F; ++f) c |= (uint64_t)(4 * pid[(size_t)j * F + f]) << field_shift(f);
-      jc[j] = c;
-    }
     ctx->plane = sp;
     int64_t R, Jr;
     phases(n_jobs, R, Jr);
-    if (ctx->pl_rows) {
-      std::vector<uint64_t> perm((size_t)(R * Jr), 0);
-      for (int64_t j = 0; j < n_jobs; ++j) perm[(size_t)((j % R) * Jr + j / R)] = jc[j];
-      jc.swap(perm);
-    }
+    // each job's code straight into its phase-major slot (row-major kernel) or job order
+    jc.assign((size_t)(ctx->pl_rows ? R * Jr : n_jobs), 0);
+    parallel_for(n_jobs, [&](int64_t j0, int64_t j1) {
+      for (int64_t j = j0; j < j1; ++j) {
+        uint64_t c = 0;
+        for (int f = 0; f < F; ++f) c |= (uint64_t)(4 * (off[f] + bd.rank[f][j])) << field_shift(f);
+        jc[ctx->pl_rows ? (size_t)((j % R) * Jr + j / R) : (size_t)j] = c;
+      }
+    });
     ctx->pl_R = R;
     ctx->pl_counts_n = R * Jr;
   } else {
@@ -1088,7 +1165,8 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   const int64_t Tpad = round_up(std::max<int64_t>(Tmax, 1), 16);
   // job codes: u16 plane indices at the kernel's slots, stored in the kernel's consumption order
   std::vector<uint16_t> codes((size_t)(R * 16 * Tpad * pe::LD_CODE), 0);
-  for (int64_t j = 0; j < n_jobs; ++j) {
+  parallel_for(n_jobs, [&](int64_t j0, int64_t j1) {
+  for (int64_t j = j0; j < j1; ++j) {
     const int64_t r = j % R, q = j / R, w = q % 16, t = q / 16;
     uint16_t* c = codes.data() + (size_t)(((r * 16 + w) * Tpad + t) * pe::LD_CODE);
     for (int i = 0; i < sp.nf; ++i) {
@@ -1106,6 +1184,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
     }
     c[pe::LD_NEED_SLOT] = (uint16_t)(sp.need_pbase + bd.rank[4][j]);
   }
+  });
   if (std::getenv("PE_LDS_DEBUG")) {   // diagnostics: the chosen configuration
     std::fprintf(stderr, "lds: W %d nblk %lld R %lld planes %d need %d fold %d |", W, (long long)nblk, (long long)R,
                  sp.nplanes, sp.nneed, sp.nfold);
