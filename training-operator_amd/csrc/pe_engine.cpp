@@ -1695,20 +1695,23 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // The resolver, the seed scorer (pe_resolver.cpp) and the launch helper hand cache lines to each
     // other every window / group: keep the three on the CPUs that share this thread's L3 (one CCD)
     // for the call -- intersected with the caller's affinity, restored on return; PE_NO_PIN=1 skips.
+    // With several ranks on one host (world > 1), rank r takes the (r mod n)-th of the n L3 domains
+    // its affinity allows, so ranks do not pile their spinning threads onto one CCD.
     struct Pin {
       cpu_set_t old_set, l3;
       bool on = false;
-      Pin() {
-        if (std::getenv("PE_NO_PIN") || pthread_getaffinity_np(pthread_self(), sizeof(old_set), &old_set) != 0 ||
-            !pe::l3_cpus(sched_getcpu(), &l3))
+      explicit Pin(int rank, int world) {
+        if (std::getenv("PE_NO_PIN") || pthread_getaffinity_np(pthread_self(), sizeof(old_set), &old_set) != 0)
           return;
+        const int cpu = world > 1 ? pe::l3_pick(old_set, rank) : sched_getcpu();
+        if (!pe::l3_cpus(cpu, &l3)) return;
         CPU_AND(&l3, &l3, &old_set);
         on = CPU_COUNT(&l3) >= 3 && pthread_setaffinity_np(pthread_self(), sizeof(l3), &l3) == 0;
       }
       ~Pin() {
         if (on) (void)pthread_setaffinity_np(pthread_self(), sizeof(old_set), &old_set);
       }
-    } pin;
+    } pin(ctx->rank, ctx->world);
     if (pipelined) {
       worker.reset(new SpinWorker(ctx->device));
       if (pin.on) worker->pin(pin.l3);

@@ -363,6 +363,21 @@ bool l3_cpus(int cpu, cpu_set_t* set) {
   return n > 0;
 }
 
+int l3_pick(const cpu_set_t& allowed, int k) {
+  std::vector<int> first;   // first allowed CPU of each L3 domain
+  cpu_set_t seen;
+  CPU_ZERO(&seen);
+  for (int c = 0; c < CPU_SETSIZE; ++c) {
+    if (!CPU_ISSET(c, &allowed) || CPU_ISSET(c, &seen)) continue;
+    cpu_set_t dom;
+    if (!l3_cpus(c, &dom)) return -1;
+    CPU_OR(&seen, &seen, &dom);
+    first.push_back(c);
+  }
+  if (first.empty() || k < 0) return -1;
+  return first[(size_t)k % first.size()];
+}
+
 void SeedScorer::compute(const DirtySet& seeds, const GroupCands& gc, const int64_t q[RD], uint32_t need,
                          SeedTop& top, std::vector<uint64_t>& out, std::vector<int32_t>& idx) {
   size_t h = 0;   // (plain key arrays only: a lazily merged shard list is the resolver's to read)

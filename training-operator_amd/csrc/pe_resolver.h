@@ -24,7 +24,13 @@ namespace pe {
 
 constexpr int RD = 4;
 
-struct NodeState {
+// One cache line per node: the host mirror is read at random node ids (one DRAM miss each, the
+// next candidates prefetched); 40-B records straddled two lines for half the ids, and the second
+// line was never prefetched.  PE_NODESTATE_ALIGN=8 restores the packed 40-B record (A/B builds).
+#ifndef PE_NODESTATE_ALIGN
+#define PE_NODESTATE_ALIGN 64
+#endif
+struct alignas(PE_NODESTATE_ALIGN) NodeState {
   int64_t res[RD];
   uint32_t labels;
 };
@@ -217,6 +223,9 @@ class DirtySet {
 
 // CPUs that share cpu's L3 (Linux sysfs); false if unknown.
 bool l3_cpus(int cpu, cpu_set_t* set);
+// A CPU of the (k mod n)-th of the n L3 domains that `allowed` touches (domains ordered by their
+// first allowed CPU); -1 if unknown.
+int l3_pick(const cpu_set_t& allowed, int k);
 
 // Per window group: the smallest keys over the window's SEEDS (nodes changed since the lists'
 // snapshot, their current state known at the window start), below the group's limit.
