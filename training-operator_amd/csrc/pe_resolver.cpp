@@ -17,8 +17,8 @@
 
 namespace pe {
 #ifdef PE_RES_PROF   // section cycle counts for tools/replay_resolver (-DPE_RES_PROF)
-struct ResProf { unsigned long long seed = 0, keys = 0, skip = 0, place = 0, fin = 0, other = 0; long skips = 0, pods = 0, groups = 0, dirty = 0, scored = 0, sready = 0, slocal = 0, sfull = 0;
-  ~ResProf() { std::fprintf(stderr, "cycles seed %.1fM keys %.1fM skip %.1fM place %.1fM fin %.1fM | skips %ld pods %ld | per group: dirty %.0f scored %.1f\n", seed / 1e6, keys / 1e6, skip / 1e6, place / 1e6, fin / 1e6, skips, pods, (double)dirty / groups, (double)scored / groups); std::fprintf(stderr, "seed tops: helper %ld local %ld full %ld\n", sready, slocal, sfull); } };
+struct ResProf { unsigned long long p1 = 0, p2 = 0, p3 = 0, la = 0, ka = 0, st = 0, seed = 0, keys = 0, skip = 0, place = 0, fin = 0, other = 0; long skips = 0, pods = 0, groups = 0, dirty = 0, scored = 0, sready = 0, slocal = 0, sfull = 0;
+  ~ResProf() { std::fprintf(stderr, "keys split: lookahead %.1fM keys_all %.1fM seed top %.1fM | place split: choose+fetch %.1fM m %.1fM upsert..key %.1fM\n", la / 1e6, ka / 1e6, st / 1e6, p1 / 1e6, p2 / 1e6, p3 / 1e6); std::fprintf(stderr, "cycles seed %.1fM keys %.1fM skip %.1fM place %.1fM fin %.1fM | skips %ld pods %ld | per group: dirty %.0f scored %.1f\n", seed / 1e6, keys / 1e6, skip / 1e6, place / 1e6, fin / 1e6, skips, pods, (double)dirty / groups, (double)scored / groups); std::fprintf(stderr, "seed tops: helper %ld local %ld full %ld\n", sready, slocal, sfull); } };
 static ResProf rp;
 #define RP_T() __rdtsc()
 #define RP_ADD(f, t) (rp.f += __rdtsc() - (t))
@@ -704,8 +704,12 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
           ++c;
         }
     }
+    RP_ADD(la, t_);
+    unsigned long long t2_ = RP_T();
     dirty_.keys_all(q, need, gc.limit, dk, dki);   // dirty keys >= limit never decide (list head or rescan)
     int32_t best = argmin();
+    RP_ADD(ka, t2_);
+    t2_ = RP_T();
     // the seeds' keys: the helper's top (or computed here when it is not ready yet)
     SeedTop local;
     const SeedTop* top = nullptr;
@@ -746,6 +750,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         sp = 0;
       }
     };
+    RP_ADD(st, t2_);
     RP_ADD(keys, t_);
 #ifdef PE_RES_PROF
     rp.groups++;
@@ -804,6 +809,8 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         }
         slot = -1;
       }
+      RP_ADD(p1, t_);
+      unsigned long long t3_ = RP_T();
       // The chosen node's key only falls while it still fits (its leftovers shrink), so it stays
       // the minimum for every following pod of the group that still fits on it: place them all
       // at once, m = min(pods left, min over q_d > 0 of res_d / q_d).
@@ -822,6 +829,8 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       }
       if (!unit)
         for (int d = 0; d < RD; ++d) st.res[d] -= m * q[d];
+      RP_ADD(p2, t3_);
+      t3_ = RP_T();
       if (slot < 0) {
         slot = dirty_.upsert(gid, st);
         if (dk.size() <= (size_t)slot) dk.resize((size_t)slot + 1);
@@ -838,6 +847,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       dk[slot] = dirty_.key_at(slot, q, need);
       if (dk[slot] != kNoKey) best = slot;
       else if (best == slot) best = argmin();
+      RP_ADD(p3, t3_);
       RP_ADD(place, t_);
 #ifdef PE_RES_PROF
       rp.pods++;
