@@ -496,6 +496,28 @@ def test_greedy_pipelined_vs_sequential(mix, N, J, topk, wg):
     np.testing.assert_array_equal(res[0], res[1])
 
 
+@pytest.mark.parametrize("mix,N,J,topk,wg", [("mixed", 4000, 600, 64, 64), ("mixed", 2000, 400, 2, 8),
+                                             ("island8", 800, 300, 4, 16), ("pytorch", 3000, 500, 1, 2)])
+def test_greedy_signalled_windows(mix, N, J, topk, wg):
+    """Pipelined walk windows are taken group by group as the device signals them (the resolver
+    starts before the slowest block is done; PE_NO_GROUP_SIGNAL=1 waits for the whole launch):
+    both equal the oracle, including small K / windows that discard speculative windows."""
+    inv = synth.make_inventory(N, 97 + N, 0.35)
+    batch = synth.make_jobs(J, 101 + J, mix)
+    res = {}
+    for sync in ("1", None):
+        if sync:
+            os.environ["PE_NO_GROUP_SIGNAL"] = sync
+        try:
+            e = Engine(0, topk=topk, window_groups=wg)
+            res[sync] = check_greedy(e, inv, batch)
+            e.place_batch(batch)   # a second batch on the same context: generations keep counting
+            e.close()
+        finally:
+            os.environ.pop("PE_NO_GROUP_SIGNAL", None)
+    np.testing.assert_array_equal(res["1"], res[None])
+
+
 @pytest.mark.parametrize("flags,resort", [(2, 0), (0, 1), (0, 64), (1, 16), (3, 0)])
 @pytest.mark.parametrize("mix,N,J,gpu_frac,topk,wg", [("mixed", 3000, 300, 0.3, 64, 64), ("pytorch", 2500, 300, 0.2, 2, 8),
                                                        ("gang8", 700, 150, 1.0, 4, 16), ("mixed", 5000, 200, 0.5, 1, 1),

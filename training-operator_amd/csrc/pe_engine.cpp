@@ -238,7 +238,8 @@ struct pe_ctx {
   DevBuf<int64_t> g_upd;
   DevBuf<uint64_t> g_kn;   // scan: node-only score terms K(n) (prep_nodes), refreshed by apply
   DevBuf<uint32_t> g_lo;   // scan: lo20(r1) / lo24(r3), [2][stride]
-  HostBuf<ReqRec> h_groups;
+  HostBuf<ReqRec> h_groups, h_groups2;   // h_groups2: the window requests of blob buffer 1 (signalled walk)
+  uint32_t walk_gen = 0;                  // generation of the last signalled walk window (never 0)
   HostBuf<uint8_t> h_out, h_out2, h_own;   // h_out2: the pipelined loop's second blob buffer
   HostBuf<int64_t> h_upd;
   // greedy sorted walk (pe_kernels.h WalkIndex; the default window path, greedy_flags bit1 = full scan)
@@ -265,7 +266,7 @@ struct pe_ctx {
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
-    g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_out.release(); h_out2.release(); h_own.release(); h_upd.release();
+    g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_groups2.release(); h_out.release(); h_out2.release(); h_own.release(); h_upd.release();
     w_sk.release(); w_kin.release(); w_rmin.release(); w_sr.release(); w_rmax.release(); w_sl.release(); w_pos.release();
     w_ror.release(); w_inovl.release(); w_ovl.release(); w_ovln.release(); w_temp.release();
     w_ovidx.release(); w_ovlab.release(); w_ovres.release(); w_stat.release();
@@ -291,6 +292,9 @@ int guarded(pe_ctx* ctx, F&& body) {
   } catch (const std::bad_alloc&) {
     ctx->err = "host allocation failed";
     return PE_ENOMEM;
+  } catch (const std::runtime_error& e) {   // pe::WindowFeed: a walk group the device never signalled
+    ctx->err = e.what();
+    return PE_EHIP;
   } catch (...) {
     ctx->err = "unexpected C++ exception";
     return PE_EINVAL;
@@ -1721,12 +1725,30 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     auto outbuf = [&](int b) { return b ? ctx->h_out2.p : ctx->h_out.p; };
     auto outbufdev = [&](int b) { return b ? ctx->h_out2.dev : ctx->h_out.dev; };
     const bool direct_out = ctx->world == 1 && !ctx->comm;
+    // Pipelined walk windows written in place are SIGNALLED per group (pe::WindowFeed): the host
+    // takes each group's list when its block is done, not at a stream sync after the slowest block.
+    // The window requests are then double-buffered like the blobs (a walk may still be running when
+    // the next window's requests are written); seeing any group of window w signalled proves that
+    // every earlier launch of the stream is complete (kernels of one stream run in order), which is
+    // what the pinned update records need.  PE_NO_GROUP_SIGNAL=1: stream sync per window instead.
+    const bool signalled = pipelined && walk && direct_out && !std::getenv("PE_NO_GROUP_SIGNAL");
+    if (signalled) hipchk(ctx->h_groups2.ensure(Wpad, kZeroCopy), "alloc pinned groups");
+    uint32_t buf_gen[2] = {0, 0};
+    pe::WindowFeed feed;
+    struct StreamIdle {
+      hipStream_t s;
+      static bool busy(void* u) { return hipStreamQuery(static_cast<StreamIdle*>(u)->s) == hipErrorNotReady; }
+    } stream_idle{s};
+    feed.idle = &StreamIdle::busy;
+    feed.idle_user = &stream_idle;
+    double feed_spin_seen = 0;   // feed.spin_ms() already counted as device wait
     auto enqueue_window = [&](const std::vector<int32_t>& groups, int b) {
       const int Wg = (int)groups.size();
       const int Wgp = (int)round_up(Wg, pe::SC_GT);
+      auto& hg = signalled && b ? ctx->h_groups2 : ctx->h_groups;
       for (int w = 0; w < Wgp; ++w) {
         const int g = groups[std::min(w, Wg - 1)];
-        fill_req(ctx->h_groups.p[w], R.scan_req(g), group_need[g]);   // island groups: count x request
+        fill_req(hg.p[w], R.scan_req(g), group_need[g]);   // island groups: count x request
       }
       // unsharded: the kernel writes the blob straight into pinned host memory (no D2H copy)
       uint8_t* const dst = direct_out ? outbufdev(b) : ctx->g_out.p;
@@ -1739,14 +1761,19 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           walk_events.push_back(evp);
           hipchk(hipEventRecord(evp.first, s), "event record");
         }
-        hipchk(pe::launch_walk(s, ctx->h_groups.dev, Wg, K, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p,
-                               ctx->Ns, (uint64_t)ctx->begin, dst),
+        uint32_t gen = 0;
+        if (signalled) {
+          if (++ctx->walk_gen == 0) ++ctx->walk_gen;
+          gen = ctx->walk_gen;
+        }
+        buf_gen[b] = gen;
+        hipchk(pe::launch_walk(s, hg.dev, Wg, K, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns,
+                               (uint64_t)ctx->begin, dst, gen),
                "launch walk");
         if (wev) hipchk(hipEventRecord(evp.second, s), "event record");
         walk_launch_groups += Wg;
       } else if (ctx->Ns > 0) {
-        hipchk(hipMemcpyAsync(ctx->g_groups.p, ctx->h_groups.p, Wgp * sizeof(ReqRec), hipMemcpyHostToDevice, s),
-               "H2D window");
+        hipchk(hipMemcpyAsync(ctx->g_groups.p, hg.p, Wgp * sizeof(ReqRec), hipMemcpyHostToDevice, s), "H2D window");
         hipchk(pe::launch_scan(s, ctx->res.p, ctx->stride, ctx->labels.p, ctx->g_kn.p, ctx->g_lo.p, ctx->Ns,
                                (uint64_t)ctx->begin, ctx->g_groups.p, Wg, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p,
                                nwaves),
@@ -1785,6 +1812,15 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       const int Wg = (int)groups.size();
       const size_t bytes = (size_t)Wg * gb;
       const auto tw = std::chrono::steady_clock::now();
+      if (signalled && buf_gen[b] != 0) {   // the first group's list (and so every earlier launch) is done
+        feed.reset(outbuf(b), Wg, K, buf_gen[b], &cands);
+        feed.wait(0);
+        feed_spin_seen = feed.spin_ms();
+        const auto th = std::chrono::steady_clock::now();
+        ctx->stats.greedy_wait_ms += std::chrono::duration<double, std::milli>(th - tw).count();
+        if (trace) tr_wait.push_back(std::chrono::duration<double, std::micro>(th - tw).count());
+        return;
+      }
       hipchk(hipStreamSynchronize(s), "sync window");
       if (use_exchange) {
         if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, outbuf(b), bytes) != 0)
@@ -1825,6 +1861,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         dump = nullptr;
       }
       if (dump) {   // {Wg, groups, blob, n_seed, seeds}: what this resolve call reads
+        if (signalled) feed.wait(groups.size() - 1);   // (diagnostics: the whole blob first)
         const int32_t wg = (int32_t)groups.size(), ns = seed ? (int32_t)seed->size() : 0;
         std::fwrite(&wg, 4, 1, dump);
         std::fwrite(groups.data(), 4, (size_t)wg, dump);
@@ -1834,12 +1871,17 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       const auto th = std::chrono::steady_clock::now();
       updates.clear();
-      const bool consumed = R.resolve(groups, cands, updates, seed);
-      if (trace) tr_res.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - th).count());
+      const bool fed = signalled && buf_gen[cb] != 0;
+      const bool consumed = R.resolve(groups, cands, updates, seed, fed ? &feed : nullptr);
+      // time the resolver spent blocked on groups not yet signalled is device wait, not host work
+      const double spun = fed ? feed.spin_ms() - feed_spin_seen : 0.0;
+      if (trace) tr_res.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - th).count() -
+                                  spun * 1e3);
       for (const pe::Update& u : updates)          // the mirror follows every placement (all shards)
         for (int d = 0; d < pe::D; ++d) ctx->m_nodes[u.gid].res[d] = u.res[d];
       ctx->stats.greedy_host_ms +=
-          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count() - spun;
+      ctx->stats.greedy_wait_ms += spun;
       return consumed;
     };
 

@@ -35,7 +35,7 @@ static_assert(sizeof(ReqRec32) == 32, "ReqRec32 must be 32 B");
 // of the inventory, so the device ships 8 B per candidate instead of a 48-B record.
 struct CandHdr {
   int32_t n;       // valid keys (ascending)
-  int32_t flags;   // bit0: merge overflowed LDS, list truncated to the exact minimum
+  int32_t flags;   // merge: bit0 = overflowed LDS, list truncated to the exact minimum; signalled walk: the window generation, written last
   uint64_t limit;  // every clean node with key < limit is in the list
 };
 static_assert(sizeof(CandHdr) == 16, "CandHdr must be 16 B");
@@ -246,9 +246,12 @@ hipError_t sort_keys_u64(void* temp, size_t* temp_bytes, const uint64_t* in, uin
 // Sorted SoA copy, pos[], round summaries from the sorted keys w.sk.
 hipError_t launch_walk_build(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
                              uint64_t id_base, const WalkIndex& w);
-// One block per group: overlay + walk, exact top-K keys and limit, same blob as merge.
+// One block per group: overlay + walk, exact top-K keys and limit, same blob as merge.  gen != 0:
+// each group's header.flags is set to gen after its keys, n and limit are visible to the host
+// (system-scope release; out is pinned host memory the host polls per group).
 hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const WalkIndex& w, const int64_t* res,
-                       int64_t stride, const uint32_t* labels, int64_t Ns, uint64_t id_base, uint8_t* out);
+                       int64_t stride, const uint32_t* labels, int64_t Ns, uint64_t id_base, uint8_t* out,
+                       uint32_t gen = 0);
 
 // upd: [n] records {local node (i64), res[4]} -> res[d][node] = value (absolute)
 // (kn, lo nullable: refreshed for the updated nodes when given; w nullable: the updated nodes

@@ -1316,19 +1316,35 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
   return sk;
 }
 
-// Group blob: header + the first nout keys of sk.
+// Group blob: header + the first nout keys of sk.  gen != 0 (walk windows written straight into
+// pinned host memory): the group is SIGNALLED -- keys, n and limit first, every thread's stores
+// made visible at system scope, then header.flags = gen as the last store -- so the host can take
+// each group as soon as its block is done instead of waiting for the whole launch.
 __device__ void write_group(const uint64_t* sk, int nout, int flags, uint64_t limit, int K, int g,
-                            uint8_t* __restrict__ out) {
+                            uint8_t* __restrict__ out, uint32_t gen = 0) {
   uint8_t* og = out + (size_t)g * cand_group_bytes(K);
   uint64_t* keys = reinterpret_cast<uint64_t*>(og + sizeof(CandHdr));
   for (int i = threadIdx.x; i < nout; i += blockDim.x) keys[i] = sk[i];
-  if (threadIdx.x == 0) {
-    CandHdr h;
-    h.n = nout;
-    h.flags = flags;
-    h.limit = limit;
-    *reinterpret_cast<CandHdr*>(og) = h;
+  CandHdr* hp = reinterpret_cast<CandHdr*>(og);
+  if (gen == 0) {
+    if (threadIdx.x == 0) {
+      CandHdr h;
+      h.n = nout;
+      h.flags = flags;
+      h.limit = limit;
+      *hp = h;
+    }
+    return;
   }
+  if (threadIdx.x == 0) {
+    hp->n = nout;
+    hp->limit = limit;
+  }
+  // the waves that stored (keys: threads < nout; header: thread 0) make their stores visible to
+  // the host, then the block agrees and thread 0 publishes the generation
+  if ((int)(threadIdx.x & ~63u) < nout || threadIdx.x < 64) __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __restrict__ cand,
@@ -1530,7 +1546,7 @@ __device__ unsigned long long walk_prof[16];
 __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict__ groups, int K, WalkIndex w,
                                                         const int64_t* __restrict__ res, int64_t stride,
                                                         const uint32_t* __restrict__ labels, int64_t Ns,
-                                                        uint64_t id_base, uint8_t* __restrict__ out) {
+                                                        uint64_t id_base, uint8_t* __restrict__ out, uint32_t gen) {
   static_assert(WK_ROUND == MG_THREADS, "the walk uses the merge's block-wide selection");
   __shared__ TopkShared s;
   __shared__ uint32_t cbits[WK_MAXR / 32];
@@ -1646,7 +1662,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   const int T = s.total;
   const uint64_t* sk = topk_sort(s, T, K);
   WPT(4);
-  write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : NO_KEY, K, g, out);
+  write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : NO_KEY, K, g, out, gen);
   if (tid == 0 && w.stat) {
     atomicAdd(&w.stat[0], (unsigned long long)rounds);
     atomicAdd(&w.stat[1], (unsigned long long)no);
@@ -1676,11 +1692,12 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
 }
 
 hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const WalkIndex& w, const int64_t* res,
-                       int64_t stride, const uint32_t* labels, int64_t Ns, uint64_t id_base, uint8_t* out) {
+                       int64_t stride, const uint32_t* labels, int64_t Ns, uint64_t id_base, uint8_t* out,
+                       uint32_t gen) {
   if (Wg <= 0) return hipSuccess;
   if (w.nr > WK_MAXR || K + 1 > WK_ROUND) return hipErrorInvalidValue;
   hipLaunchKernelGGL(walk_kernel, dim3((unsigned)Wg), dim3(WK_ROUND), 0, s, groups, K, w, res, stride, labels, Ns,
-                     id_base, out);
+                     id_base, out, gen);
 #ifdef PE_WALK_PROF
   static int launches = 0;
   if (++launches % 500 == 0) {

@@ -2,6 +2,9 @@
 #include "pe_resolver.h"
 
 #include <algorithm>
+#include <chrono>
+#include <stdexcept>
+#include <string>
 #include <cstring>
 #include <numeric>
 #include <utility>
@@ -297,6 +300,69 @@ void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::v
   }
 }
 
+// One group of a one-shard key blob: the list points into the blob.
+static void parse_group_keys(const uint8_t* base, GroupCands& gc) {
+  int32_t n;
+  uint64_t limit;
+  std::memcpy(&n, base, 4);
+  std::memcpy(&limit, base + 8, 8);
+  gc.keyed = true;
+  gc.data = nullptr;
+  gc.merged.clear();
+  gc.part.clear();
+  gc.part_n.clear();
+  gc.limit = limit;
+  gc.keys = reinterpret_cast<const uint64_t*>(base + 16);
+  gc.n = (size_t)std::max(n, 0);
+  for (int l = 0; l < 4; ++l) __builtin_prefetch(gc.keys + 8 * l);   // list heads, fresh from the device
+}
+
+void WindowFeed::reset(const uint8_t* blob, int n_groups, int K, uint32_t gen, std::vector<GroupCands>* cands) {
+  blob_ = blob;
+  n_ = (size_t)std::max(n_groups, 0);
+  gb_ = 16 + (size_t)K * 8;
+  gen_ = gen;
+  cands_ = cands;
+  cands->resize(n_);
+  parsed_.store(0, std::memory_order_relaxed);
+  spin_ms_ = 0;
+}
+
+bool WindowFeed::signalled(size_t w) const {
+  const int32_t* f = reinterpret_cast<const int32_t*>(blob_ + w * gb_ + 4);
+  return (uint32_t)__atomic_load_n(f, __ATOMIC_ACQUIRE) == gen_;
+}
+
+void WindowFeed::advance() {
+  size_t p = parsed_.load(std::memory_order_relaxed);
+  const size_t p0 = p;
+  while (p < n_ && signalled(p)) {
+    parse_group_keys(blob_ + p * gb_, (*cands_)[p]);
+    ++p;
+  }
+  if (p != p0) parsed_.store(p, std::memory_order_release);
+}
+
+void WindowFeed::wait(size_t w) {
+  if (w >= n_) return;
+  advance();
+  if (w < parsed_.load(std::memory_order_relaxed)) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 1;; ++spin) {
+    _mm_pause();
+    if (signalled(parsed_.load(std::memory_order_relaxed))) {
+      advance();
+      if (w < parsed_.load(std::memory_order_relaxed)) break;
+    }
+    if ((spin & 4095) == 0 && idle && !idle(idle_user)) {
+      advance();   // the device is idle: every group it will ever signal is visible now
+      if (w < parsed_.load(std::memory_order_relaxed)) break;
+      throw std::runtime_error("walk window: group " + std::to_string(w) + " was never signalled");
+    }
+  }
+  spin_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 void parse_window_keys(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands) {
   const size_t gb = 16 + (size_t)K * 8;
   const size_t shard_bytes = (size_t)n_groups * gb;
@@ -411,10 +477,12 @@ SeedScorer::~SeedScorer() {
 }
 
 void SeedScorer::start(const DirtySet* seeds, const std::vector<int32_t>* groups,
-                       const std::vector<GroupCands>* cands, const int64_t* scan_req, const uint32_t* need) {
+                       const std::vector<GroupCands>* cands, const int64_t* scan_req, const uint32_t* need,
+                       const WindowFeed* feed) {
   seeds_ = seeds;
   groups_ = groups;
   cands_ = cands;
+  feed_ = feed;
   req_ = scan_req;
   need_ = need;
   if (tops_.size() < groups->size()) tops_.resize(groups->size());
@@ -468,6 +536,23 @@ void SeedScorer::loop() {
       if (state_.load(std::memory_order_acquire) != 1) break;   // cancelled: the resolver moved on
       wi = std::max(wi, main_wi_.load(std::memory_order_relaxed) + 1);   // leapfrog a resolver ahead
       if (wi >= W) break;
+      if (feed_ && wi >= feed_->parsed()) {   // its list has not arrived yet: wait (or be overtaken)
+        bool go = true;
+        for (int spin = 0; wi >= feed_->parsed(); ++spin) {
+          if (state_.load(std::memory_order_acquire) != 1) {
+            go = false;
+            break;
+          }
+          if (spin < 4096) _mm_pause();
+          else std::this_thread::yield();
+          wi = std::max(wi, main_wi_.load(std::memory_order_relaxed) + 1);
+          if (wi >= W) {
+            go = false;
+            break;
+          }
+        }
+        if (!go) break;
+      }
       const int32_t g = (*groups_)[wi];
       try {
         compute(*seeds_, (*cands_)[wi], req_ + (int64_t)g * RD, need_[g], tops_[wi], out_, idx_);
@@ -631,7 +716,7 @@ void Resolver::next_window_from(const Cursor& from, int max_groups, int64_t max_
 }
 
 bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<GroupCands>& cands,
-                       std::vector<Update>& updates, const std::vector<Update>* seed) {
+                       std::vector<Update>& updates, const std::vector<Update>* seed, WindowFeed* feed) {
   bool consumed = true;
   unsigned long long t_ = RP_T();
   // Pipelined windows: the seeds (dirty for the whole window, their state known) are kept apart
@@ -650,8 +735,10 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       st.labels = u.labels;
       seeds_.upsert(u.gid, st);
     }
-    scorer_.start(&seeds_, &groups, &cands, qeff_.data(), need_);
+    scorer_.start(&seeds_, &groups, &cands, qeff_.data(), need_, feed);
   }
+  if (feed) feed->advance();
+  auto have = [&](size_t w) { return !feed || w < feed->parsed(); };   // list of group w is there
   auto is_dirty = [&](int64_t gid) { return dirty_.contains(gid) || (useS && seeds_.contains(gid)); };
   RP_ADD(seed, t_);
   for (int32_t g : groups) {   // the window's group records (scattered over the batch arrays)
@@ -662,7 +749,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
   }
   head_.assign(groups.size(), 0);
   for (size_t w = 0; w < std::min<size_t>(kLookStates, groups.size()); ++w)   // the first groups' list heads
-    if (cands[w].keyed)
+    if (have(w) && cands[w].keyed)
       for (size_t i = 0; i < std::min<size_t>(4, cands[w].size()); ++i)
         __builtin_prefetch(&mirror_.nodes[cands[w].key(i) & 0xFFFFFFull]);
   size_t wi = 0;
@@ -681,6 +768,10 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
   while (!done() && wi < groups.size()) {
     while (wi < groups.size() && groups[wi] != g_) ++wi;  // groups of failed jobs are skipped
     if (wi == groups.size()) break;
+    if (feed) {
+      feed->advance();
+      if (wi >= feed->parsed()) feed->wait(wi);
+    }
     const GroupCands& gc = cands[wi];
     const int64_t* q = scan_req(g_);   // an island group is one unit of count x request
     const uint32_t need = need_[g_];
@@ -689,9 +780,9 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     // Look ahead: the list lines of the group kLookLines ahead on their way; the first clean entries
     // of the group kLookStates ahead found (the dirty entries before them skipped for good -- the
     // dirty set only grows during a resolve) and their mirror states prefetched.
-    if (wi + kLookLines < groups.size() && cands[wi + kLookLines].keys)
+    if (wi + kLookLines < groups.size() && have(wi + kLookLines) && cands[wi + kLookLines].keys)
       for (int l = 0; l < 2; ++l) __builtin_prefetch(cands[wi + kLookLines].keys + 8 * l);
-    if (wi + kLookStates < groups.size() && cands[wi + kLookStates].keyed) {
+    if (wi + kLookStates < groups.size() && have(wi + kLookStates) && cands[wi + kLookStates].keyed) {
       const size_t wn = wi + kLookStates;
       const GroupCands& gn = cands[wn];
       size_t p = useS && scorer_.ready(wn) ? scorer_.top(wn).head : 0;   // (the helper skipped the seeds)

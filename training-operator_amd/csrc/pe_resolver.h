@@ -117,6 +117,35 @@ void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::v
 // keys.  Lists point into the blob when n_shards == 1.
 void parse_window_keys(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands);
 
+// Pipelined walk windows (engine, one shard): the device writes each group's key list straight
+// into pinned host memory and SIGNALS it -- keys, n and limit first, then header.flags = the
+// window's generation (system-scope release).  The feed hands the groups to the resolver as they
+// arrive, so resolving starts when the first group is done instead of when the slowest one is.
+// Only the resolver thread parses (fills cands[w], then publishes parsed() with release); the
+// seed helper reads groups below parsed() only.
+class WindowFeed {
+ public:
+  void reset(const uint8_t* blob, int n_groups, int K, uint32_t gen, std::vector<GroupCands>* cands);
+  size_t parsed() const { return parsed_.load(std::memory_order_acquire); }
+  size_t size() const { return n_; }
+  // resolver thread: parse every group signalled so far (never blocks)
+  void advance();
+  // resolver thread: block until group w is parsed.  While spinning, idle(user) is called every
+  // few thousand polls; false aborts (throws std::runtime_error).
+  void wait(size_t w);
+  bool (*idle)(void*) = nullptr;
+  void* idle_user = nullptr;
+  double spin_ms() const { return spin_ms_; }   // time spent blocked in wait() since reset
+ private:
+  bool signalled(size_t w) const;
+  const uint8_t* blob_ = nullptr;
+  size_t n_ = 0, gb_ = 0;
+  uint32_t gen_ = 0;
+  std::vector<GroupCands>* cands_ = nullptr;
+  std::atomic<size_t> parsed_{0};
+  double spin_ms_ = 0;
+};
+
 // Node id -> small index, open addressing (linear probing) sized to the live entries: the dirty
 // set and a job's nodes hold hundreds of ids out of up to 2^24, so the table stays in L1/L2 where a
 // direct-mapped array over all ids would miss in cache on every lookup.
@@ -251,7 +280,7 @@ class SeedScorer {
   // Main thread: start scoring a window (seeds, cands and the request arrays must stay unchanged
   // until stop()).
   void start(const DirtySet* seeds, const std::vector<int32_t>* groups, const std::vector<GroupCands>* cands,
-             const int64_t* scan_req, const uint32_t* need);
+             const int64_t* scan_req, const uint32_t* need, const WindowFeed* feed = nullptr);
   bool ready(size_t wi) const { return ready_[wi].load(std::memory_order_acquire) == gen_; }
   const SeedTop& top(size_t wi) const { return tops_[wi]; }
   // the resolver is at group wi: the helper skips what it would finish too late
@@ -273,6 +302,7 @@ class SeedScorer {
   const DirtySet* seeds_ = nullptr;
   const std::vector<int32_t>* groups_ = nullptr;
   const std::vector<GroupCands>* cands_ = nullptr;
+  const WindowFeed* feed_ = nullptr;   // groups at or above feed_->parsed() are not there yet
   const int64_t* req_ = nullptr;
   const uint32_t* need_ = nullptr;
   std::vector<SeedTop> tops_;
@@ -299,8 +329,9 @@ class Resolver {
   // seed (pipelined form): nodes changed since the snapshot the candidates were scanned on, with
   // their current state -- they start dirty, so the lists' clean entries stay exact; only nodes
   // changed in THIS window are returned as updates.
+  // feed (pipelined walk windows): cands fill in as the device signals each group (see WindowFeed).
   bool resolve(const std::vector<int32_t>& groups, const std::vector<GroupCands>& cands,
-               std::vector<Update>& updates, const std::vector<Update>* seed = nullptr);
+               std::vector<Update>& updates, const std::vector<Update>* seed = nullptr, WindowFeed* feed = nullptr);
 
   // The request a group's candidate lists are scanned for: the pod request, or count x request
   // for an island group (need bit 31: its pods are placed as one unit on one node).
