@@ -715,6 +715,16 @@ void Resolver::next_window_from(const Cursor& from, int max_groups, int64_t max_
   *end = Cursor{oi, g, p};
 }
 
+// The dirty set holds exactly these updates, in order (it produced them).
+static bool same_updates(const DirtySet& d, const std::vector<Update>& u) {
+  if (d.size() != u.size()) return false;
+  for (size_t i = 0; i < u.size(); ++i)
+    if (d.gid[i] != u[i].gid || d.r0[i] != u[i].res[0] || d.r1[i] != u[i].res[1] || d.r2[i] != u[i].res[2] ||
+        d.r3[i] != u[i].res[3] || d.lab[i] != u[i].labels)
+      return false;
+  return true;
+}
+
 bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<GroupCands>& cands,
                        std::vector<Update>& updates, const std::vector<Update>* seed, WindowFeed* feed) {
   bool consumed = true;
@@ -728,12 +738,16 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     ~ScorerStop() { s.stop(); }
   } scorer_stop{scorer_};
   if (useS) {
-    seeds_.clear();
-    for (const Update& u : *seed) {
-      NodeState st;
-      for (int d = 0; d < RD; ++d) st.res[d] = u.res[d];
-      st.labels = u.labels;
-      seeds_.upsert(u.gid, st);
+    if (prev_ok_ && same_updates(prev_, *seed)) {
+      std::swap(seeds_, prev_);   // the previous window's changes, as this window's seeds
+    } else {
+      seeds_.clear();
+      for (const Update& u : *seed) {
+        NodeState st;
+        for (int d = 0; d < RD; ++d) st.res[d] = u.res[d];
+        st.labels = u.labels;
+        seeds_.upsert(u.gid, st);
+      }
     }
     scorer_.start(&seeds_, &groups, &cands, qeff_.data(), need_, feed);
   }
@@ -965,7 +979,9 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     u.labels = st.labels;
     updates.push_back(u);
   }
-  dirty_.clear();
+  prev_.clear();               // (last window's changes, or the seeds taken over from them)
+  std::swap(prev_, dirty_);    // kept: the next window's seeds if it is pipelined on this one
+  prev_ok_ = true;
   RP_ADD(fin, t_);
   if (!consumed) ++rescans_;
   return consumed;

@@ -372,6 +372,10 @@ class Resolver {
   // pipelined windows: the seeds live here (not in dirty_, which then holds the window's own
   // changes only); their per-group keys come from the scorer's helper thread
   DirtySet seeds_;
+  // the previous resolve's changes (its dirty set, kept instead of cleared): the next pipelined
+  // window's seeds are exactly those updates, so the set is taken over as is (no re-insertion)
+  DirtySet prev_;
+  bool prev_ok_ = false;
   std::vector<uint64_t> sk_out_;
   std::vector<int32_t> sk_idx_;
   std::vector<uint64_t> sfull_;      // a group's every seed key below the limit (truncated top)
