@@ -240,6 +240,7 @@ struct pe_ctx {
   DevBuf<uint32_t> g_lo;   // scan: lo20(r1) / lo24(r3), [2][stride]
   HostBuf<ReqRec> h_groups, h_groups2;   // h_groups2: the window requests of blob buffer 1 (signalled walk)
   uint32_t walk_gen = 0;                  // generation of the last signalled walk window (never 0)
+  int pin_cpu = -2;                       // greedy thread pinning at world > 1: a CPU of this rank's L3 (-2: not chosen yet)
   HostBuf<uint8_t> h_out, h_out2, h_own;   // h_out2: the pipelined loop's second blob buffer
   HostBuf<int64_t> h_upd;
   // greedy sorted walk (pe_kernels.h WalkIndex; the default window path, greedy_flags bit1 = full scan)
@@ -1704,10 +1705,11 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     struct Pin {
       cpu_set_t old_set, l3;
       bool on = false;
-      explicit Pin(int rank, int world) {
+      Pin(int rank, int world, int& picked) {
         if (std::getenv("PE_NO_PIN") || pthread_getaffinity_np(pthread_self(), sizeof(old_set), &old_set) != 0)
           return;
-        const int cpu = world > 1 ? pe::l3_pick(old_set, rank) : sched_getcpu();
+        if (world > 1 && picked == -2) picked = pe::l3_pick(old_set, rank);   // sysfs walk once per context
+        const int cpu = world > 1 ? picked : sched_getcpu();
         if (!pe::l3_cpus(cpu, &l3)) return;
         CPU_AND(&l3, &l3, &old_set);
         on = CPU_COUNT(&l3) >= 3 && pthread_setaffinity_np(pthread_self(), sizeof(l3), &l3) == 0;
@@ -1715,7 +1717,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       ~Pin() {
         if (on) (void)pthread_setaffinity_np(pthread_self(), sizeof(old_set), &old_set);
       }
-    } pin(ctx->rank, ctx->world);
+    } pin(ctx->rank, ctx->world, ctx->pin_cpu);
     if (pipelined) {
       worker.reset(new SpinWorker(ctx->device));
       if (pin.on) worker->pin(pin.l3);
