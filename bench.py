@@ -338,8 +338,9 @@ def main(argv=None):
             eng.fit_mask_run()
         ev.record(e1, stream)
         eng.synchronize()
+        t1 = time.perf_counter()      # this rank's K steps are done (the closing barrier is not timed)
         barrier()
-        wall = allmax(time.perf_counter() - t0)
+        wall = allmax(t1 - t0)        # from the common start to the last rank's finish
         return wall, ev.elapsed_ms(e0, e1) / steps, fit_path_of(eng.stats(), st0, blocks), feas
 
     elapsed, kern_ms, fit_path, feasible = time_fit(req, need, args.steps, args.warmup, "headline")
