@@ -485,15 +485,13 @@ void SeedScorer::start(const DirtySet* seeds, const std::vector<int32_t>* groups
   feed_ = feed;
   req_ = scan_req;
   need_ = need;
-  if (tops_.size() < groups->size()) tops_.resize(groups->size());
   if (cap_ < groups->size()) {
     cap_ = std::max<size_t>(groups->size(), 2 * cap_);
-    ready_.reset(new std::atomic<uint32_t>[cap_]);
-    for (size_t i = 0; i < cap_; ++i) ready_[i].store(0, std::memory_order_relaxed);
+    slots_.reset(new TopSlot[cap_]);
     gen_ = 0;
   }
   if (++gen_ == 0) {   // generation wrap-around: clear the flags
-    for (size_t i = 0; i < cap_; ++i) ready_[i].store(0, std::memory_order_relaxed);
+    for (size_t i = 0; i < cap_; ++i) slots_[i].gen.store(0, std::memory_order_relaxed);
     gen_ = 1;
   }
   main_wi_.store(0, std::memory_order_relaxed);
@@ -555,11 +553,11 @@ void SeedScorer::loop() {
       }
       const int32_t g = (*groups_)[wi];
       try {
-        compute(*seeds_, (*cands_)[wi], req_ + (int64_t)g * RD, need_[g], tops_[wi], out_, idx_);
+        compute(*seeds_, (*cands_)[wi], req_ + (int64_t)g * RD, need_[g], slots_[wi].top, out_, idx_);
       } catch (...) {   // (bad_alloc) the resolver scores the remaining groups itself
         break;
       }
-      ready_[wi].store(gen, std::memory_order_release);
+      slots_[wi].gen.store(gen, std::memory_order_release);
     }
     // done with the window: wait for stop() (state 2) before going idle
     for (int spin = 0; state_.load(std::memory_order_acquire) == 1; ++spin)

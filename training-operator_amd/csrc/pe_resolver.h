@@ -281,8 +281,8 @@ class SeedScorer {
   // until stop()).
   void start(const DirtySet* seeds, const std::vector<int32_t>* groups, const std::vector<GroupCands>* cands,
              const int64_t* scan_req, const uint32_t* need, const WindowFeed* feed = nullptr);
-  bool ready(size_t wi) const { return ready_[wi].load(std::memory_order_acquire) == gen_; }
-  const SeedTop& top(size_t wi) const { return tops_[wi]; }
+  bool ready(size_t wi) const { return slots_[wi].gen.load(std::memory_order_acquire) == gen_; }
+  const SeedTop& top(size_t wi) const { return slots_[wi].top; }
   // the resolver is at group wi: the helper skips what it would finish too late
   void at(size_t wi) { main_wi_.store(wi, std::memory_order_relaxed); }
   void stop();   // cancel the window and wait until the helper is idle
@@ -294,7 +294,14 @@ class SeedScorer {
   void loop();
   std::unique_ptr<std::thread> th_;
   std::atomic<int> state_{0};            // 0 idle, 1 window posted, 2 cancel, 3 exit
-  std::unique_ptr<std::atomic<uint32_t>[]> ready_;   // ready_[wi] == gen_: tops_[wi] is final
+  // One slot per window group, its own cache lines: the ready generation sits on the same line as
+  // the top's head and first keys, so the resolver's check-and-read of a group is one line handed
+  // over from the helper (flags packed 16 to a line ping-ponged between the two cores).
+  struct alignas(64) TopSlot {
+    std::atomic<uint32_t> gen{0};   // == gen_: top is final for this window
+    SeedTop top;
+  };
+  std::unique_ptr<TopSlot[]> slots_;
   size_t cap_ = 0;
   uint32_t gen_ = 0;                                  // window generation (written before posting)
   std::atomic<size_t> main_wi_{0};
@@ -305,7 +312,6 @@ class SeedScorer {
   const WindowFeed* feed_ = nullptr;   // groups at or above feed_->parsed() are not there yet
   const int64_t* req_ = nullptr;
   const uint32_t* need_ = nullptr;
-  std::vector<SeedTop> tops_;
   std::vector<uint64_t> out_;
   std::vector<int32_t> idx_;
 };
