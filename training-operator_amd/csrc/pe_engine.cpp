@@ -39,12 +39,20 @@ template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
-  hipError_t ensure(size_t count) {
+  // flags: hipExtMallocWithFlags flags (hipDeviceMallocContiguous falls back to a plain hipMalloc
+  // when the driver cannot provide it)
+  hipError_t ensure(size_t count, unsigned flags = 0) {
     if (count <= n && p) return hipSuccess;
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
-    hipError_t e = hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T));
+    const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+    hipError_t e = hipErrorOutOfMemory;
+    if (flags) {
+      e = hipExtMallocWithFlags((void**)&p, bytes, flags);
+      if (e != hipSuccess) (void)hipGetLastError();
+    }
+    if (e != hipSuccess) e = hipMalloc((void**)&p, bytes);
     if (e == hipSuccess) n = count;
     return e;
   }
@@ -1294,7 +1302,8 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
                             : ctx->fit_path == 3 ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->pl_nblk * 128
                             : ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
                                                  : (size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4;
-  hipchk(ctx->mask.ensure(mask_words), "alloc fit mask");
+  static const unsigned mask_flags = std::getenv("PE_MASK_CONTIG") ? hipDeviceMallocContiguous : 0u;
+  hipchk(ctx->mask.ensure(mask_words, mask_flags), "alloc fit mask");
   const int64_t n_counts = std::max<int64_t>(Jp, ctx->fit_path == 3 ? ctx->pl_counts_n : 0);
   hipchk(ctx->counts.ensure(n_counts), "alloc fit counts");
   hipchk(ctx->h_counts.ensure(n_counts), "alloc pinned counts");
