@@ -213,6 +213,7 @@ struct pe_ctx {
   int64_t pl_nblk = 0;                   // planes path: 8192-node blocks
   bool pl_rows = true;                   // planes path: row-major sweep kernel (else block-major streams)
   int64_t pl_R = 1;                      // row-major kernel: job phases of the uploaded batch
+  int64_t pl_pitch = 0;                  // row-major mask pitch in 8192-node blocks (>= pl_nblk)
   // A batch with more than PL_MAX distinct (dimension, value) pairs is split into plane sets of at
   // most PL_MAX pairs each (row-major layout only); each set is encoded and swept on its own by
   // the indexed-row kernel, its jobs' codes carrying their mask rows.
@@ -882,6 +883,10 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd, bool 
   // field f's plane index sits at bits 0/7/14/21 (dims) and 32 (need) as 4 x index (register offset)
   auto field_shift = [](int f) { return f < pe::D ? 7 * f : 32; };
   ctx->pl_nblk = (std::max<int64_t>(ctx->Ns, 1) + pe::PL_BLK - 1) / pe::PL_BLK;
+  // row-major mask pitch in blocks (PE_ROW_PITCH_BLOCKS: a study knob; the words past nblk are
+  // never written)
+  static const int64_t pitch_env = std::getenv("PE_ROW_PITCH_BLOCKS") ? std::atoll(std::getenv("PE_ROW_PITCH_BLOCKS")) : 0;
+  ctx->pl_pitch = std::max(ctx->pl_nblk, pitch_env);
   // phases of a set of J jobs: one wave per SIMD (1024 on 256 CUs) = nblk x R; codes phase-major.
   // (Padding the row to 1024 / R blocks, i.e. an aligned 1 MiB store window, was measured no
   // faster: profiles/r5c_row_pitch.txt.)
@@ -1299,7 +1304,8 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
     }
   }
   const size_t mask_words = ctx->fit_path == 4   ? (size_t)(n_jobs + 1) * ctx->lds_pitch   // + the scratch row
-                            : ctx->fit_path == 3 ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->pl_nblk * 128
+                            : ctx->fit_path == 3 ? (size_t)std::max<int64_t>(n_jobs, 1) *
+                                                       (ctx->pl_rows ? ctx->pl_pitch : ctx->pl_nblk) * 128
                             : ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
                                                  : (size_t)Jp * std::max<int64_t>(ctx->Wt, 1) * 4;
   static const unsigned mask_flags = std::getenv("PE_MASK_CONTIG") ? hipDeviceMallocContiguous : 0u;
@@ -1341,7 +1347,7 @@ static void fit_run(pe_ctx* ctx) {
              "launch encode_planes_sets");
       hipchk(pe::launch_fit_mask_planes_sets(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p,
                                              ctx->pl_meta_d.p, ns, ctx->pl_sets[0].R,
-                                             reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p),
+                                             reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p, ctx->pl_pitch),
              "launch fit_mask_planes_sets");
       ctx->stats.fit_runs_planes += 1;
       ctx->stats.fit_runs_sets += 1;
@@ -1353,7 +1359,7 @@ static void fit_run(pe_ctx* ctx) {
            "launch encode_planes");
     if (ctx->pl_rows) {
       hipchk(pe::launch_fit_mask_planes_rows(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p, J, ctx->pl_R,
-                                             reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p),
+                                             reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p, ctx->pl_pitch),
              "launch fit_mask_planes_rows");
     } else {
       const int64_t ranges = std::max<int64_t>(1, (16384 + ctx->pl_nblk - 1) / ctx->pl_nblk);
@@ -1443,7 +1449,7 @@ int pe_fit_mask_rows(pe_ctx* ctx, int64_t row0, int64_t n_rows, uint64_t* out) {
     if (n_rows == 0 || ctx->Wn == 0) return PE_OK;
     need_ptr(out, "out");
     if ((ctx->fit_path == 3 && ctx->pl_rows) || ctx->fit_path == 4) {   // row-major
-      const int64_t pitch = ctx->fit_path == 4 ? ctx->lds_pitch : ctx->pl_nblk * 128;
+      const int64_t pitch = ctx->fit_path == 4 ? ctx->lds_pitch : ctx->pl_pitch * 128;
       hipchk(hipMemcpy2DAsync(out, (size_t)ctx->Wn * 8, ctx->mask.p + (size_t)row0 * pitch, (size_t)pitch * 8,
                               (size_t)ctx->Wn * 8, (size_t)n_rows, hipMemcpyDeviceToHost, ctx->stream),
              "D2H mask rows");
@@ -2001,7 +2007,7 @@ int pe_fit_mask_layout(const pe_ctx* ctx, int32_t* layout) {
 
 int pe_fit_mask_row_pitch(const pe_ctx* ctx, int64_t* words) {
   if (!ctx || !words) return PE_EINVAL;
-  *words = ctx->fit_path == 4 ? ctx->lds_pitch : ctx->fit_path == 3 && ctx->pl_rows ? ctx->pl_nblk * 128 : 0;
+  *words = ctx->fit_path == 4 ? ctx->lds_pitch : ctx->fit_path == 3 && ctx->pl_rows ? ctx->pl_pitch * 128 : 0;
   return PE_OK;
 }
 

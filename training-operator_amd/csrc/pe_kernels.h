@@ -134,8 +134,10 @@ hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t
 // (blk, r) takes jobs r, r+R, ...; u32 word w of row j at j * nblk * 256 + w.  jcode and counts are
 // phase-major: entry r * Jr + i belongs to job r + R * i (Jr = ceil(J / R) rounded up to 4), so
 // every wave reads and counts a contiguous run.
+// pitch_blk >= nblk: mask row pitch in 8192-node blocks (1 KiB each; words past nblk are not written)
 hipError_t launch_fit_mask_planes_rows(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
-                                       int64_t J, int64_t R, uint32_t* mask, unsigned long long* counts);
+                                       int64_t J, int64_t R, uint32_t* mask, unsigned long long* counts,
+                                       int64_t pitch_blk);
 // Plane-set form (batches with more than PL_MAX distinct request values), all sets in one launch
 // each: encode writes set t's planes at planes + t * nblk * PL_MAX * 256; the sweep has the rows
 // kernel's grid (R phases common to all sets); set t's codes and counts start at meta[3t] (phase-
@@ -144,7 +146,7 @@ hipError_t launch_encode_planes_sets(hipStream_t s, const int64_t* res, int64_t 
                                      int64_t Ns, int64_t nblk, const PlaneSpec* specs, int nsets, uint32_t* planes);
 hipError_t launch_fit_mask_planes_sets(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
                                        const int64_t* meta, int nsets, int64_t R, uint32_t* mask,
-                                       unsigned long long* counts);
+                                       unsigned long long* counts, int64_t pitch_blk);
 
 // ---- LDS digit-plane path (fit mask, any number of distinct request values).  Per dimension the
 // host ranks the batch's distinct request values v_1 < ... < v_m; a job asks rank c (v_c = its

@@ -730,7 +730,8 @@ __device__ __forceinline__ void rows_batch(uint32_t (&p)[64], uint32_t lo, uint3
 __global__ __launch_bounds__(256) void fit_mask_planes_rows_kernel(const uint32_t* __restrict__ planes, int64_t nblk,
                                                                    const uint64_t* __restrict__ jcode, int64_t J,
                                                                    int64_t R, int64_t Jr, uint32_t* __restrict__ mask,
-                                                                   unsigned long long* __restrict__ counts) {
+                                                                   unsigned long long* __restrict__ counts,
+                                                                   int64_t row_vec) {
   static_assert(PL_MAX == 32 && PL_R == 4, "register map assumes 32 planes x 4 words");
   const int lane = threadIdx.x & 63;
   const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -740,7 +741,7 @@ __global__ __launch_bounds__(256) void fit_mask_planes_rows_kernel(const uint32_
   const u32x4* pb = reinterpret_cast<const u32x4*>(planes + blk * PL_MAX * (64 * PL_R)) + lane;
   const u32x32 A = load_planes8(pb), B = load_planes8(pb + 8 * 64), C = load_planes8(pb + 16 * 64),
                Dq = load_planes8(pb + 24 * 64);
-  const int64_t row_vec = nblk * 64;           // u32x4 per row
+  // row_vec: u32x4 per row (the pitch, >= nblk * 64)
   u32x4* const rows0 = reinterpret_cast<u32x4*>(mask) + blk * 64;   // this block's column, row 0
   u32x4* out = rows0 + lane;
   const uint64_t* jc = jcode + r * Jr;         // this phase's codes, contiguous
@@ -784,12 +785,14 @@ __global__ __launch_bounds__(256) void fit_mask_planes_rows_kernel(const uint32_
 }
 
 hipError_t launch_fit_mask_planes_rows(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
-                                       int64_t J, int64_t R, uint32_t* mask, unsigned long long* counts) {
+                                       int64_t J, int64_t R, uint32_t* mask, unsigned long long* counts,
+                                       int64_t pitch_blk) {
   if (J <= 0 || nblk <= 0 || R <= 0) return hipSuccess;
+  if (pitch_blk < nblk) return hipErrorInvalidValue;
   const int64_t Jr = ((J + R - 1) / R + 3) / 4 * 4;   // phase stride (the engine pads codes alike)
   const int64_t waves = nblk * R;
   hipLaunchKernelGGL(fit_mask_planes_rows_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, planes, nblk,
-                     jcode, J, R, Jr, mask, counts);
+                     jcode, J, R, Jr, mask, counts, pitch_blk * 64);
   return hipGetLastError();
 }
 
@@ -848,14 +851,14 @@ __global__ __launch_bounds__(256) void fit_mask_planes_sets_kernel(const uint32_
                                                                    const uint64_t* __restrict__ jcode,
                                                                    const int64_t* __restrict__ meta, int nsets,
                                                                    int64_t R, uint32_t* __restrict__ mask,
-                                                                   unsigned long long* __restrict__ counts) {
+                                                                   unsigned long long* __restrict__ counts,
+                                                                   int64_t row_vec) {   // u32x4 per row (pitch)
   static_assert(PL_MAX == 32 && PL_R == 4, "register map assumes 32 planes x 4 words");
   const int lane = threadIdx.x & 63;
   const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = wave_id % nblk;
   const int64_t r = wave_id / nblk;
   if (r >= R) return;
-  const int64_t row_vec = nblk * 64;           // u32x4 per row
   u32x4* const col = reinterpret_cast<u32x4*>(mask) + blk * 64 + lane;
   uint32_t sigma;                              // lane l of a batch sum counts batch job sigma
   {
@@ -886,11 +889,12 @@ __global__ __launch_bounds__(256) void fit_mask_planes_sets_kernel(const uint32_
 
 hipError_t launch_fit_mask_planes_sets(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
                                        const int64_t* meta, int nsets, int64_t R, uint32_t* mask,
-                                       unsigned long long* counts) {
+                                       unsigned long long* counts, int64_t pitch_blk) {
   if (nblk <= 0 || R <= 0 || nsets <= 0) return hipSuccess;
+  if (pitch_blk < nblk) return hipErrorInvalidValue;
   const int64_t waves = nblk * R;
   hipLaunchKernelGGL(fit_mask_planes_sets_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, planes, nblk,
-                     jcode, meta, nsets, R, mask, counts);
+                     jcode, meta, nsets, R, mask, counts, pitch_blk * 64);
   return hipGetLastError();
 }
 
