@@ -27,12 +27,18 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("world,mix,n_nodes,n_jobs", [(2, "mixed", 20000, 600), (3, "gang8", 9000, 300)])
-def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs):
+@pytest.mark.parametrize("world,mix,n_nodes,n_jobs,host_merge", [(2, "mixed", 20000, 600, False),
+                                                                 (3, "gang8", 9000, 300, False),
+                                                                 (2, "island8", 6000, 300, True)])
+def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, host_merge):
+    """host_merge False: the gathered shard lists are merged on the device (merge_shards, the
+    default); True: PE_HOST_MERGE=1, the host's lazy k-way merge."""
     port = free_port()
     env = dict(os.environ)
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PE_HOST_MERGE"):
         env.pop(k, None)
+    if host_merge:
+        env["PE_HOST_MERGE"] = "1"
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "mp_shard_worker.py"), str(r), str(world), str(port),
                                mix, str(n_nodes), str(n_jobs), str(tmp_path)], env=env, stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(world)]

@@ -418,14 +418,23 @@ def test_greedy_sharded_exchange():
         e.close()
 
 
-def test_greedy_rccl_single_rank():
-    """The RCCL window path (ncclAllGather of the candidate blobs) on a 1-rank communicator."""
+@pytest.mark.parametrize("host_merge,flags", [(False, 0), (False, 1), (True, 0), (False, 2)])
+def test_greedy_rccl_single_rank(host_merge, flags):
+    """The RCCL window path (ncclAllGather of the candidate blobs) on a 1-rank communicator: the
+    gathered lists merged on the device and signalled per group (default), the same synced
+    (greedy_flags bit0: sequential windows) or from the full scan (bit1), or merged on the host
+    (PE_HOST_MERGE=1)."""
     from placement import comm_id
-    e = Engine(0, world_size=1, comm=comm_id(), topk=8, window_groups=16)
-    inv = synth.make_inventory(3000, 83, 0.25)
-    batch = synth.make_jobs(250, 89, "mixed")
-    check_greedy(e, inv, batch)
-    e.close()
+    if host_merge:
+        os.environ["PE_HOST_MERGE"] = "1"
+    try:
+        e = Engine(0, world_size=1, comm=comm_id(), topk=8, window_groups=16, greedy_flags=flags)
+        inv = synth.make_inventory(3000, 83, 0.25)
+        batch = synth.make_jobs(250, 89, "mixed")
+        check_greedy(e, inv, batch)
+        e.close()
+    finally:
+        os.environ.pop("PE_HOST_MERGE", None)
 
 
 def test_greedy_reset_residuals(eng):

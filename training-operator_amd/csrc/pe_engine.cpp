@@ -251,6 +251,7 @@ struct pe_ctx {
   uint32_t walk_gen = 0;                  // generation of the last signalled walk window (never 0)
   int pin_cpu = -2;                       // greedy thread pinning at world > 1: a CPU of this rank's L3 (-2: not chosen yet)
   HostBuf<uint8_t> h_out, h_out2, h_own;   // h_out2: the pipelined loop's second blob buffer
+  HostBuf<uint8_t> h_merged;                // host-exchange windows: the device-merged lists
   HostBuf<int64_t> h_upd;
   // greedy sorted walk (pe_kernels.h WalkIndex; the default window path, greedy_flags bit1 = full scan)
   bool walk = true;
@@ -276,7 +277,7 @@ struct pe_ctx {
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
-    g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_groups2.release(); h_out.release(); h_out2.release(); h_own.release(); h_upd.release();
+    g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_groups2.release(); h_out.release(); h_out2.release(); h_own.release(); h_merged.release(); h_upd.release();
     w_sk.release(); w_kin.release(); w_rmin.release(); w_sr.release(); w_rmax.release(); w_sl.release(); w_pos.release();
     w_ror.release(); w_inovl.release(); w_ovl.release(); w_ovln.release(); w_temp.release();
     w_ovidx.release(); w_ovlab.release(); w_ovres.release(); w_stat.release();
@@ -1748,8 +1749,16 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // the next window's requests are written); seeing any group of window w signalled proves that
     // every earlier launch of the stream is complete (kernels of one stream run in order), which is
     // what the pinned update records need.  PE_NO_GROUP_SIGNAL=1: stream sync per window instead.
-    const bool signalled = pipelined && walk && direct_out && !std::getenv("PE_NO_GROUP_SIGNAL");
+    // Multi-rank windows (RCCL all-gather, or the host exchange): the gathered shard lists are merged
+    // on the device into one list per group (merge_shards), written into pinned host memory and
+    // signalled like an unsharded walk window -- no D2H of every shard's lists, no host k-way merge.
+    // PE_HOST_MERGE=1: the gathered blob is copied and merged lazily on the host instead.
+    const bool dev_merge = !direct_out && (int64_t)ctx->world * K <= pe::MG_CAP && !std::getenv("PE_HOST_MERGE");
+    const bool signalled = pipelined && !std::getenv("PE_NO_GROUP_SIGNAL") && (direct_out ? walk : dev_merge);
     if (signalled) hipchk(ctx->h_groups2.ensure(Wpad, kZeroCopy), "alloc pinned groups");
+    if (dev_merge && use_exchange) hipchk(ctx->h_merged.ensure((size_t)Wmax * gb, kZeroCopy), "alloc pinned merged");
+    const uint8_t* last_blob = nullptr;   // the parsed blob of the window being resolved (one list per group
+                                          // unless the shards are merged on the host)
     uint32_t buf_gen[2] = {0, 0};
     pe::WindowFeed feed;
     struct StreamIdle {
@@ -1769,6 +1778,12 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       // unsharded: the kernel writes the blob straight into pinned host memory (no D2H copy)
       uint8_t* const dst = direct_out ? outbufdev(b) : ctx->g_out.p;
+      uint32_t gen = 0;   // signalled window: its generation (the walk's or the shard merge's)
+      if (signalled) {
+        if (++ctx->walk_gen == 0) ++ctx->walk_gen;
+        gen = ctx->walk_gen;
+      }
+      buf_gen[b] = gen;
       if (walk) {   // one 64-B request per block: read from pinned host memory, no H2D copy
         if (ctx->w_est > ctx->resort_nodes) walk_resort(ctx);
         std::pair<hipEvent_t, hipEvent_t> evp{nullptr, nullptr};
@@ -1778,14 +1793,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           walk_events.push_back(evp);
           hipchk(hipEventRecord(evp.first, s), "event record");
         }
-        uint32_t gen = 0;
-        if (signalled) {
-          if (++ctx->walk_gen == 0) ++ctx->walk_gen;
-          gen = ctx->walk_gen;
-        }
-        buf_gen[b] = gen;
         hipchk(pe::launch_walk(s, hg.dev, Wg, K, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns,
-                               (uint64_t)ctx->begin, dst, gen),
+                               (uint64_t)ctx->begin, dst, direct_out ? gen : 0u),
                "launch walk");
         if (wev) hipchk(hipEventRecord(evp.second, s), "event record");
         walk_launch_groups += Wg;
@@ -1817,8 +1826,11 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
       } else {
         ncclchk(ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
-        hipchk(hipMemcpyAsync(outbuf(b), ctx->g_gath.p, bytes * ctx->world, hipMemcpyDeviceToHost, s),
-               "D2H gathered");
+        if (dev_merge)
+          hipchk(pe::launch_merge_shards(s, ctx->g_gath.p, ctx->world, Wg, K, outbufdev(b), gen), "launch merge_shards");
+        else
+          hipchk(hipMemcpyAsync(outbuf(b), ctx->g_gath.p, bytes * ctx->world, hipMemcpyDeviceToHost, s),
+                 "D2H gathered");
       }
       ctx->stats.windows += 1;
       ctx->stats.groups_scanned += Wg;
@@ -1830,6 +1842,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       const size_t bytes = (size_t)Wg * gb;
       const auto tw = std::chrono::steady_clock::now();
       if (signalled && buf_gen[b] != 0) {   // the first group's list (and so every earlier launch) is done
+        last_blob = outbuf(b);
         feed.reset(outbuf(b), Wg, K, buf_gen[b], &cands);
         feed.wait(0);
         feed_spin_seen = feed.spin_ms();
@@ -1839,14 +1852,21 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         return;
       }
       hipchk(hipStreamSynchronize(s), "sync window");
+      last_blob = outbuf(b);
       if (use_exchange) {
         if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, outbuf(b), bytes) != 0)
           raise(PE_ERCCL, "exchange callback failed");
+        if (dev_merge) {   // the gathered blob (pinned) merged by the device into h_merged
+          hipchk(pe::launch_merge_shards(s, outbufdev(b), ctx->world, Wg, K, ctx->h_merged.dev, 0u),
+                 "launch merge_shards");
+          hipchk(hipStreamSynchronize(s), "sync merge");
+          last_blob = ctx->h_merged.p;
+        }
       }
       const auto th = std::chrono::steady_clock::now();
       ctx->stats.greedy_wait_ms += std::chrono::duration<double, std::milli>(th - tw).count();
       if (trace) tr_wait.push_back(std::chrono::duration<double, std::micro>(th - tw).count());
-      pe::parse_window_keys(outbuf(b), ctx->world, Wg, K, cands);   // lists point into the blob
+      pe::parse_window_keys(last_blob, dev_merge ? 1 : ctx->world, Wg, K, cands);   // lists point into the blob
 
       ctx->stats.greedy_host_ms +=
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
@@ -1882,7 +1902,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         const int32_t wg = (int32_t)groups.size(), ns = seed ? (int32_t)seed->size() : 0;
         std::fwrite(&wg, 4, 1, dump);
         std::fwrite(groups.data(), 4, (size_t)wg, dump);
-        std::fwrite(outbuf(cb), 1, (size_t)wg * gb * ctx->world, dump);
+        std::fwrite(last_blob, 1, (size_t)wg * gb * (dev_merge || direct_out ? 1 : ctx->world), dump);
         std::fwrite(&ns, 4, 1, dump);
         if (ns) std::fwrite(seed->data(), sizeof(pe::Update), (size_t)ns, dump);
       }

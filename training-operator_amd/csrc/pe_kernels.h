@@ -248,6 +248,10 @@ hipError_t sort_keys_u64(void* temp, size_t* temp_bytes, const uint64_t* in, uin
 // Sorted SoA copy, pos[], round summaries from the sorted keys w.sk.
 hipError_t launch_walk_build(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
                              uint64_t id_base, const WalkIndex& w);
+// Multi-rank window: world gathered shard blobs (key lists) -> one list per group (the K smallest
+// keys below the smallest shard limit, limit = the (K+1)-th or that minimum); gen != 0 signals each
+// group as the walk does.  world * K <= MG_CAP.
+hipError_t launch_merge_shards(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen);
 // One block per group: overlay + walk, exact top-K keys and limit, same blob as merge.  gen != 0:
 // each group's header.flags is set to gen after its keys, n and limit are visible to the host
 // (system-scope release; out is pinned host memory the host polls per group).

@@ -1427,6 +1427,47 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
   write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : G, K, g, out);
 }
 
+// Shard merge (multi-rank greedy): after the all-gather every rank holds each shard's list of each
+// window group (world consecutive blobs, group g of shard r at r * Wg * gb + g * gb).  One block per
+// group keeps the keys below L = the smallest shard limit (every shard lists all its keys below its
+// own limit, so every key below L is there), selects the K + 1 smallest and writes ONE list with
+// limit = the (K+1)-th key, or L -- the unsharded window's blob, signalled (gen) when the host takes
+// groups as they arrive.  world * K <= MG_CAP (the host checks).
+__global__ __launch_bounds__(MG_THREADS) void merge_shards_kernel(const uint8_t* __restrict__ gath, int world, int Wg,
+                                                                  int K, uint8_t* __restrict__ out, uint32_t gen) {
+  __shared__ TopkShared s;
+  const int g = blockIdx.x;
+  const int tid = threadIdx.x;
+  const size_t gb = cand_group_bytes(K);
+  const size_t shard_bytes = (size_t)Wg * gb;
+  uint64_t L = NO_KEY;
+  for (int r = 0; r < world; ++r)
+    L = umin64(L, reinterpret_cast<const CandHdr*>(gath + r * shard_bytes + (size_t)g * gb)->limit);
+  if (tid == 0) s.total = 0;
+  __syncthreads();
+  for (int r = 0; r < world; ++r) {
+    const uint8_t* base = gath + r * shard_bytes + (size_t)g * gb;
+    const int n = min(reinterpret_cast<const CandHdr*>(base)->n, K);
+    const uint64_t* keys = reinterpret_cast<const uint64_t*>(base + sizeof(CandHdr));
+    for (int i0 = 0; i0 < n; i0 += MG_THREADS) {   // block-uniform bound: topk_append is wave-collective
+      const int i = i0 + tid;
+      const uint64_t k = i < n ? keys[i] : NO_KEY;
+      topk_append(s, k, k < L);
+    }
+  }
+  __syncthreads();
+  const int T = s.total;
+  const uint64_t* sk = topk_sort(s, T, K);
+  write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : L, K, g, out, gen);
+}
+
+hipError_t launch_merge_shards(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen) {
+  if (Wg <= 0) return hipSuccess;
+  if (world < 1 || K < 1 || (int64_t)world * K > MG_CAP) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(merge_shards_kernel, dim3(Wg), dim3(MG_THREADS), 0, s, gath, world, Wg, K, out, gen);
+  return hipGetLastError();
+}
+
 hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt, const uint64_t* bound, int nwaves,
                         int K, uint8_t* out, int Wg) {
   if (Wg <= 0) return hipSuccess;
