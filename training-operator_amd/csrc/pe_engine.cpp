@@ -1606,6 +1606,17 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       no_need.assign((size_t)std::max<int64_t>(G, 1), 0u);
       group_need = no_need.data();
     }
+    // Device preparation first (asynchronous): it runs while the host builds the resolver.
+    hipchk(ctx->g_kn.ensure((size_t)std::max<int64_t>(ctx->stride, 1)), "alloc node keys");
+    hipchk(ctx->g_lo.ensure((size_t)2 * std::max<int64_t>(ctx->stride, 1)), "alloc node lows");
+    // residuals may have changed since the last call (reset, pe_update_nodes): one pass over the shard
+    hipchk(pe::launch_prep_nodes(ctx->stream, ctx->res.p, ctx->stride, ctx->Ns, (uint64_t)ctx->begin, ctx->g_kn.p,
+                                 ctx->g_lo.p),
+           "launch prep_nodes");
+    const bool walk = ctx->walk && ctx->Ns > 0;
+    hipchk(ctx->w_stat.ensure(2), "alloc walk counters");
+    hipchk(hipMemsetAsync(ctx->w_stat.p, 0, 2 * sizeof(unsigned long long), ctx->stream), "memset walk counters");
+    if (walk) walk_resort(ctx);
     pe::Resolver R(n_jobs, job_group_off, priority, group_count, group_req, group_need);
     R.set_mirror(pe::Mirror{ctx->m_nodes.data(), ctx->n_total});
     // PE_DUMP_WINDOWS=<file>: record the batch and every window's groups + blob (host resolver
@@ -1681,16 +1692,6 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       hipchk(ctx->g_gath.ensure((size_t)Wmax * gb * ctx->world), "alloc gather");
       hipchk(ctx->h_own.ensure((size_t)Wmax * gb), "alloc pinned own");
     }
-    hipchk(ctx->g_kn.ensure((size_t)std::max<int64_t>(ctx->stride, 1)), "alloc node keys");
-    hipchk(ctx->g_lo.ensure((size_t)2 * std::max<int64_t>(ctx->stride, 1)), "alloc node lows");
-    // residuals may have changed since the last call (reset, pe_update_nodes): one pass over the shard
-    hipchk(pe::launch_prep_nodes(ctx->stream, ctx->res.p, ctx->stride, ctx->Ns, (uint64_t)ctx->begin, ctx->g_kn.p,
-                                 ctx->g_lo.p),
-           "launch prep_nodes");
-    const bool walk = ctx->walk && ctx->Ns > 0;
-    hipchk(ctx->w_stat.ensure(2), "alloc walk counters");
-    hipchk(hipMemsetAsync(ctx->w_stat.p, 0, 2 * sizeof(unsigned long long), ctx->stream), "memset walk counters");
-    if (walk) walk_resort(ctx);
     // PE_WALK_EVENTS=1: hipEvents around every walk launch, summed into stats.walk_ms (diagnostics:
     // the greedy roofline of bench.py; the events cost a few us of host time per window)
     const bool wev = walk && std::getenv("PE_WALK_EVENTS") != nullptr;
