@@ -12,6 +12,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <deque>
 #include <atomic>
 #include <chrono>
 #include <exception>
@@ -248,6 +249,9 @@ struct pe_ctx {
   DevBuf<uint64_t> g_kn;   // scan: node-only score terms K(n) (prep_nodes), refreshed by apply
   DevBuf<uint32_t> g_lo;   // scan: lo20(r1) / lo24(r3), [2][stride]
   HostBuf<ReqRec> h_groups, h_groups2;   // h_groups2: the window requests of blob buffer 1 (signalled walk)
+  HostBuf<ReqRec> h_groupsx[2];           // blob buffers 2, 3 (pipeline depth 2, 3)
+  HostBuf<uint8_t> h_outx[2];             // blob buffers 2, 3
+  HostBuf<int64_t> h_updx[2];             // update staging slots 1, 2 (pipeline depth 2, 3)
   uint32_t walk_gen = 0;                  // generation of the last signalled walk window (never 0)
   int pin_cpu = -2;                       // greedy thread pinning at world > 1: a CPU of this rank's L3 (-2: not chosen yet)
   HostBuf<uint8_t> h_out, h_out2, h_own;   // h_out2: the pipelined loop's second blob buffer
@@ -278,6 +282,11 @@ struct pe_ctx {
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
     g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_groups2.release(); h_out.release(); h_out2.release(); h_own.release(); h_merged.release(); h_upd.release();
+    for (int i = 0; i < 2; ++i) {
+      h_groupsx[i].release();
+      h_outx[i].release();
+      h_updx[i].release();
+    }
     w_sk.release(); w_kin.release(); w_rmin.release(); w_sr.release(); w_rmax.release(); w_sl.release(); w_pos.release();
     w_ror.release(); w_inovl.release(); w_ovl.release(); w_ovln.release(); w_temp.release();
     w_ovidx.release(); w_ovlab.release(); w_ovres.release(); w_stat.release();
@@ -1741,8 +1750,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     }
     // blob buffer b (0: h_out, 1: h_out2): the pipelined loop D2Hs the next window's blob while the
     // host still resolves from the current one's
-    auto outbuf = [&](int b) { return b ? ctx->h_out2.p : ctx->h_out.p; };
-    auto outbufdev = [&](int b) { return b ? ctx->h_out2.dev : ctx->h_out.dev; };
+    auto outbuf = [&](int b) { return b == 0 ? ctx->h_out.p : b == 1 ? ctx->h_out2.p : ctx->h_outx[b - 2].p; };
+    auto outbufdev = [&](int b) { return b == 0 ? ctx->h_out.dev : b == 1 ? ctx->h_out2.dev : ctx->h_outx[b - 2].dev; };
     const bool direct_out = ctx->world == 1 && !ctx->comm;
     // Pipelined walk windows written in place are SIGNALLED per group (pe::WindowFeed): the host
     // takes each group's list when its block is done, not at a stream sync after the slowest block.
@@ -1756,11 +1765,24 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // PE_HOST_MERGE=1: the gathered blob is copied and merged lazily on the host instead.
     const bool dev_merge = !direct_out && (int64_t)ctx->world * K <= pe::MG_CAP && !std::getenv("PE_HOST_MERGE");
     const bool signalled = pipelined && !std::getenv("PE_NO_GROUP_SIGNAL") && (direct_out ? walk : dev_merge);
+    // Pipeline depth D (signalled windows; PE_PIPE_DEPTH, 1..3, default 1): windows i+1 .. i+D are
+    // scanned while window i is resolved (D + 1 blob / request buffers, D update staging slots).
+    const int depth = !pipelined ? 0 : !signalled ? 1 : [] {
+      const char* e = std::getenv("PE_PIPE_DEPTH");
+      return e ? std::min(3, std::max(1, std::atoi(e))) : 1;
+    }();
     if (signalled) hipchk(ctx->h_groups2.ensure(Wpad, kZeroCopy), "alloc pinned groups");
+    for (int b = 2; b <= depth; ++b) {
+      hipchk(ctx->h_groupsx[b - 2].ensure(Wpad, kZeroCopy), "alloc pinned groups");
+      hipchk(ctx->h_outx[b - 2].ensure((size_t)Wmax * gb * ctx->world, kZeroCopy), "alloc pinned out");
+    }
+    auto hgroups = [&](int b) -> HostBuf<ReqRec>& {
+      return !signalled || b == 0 ? ctx->h_groups : b == 1 ? ctx->h_groups2 : ctx->h_groupsx[b - 2];
+    };
     if (dev_merge && use_exchange) hipchk(ctx->h_merged.ensure((size_t)Wmax * gb, kZeroCopy), "alloc pinned merged");
     const uint8_t* last_blob = nullptr;   // the parsed blob of the window being resolved (one list per group
                                           // unless the shards are merged on the host)
-    uint32_t buf_gen[2] = {0, 0};
+    uint32_t buf_gen[4] = {0, 0, 0, 0};
     pe::WindowFeed feed;
     struct StreamIdle {
       hipStream_t s;
@@ -1772,7 +1794,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     auto enqueue_window = [&](const std::vector<int32_t>& groups, int b) {
       const int Wg = (int)groups.size();
       const int Wgp = (int)round_up(Wg, pe::SC_GT);
-      auto& hg = signalled && b ? ctx->h_groups2 : ctx->h_groups;
+      auto& hg = hgroups(b);
       for (int w = 0; w < Wgp; ++w) {
         const int g = groups[std::min(w, Wg - 1)];
         fill_req(hg.p[w], R.scan_req(g), group_need[g]);   // island groups: count x request
@@ -1874,19 +1896,21 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     };
     // ---- residual updates of this shard H2D + apply (the pinned staging buffer is reused only
     //      after the next collect_window's stream sync)
-    auto enqueue_apply = [&](const std::vector<pe::Update>& updates) {
+    // (slot: the staging buffer; the pipelined loop rotates D of them, see the loop below)
+    auto enqueue_apply = [&](const std::vector<pe::Update>& updates, int slot) {
       int64_t nu = 0;
-      hipchk(ctx->h_upd.ensure(std::max<size_t>(updates.size(), 1) * (pe::D + 1), kZeroCopy), "alloc pinned upd");
+      HostBuf<int64_t>& hu = slot == 0 ? ctx->h_upd : ctx->h_updx[slot - 1];
+      hipchk(hu.ensure(std::max<size_t>(updates.size(), 1) * (pe::D + 1), kZeroCopy), "alloc pinned upd");
       for (const pe::Update& u : updates) {
         if (u.gid < ctx->begin || u.gid >= ctx->end) continue;
-        int64_t* o = ctx->h_upd.p + nu * (pe::D + 1);
+        int64_t* o = hu.p + nu * (pe::D + 1);
         o[0] = u.gid - ctx->begin;
         for (int d = 0; d < pe::D; ++d) o[1 + d] = u.res[d];
         ++nu;
       }
       if (nu > 0) {   // the kernel reads the pinned records directly (no H2D copy)
         const pe::WalkIndex w = walk_index(ctx);
-        hipchk(pe::launch_apply(s, ctx->res.p, ctx->stride, ctx->h_upd.dev, nu, (uint64_t)ctx->begin, ctx->g_kn.p,
+        hipchk(pe::launch_apply(s, ctx->res.p, ctx->stride, hu.dev, nu, (uint64_t)ctx->begin, ctx->g_kn.p,
                                 ctx->g_lo.p, ctx->labels.p, walk ? &w : nullptr),
                "launch apply");
         ctx->w_est += nu;
@@ -1923,47 +1947,85 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       return consumed;
     };
 
-    std::vector<int32_t> cur, nxt;
-    std::vector<pe::Update> pending, seed;
-    pe::Cursor cur_end, nxt_end;
-    R.next_window_from(R.cursor(), Wmax, ctx->window_pods, cur, &cur_end);
-    if (!cur.empty()) enqueue_window(cur, cb);
-    while (!cur.empty()) {
-      collect_window(cur, cb);                   // cur's lists: snapshot = device state at its launch
+    // Pipelined (exact), depth D: while the host resolves window i, the device holds windows
+    // i+1 .. i+D scanned (or scanning), each speculating that the windows before it are consumed.  A
+    // window scanned after the updates of the epoch's windows < v were applied misses the changes of
+    // windows v .. i-1, which its resolution takes as dirty seeds (their current states are known
+    // here).  Each iteration the helper thread applies the previous window's updates and scans the
+    // window D ahead into the next free buffer.  A window cut short, or a cursor that did not land
+    // where the speculation started, syncs, applies everything and restarts from the cursor.
+    // Staging-buffer reuse: the apply posted in iteration j is followed, in the same post, by the
+    // scan of window j + D; the slot is written again in iteration j + D, when that window's first
+    // group has been seen, i.e. after every earlier launch of the stream finished.  Blob / request
+    // buffer b is reused D + 1 windows later, after the windows in between were resolved.
+    struct Flight {
+      std::vector<int32_t> groups;
+      pe::Cursor end;
+      int buf = 0;
+      size_t ver = 0;   // updates of the epoch's windows [0, ver) were applied before its scan
+    };
+    std::deque<Flight> fl;
+    std::vector<std::vector<pe::Update>> hist;   // updates of the epoch's resolved windows
+    size_t n_app = 0;                             // of which posted for apply
+    int next_buf = 0, upd_slot = 0;
+    const int nbuf = std::max(depth, 1) + 1;
+    auto add_flight = [&](const pe::Cursor& from) -> Flight* {   // main thread; nullptr: no window left
+      Flight f;
+      R.next_window_from(from, Wmax, ctx->window_pods, f.groups, &f.end);
+      if (f.groups.empty()) return nullptr;
+      f.buf = next_buf;
+      next_buf = (next_buf + 1) % nbuf;
+      f.ver = hist.size();
+      fl.push_back(std::move(f));
+      return &fl.back();
+    };
+    auto restart = [&]() {   // nothing in flight, every update applied: a fresh epoch at the cursor
+      fl.clear();
+      hist.clear();
+      n_app = 0;
+      next_buf = 0;
+      if (Flight* f = add_flight(R.cursor())) enqueue_window(f->groups, f->buf);
+    };
+    restart();
+    std::vector<pe::Update> seed, upd;
+    while (!fl.empty()) {
+      Flight& cur = fl.front();
+      cb = cur.buf;
+      collect_window(cur.groups, cur.buf);       // cur's lists: snapshot = device state at its launch
       if (!pipelined) {
-        std::vector<pe::Update> upd;
-        timed_resolve(cur, upd, nullptr);
-        enqueue_apply(upd);
+        timed_resolve(cur.groups, upd, nullptr);
+        enqueue_apply(upd, 0);
         if (R.done()) break;
-        R.next_window_from(R.cursor(), Wmax, ctx->window_pods, cur, &cur_end);
-        if (!cur.empty()) enqueue_window(cur, cb);
+        fl.clear();
+        next_buf = 0;
+        if (Flight* f = add_flight(R.cursor())) enqueue_window(f->groups, f->buf);
         continue;
       }
-      // Pipelined (exact): the device applies the previous window's updates and scans the window
-      // that follows cur -- speculating that cur is consumed -- while the host resolves cur.  The
-      // next window's lists then miss only cur's own changes, which its resolution takes as dirty
-      // seeds (current state known here).  A window cut short, or a cursor that did not land where
-      // the speculation started, discards the speculative scan and rescans from the cursor.
-      R.next_window_from(cur_end, Wmax, ctx->window_pods, nxt, &nxt_end);
-      // the helper thread issues the device work (everything up to the previous window applied,
-      // then nxt scanned into the other blob buffer: cur's lists stay valid) while this thread
-      // resolves cur
-      std::vector<pe::Update> pend;
-      pend.swap(pending);
-      const int nb = 1 - cb;
-      worker->post([&, nb] {
+      // the helper: previous windows' updates applied, then windows scanned up to D ahead
+      std::vector<std::pair<const std::vector<pe::Update>*, int>> to_apply;
+      for (; n_app < hist.size(); ++n_app) {
+        to_apply.emplace_back(&hist[n_app], upd_slot);
+        upd_slot = (upd_slot + 1) % std::max(depth, 1);
+      }
+      std::vector<Flight*> to_scan;
+      while ((int)fl.size() < depth + 1)
+        if (Flight* f = add_flight(fl.back().end)) to_scan.push_back(f);
+        else break;
+      worker->post([&, to_apply, to_scan] {
         const auto tp = std::chrono::steady_clock::now();
         if (trace) helper_cpu = sched_getcpu();
-        enqueue_apply(pend);
-        if (!nxt.empty()) enqueue_window(nxt, nb);
+        for (const auto& a : to_apply) enqueue_apply(*a.first, a.second);
+        for (Flight* f : to_scan) enqueue_window(f->groups, f->buf);
         if (trace) tr_post.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
       });
-      std::vector<pe::Update> upd;
+      // seeds: the changes of the windows resolved since cur's scan (later states overwrite)
+      seed.clear();
+      for (size_t k = cur.ver; k < hist.size(); ++k) seed.insert(seed.end(), hist[k].begin(), hist[k].end());
       bool consumed = false;
       try {
-        consumed = timed_resolve(cur, upd, &seed);
+        consumed = timed_resolve(cur.groups, upd, &seed);
       } catch (...) {
-        // the helper task still reads pend / nxt (locals of this loop): let it finish before the
+        // the helper task still reads the flights and update sets: let it finish before the
         // unwinding frees them, then report the resolver's error (the helper's is secondary)
         try {
           worker->wait();
@@ -1972,24 +2034,23 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         throw;
       }
       worker->wait();
-      if (R.done()) {
-        hipchk(hipStreamSynchronize(s), "sync speculative");
-        enqueue_apply(upd);
-        break;
-      }
-      if (consumed && !nxt.empty() && R.cursor() == cur_end) {
-        cur.swap(nxt);
-        cur_end = nxt_end;
-        cb = 1 - cb;
-        seed = upd;                              // nxt's scan did not see cur's changes
-        pending = std::move(upd);
+      const bool landed = consumed && R.cursor() == cur.end && fl.size() > 1;
+      if (landed && !R.done()) {
+        hist.push_back(std::move(upd));
+        upd = {};
+        fl.pop_front();
         continue;
       }
-      hipchk(hipStreamSynchronize(s), "sync discarded");   // speculative work done and dropped
-      enqueue_apply(upd);
-      seed.clear();
-      R.next_window_from(R.cursor(), Wmax, ctx->window_pods, cur, &cur_end);
-      if (!cur.empty()) enqueue_window(cur, cb);
+      // done, or speculation dropped: finish the device work, apply what is left, in order (one
+      // launch per window: a node may be in several windows' updates)
+      hipchk(hipStreamSynchronize(s), "sync speculative");
+      for (; n_app < hist.size(); ++n_app) {   // (depth > 1 only; slot 0 is rewritten after each)
+        enqueue_apply(hist[n_app], 0);
+        hipchk(hipStreamSynchronize(s), "sync apply");
+      }
+      enqueue_apply(upd, 0);
+      if (R.done()) break;
+      restart();
     }
     hipchk(hipStreamSynchronize(s), "sync greedy");
     if (walk) {
