@@ -1344,9 +1344,14 @@ __device__ void write_group(const uint64_t* sk, int nout, int flags, uint64_t li
     hp->n = nout;
     hp->limit = limit;
   }
-  // the waves that stored (keys: threads < nout; header: thread 0) make their stores visible to
-  // the host, then the block agrees and thread 0 publishes the generation
+  // the waves that stored (keys: threads < nout; header: thread 0) wait until their stores have
+  // left the CU (vmcnt 0), the block agrees, and thread 0's system-scope release (L2 write-back,
+  // then the flag store) publishes the generation after all of them
+#ifdef PE_SIGNAL_FULL_FENCE
   if ((int)(threadIdx.x & ~63u) < nout || threadIdx.x < 64) __threadfence_system();
+#else
+  if ((int)(threadIdx.x & ~63u) < nout || threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
