@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <deque>
+#include <condition_variable>
 #include <atomic>
 #include <chrono>
 #include <exception>
@@ -658,6 +659,103 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
 
 // ------------------------------------------------------------------ fit mask
 
+// Persistent helpers for the batch planning (pe_jobs_upload is on the batch's path; creating and
+// joining a thread per task cost tens of us each).  run(n, f): f(0) on the caller, f(1 .. n-1) on
+// up to 7 pool threads, returns when all are done, rethrows the first exception.  The threads
+// sleep on a condition variable between calls; the pool lives for the process.
+// PE_NO_POOL=1: a thread per task instead (A/B).
+class PlanPool {
+ public:
+  static constexpr int kMax = 8;
+  static PlanPool& get() {
+    static PlanPool* p = new PlanPool();   // never destroyed: its threads may still wait at exit
+    return *p;
+  }
+  void run(int n, const std::function<void(int)>& f) {
+    n = std::max(1, std::min(n, kMax));
+    std::vector<std::exception_ptr> err((size_t)n);
+    if (n > 1 && std::getenv("PE_NO_POOL")) {
+      std::vector<std::thread> th;
+      for (int t = 1; t < n; ++t)
+        th.emplace_back([&, t] {
+          try {
+            f(t);
+          } catch (...) {
+            err[(size_t)t] = std::current_exception();
+          }
+        });
+      try {
+        f(0);
+      } catch (...) {
+        err[0] = std::current_exception();
+      }
+      for (auto& x : th) x.join();
+    } else if (n > 1) {
+      std::lock_guard<std::mutex> serial(call_mu_);   // one planning call at a time on the pool
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        while ((int)th_.size() < n - 1) {
+          const int id = (int)th_.size();
+          th_.emplace_back([this, id] { loop(id); });
+        }
+        task_ = &f;
+        errs_ = &err;
+        want_ = n - 1;
+        left_ = n - 1;
+        ++gen_;
+      }
+      cv_.notify_all();
+      try {
+        f(0);
+      } catch (...) {
+        err[0] = std::current_exception();
+      }
+      std::unique_lock<std::mutex> lk(mu_);
+      done_cv_.wait(lk, [this] { return left_ == 0; });
+      task_ = nullptr;
+    } else {
+      try {
+        f(0);
+      } catch (...) {
+        err[0] = std::current_exception();
+      }
+    }
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
+  }
+
+ private:
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      std::vector<std::exception_ptr>* errs;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (id >= want_) continue;   // not needed for this call
+        f = task_;
+        errs = errs_;
+      }
+      try {
+        (*f)(id + 1);
+      } catch (...) {
+        (*errs)[(size_t)id + 1] = std::current_exception();
+      }
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--left_ == 0) done_cv_.notify_one();
+    }
+  }
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> th_;
+  const std::function<void(int)>* task_ = nullptr;
+  std::vector<std::exception_ptr>* errs_ = nullptr;
+  int want_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+};
+
 // body(j0, j1) over [0, n) in contiguous chunks: on up to 8 threads for large batches (the batch
 // planning is on the upload's path), inline for small ones.  Exceptions are rethrown here.
 extern "C++" {
@@ -668,24 +766,7 @@ static void parallel_for(int64_t n, Body body) {
     body(0, n);
     return;
   }
-  std::vector<std::exception_ptr> err((size_t)nt);
-  std::vector<std::thread> th;
-  for (int64_t t = 1; t < nt; ++t)
-    th.emplace_back([&, t] {
-      try {
-        body(n * t / nt, n * (t + 1) / nt);
-      } catch (...) {
-        err[(size_t)t] = std::current_exception();
-      }
-    });
-  try {
-    body(0, n / nt);
-  } catch (...) {
-    err[0] = std::current_exception();
-  }
-  for (auto& x : th) x.join();
-  for (auto& e : err)
-    if (e) std::rethrow_exception(e);
+  PlanPool::get().run((int)nt, [&](int t) { body(n * t / nt, n * (t + 1) / nt); });
 }
 }  // extern "C++"
 
@@ -764,24 +845,7 @@ static void build_dict(BatchDict& bd, int64_t n_jobs, const int64_t* req, const 
     return;
   }
   // large batches: the five independent fields on five threads (the upload is on the batch's path)
-  std::exception_ptr err[BatchDict::F];
-  std::vector<std::thread> th;
-  for (int f = 1; f < BatchDict::F; ++f)
-    th.emplace_back([&, f] {
-      try {
-        field(f);
-      } catch (...) {
-        err[f] = std::current_exception();
-      }
-    });
-  try {
-    field(0);
-  } catch (...) {
-    err[0] = std::current_exception();
-  }
-  for (auto& t : th) t.join();
-  for (auto& e : err)
-    if (e) std::rethrow_exception(e);
+  PlanPool::get().run(BatchDict::F, [&](int f) { field(f); });
 }
 
 // Dictionary codes of one batch (pe_kernels.h, CodeSpec): per dimension the sorted distinct request
