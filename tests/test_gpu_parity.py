@@ -108,6 +108,30 @@ def test_pg_min_resources_random_vs_oracle(eng, mode, big):
         assert want[3].sum() > 0      # overflow path exercised and flagged identically
 
 
+@pytest.mark.parametrize("C,bad", [(1000, 777), (400_000, 1_234_567), (400_000, 4 * 400_000 - 1), (400_000, None)])
+def test_pg_min_resources_input_validation(eng, C, bad):
+    """Input checks (negative requests, non-monotonic offsets) report the FIRST offending index,
+    on small arrays and on ones large enough to be scanned by the planning pool's threads."""
+    from placement import PlacementError
+    jgo = np.arange(C + 1, dtype=np.int32)
+    rep = np.ones(C, np.int32)
+    mm = np.ones(C, np.int32)
+    req = np.ones((C, 4), np.int64)
+    fl = np.full(C, 15, np.uint8)
+    if bad is None:
+        out = eng.pg_min_resources(V1, jgo, mm, rep, jgo.copy(), req, fl)
+        assert (out[0] == 1).all()
+        gco = jgo.copy()
+        gco[C // 2 + 1] = gco[C // 2] - 1                  # non-monotonic group offsets
+        with pytest.raises(PlacementError, match="not monotonic"):
+            eng.pg_min_resources(V1, jgo, mm, rep, gco, req, fl)
+        return
+    req.flat[bad] = -1
+    req.flat[min(bad + 5, req.size - 1)] = -7              # a later one must not be the one reported
+    with pytest.raises(PlacementError, match=f"negative request at index {bad}$"):
+        eng.pg_min_resources(V1, jgo, mm, rep, jgo.copy(), req, fl)
+
+
 def test_pg_min_resources_empty(eng):
     z = np.zeros(1, np.int32)
     out = eng.pg_min_resources(V2, z, None, np.zeros(0, np.int32), z, np.zeros((0, 4), np.int64), np.zeros(0, np.uint8))

@@ -326,15 +326,142 @@ void need_ptr(const void* p, const char* name) {
   if (!p) raise(PE_EINVAL, std::string(name) + " is NULL");
 }
 
+// Persistent helpers for the batch planning (pe_jobs_upload is on the batch's path; creating and
+// joining a thread per task cost tens of us each).  run(n, f): f(0) on the caller, f(1 .. n-1) on
+// up to 7 pool threads, returns when all are done, rethrows the first exception.  The threads
+// sleep on a condition variable between calls; the pool lives for the process.
+// PE_NO_POOL=1: a thread per task instead (A/B).
+class PlanPool {
+ public:
+  static constexpr int kMax = 8;
+  static PlanPool& get() {
+    static PlanPool* p = new PlanPool();   // never destroyed: its threads may still wait at exit
+    return *p;
+  }
+  void run(int n, const std::function<void(int)>& f) {
+    n = std::max(1, std::min(n, kMax));
+    std::vector<std::exception_ptr> err((size_t)n);
+    if (n > 1 && std::getenv("PE_NO_POOL")) {
+      std::vector<std::thread> th;
+      for (int t = 1; t < n; ++t)
+        th.emplace_back([&, t] {
+          try {
+            f(t);
+          } catch (...) {
+            err[(size_t)t] = std::current_exception();
+          }
+        });
+      try {
+        f(0);
+      } catch (...) {
+        err[0] = std::current_exception();
+      }
+      for (auto& x : th) x.join();
+    } else if (n > 1) {
+      std::lock_guard<std::mutex> serial(call_mu_);   // one planning call at a time on the pool
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        while ((int)th_.size() < n - 1) {
+          const int id = (int)th_.size();
+          th_.emplace_back([this, id] { loop(id); });
+        }
+        task_ = &f;
+        errs_ = &err;
+        want_ = n - 1;
+        left_ = n - 1;
+        ++gen_;
+      }
+      cv_.notify_all();
+      try {
+        f(0);
+      } catch (...) {
+        err[0] = std::current_exception();
+      }
+      std::unique_lock<std::mutex> lk(mu_);
+      done_cv_.wait(lk, [this] { return left_ == 0; });
+      task_ = nullptr;
+    } else {
+      try {
+        f(0);
+      } catch (...) {
+        err[0] = std::current_exception();
+      }
+    }
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
+  }
+
+ private:
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      std::vector<std::exception_ptr>* errs;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (id >= want_) continue;   // not needed for this call
+        f = task_;
+        errs = errs_;
+      }
+      try {
+        (*f)(id + 1);
+      } catch (...) {
+        (*errs)[(size_t)id + 1] = std::current_exception();
+      }
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--left_ == 0) done_cv_.notify_one();
+    }
+  }
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> th_;
+  const std::function<void(int)>* task_ = nullptr;
+  std::vector<std::exception_ptr>* errs_ = nullptr;
+  int want_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+};
+
+// The first index in [0, n) where bad(i) holds, or n: chunks of 4096 reduced branch-free (the
+// loops vectorise), on the planning pool for large arrays (the aggregation validates ~10^7 values
+// per call).
+template <class Bad>
+int64_t first_bad(int64_t n, Bad bad) {
+  constexpr int64_t kChunk = 4096;
+  auto scan = [&](int64_t b, int64_t e) -> int64_t {
+    for (int64_t c = b; c < e; c += kChunk) {
+      const int64_t ce = std::min(e, c + kChunk);
+      bool any = false;
+      for (int64_t i = c; i < ce; ++i) any |= bad(i);
+      if (any)
+        for (int64_t i = c; i < ce; ++i)
+          if (bad(i)) return i;
+    }
+    return e;
+  };
+  if (n < (int64_t(1) << 20)) return scan(0, n);
+  constexpr int kT = 8;
+  int64_t first[kT];
+  PlanPool::get().run(kT, [&](int t) {
+    const int64_t b = n * t / kT, e = n * (t + 1) / kT;
+    const int64_t r = scan(b, e);
+    first[t] = r < e ? r : n;
+  });
+  int64_t r = n;
+  for (int t = 0; t < kT; ++t) r = std::min(r, first[t]);
+  return r;
+}
+
 void check_req(const int64_t* req, int64_t n, const char* what) {
-  for (int64_t i = 0; i < n * pe::D; ++i)
-    if (req[i] < 0) raise(PE_EINVAL, std::string(what) + ": negative request at index " + std::to_string(i));
+  const int64_t i = first_bad(n * pe::D, [req](int64_t k) { return req[k] < 0; });
+  if (i < n * pe::D) raise(PE_EINVAL, std::string(what) + ": negative request at index " + std::to_string(i));
 }
 
 void check_offsets(const int32_t* off, int64_t n, int64_t limit, const char* what) {
   if (off[0] != 0) raise(PE_EINVAL, std::string(what) + "[0] must be 0");
-  for (int64_t i = 0; i < n; ++i)
-    if (off[i + 1] < off[i]) raise(PE_EINVAL, std::string(what) + " is not monotonic");
+  if (first_bad(n, [off](int64_t i) { return off[i + 1] < off[i]; }) < n)
+    raise(PE_EINVAL, std::string(what) + " is not monotonic");
   if (limit >= 0 && off[n] > limit) raise(PE_EINVAL, std::string(what) + " exceeds its array");
 }
 
@@ -658,103 +785,6 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
 }
 
 // ------------------------------------------------------------------ fit mask
-
-// Persistent helpers for the batch planning (pe_jobs_upload is on the batch's path; creating and
-// joining a thread per task cost tens of us each).  run(n, f): f(0) on the caller, f(1 .. n-1) on
-// up to 7 pool threads, returns when all are done, rethrows the first exception.  The threads
-// sleep on a condition variable between calls; the pool lives for the process.
-// PE_NO_POOL=1: a thread per task instead (A/B).
-class PlanPool {
- public:
-  static constexpr int kMax = 8;
-  static PlanPool& get() {
-    static PlanPool* p = new PlanPool();   // never destroyed: its threads may still wait at exit
-    return *p;
-  }
-  void run(int n, const std::function<void(int)>& f) {
-    n = std::max(1, std::min(n, kMax));
-    std::vector<std::exception_ptr> err((size_t)n);
-    if (n > 1 && std::getenv("PE_NO_POOL")) {
-      std::vector<std::thread> th;
-      for (int t = 1; t < n; ++t)
-        th.emplace_back([&, t] {
-          try {
-            f(t);
-          } catch (...) {
-            err[(size_t)t] = std::current_exception();
-          }
-        });
-      try {
-        f(0);
-      } catch (...) {
-        err[0] = std::current_exception();
-      }
-      for (auto& x : th) x.join();
-    } else if (n > 1) {
-      std::lock_guard<std::mutex> serial(call_mu_);   // one planning call at a time on the pool
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        while ((int)th_.size() < n - 1) {
-          const int id = (int)th_.size();
-          th_.emplace_back([this, id] { loop(id); });
-        }
-        task_ = &f;
-        errs_ = &err;
-        want_ = n - 1;
-        left_ = n - 1;
-        ++gen_;
-      }
-      cv_.notify_all();
-      try {
-        f(0);
-      } catch (...) {
-        err[0] = std::current_exception();
-      }
-      std::unique_lock<std::mutex> lk(mu_);
-      done_cv_.wait(lk, [this] { return left_ == 0; });
-      task_ = nullptr;
-    } else {
-      try {
-        f(0);
-      } catch (...) {
-        err[0] = std::current_exception();
-      }
-    }
-    for (auto& e : err)
-      if (e) std::rethrow_exception(e);
-  }
-
- private:
-  void loop(int id) {
-    uint64_t seen = 0;
-    for (;;) {
-      const std::function<void(int)>* f;
-      std::vector<std::exception_ptr>* errs;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (id >= want_) continue;   // not needed for this call
-        f = task_;
-        errs = errs_;
-      }
-      try {
-        (*f)(id + 1);
-      } catch (...) {
-        (*errs)[(size_t)id + 1] = std::current_exception();
-      }
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--left_ == 0) done_cv_.notify_one();
-    }
-  }
-  std::mutex call_mu_, mu_;
-  std::condition_variable cv_, done_cv_;
-  std::vector<std::thread> th_;
-  const std::function<void(int)>* task_ = nullptr;
-  std::vector<std::exception_ptr>* errs_ = nullptr;
-  int want_ = 0, left_ = 0;
-  uint64_t gen_ = 0;
-};
 
 // body(j0, j1) over [0, n) in contiguous chunks: on up to 8 threads for large batches (the batch
 // planning is on the upload's path), inline for small ones.  Exceptions are rethrown here.
