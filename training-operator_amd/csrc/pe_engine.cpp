@@ -255,7 +255,7 @@ struct pe_ctx {
   HostBuf<int64_t> h_updx[2];             // update staging slots 1, 2 (pipeline depth 2, 3)
   uint32_t walk_gen = 0;                  // generation of the last signalled walk window (never 0)
   int pin_cpu = -2;                       // greedy thread pinning at world > 1: a CPU of this rank's L3 (-2: not chosen yet)
-  HostBuf<uint8_t> h_out, h_out2, h_own;   // h_out2: the pipelined loop's second blob buffer
+  HostBuf<uint8_t> h_out, h_out2, h_own;   // h_out2: the pipelined loop's second blob buffer (h_outx: 3rd, 4th)
   HostBuf<uint8_t> h_merged;                // host-exchange windows: the device-merged lists
   HostBuf<int64_t> h_upd;
   // greedy sorted walk (pe_kernels.h WalkIndex; the default window path, greedy_flags bit1 = full scan)
@@ -1842,8 +1842,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       worker.reset(new SpinWorker(ctx->device));
       if (pin.on) worker->pin(pin.l3);
     }
-    // blob buffer b (0: h_out, 1: h_out2): the pipelined loop D2Hs the next window's blob while the
-    // host still resolves from the current one's
+    // blob buffer b (0: h_out, 1: h_out2, 2-3: h_outx): the windows scanned ahead land in their own
+    // buffers while the host still resolves from the current one's
     auto outbuf = [&](int b) { return b == 0 ? ctx->h_out.p : b == 1 ? ctx->h_out2.p : ctx->h_outx[b - 2].p; };
     auto outbufdev = [&](int b) { return b == 0 ? ctx->h_out.dev : b == 1 ? ctx->h_out2.dev : ctx->h_outx[b - 2].dev; };
     const bool direct_out = ctx->world == 1 && !ctx->comm;
@@ -1988,9 +1988,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       ctx->stats.greedy_host_ms +=
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
     };
-    // ---- residual updates of this shard H2D + apply (the pinned staging buffer is reused only
-    //      after the next collect_window's stream sync)
-    // (slot: the staging buffer; the pipelined loop rotates D of them, see the loop below)
+    // ---- residual updates of this shard: the apply kernel reads the records from pinned staging
+    //      slot `slot` (no H2D copy); a slot is rewritten only once a later launch is known to have
+    //      started (a signalled group seen, or a stream sync) -- the pipelined loop below rotates D
     auto enqueue_apply = [&](const std::vector<pe::Update>& updates, int slot) {
       int64_t nu = 0;
       HostBuf<int64_t>& hu = slot == 0 ? ctx->h_upd : ctx->h_updx[slot - 1];
