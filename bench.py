@@ -56,7 +56,7 @@ def parse_args(argv=None):
     ap.add_argument("--nodes", type=int, default=1_000_000)
     ap.add_argument("--fit-jobs", type=int, default=100_000)
     ap.add_argument("--greedy-jobs", type=int, default=10_000)
-    ap.add_argument("--greedy-steps", type=int, default=2)
+    ap.add_argument("--greedy-steps", type=int, default=5)
     ap.add_argument("--topk", type=int, default=0)
     ap.add_argument("--window-groups", type=int, default=0)
     ap.add_argument("--window-pods", type=int, default=0)
