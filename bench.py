@@ -35,6 +35,10 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # chip-wide integer VALU issue ceiling, wave-instructions/s: profiles/r1_ubench_valu.txt
 # (v_add_u32 / v_addc_co at 8 waves per SIMD: 4.24 cycles per wave-instruction per SIMD, 256 CUs x 4 SIMDs)
 VALU_ISSUE_CEILING = 5.79e11
+# a committed profile's step time may differ from this run's by this fraction and still count as the
+# same kernel (identical sources and workload are checked separately): boxes and mask allocations
+# move the fit step by up to ~9 % (2.16-2.36 ms, profiles/r8_fit_waves.txt)
+PROFILE_TOL = 0.10
 # per fit path: the kernels of one fit step (the first is the dominant one, the roofline's kernel)
 STEP_KERNELS = {
     "planes": ("pe::fit_mask_planes_rows_kernel", "pe::encode_planes_kernel"),
@@ -159,7 +163,9 @@ def profile_summary():
 
 def profile_check(path: str, n_nodes: int, n_jobs: int, kern_ms: float, src_hash: str):
     """Compare the committed profile with this run: same engine sources, same workload, and a fit
-    step (sum of the step kernels' average durations) within 5 % of this run's hipEvent time.
+    step (sum of the step kernels' average durations) within PROFILE_TOL of this run's hipEvent time
+    (the same kernel measures 2.16-2.36 ms across boxes and mask allocations, profiles/r8_fit_waves.txt;
+    the traffic is a property of the code and the workload, which the hash and workload checks pin).
     Returns the roofline fields taken from it (traffic and counters are null unless all hold)."""
     tag, summ = profile_summary()
     out = {"profile": None, "profile_kernel_ms": None, "profile_step_ms": None, "profile_matches": False,
@@ -175,7 +181,7 @@ def profile_check(path: str, n_nodes: int, n_jobs: int, kern_ms: float, src_hash
     out["profile_step_ms"] = sum(kernels[k]["avg_ns"] for k in names if k in kernels) / 1e6
     wl = summ.get("workload", {})
     same = (summ.get("source_hash") == src_hash and wl.get("nodes") == n_nodes and wl.get("jobs") == n_jobs
-            and abs(out["profile_step_ms"] - kern_ms) <= 0.05 * kern_ms)
+            and abs(out["profile_step_ms"] - kern_ms) <= PROFILE_TOL * kern_ms)
     out["profile_matches"] = bool(same)
     if same:
         p = summ.get("pmc", {}).get(names[0], {})
@@ -378,7 +384,8 @@ def main(argv=None):
                              "kernel) on this rank's shard; achieved = algorithmic bytes (shard nodes x 36 + jobs x 44 + "
                              "jobs x ceil(shard/64) x 8) / kernel_ms; traffic / valu_issue_frac come from the committed "
                              "profile only when it was taken on the same engine sources and workload and its step time "
-                             "agrees with kernel_ms within 5 % (profile_matches)"},
+                             f"agrees with kernel_ms within {PROFILE_TOL:.0%} (profile_matches; box-to-box spread of the "
+                             "same kernel ~9 %)"},
     }
 
     if world > 1:
