@@ -36,9 +36,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # (v_add_u32 / v_addc_co at 8 waves per SIMD: 4.24 cycles per wave-instruction per SIMD, 256 CUs x 4 SIMDs)
 VALU_ISSUE_CEILING = 5.79e11
 # a committed profile's step time may differ from this run's by this fraction and still count as the
-# same kernel (identical sources and workload are checked separately): boxes and mask allocations
-# move the fit step by up to ~9 % (2.16-2.36 ms, profiles/r8_fit_waves.txt)
-PROFILE_TOL = 0.10
+# same kernel (identical sources and workload are checked separately).  Kept tight on purpose: boxes
+# and mask allocations move the fit step by up to ~9 % (2.16-2.36 ms, profiles/r8_fit_waves.txt), and
+# a run outside 5 % reports traffic null rather than borrow counters from a different-speed run; the
+# delta is printed beside the borrowed counters (profile_step_delta)
+PROFILE_TOL = 0.05
 # per fit path: the kernels of one fit step (the first is the dominant one, the roofline's kernel)
 STEP_KERNELS = {
     "planes": ("pe::fit_mask_planes_rows_kernel", "pe::encode_planes_kernel"),
@@ -152,6 +154,66 @@ def pg_slice(agg, a: int, b: int):
     return (jgo[a:b + 1] - g0, mm[a:b], rep[g0:g1], gco[g0:g1 + 1] - c0, cont[c0:c1], flags[c0:c1])
 
 
+AGG_LATENCY_JOBS = (1, 16, 256)
+
+
+def agg_raw_call(fn, head, mode, sub):
+    """A zero-argument closure calling a pe_pg_min_resources-shaped C function on the CSR batch `sub`
+    (pg_slice output) with the ctypes pointers built once: what is timed per call is the C call
+    (plus the ctypes dispatch, reported separately as ctypes_call_us), not numpy conversions.
+    Returns (call, outputs)."""
+    import numpy as np
+    jgo, mm, rep, gco, cont, flags = [np.ascontiguousarray(a) for a in sub]
+    J = len(jgo) - 1
+    outs = (np.zeros((J, 4), np.int64), np.zeros(J, np.uint8), np.zeros(J, np.int32), np.zeros(J, np.uint8))
+    keep = (jgo, mm, rep, gco, cont, flags) + outs
+    ptrs = [a.ctypes.data_as(ctypes.c_void_p) for a in keep]
+    args = tuple(head) + (mode, J, *ptrs)
+
+    def call():
+        return fn(*args)
+    call.keep = keep
+    return call, outs
+
+
+def pcie_rates():
+    """Pinned H2D / D2H rates of 128 MB copies on this box (torch pinned tensors), GB/s."""
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return None
+        h = torch.empty(128 << 20, dtype=torch.uint8, pin_memory=True)
+        d = torch.empty(128 << 20, dtype=torch.uint8, device="cuda")
+        rates = {}
+        for name, dst, src in (("h2d_gbs", d, h), ("d2h_gbs", h, d)):
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                dst.copy_(src, non_blocking=True)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            rates[name] = (128 << 20) / sorted(ts)[2] / 1e9
+        del h, d
+        return rates
+    except Exception:   # noqa: BLE001 -- a reported figure, never a reason to fail the bench
+        return None
+
+
+def time_calls(call, reps: int, warm: int = 20):
+    """Median and p90 wall time of one call, microseconds."""
+    for _ in range(warm):
+        call()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter_ns()
+        call()
+        ts.append(time.perf_counter_ns() - t0)
+    ts.sort()
+    return ts[len(ts) // 2] / 1e3, ts[int(len(ts) * 0.9)] / 1e3
+
+
 def profile_summary():
     """The committed profile profiles/LATEST names (summary.json), or None."""
     try:
@@ -179,6 +241,7 @@ def profile_check(path: str, n_nodes: int, n_jobs: int, kern_ms: float, src_hash
         return out
     out["profile_kernel_ms"] = kernels[names[0]]["avg_ns"] / 1e6
     out["profile_step_ms"] = sum(kernels[k]["avg_ns"] for k in names if k in kernels) / 1e6
+    out["profile_step_delta"] = out["profile_step_ms"] / kern_ms - 1.0
     wl = summ.get("workload", {})
     same = (summ.get("source_hash") == src_hash and wl.get("nodes") == n_nodes and wl.get("jobs") == n_jobs
             and abs(out["profile_step_ms"] - kern_ms) <= PROFILE_TOL * kern_ms)
@@ -378,14 +441,15 @@ def main(argv=None):
                      "traffic_source": prof["traffic_source"], "kernel_ms": kern_ms,
                      "profile_kernel_ms": prof["profile_kernel_ms"], "profile_step_ms": prof["profile_step_ms"],
                      "profile": prof["profile"], "profile_matches": prof["profile_matches"],
+                     "profile_step_delta": prof.get("profile_step_delta"),
                      "source_hash": src_hash, "alg_bytes_per_launch": alg, "fit_path": fit_path,
                      "valu_issue_frac": valu_frac,
                      "note": "kernel_ms = hipEvent time on the engine stream / fit step (count memset, node encode, fit "
                              "kernel) on this rank's shard; achieved = algorithmic bytes (shard nodes x 36 + jobs x 44 + "
                              "jobs x ceil(shard/64) x 8) / kernel_ms; traffic / valu_issue_frac come from the committed "
                              "profile only when it was taken on the same engine sources and workload and its step time "
-                             f"agrees with kernel_ms within {PROFILE_TOL:.0%} (profile_matches; box-to-box spread of the "
-                             "same kernel ~9 %)"},
+                             f"agrees with kernel_ms within {PROFILE_TOL:.0%} (profile_matches; profile_step_delta = "
+                             "profile step / this run's step - 1): those counters are the profile's, not this run's"},
     }
 
     if world > 1:
@@ -440,28 +504,77 @@ def main(argv=None):
         eng.fit_mask_run()
         eng.synchronize()
 
-        # PodGroup MinResources aggregation (v1 CalcPGMinResources over a batch), end to end per call; jobs
-        # are independent, so at N > 1 every rank aggregates its contiguous slice of the batch
+        # PodGroup MinResources aggregation (v1 CalcPGMinResources).  The operator calls it once per job
+        # per reconcile (job.go:275-277,455-457; coscheduling.go:103-118), so the per-call latency at
+        # J = 1 / 16 / 256 is the figure that decides whether the drop-in beats the code it replaces;
+        # the 1M-job batch is the throughput line.  Jobs are independent: at N > 1 every rank
+        # aggregates its contiguous slice of the batch.
         agg = synth.make_pg_batch(args.agg_jobs, synth.SEED["cfg3"])
+        lat = {}
+        call0 = eng.lib.pe_abi_version
+        ctypes_us = time_calls(call0, 2000)[0]
+        for Jn in AGG_LATENCY_JOBS:
+            sub = pg_slice(agg, 0, Jn)
+            call, outs = agg_raw_call(eng.lib.pe_pg_min_resources, (eng.h,), 1, sub)
+            assert call() in (0, -2)
+            med, p90 = time_calls(call, 400)
+            os.environ["PE_AGG_DEVICE"] = "1"     # the r2 call path (six H2D + four D2H copies), same box
+            try:
+                dmed, _ = time_calls(call, 200)
+            finally:
+                del os.environ["PE_AGG_DEVICE"]
+            lat[str(Jn)] = {"median_us": med, "p90_us": p90, "r2_path_median_us": dmed,
+                            "alg_bytes": agg_bytes(sub[0], sub[3])}
         lo_j, hi_j = rank * args.agg_jobs // world, (rank + 1) * args.agg_jobs // world
         mine = pg_slice(agg, lo_j, hi_j)
         eng.pg_min_resources(1, *mine)
-        ts = []
-        for _ in range(3):
+        e0, e1 = ev.create(), ev.create()
+        ts, ks = [], []
+        for _ in range(5):
             barrier()
             t0 = time.perf_counter()
+            ev.record(e0, stream)
             eng.pg_min_resources(1, *mine)
+            ev.record(e1, stream)
             ts.append(allmax(time.perf_counter() - t0))
+            ks.append(ev.elapsed_ms(e0, e1))
         at = float(np.median(ts))
+        kms = float(np.median(ks))
+        os.environ["PE_AGG_DEVICE"] = "1"
+        try:
+            dts = []
+            for _ in range(3):
+                barrier()
+                t0 = time.perf_counter()
+                eng.pg_min_resources(1, *mine)
+                dts.append(allmax(time.perf_counter() - t0))
+        finally:
+            del os.environ["PE_AGG_DEVICE"]
         ab = agg_bytes(agg[0], agg[3])
-        out["aggregation"] = {"workload": f"{args.agg_jobs} v1 PyTorchJob-like jobs (Master 1 + Worker 0-63, 1-2 "
-                                          "containers), CalcPGMinResources on the GPU incl. H2D/D2H"
-                                          + (f", split over {world} ranks ({hi_j - lo_j} jobs on rank {rank})"
-                                             if world > 1 else ""),
-                              "jobs_per_s": args.agg_jobs / at, "ms_per_call": at * 1e3, "alg_bytes": ab,
-                              "achieved_gbs": ab / at / 1e9,
-                              "note": "PCIe-inclusive (the ABI hands over host buffers): bound by the H2D/D2H copies; "
-                                      "time = max over ranks"}
+        mb = agg_bytes(mine[0], mine[3])
+        pcie = pcie_rates()
+        out["aggregation"] = {
+            "workload": f"{args.agg_jobs} v1 PyTorchJob-like jobs (Master 1 + Worker 0-63, 1-2 containers), "
+                        "CalcPGMinResources on the GPU, host arrays in and out (the C ABI's contract)"
+                        + (f", split over {world} ranks ({hi_j - lo_j} jobs on rank {rank})" if world > 1 else ""),
+            "jobs_per_s": args.agg_jobs / at, "ms_per_call": at * 1e3, "alg_bytes": ab,
+            "achieved_gbs": ab / at / 1e9, "r2_path_ms_per_call": float(np.median(dts)) * 1e3,
+            "pcie": pcie,
+            "pcie_bound_ms": (mb / pcie["h2d_gbs"] / 1e6) if pcie else None,
+            "latency_us": lat, "ctypes_call_us": ctypes_us,
+            "roofline": {"bound": "pcie", "kernel": "pe::pg_agg_seg_kernel", "kernel_ms": kms,
+                         "achieved": mb / (kms * 1e-3) / 1e9, "unit": "GB/s",
+                         "peak": pcie["h2d_gbs"] if pcie else None,
+                         "frac": (mb / (kms * 1e-3) / 1e9 / pcie["h2d_gbs"]) if pcie else None,
+                         "hbm_frac": mb / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "note": "kernel_ms = hipEvents around the call on the engine stream (its only device work is "
+                                 "the one launch); the kernel reads the packed batch over PCIe (zero-copy) and writes "
+                                 "the outputs into pinned host memory, so the bound is the link, peak = this box's "
+                                 "measured pinned H2D rate; hbm_frac against 8 TB/s for reference"},
+            "note": "latency_us: one pe_pg_min_resources call on the first J jobs (median / p90 of 400, ctypes pointers "
+                    "built once; ctypes_call_us = the dispatch cost of an empty ABI call, included); r2_path = the "
+                    "round-2 call path (PE_AGG_DEVICE=1: six H2D + four D2H copies + stream sync) on the same box; "
+                    "ms_per_call = max over ranks"}
 
     if not args.no_greedy:
         batch = synth.make_jobs(args.greedy_jobs, synth.SEED["cfg3"], "mixed")
@@ -579,6 +692,34 @@ def main(argv=None):
                                "threads_note": "threads = this box's CPU share (OMP_NUM_THREADS, else the affinity "
                                                "mask); nproc counts the whole machine, shared with other GPUs' jobs",
                                "counts_match_gpu": bool(np.array_equal(ocounts, gpu_counts))}
+        if "aggregation" in out:
+            # the same aggregation rule on the CPU (oracle.c orc_pg_min_resources, one thread, the same CSR
+            # arrays), per call at the operator's sizes and on the whole batch; outputs checked equal to the GPU's
+            ol = oracle.lib()
+            clat = {}
+            same = True
+            for Jn in AGG_LATENCY_JOBS:
+                sub = pg_slice(agg, 0, Jn)
+                ccall, couts = agg_raw_call(ol.orc_pg_min_resources, (), 1, sub)
+                gcall, gouts = agg_raw_call(eng.lib.pe_pg_min_resources, (eng.h,), 1, sub)
+                ccall()
+                gcall()
+                same &= all(np.array_equal(a, b) for a, b in zip(couts, gouts))
+                clat[str(Jn)] = {"median_us": time_calls(ccall, 400)[0]}
+            ccall, couts = agg_raw_call(ol.orc_pg_min_resources, (), 1, agg)
+            reps = []
+            for _ in range(3):
+                c0 = time.perf_counter()
+                ccall()
+                reps.append(time.perf_counter() - c0)
+            gout = eng.pg_min_resources(1, *agg)
+            same &= all(np.array_equal(a, b) for a, b in zip(couts, gout))
+            out["cpu_baseline"]["aggregation"] = {
+                "jobs_per_s": args.agg_jobs / float(np.median(reps)), "ms_per_call": float(np.median(reps)) * 1e3,
+                "cores": 1, "kind": "port", "latency_us": clat, "outputs_match_gpu": bool(same),
+                "sample": f"C oracle orc_pg_min_resources (oracle/oracle.c, single thread, {cpu_model()}) on the same "
+                          f"CSR arrays: the first 1 / 16 / 256 jobs per call (median of 400) and all {args.agg_jobs} "
+                          "jobs (median of 3); the Go reference (map + resource.Quantity per pod) cannot be timed here"}
         if "greedy" in out:
             # the same algorithm on the CPU: windowed protocol (K = 256, 128 groups / 1024 pods per window, the engine defaults),
             # each window's candidate lists built by the C oracle over all 1M nodes (OpenMP over groups),

@@ -26,9 +26,12 @@ import (
 	v1 "k8s.io/api/core/v1"
 )
 
-// flattenV1 builds the one-job v1 CSR of CalcPGMinResources(minMember, replicas, pcGetFunc).
+// flattenV1 builds the one-job v1 CSR of CalcPGMinResources(minMember, replicas, pcGetFunc), and the
+// print formats the reference's AddResourceList sums end with (hip.FormatAcc, util.go:79-104): the
+// same walk over the pods util.go:126-141 counts (a type's second pod only re-adds the formats of
+// its first, so at most two per type are replayed).
 func flattenV1(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpec, pcGetFunc PriorityClassGetFunc,
-	gpuName string) (*hip.CSR, error) {
+	gpuName string) (*hip.CSR, *hip.FormatAcc, error) {
 	type typed struct {
 		name     string
 		priority int32
@@ -49,24 +52,43 @@ func flattenV1(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpe
 		return order[i].name < order[j].name
 	})
 	b := &hip.CSR{}
+	acc := &hip.FormatAcc{}
+	podCnt := int64(0)
 	for _, t := range order {
 		for _, c := range t.spec.Template.Spec.Containers {
-			rl := c.Resources.Requests
-			if rl == nil { // AddResourceList: Limits only when Requests is nil (util.go:90-92)
-				rl = c.Resources.Limits
-			}
-			if err := b.AddContainer(rl, hip.KindContainer, gpuName); err != nil {
-				return nil, err
+			if err := b.AddContainer(effectiveList(c), hip.KindContainer, gpuName); err != nil {
+				return nil, nil, err
 			}
 		}
 		replicasOrNil := int32(-1)
 		if t.spec.Replicas != nil {
 			replicasOrNil = *t.spec.Replicas
+			k := int64(*t.spec.Replicas)
+			if room := int64(minMember) - podCnt; room < k {
+				k = room
+			}
+			for pod := int64(0); pod < k && pod < 2; pod++ {
+				for _, c := range t.spec.Template.Spec.Containers {
+					acc.AddList(effectiveList(c), gpuName, 1)
+				}
+			}
+			if k > 0 {
+				podCnt += k
+			}
 		}
 		b.EndGroup(replicasOrNil)
 	}
 	b.EndJob(minMember)
-	return b, nil
+	return b, acc, nil
+}
+
+// effectiveList is what AddResourceList adds for a container: Requests, or Limits only when the
+// Requests map is nil (util.go:90-92; an empty non-nil map does not fall back).
+func effectiveList(c v1.Container) v1.ResourceList {
+	if c.Resources.Requests == nil {
+		return c.Resources.Limits
+	}
+	return c.Resources.Requests
 }
 
 // CalcPGMinResourcesEngine returns a CalcPGMinResources with the pod counting and the resource sums
@@ -74,7 +96,7 @@ func flattenV1(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpe
 func CalcPGMinResourcesEngine(eng *hip.Engine, gpuName string) func(int32, map[apiv1.ReplicaType]*apiv1.ReplicaSpec,
 	PriorityClassGetFunc) *v1.ResourceList {
 	return func(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpec, pcGetFunc PriorityClassGetFunc) *v1.ResourceList {
-		csr, err := flattenV1(minMember, replicas, pcGetFunc, gpuName)
+		csr, formats, err := flattenV1(minMember, replicas, pcGetFunc, gpuName)
 		if err != nil {
 			return CalcPGMinResources(minMember, replicas, pcGetFunc) // exact reference path
 		}
@@ -82,7 +104,7 @@ func CalcPGMinResourcesEngine(eng *hip.Engine, gpuName string) func(int32, map[a
 		if err != nil || agg.Overflow[0] != 0 {
 			return CalcPGMinResources(minMember, replicas, pcGetFunc)
 		}
-		rl := agg.Unflatten(0, gpuName, nil)
+		rl := agg.Unflatten(0, gpuName, formats.Formats()) // printed as the reference's sums print
 		return &rl
 	}
 }

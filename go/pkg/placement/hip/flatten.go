@@ -95,7 +95,7 @@ func (b *CSR) EndJob(minMember int32) {
 // included, as the reference's maps hold them).  formats, when given, is the Quantity format per
 // dimension the reference's Add would have kept (the first contributing quantity's), so that
 // String() prints identically; equality (Cmp) never depends on it.
-func (a *Agg) Unflatten(j int, gpuName string, formats *[4]resource.Format) corev1.ResourceList {
+func (a *Agg) Unflatten(j int, gpuName string, formats *[Dims]resource.Format) corev1.ResourceList {
 	names := DimNames(gpuName)
 	out := corev1.ResourceList{}
 	for d := 0; d < Dims; d++ {
@@ -117,4 +117,58 @@ func (a *Agg) Unflatten(j int, gpuName string, formats *[4]resource.Format) core
 		}
 	}
 	return out
+}
+
+// FormatAcc replays the print formats the reference's sums end with, per engine dimension, so that
+// Unflatten's quantities print exactly as the reference's (values never depend on it):
+//   - AddResourceList (util.go:79-104) deep-copies a key's first quantity (its format), then
+//     Quantity.Add adopts the addend's format while the running value is still 0 (apimachinery
+//     quantity.go Add: `if q.i.value == 0 { q.Format = y.Format }`, the same on the inf.Dec path);
+//   - Build (coscheduling.go:108-118) starts each key from a zero Quantity{} and Adds
+//     quantity.Mul(replicas), so the same rule holds (a product with 0 replicas is a zero addend).
+// So a key prints in the format of its first nonzero contribution, or of the last one when all are
+// zero -- the rule kf::FormatAcc / MinResourcesFormatsV1 implement in the C++ host mirror.
+type FormatAcc struct {
+	fmt     [Dims]resource.Format
+	seen    [Dims]bool
+	nonzero [Dims]bool
+}
+
+// Add one contribution of dimension d (zero = a zero-valued addend, e.g. a product with 0 replicas).
+func (a *FormatAcc) Add(d int, q resource.Quantity, zero bool) {
+	if !a.seen[d] {
+		a.seen[d] = true
+		a.fmt[d] = q.Format
+		a.nonzero[d] = !zero
+		return
+	}
+	if !a.nonzero[d] {
+		a.fmt[d] = q.Format
+	}
+	if !zero {
+		a.nonzero[d] = true
+	}
+}
+
+// AddList adds every key of rl that is an engine dimension, scaled by `scale` for the zero test.
+func (a *FormatAcc) AddList(rl corev1.ResourceList, gpuName string, scale int64) {
+	names := DimNames(gpuName)
+	for key, q := range rl {
+		for d, n := range names {
+			if n == key {
+				a.Add(d, q, q.IsZero() || scale == 0)
+			}
+		}
+	}
+}
+
+// Formats is Unflatten's formats argument (dimensions never added keep the defaults).
+func (a *FormatAcc) Formats() *[Dims]resource.Format {
+	out := [Dims]resource.Format{resource.DecimalSI, resource.BinarySI, resource.DecimalSI, resource.BinarySI}
+	for d := 0; d < Dims; d++ {
+		if a.seen[d] {
+			out[d] = a.fmt[d]
+		}
+	}
+	return &out
 }

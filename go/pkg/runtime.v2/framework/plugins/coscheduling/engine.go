@@ -64,35 +64,42 @@ func NewWithEngine(eng *hip.Engine, gpuName string) func(ctx context.Context, c 
 
 // flattenInfo turns info.TotalRequests into the engine's v2 CSR: one job, one group per entry
 // (Replicas, and its PodRequests as one container record -- NewInfo has already applied kueue's
-// TotalRequests, runtime.go:130-136).  Entries in name order (the sum does not depend on it).
-func flattenInfo(info *runtime.Info, gpuName string) (*hip.CSR, error) {
+// TotalRequests, runtime.go:130-136).  Entries in name order: the sums do not depend on it, and the
+// print formats (hip.FormatAcc: the first nonzero quantity x replicas Build adds per key) follow
+// one of the orders the reference's map range can take.
+func flattenInfo(info *runtime.Info, gpuName string) (*hip.CSR, *hip.FormatAcc, error) {
 	names := make([]string, 0, len(info.TotalRequests))
 	for name := range info.TotalRequests {
 		names = append(names, name)
 	}
 	sort.Strings(names)
 	b := &hip.CSR{}
+	acc := &hip.FormatAcc{}
 	for _, name := range names {
 		trr := info.TotalRequests[name]
 		if err := b.AddContainer(trr.PodRequests, hip.KindContainer, gpuName); err != nil {
-			return nil, err
+			return nil, nil, err
 		}
+		acc.AddList(trr.PodRequests, gpuName, int64(trr.Replicas))
 		b.EndGroup(trr.Replicas)
 	}
 	b.EndJob(0)
-	return b, nil
+	return b, acc, nil
 }
 
-// unflatten is job 0's ResourceList.
-func unflatten(agg *hip.Agg, gpuName string) corev1.ResourceList { return agg.Unflatten(0, gpuName, nil) }
+// unflatten is job 0's ResourceList, printed in the formats the reference's Build would print.
+func unflatten(agg *hip.Agg, gpuName string, formats *hip.FormatAcc) corev1.ResourceList {
+	return agg.Unflatten(0, gpuName, formats.Formats())
+}
 
-// Build is coscheduling.go:103-148 with the aggregation (:108-118) on the engine.
+// Build is coscheduling.go:103-148 with the aggregation (:108-118) on the engine; the PodGroup is
+// emitted by buildPodGroup, the one copy of :119-147 both Builds call.
 func (c *EngineCoScheduling) Build(ctx context.Context, obj client.Object, info *runtime.Info,
 	trainJob *kubeflowv2.TrainJob) (client.Object, error) {
 	if info == nil || info.RuntimePolicy.PodGroupPolicy == nil || info.RuntimePolicy.PodGroupPolicy.Coscheduling == nil || trainJob == nil {
 		return nil, nil
 	}
-	csr, err := flattenInfo(info, c.gpuName)
+	csr, formats, err := flattenInfo(info, c.gpuName)
 	if err != nil {
 		return c.CoScheduling.Build(ctx, obj, info, trainJob) // exact reference path (inf.Dec, other keys)
 	}
@@ -103,6 +110,17 @@ func (c *EngineCoScheduling) Build(ctx context.Context, obj client.Object, info 
 	if agg.Overflow[0] != 0 {
 		return c.CoScheduling.Build(ctx, obj, info, trainJob)
 	}
+	return c.CoScheduling.buildPodGroup(ctx, info, trainJob, agg.Members[0], unflatten(agg, c.gpuName, formats))
+}
+
+// buildPodGroup is the PodGroup emission of coscheduling.go:119-147 -- the object, its controller
+// reference, the existing object's Get and needsCreateOrUpdate (:150-153) -- factored out of Build so
+// that one copy serves both plugins.  The reference's Build ends in it after its own aggregation
+// loop (INTEGRATION.md, "v2 plugin"):
+//
+//	return c.buildPodGroup(ctx, info, trainJob, totalMembers, totalResources)
+func (c *CoScheduling) buildPodGroup(ctx context.Context, info *runtime.Info, trainJob *kubeflowv2.TrainJob,
+	members int32, resources corev1.ResourceList) (client.Object, error) {
 	newPG := &schedulerpluginsv1alpha1.PodGroup{
 		TypeMeta: metav1.TypeMeta{
 			APIVersion: schedulerpluginsv1alpha1.SchemeGroupVersion.String(),
@@ -114,8 +132,8 @@ func (c *EngineCoScheduling) Build(ctx context.Context, obj client.Object, info 
 		},
 		Spec: schedulerpluginsv1alpha1.PodGroupSpec{
 			ScheduleTimeoutSeconds: info.RuntimePolicy.PodGroupPolicy.Coscheduling.ScheduleTimeoutSeconds,
-			MinMember:              agg.Members[0],
-			MinResources:           unflatten(agg, c.gpuName),
+			MinMember:              members,
+			MinResources:           resources,
 		},
 	}
 	if err := ctrlutil.SetControllerReference(trainJob, newPG, c.scheme); err != nil {

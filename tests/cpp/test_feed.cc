@@ -15,6 +15,9 @@
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include "pe_resolver.h"
 
 static int failed = 0;
@@ -208,7 +211,58 @@ static void test_fed_resolve(unsigned seed_base) {
   std::printf("ok   fed resolve == parsed resolve (seed %u)\n", seed_base);
 }
 
+// SeedScorer start()/stop() back to back (advisor r2: a stale cancel read by the helper must not
+// acknowledge the next window).  After stop() returns, the window's inputs are rewritten at once:
+// a helper still inside the window would race with it (ThreadSanitizer) or see torn inputs.  The
+// -DPE_SEED_TEST_YIELD build yields between the helper's state read and its action.
+static void test_scorer_handshake() {
+  std::mt19937 rng(7);
+  pe::DirtySet seeds;
+  for (int i = 0; i < 64; ++i) {
+    pe::NodeState st{};
+    for (int d = 0; d < pe::RD; ++d) st.res[d] = 1000 + (int64_t)(rng() % 1000);
+    seeds.upsert(i * 3, st);
+  }
+  std::vector<int64_t> req(4 * 8, 1);
+  std::vector<uint32_t> need(8, 0);
+  // one CPU for this thread and the helper (it inherits the mask): every yield is a real switch
+  cpu_set_t old_set, one;
+  (void)pthread_getaffinity_np(pthread_self(), sizeof(old_set), &old_set);
+  CPU_ZERO(&one);
+  CPU_SET(sched_getcpu(), &one);
+  (void)pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+  int cycles = 0;
+  {
+  pe::SeedScorer sc;
+  for (int it = 0; it < 20000; ++it) {
+    std::vector<int32_t> groups((size_t)(1 + rng() % 8));
+    for (size_t i = 0; i < groups.size(); ++i) groups[i] = (int32_t)i;
+    std::vector<pe::GroupCands> cands(groups.size());
+    std::vector<uint64_t> keys(16);
+    for (size_t i = 0; i < keys.size(); ++i) keys[i] = ((uint64_t)(i + 1) << 24) | (uint64_t)(1000 + i);
+    for (auto& gc : cands) {
+      gc.keys = keys.data();
+      gc.keyed = true;
+      gc.n = keys.size();
+      gc.limit = kNoKey;
+    }
+    sc.start(&seeds, &groups, &cands, req.data(), need.data());
+    if (rng() % 3 == 0) std::this_thread::yield();
+    sc.stop();
+    // the helper is idle now: clobber what it read
+    for (auto& gc : cands) gc.keys = nullptr, gc.n = 0;
+    std::fill(keys.begin(), keys.end(), 0);
+    groups.assign(groups.size(), -1);
+    ++cycles;
+  }
+  }
+  (void)pthread_setaffinity_np(pthread_self(), sizeof(old_set), &old_set);
+  CHECK(cycles == 20000);
+  std::printf("ok   seed scorer start/stop handshake (%d cycles)\n", cycles);
+}
+
 int main() {
+  test_scorer_handshake();
   test_order_and_wait();
   for (unsigned s = 1; s <= 6; ++s) test_fed_resolve(s);
   std::printf("%d failed checks\n", failed);

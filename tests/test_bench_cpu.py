@@ -80,7 +80,9 @@ def test_profile_check_requires_same_build(tmp_path, monkeypatch):
     ok = bench.profile_check("planes", 100, 10, 1.03, "abc")
     assert ok["profile_matches"] and ok["traffic"] == 123.0 and abs(ok["profile_step_ms"] - 1.02) < 1e-9
     assert not bench.profile_check("planes", 100, 10, 1.03, "other")["profile_matches"]     # other build
-    assert bench.profile_check("planes", 100, 10, 1.20, "abc")["traffic"] is None          # > 5 % apart
+    assert bench.PROFILE_TOL == 0.05                                                      # pinned tolerance
+    assert bench.profile_check("planes", 100, 10, 1.08, "abc")["traffic"] is None          # > 5 % apart
+    assert bench.profile_check("planes", 100, 10, 1.20, "abc")["traffic"] is None
     assert bench.profile_check("planes", 100, 11, 1.03, "abc")["traffic"] is None          # other workload
 
 

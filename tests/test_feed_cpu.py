@@ -25,6 +25,13 @@ def build_and_run(out, flags):
 def test_window_feed(tmp_path):
     out = build_and_run(str(tmp_path / "feed_tests"), ["-O2"])
     assert out.count("ok   fed resolve") == 6
+    assert "ok   seed scorer start/stop handshake" in out
+
+
+def test_seed_scorer_handshake_forced_yield(tmp_path):
+    """The helper yields between reading its state and acting on it (PE_SEED_TEST_YIELD)."""
+    out = build_and_run(str(tmp_path / "feed_yield"), ["-O2", "-DPE_SEED_TEST_YIELD"])
+    assert "ok   seed scorer start/stop handshake" in out
 
 
 def test_window_feed_tsan(tmp_path):
@@ -32,4 +39,4 @@ def test_window_feed_tsan(tmp_path):
                            input="int main(){}", text=True, capture_output=True)
     if probe.returncode != 0:
         pytest.skip("no ThreadSanitizer runtime")
-    build_and_run(str(tmp_path / "feed_tsan"), ["-O1", "-g", "-fsanitize=thread"])
+    build_and_run(str(tmp_path / "feed_tsan"), ["-O1", "-g", "-fsanitize=thread", "-DPE_SEED_TEST_YIELD"])

@@ -12,6 +12,9 @@ GO = os.path.join(ROOT, "go", "pkg")
 HIP_GO = os.path.join(GO, "placement", "hip", "hip.go")
 COSCHED_GO = os.path.join(GO, "runtime.v2", "framework", "plugins", "coscheduling", "engine.go")
 V1_GO = os.path.join(GO, "controller.v1", "common", "engine.go")
+ORACLE_GO = os.path.join(GO, "placement", "hip", "oracle.go")
+FLATTEN_GO = os.path.join(GO, "placement", "hip", "flatten.go")
+ORACLE_C = os.path.join(ROOT, "oracle", "oracle.c")
 
 
 def strip_c_comments(text):
@@ -87,14 +90,59 @@ def test_cgo_preamble_and_package():
 @pytest.mark.parametrize("path,needles", [
     (COSCHED_GO, ["package coscheduling", "func NewWithEngine(", "func flattenInfo(", "func unflatten(",
                   "PGMinResources(hip.ModeV2", "needsCreateOrUpdate(oldPG, newPG", "SetControllerReference",
-                  "c.CoScheduling.Build(ctx, obj, info, trainJob)", "framework.ComponentBuilderPlugin"]),
+                  "c.CoScheduling.Build(ctx, obj, info, trainJob)", "framework.ComponentBuilderPlugin",
+                  # the PodGroup emission (coscheduling.go:119-147) exists once, as a helper both Builds call
+                  "func (c *CoScheduling) buildPodGroup(", "return c.CoScheduling.buildPodGroup(ctx, info, trainJob",
+                  # print formats of the reference's Build sums (first nonzero quantity x replicas per key)
+                  "acc.AddList(trr.PodRequests, gpuName, int64(trr.Replicas))", "formats.Formats()"]),
     (V1_GO, ["package common", "func flattenV1(", "func CalcPGMinResourcesEngine(", "PGMinResources(hip.ModeV1",
-             "c.Resources.Limits", "CalcPGMinResources(minMember, replicas, pcGetFunc)", "pc.Value"]),
+             "c.Resources.Limits", "CalcPGMinResources(minMember, replicas, pcGetFunc)", "pc.Value",
+             # print formats of AddResourceList's sums, replayed over the counted pods (util.go:79-104,126-141)
+             "acc.AddList(effectiveList(c), gpuName, 1)", "agg.Unflatten(0, gpuName, formats.Formats())"]),
+    (FLATTEN_GO, ["type FormatAcc struct", "func (a *FormatAcc) Add(", "func (a *FormatAcc) Formats()",
+                  "if !a.nonzero[d] {"]),
 ])
 def test_adapters(path, needles):
     text = open(path).read()
     for n in needles:
         assert n in text, (os.path.basename(path), n)
+
+
+def test_podgroup_emission_not_duplicated():
+    """coscheduling.go:119-147 (PodGroup literal, owner reference, old-PG Get) is typed once, in
+    buildPodGroup; the engine's Build only calls it."""
+    text = open(COSCHED_GO).read()
+    assert text.count("schedulerpluginsv1alpha1.PodGroup{") == 2          # the new object and the Get target
+    assert text.count("SetControllerReference") == 1 and text.count("c.client.Get(") == 1
+    build = text[text.index("func (c *EngineCoScheduling) Build("):text.index("func (c *CoScheduling) buildPodGroup(")]
+    assert "PodGroupSpec{" not in build and "c.client.Get(" not in build
+
+
+def test_go_cpu_oracle_matches_c_oracle():
+    """go/pkg/placement/hip/oracle.go (the north star's Go CPU oracle of the best-fit rule, in the
+    plugin's package) restates oracle/oracle.c function for function with the same constants."""
+    go = open(ORACLE_GO).read()
+    c = open(ORACLE_C).read()
+    for fn in ("func fits(", "func Score(", "func Key(", "func argminKey(", "func FitMaskCPU(", "func PlaceGreedyCPU(",
+               "func mulOvf("):
+        assert fn in go, fn
+    for cfn in ("static inline int fits(", "uint64_t orc_score(", "static inline uint64_t node_key(",
+                "static uint64_t argmin_key(", "int orc_fit_mask(", "int64_t orc_place_greedy("):
+        assert cfn in c, cfn
+    # score / key constants: SCORE_MAX = 2^40 - 1, shifts mem >> 20, gpu << 20 (saturating at 2^20),
+    # eph >> 24, key = score << 24 | 24-bit node id
+    assert "#define SCORE_MAX ((uint64_t)0xFFFFFFFFFFull)" in c and "ScoreMax   = uint64(1)<<40 - 1" in go
+    assert "(uint64_t)left[1] >> 20" in c and "MemShift   = 20" in go and "uint64(left[1]) >> MemShift" in go
+    assert "((uint64_t)left[2] << 20)" in c and "(1ull << 20)" in c
+    assert "GPUShift   = 20" in go and "uint64(left[2]) >= 1<<20" in go and "uint64(left[2]) << GPUShift" in go
+    assert "(uint64_t)left[3] >> 24" in c and "EphShift   = 24" in go and "uint64(left[3]) >> EphShift" in go
+    assert "(orc_score(left) << 24) | gid" in c and "KeyShift   = 24" in go and "Score(&left)<<KeyShift | gid" in go
+    assert "k & 0xFFFFFFull" in c and "NodeIDMask = uint64(1)<<KeyShift - 1" in go
+    assert int(re.search(r"ORC_NEED_ISLAND\s+(0x[0-9a-fA-F]+)u?", c).group(1), 16) == 0x80000000
+    assert "LabelIsland = uint32(0x80000000)" in go
+    # greedy order: priority desc, index asc (stable); all-or-nothing rollback; island unit = count x request
+    assert "sort.SliceStable(order, func(a, b int) bool { return priority[order[a]] > priority[order[b]] })" in go
+    assert "mulOvf(q[d], int64(groupCount[g]))" in go and "take(int64(n), &q, -1)" in go
 
 
 def test_go_files_are_balanced():

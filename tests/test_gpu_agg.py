@@ -1,0 +1,91 @@
+"""pe_pg_min_resources call path (round 3): the batch is packed into <= 256-job segments in pinned
+host memory and each block stages its segment in LDS over PCIe (pe_kernels.h AggSegHdr); a one-segment
+call waits on a flag in pinned memory instead of a stream sync.  Parity vs the C oracle
+(oracle/oracle.c orc_pg_min_resources, a restatement of util.go:108-145 / coscheduling.go:108-118)
+across segment boundaries, oversized segments read in place, the flag path and the r2 device path."""
+
+import numpy as np
+import pytest
+
+import oracle
+from placement import V1, V2, Engine
+from test_gpu_parity import random_csr
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = Engine(0, gpu_resource_name="nvidia.com/gpu")
+    yield e
+    e.close()
+
+
+def _check(eng, mode, arrs):
+    got = eng.pg_min_resources(mode, *arrs)
+    want = oracle.pg_min_resources(mode, *arrs)
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("mode", [V1, V2])
+@pytest.mark.parametrize("J", [1, 2, 17, 255, 256, 257, 511, 1000, 33000, 70001])
+def test_agg_segment_sizes(eng, mode, J):
+    """One segment (flag path) up to 256 jobs, then several; 33k+ jobs take the multi-range planner."""
+    _check(eng, mode, random_csr(J, 100 + J + mode, big=(J % 2 == 1)))
+
+
+def _one_job_csr(n_groups, n_cont_per_group, seed):
+    rng = np.random.default_rng(seed)
+    jgo = np.array([0, n_groups], np.int32)
+    rep = rng.integers(-1, 5, n_groups).astype(np.int32)
+    gco = (np.arange(n_groups + 1) * n_cont_per_group).astype(np.int32)
+    C = int(gco[-1])
+    req = rng.integers(0, 2**30, (C, 4), dtype=np.int64)
+    fl = (rng.integers(0, 16, C) | (rng.integers(0, 4, C) << 4)).astype(np.uint8)
+    mm = np.array([int(rep.clip(0).sum()) // 2 + 1], np.int32)
+    return jgo, mm, rep, gco, req, fl
+
+
+def _concat(parts):
+    """CSR batches back to back."""
+    jgo, mm, rep, gco, req, fl = [np.zeros(1, np.int32)], [], [], [np.zeros(1, np.int32)], [], []
+    g_off = c_off = 0
+    for p in parts:
+        jgo.append(p[0][1:] + g_off)
+        mm.append(p[1])
+        rep.append(p[2])
+        gco.append(p[3][1:] + c_off)
+        req.append(p[4].reshape(-1, 4))
+        fl.append(p[5])
+        g_off += int(p[0][-1])
+        c_off += int(p[3][-1])
+    return (np.concatenate(jgo).astype(np.int32), np.concatenate(mm).astype(np.int32),
+            np.concatenate(rep).astype(np.int32), np.concatenate(gco).astype(np.int32),
+            np.concatenate(req).astype(np.int64), np.concatenate(fl).astype(np.uint8))
+
+
+@pytest.mark.parametrize("mode", [V1, V2])
+def test_agg_oversized_segments(eng, mode):
+    """A job whose groups and containers exceed one segment's LDS budget (48 KB) is read in place,
+    alone or between ordinary jobs; also a job with thousands of groups."""
+    big_c = _one_job_csr(4, 600, 1)            # 2400 containers x 33 B > 48 KB
+    big_g = _one_job_csr(9000, 0, 2)           # 9000 groups, no containers
+    for arrs in (big_c, big_g, _concat([random_csr(300, 3), big_c, random_csr(10, 4), big_g, random_csr(600, 5)])):
+        _check(eng, mode, arrs)
+
+
+def test_agg_alternating_calls(eng):
+    """Small (flag) and large (stream sync) calls interleaved: buffers grow and are reused, flag
+    generations advance."""
+    for i in range(30):
+        J = [1, 5000, 3, 256, 100000][i % 5]
+        _check(eng, V1 if i % 2 else V2, random_csr(J, 500 + i))
+
+
+def test_agg_device_path_ab(eng, monkeypatch):
+    """PE_AGG_DEVICE=1 (the r2 call path, kept for A/B) still agrees with the oracle."""
+    monkeypatch.setenv("PE_AGG_DEVICE", "1")
+    for J in (1, 300, 20000):
+        _check(eng, V1, random_csr(J, 900 + J))
+        _check(eng, V2, random_csr(J, 901 + J, big=True))

@@ -237,7 +237,12 @@ struct pe_ctx {
   DevBuf<uint64_t> mask;
   DevBuf<unsigned long long> counts;
   HostBuf<unsigned long long> h_counts;
-  // aggregation
+  // aggregation: segmented batch and outputs in pinned, device-mapped host memory (pe_kernels.h
+  // AggSegHdr); the device-resident arrays below only serve the PE_AGG_DEVICE=1 A/B path
+  HostBuf<uint8_t> a_stage, a_outh;
+  HostBuf<int64_t> a_segoff;
+  HostBuf<uint32_t> a_flag;
+  uint32_t agg_gen = 0;
   DevBuf<int32_t> a_jgo, a_mm, a_rep, a_gco, a_mem;
   DevBuf<int64_t> a_req, a_out;
   DevBuf<uint8_t> a_fl, a_pres, a_ovf;
@@ -279,6 +284,7 @@ struct pe_ctx {
     code_vals.release(); code_needs.release(); code_jobs.release(); code_x.release(); counts.release(); h_counts.release();
     planes.release(); plane_jobs.release();
     lds_spec_d.release(); lds_vals.release(); lds_codes.release(); lds_ranks.release(); lds_aux.release();
+    a_stage.release(); a_outh.release(); a_segoff.release(); a_flag.release();
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
@@ -463,6 +469,18 @@ void check_offsets(const int32_t* off, int64_t n, int64_t limit, const char* wha
   if (first_bad(n, [off](int64_t i) { return off[i + 1] < off[i]; }) < n)
     raise(PE_EINVAL, std::string(what) + " is not monotonic");
   if (limit >= 0 && off[n] > limit) raise(PE_EINVAL, std::string(what) + " exceeds its array");
+}
+
+// body(j0, j1) over [0, n) in contiguous chunks: on up to 8 threads for large batches (the batch
+// planning is on the upload's path), inline for small ones.  Exceptions are rethrown here.
+template <class Body>
+void parallel_for(int64_t n, Body body) {
+  const int64_t nt = n < 32768 ? 1 : std::min<int64_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+  if (nt <= 1) {
+    body(0, n);
+    return;
+  }
+  PlanPool::get().run((int)nt, [&](int t) { body(n * t / nt, n * (t + 1) / nt); });
 }
 
 void fill_req(ReqRec& r, const int64_t* q, uint32_t need) {
@@ -718,6 +736,88 @@ int pe_read_residuals(pe_ctx* ctx, int64_t* res_out) {
   });
 }
 
+}  // extern "C"
+
+namespace {
+
+// One segment of the packed aggregation batch (pe_kernels.h AggSegHdr).
+struct AggSeg {
+  int64_t j0;
+  int32_t nj, ng, nc;
+  int64_t bytes;
+};
+
+// Wait for the one-segment aggregation kernel's flag (pinned host memory, written after its outputs).
+// The stream is polled now and then: a faulted kernel surfaces as its HIP error, a kernel that ended
+// without the flag as PE_EHIP.
+void agg_wait_flag(pe_ctx* ctx, uint32_t gen) {
+  for (unsigned spin = 1;; ++spin) {
+    if (__atomic_load_n(ctx->a_flag.p, __ATOMIC_ACQUIRE) == gen) return;
+    _mm_pause();
+    if ((spin & 1023) == 0) {
+      const hipError_t e = hipStreamQuery(ctx->stream);
+      if (e == hipErrorNotReady) continue;
+      hipchk(e, "aggregation kernel");
+      if (__atomic_load_n(ctx->a_flag.p, __ATOMIC_ACQUIRE) == gen) return;
+      raise(PE_EHIP, "aggregation kernel finished without signalling");
+    }
+  }
+}
+
+// The r2 call path (device copies of the six input arrays, four D2H copies): PE_AGG_DEVICE=1 A/B.
+void agg_device_path(pe_ctx* ctx, int32_t mode, int64_t n_jobs, int64_t G, int64_t C, const int32_t* job_group_off,
+                     const int32_t* min_member, const int32_t* group_replicas, const int32_t* group_cont_off,
+                     const int64_t* cont_req, const uint8_t* cont_flags, int64_t* out_min_res, uint8_t* out_present,
+                     int32_t* out_members, uint8_t* out_overflow) {
+  if (C > 0) check_req(cont_req, C, "cont_req");
+  hipStream_t s = ctx->stream;
+  hipchk(ctx->a_jgo.ensure(n_jobs + 1), "alloc");
+  hipchk(ctx->a_mm.ensure(n_jobs), "alloc");
+  hipchk(ctx->a_rep.ensure(G), "alloc");
+  hipchk(ctx->a_gco.ensure(G + 1), "alloc");
+  hipchk(ctx->a_req.ensure((size_t)C * pe::D), "alloc");
+  hipchk(ctx->a_fl.ensure(C), "alloc");
+  hipchk(ctx->a_out.ensure((size_t)n_jobs * pe::D), "alloc");
+  hipchk(ctx->a_pres.ensure(n_jobs), "alloc");
+  hipchk(ctx->a_mem.ensure(n_jobs), "alloc");
+  hipchk(ctx->a_ovf.ensure(n_jobs), "alloc");
+  hipchk(hipMemcpyAsync(ctx->a_jgo.p, job_group_off, (n_jobs + 1) * 4, hipMemcpyHostToDevice, s), "H2D");
+  if (mode == PE_MODE_V1) hipchk(hipMemcpyAsync(ctx->a_mm.p, min_member, n_jobs * 4, hipMemcpyHostToDevice, s), "H2D");
+  if (G > 0) {
+    hipchk(hipMemcpyAsync(ctx->a_rep.p, group_replicas, G * 4, hipMemcpyHostToDevice, s), "H2D");
+    hipchk(hipMemcpyAsync(ctx->a_gco.p, group_cont_off, (G + 1) * 4, hipMemcpyHostToDevice, s), "H2D");
+  }
+  if (C > 0) {
+    hipchk(hipMemcpyAsync(ctx->a_req.p, cont_req, (size_t)C * pe::D * 8, hipMemcpyHostToDevice, s), "H2D");
+    hipchk(hipMemcpyAsync(ctx->a_fl.p, cont_flags, C, hipMemcpyHostToDevice, s), "H2D");
+  }
+  hipchk(pe::launch_pg_min_resources(s, mode, n_jobs, ctx->a_jgo.p, ctx->a_mm.p, ctx->a_rep.p, ctx->a_gco.p,
+                                     ctx->a_req.p, ctx->a_fl.p, ctx->a_out.p, ctx->a_pres.p, ctx->a_mem.p, ctx->a_ovf.p),
+         "launch pg_min_resources");
+  hipchk(hipMemcpyAsync(out_min_res, ctx->a_out.p, (size_t)n_jobs * pe::D * 8, hipMemcpyDeviceToHost, s), "D2H");
+  hipchk(hipMemcpyAsync(out_present, ctx->a_pres.p, n_jobs, hipMemcpyDeviceToHost, s), "D2H");
+  hipchk(hipMemcpyAsync(out_members, ctx->a_mem.p, n_jobs * 4, hipMemcpyDeviceToHost, s), "D2H");
+  hipchk(hipMemcpyAsync(out_overflow, ctx->a_ovf.p, n_jobs, hipMemcpyDeviceToHost, s), "D2H");
+  hipchk(hipStreamSynchronize(s), "sync pg_min_resources");
+}
+
+// Grow-only pinned buffer (a 1M-job batch needs ~170 MB; hipHostMalloc costs ms, so keep it).
+template <class T>
+void ensure_pinned(HostBuf<T>& b, size_t count, const char* what) {
+  if (count <= b.n && b.p) return;
+  hipchk(b.ensure(std::max(count, b.n + b.n / 2), kZeroCopy), what);
+}
+
+}  // namespace
+
+extern "C" {
+
+// Call path (pe_kernels.h AggSegHdr): validate + pack the batch into segments of <= 256 jobs in a
+// pinned, device-mapped staging buffer (on the planning pool for large batches), one launch (one
+// block per segment: the segment comes into LDS over PCIe in one round of coalesced 16-B loads),
+// outputs written by the kernel straight into a pinned buffer in the caller's layout, then copied
+// out.  One segment (the operator's per-reconcile call: one job) waits on a flag the kernel stores
+// in pinned memory instead of a stream synchronisation.  No input ever goes through a DMA copy.
 int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t* job_group_off,
                         const int32_t* min_member, const int32_t* group_replicas, const int32_t* group_cont_off,
                         const int64_t* cont_req, const uint8_t* cont_flags, int64_t* out_min_res,
@@ -743,62 +843,134 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
     if (C > 0) {
       need_ptr(cont_req, "cont_req");
       need_ptr(cont_flags, "cont_flags");
-      check_req(cont_req, C, "cont_req");
     }
-    hipStream_t s = ctx->stream;
-    hipchk(ctx->a_jgo.ensure(n_jobs + 1), "alloc");
-    hipchk(ctx->a_mm.ensure(n_jobs), "alloc");
-    hipchk(ctx->a_rep.ensure(G), "alloc");
-    hipchk(ctx->a_gco.ensure(G + 1), "alloc");
-    hipchk(ctx->a_req.ensure((size_t)C * pe::D), "alloc");
-    hipchk(ctx->a_fl.ensure(C), "alloc");
-    hipchk(ctx->a_out.ensure((size_t)n_jobs * pe::D), "alloc");
-    hipchk(ctx->a_pres.ensure(n_jobs), "alloc");
-    hipchk(ctx->a_mem.ensure(n_jobs), "alloc");
-    hipchk(ctx->a_ovf.ensure(n_jobs), "alloc");
-    hipchk(hipMemcpyAsync(ctx->a_jgo.p, job_group_off, (n_jobs + 1) * 4, hipMemcpyHostToDevice, s), "H2D");
-    if (mode == PE_MODE_V1) hipchk(hipMemcpyAsync(ctx->a_mm.p, min_member, n_jobs * 4, hipMemcpyHostToDevice, s), "H2D");
-    if (G > 0) {
-      hipchk(hipMemcpyAsync(ctx->a_rep.p, group_replicas, G * 4, hipMemcpyHostToDevice, s), "H2D");
-      hipchk(hipMemcpyAsync(ctx->a_gco.p, group_cont_off, (G + 1) * 4, hipMemcpyHostToDevice, s), "H2D");
-    }
-    if (C > 0) {
-      hipchk(hipMemcpyAsync(ctx->a_req.p, cont_req, (size_t)C * pe::D * 8, hipMemcpyHostToDevice, s), "H2D");
-      hipchk(hipMemcpyAsync(ctx->a_fl.p, cont_flags, C, hipMemcpyHostToDevice, s), "H2D");
-    }
-    hipchk(pe::launch_pg_min_resources(s, mode, n_jobs, ctx->a_jgo.p, ctx->a_mm.p, ctx->a_rep.p, ctx->a_gco.p,
-                                       ctx->a_req.p, ctx->a_fl.p, ctx->a_out.p, ctx->a_pres.p, ctx->a_mem.p,
-                                       ctx->a_ovf.p),
-           "launch pg_min_resources");
-    hipchk(hipMemcpyAsync(out_min_res, ctx->a_out.p, (size_t)n_jobs * pe::D * 8, hipMemcpyDeviceToHost, s), "D2H");
-    hipchk(hipMemcpyAsync(out_present, ctx->a_pres.p, n_jobs, hipMemcpyDeviceToHost, s), "D2H");
-    hipchk(hipMemcpyAsync(out_members, ctx->a_mem.p, n_jobs * 4, hipMemcpyDeviceToHost, s), "D2H");
-    hipchk(hipMemcpyAsync(out_overflow, ctx->a_ovf.p, n_jobs, hipMemcpyDeviceToHost, s), "D2H");
-    hipchk(hipStreamSynchronize(s), "sync pg_min_resources");
-    for (int64_t j = 0; j < n_jobs; ++j)
-      if (out_overflow[j]) {
-        ctx->err = "int64 overflow in job " + std::to_string(j);
-        return PE_EOVERFLOW;
+    if (std::getenv("PE_AGG_DEVICE")) {
+      agg_device_path(ctx, mode, n_jobs, G, C, job_group_off, min_member, group_replicas, group_cont_off, cont_req,
+                      cont_flags, out_min_res, out_present, out_members, out_overflow);
+    } else {
+      const bool v1 = mode == PE_MODE_V1;
+      const int32_t* gco = G > 0 ? group_cont_off : nullptr;
+      // 1. segments, per job range (one range below 32k jobs; segments never span ranges)
+      const int T = n_jobs < 32768 ? 1 : 8;
+      std::vector<std::vector<AggSeg>> segs((size_t)T);
+      auto plan = [&](int t) {
+        const int64_t ja = n_jobs * t / T, jb = n_jobs * (t + 1) / T;
+        auto& out = segs[(size_t)t];
+        out.reserve((size_t)((jb - ja) / pe::AGG_SEG_JOBS + 1));
+        int64_t off[7];
+        for (int64_t j = ja; j < jb;) {
+          AggSeg sg{j, 0, 0, 0, 0};
+          while (j < jb && sg.nj < pe::AGG_SEG_JOBS) {
+            const int64_t g0 = job_group_off[j], g1 = job_group_off[j + 1];
+            const int64_t nc = gco ? (int64_t)gco[g1] - gco[g0] : 0;
+            pe::agg_seg_layout(sg.nj + 1, sg.ng + (g1 - g0), sg.nc + nc, v1, off);
+            if (sg.nj > 0 && off[6] > pe::AGG_SEG_BYTES) break;
+            ++sg.nj;
+            sg.ng += (int32_t)(g1 - g0);
+            sg.nc += (int32_t)nc;
+            sg.bytes = off[6];
+            ++j;
+          }
+          out.push_back(sg);
+        }
+      };
+      if (T == 1) plan(0);
+      else PlanPool::get().run(T, plan);
+      std::vector<size_t> first((size_t)T + 1, 0);
+      for (int t = 0; t < T; ++t) first[t + 1] = first[t] + segs[t].size();
+      const int64_t nseg = (int64_t)first[T];
+      ensure_pinned(ctx->a_segoff, (size_t)nseg + 1, "alloc pinned segment offsets");
+      int64_t* so = ctx->a_segoff.p;
+      so[0] = 0;
+      for (int t = 0, k = 0; t < T; ++t)
+        for (const AggSeg& sg : segs[t]) so[k + 1] = so[k] + sg.bytes, ++k;
+      const int64_t total = so[nseg];
+      int64_t oo[4];
+      pe::agg_out_layout(n_jobs, oo);
+      const int64_t out_bytes = oo[3] + pe::agg_r16(n_jobs);
+      ensure_pinned(ctx->a_stage, (size_t)total, "alloc pinned aggregation batch");
+      ensure_pinned(ctx->a_outh, (size_t)out_bytes, "alloc pinned aggregation outputs");
+      if (!ctx->a_flag.p) hipchk(ctx->a_flag.ensure(16, kZeroCopy), "alloc pinned flag");
+      // 2. pack (and the negative-request check, on the copied values)
+      std::vector<int64_t> bad((size_t)T, INT64_MAX);
+      auto pack = [&](int t) {
+        size_t k = first[t];
+        for (const AggSeg& sg : segs[t]) {
+          uint8_t* b = ctx->a_stage.p + so[k++];
+          pe::AggSegHdr h{};
+          h.j0 = sg.j0;
+          h.nj = sg.nj;
+          h.ng = sg.ng;
+          h.nc = sg.nc;
+          std::memcpy(b, &h, sizeof(h));
+          int64_t off[7];
+          pe::agg_seg_layout(sg.nj, sg.ng, sg.nc, v1, off);
+          const int32_t g0 = job_group_off[sg.j0];
+          int32_t* jl = reinterpret_cast<int32_t*>(b + off[0]);
+          for (int32_t i = 0; i <= sg.nj; ++i) jl[i] = job_group_off[sg.j0 + i] - g0;
+          if (v1) std::memcpy(b + off[1], min_member + sg.j0, (size_t)sg.nj * 4);
+          if (sg.ng > 0) {
+            std::memcpy(b + off[2], group_replicas + g0, (size_t)sg.ng * 4);
+            const int32_t c0 = gco[g0];
+            int32_t* gl = reinterpret_cast<int32_t*>(b + off[3]);
+            for (int32_t i = 0; i <= sg.ng; ++i) gl[i] = gco[g0 + i] - c0;
+            if (sg.nc > 0) {
+              const int64_t* q = cont_req + (int64_t)c0 * pe::D;
+              const int64_t nq = (int64_t)sg.nc * pe::D;
+              std::memcpy(b + off[4], q, (size_t)nq * 8);
+              std::memcpy(b + off[5], cont_flags + c0, (size_t)sg.nc);
+              int64_t any = 0;
+              for (int64_t i = 0; i < nq; ++i) any |= q[i];
+              if (any < 0 && bad[t] == INT64_MAX)
+                for (int64_t i = 0; i < nq; ++i)
+                  if (q[i] < 0) {
+                    bad[t] = (int64_t)c0 * pe::D + i;
+                    break;
+                  }
+            }
+          } else {
+            reinterpret_cast<int32_t*>(b + off[3])[0] = 0;
+          }
+        }
+      };
+      if (T == 1) pack(0);
+      else PlanPool::get().run(T, pack);
+      const int64_t first_neg = *std::min_element(bad.begin(), bad.end());
+      if (first_neg != INT64_MAX) raise(PE_EINVAL, "cont_req: negative request at index " + std::to_string(first_neg));
+      // 3. one launch; 4. outputs
+      uint8_t* const od = ctx->a_outh.dev;
+      if (nseg == 1) {
+        if (++ctx->agg_gen == 0) ++ctx->agg_gen;
+        hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, nullptr, 1, total, od, n_jobs,
+                                          ctx->a_flag.dev, ctx->agg_gen),
+               "launch pg_agg_segments");
+        agg_wait_flag(ctx, ctx->agg_gen);
+      } else {
+        hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, ctx->a_segoff.dev, nseg, 0, od, n_jobs,
+                                          nullptr, 0),
+               "launch pg_agg_segments");
+        hipchk(hipStreamSynchronize(ctx->stream), "sync pg_agg_segments");
       }
+      const uint8_t* oh = ctx->a_outh.p;
+      auto unpack = [&](int64_t a, int64_t e) {
+        std::memcpy(out_min_res + a * pe::D, oh + oo[0] + a * 32, (size_t)(e - a) * 32);
+        std::memcpy(out_members + a, oh + oo[1] + a * 4, (size_t)(e - a) * 4);
+        std::memcpy(out_present + a, oh + oo[2] + a, (size_t)(e - a));
+        std::memcpy(out_overflow + a, oh + oo[3] + a, (size_t)(e - a));
+      };
+      if (T == 1) unpack(0, n_jobs);
+      else parallel_for(n_jobs, unpack);
+    }
+    const void* o1 = std::memchr(out_overflow, 1, (size_t)n_jobs);
+    if (o1) {
+      ctx->err = "int64 overflow in job " + std::to_string(static_cast<const uint8_t*>(o1) - out_overflow);
+      return PE_EOVERFLOW;
+    }
     return PE_OK;
   });
 }
 
 // ------------------------------------------------------------------ fit mask
-
-// body(j0, j1) over [0, n) in contiguous chunks: on up to 8 threads for large batches (the batch
-// planning is on the upload's path), inline for small ones.  Exceptions are rethrown here.
-extern "C++" {
-template <class Body>
-static void parallel_for(int64_t n, Body body) {
-  const int64_t nt = n < 32768 ? 1 : std::min<int64_t>(8, std::max(1u, std::thread::hardware_concurrency()));
-  if (nt <= 1) {
-    body(0, n);
-    return;
-  }
-  PlanPool::get().run((int)nt, [&](int t) { body(n * t / nt, n * (t + 1) / nt); });
-}
-}  // extern "C++"
 
 // The batch's dictionary, built once per upload and shared by every fit path's planning: per field
 // (dims 0-3, field 4 = label need) the distinct values ascending and each job's index into them.
@@ -1880,7 +2052,14 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     pe::WindowFeed feed;
     struct StreamIdle {
       hipStream_t s;
-      static bool busy(void* u) { return hipStreamQuery(static_cast<StreamIdle*>(u)->s) == hipErrorNotReady; }
+      // a faulted walk / merge kernel surfaces as its own HIP error (PE_EHIP with the HIP string),
+      // not as the feed's "never signalled"
+      static bool busy(void* u) {
+        const hipError_t e = hipStreamQuery(static_cast<StreamIdle*>(u)->s);
+        if (e == hipErrorNotReady) return true;
+        hipchk(e, "walk window stream");
+        return false;
+      }
     } stream_idle{s};
     feed.idle = &StreamIdle::busy;
     feed.idle_user = &stream_idle;

@@ -53,7 +53,49 @@ constexpr int MG_CAP = 8192;   // merge: LDS candidate capacity per group
 constexpr int MG_THREADS = 1024;
 constexpr int MG_SEL = 1024;   // merge: keys kept after the histogram cut (sorted instead of all)
 
+// ---- PodGroup aggregation call path (pe_pg_min_resources).  The host packs the batch into
+// SEGMENTS in one pinned, device-mapped staging buffer: a segment holds up to AGG_SEG_JOBS
+// consecutive jobs with their groups and containers, offsets rebased to the segment, every
+// section 16-B aligned, so one block copies its whole segment into LDS with one round trip of
+// coalesced 16-B zero-copy reads (no DMA, no device copy of the inputs) and runs one job per lane
+// from LDS.  Outputs go straight into a pinned output buffer in the caller's layout.  A segment
+// larger than AGG_SEG_BYTES (one job with very many groups / containers) is read in place.
+constexpr int AGG_SEG_JOBS = 256;
+constexpr int64_t AGG_SEG_BYTES = 48 * 1024;
+struct AggSegHdr {
+  int64_t j0;            // first job of the segment (index in the call's batch)
+  int32_t nj, ng, nc;    // jobs, groups, containers
+  int32_t pad_[3];
+};
+static_assert(sizeof(AggSegHdr) == 32, "AggSegHdr must be 32 B");
+__host__ __device__ inline int64_t agg_r16(int64_t x) { return (x + 15) & ~int64_t(15); }
+// byte offsets of the sections in a segment: [0] jgo (nj+1 i32), [1] min_member (nj i32, V1 only),
+// [2] replicas (ng i32), [3] gco (ng+1 i32), [4] req (nc x 4 i64), [5] flags (nc u8), [6] = size
+__host__ __device__ inline void agg_seg_layout(int64_t nj, int64_t ng, int64_t nc, bool v1, int64_t off[7]) {
+  off[0] = (int64_t)sizeof(AggSegHdr);
+  off[1] = off[0] + agg_r16((nj + 1) * 4);
+  off[2] = off[1] + (v1 ? agg_r16(nj * 4) : 0);
+  off[3] = off[2] + agg_r16(ng * 4);
+  off[4] = off[3] + agg_r16((ng + 1) * 4);
+  off[5] = off[4] + nc * 32;
+  off[6] = off[5] + agg_r16(nc);
+}
+// Output buffer layout (the caller's arrays back to back): res [J][4] i64, members [J] i32,
+// present [J] u8, overflow [J] u8, each 16-B aligned.
+__host__ __device__ inline void agg_out_layout(int64_t J, int64_t off[4]) {
+  off[0] = 0;
+  off[1] = agg_r16(J * 32);
+  off[2] = off[1] + agg_r16(J * 4);
+  off[3] = off[2] + agg_r16(J);
+}
+
 // ---- launch wrappers (return hipError_t of the launch)
+// Segmented aggregation: nseg segments; segment s spans blob[seg_off[s], seg_off[s+1]) (seg_off
+// may be NULL for one segment of nbytes0 bytes at blob[0]).  out = output buffer (agg_out_layout,
+// J jobs).  flag != NULL (one segment only): after the outputs are visible system-wide, block 0
+// stores flag_val there (release, system scope) -- the host waits on it instead of the stream.
+hipError_t launch_pg_agg_segments(hipStream_t s, int mode, const uint8_t* blob, const int64_t* seg_off, int64_t nseg,
+                                  int64_t nbytes0, uint8_t* out, int64_t J, uint32_t* flag, uint32_t flag_val);
 hipError_t launch_pg_min_resources(hipStream_t s, int mode, int64_t n_jobs, const int32_t* job_group_off,
                                    const int32_t* min_member, const int32_t* group_replicas,
                                    const int32_t* group_cont_off, const int64_t* cont_req,

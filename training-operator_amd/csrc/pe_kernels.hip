@@ -29,48 +29,55 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 __device__ __forceinline__ bool add_ovf(int64_t a, int64_t b, int64_t* r) { return __builtin_add_overflow(a, b, r); }
 __device__ __forceinline__ bool mul_ovf(int64_t a, int64_t b, int64_t* r) { return __builtin_mul_overflow(a, b, r); }
 
-__global__ __launch_bounds__(256) void pg_min_resources_kernel(
-    int mode, int64_t n_jobs, const int32_t* __restrict__ job_group_off, const int32_t* __restrict__ min_member,
-    const int32_t* __restrict__ group_replicas, const int32_t* __restrict__ group_cont_off,
-    const int64_t* __restrict__ cont_req, const uint8_t* __restrict__ cont_flags, int64_t* __restrict__ out_res,
-    uint8_t* __restrict__ out_present, int32_t* __restrict__ out_members, uint8_t* __restrict__ out_overflow) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_jobs) return;
-  int64_t acc[D] = {0, 0, 0, 0};
-  uint32_t pres = 0, members = 0;
-  bool ovf = false;
-  int32_t pod_cnt = 0;
-  const int32_t mm = mode == 1 ? min_member[j] : 0;
-  for (int32_t g = job_group_off[j]; g < job_group_off[j + 1]; ++g) {
-    const int32_t r = group_replicas[g];
+// One job of CalcPGMinResources (V1) / CoScheduling.Build (V2): groups [g0, g1) of replicas rep[],
+// containers of group g [gco[g], gco[g+1]) in req[][4] / fl[].  Generic pointers: the segmented
+// kernel runs it from LDS, the device-resident kernel from global memory.
+struct AggJob {
+  int64_t acc[D];
+  uint32_t pres, members;
+  int32_t pod_cnt;
+  bool ovf;
+};
+
+__device__ __forceinline__ AggJob agg_job(int mode, int32_t mm, int32_t g0, int32_t g1, const int32_t* rep,
+                                          const int32_t* gco, const int64_t* req, const uint8_t* fl) {
+  AggJob o;
+#pragma unroll
+  for (int d = 0; d < D; ++d) o.acc[d] = 0;
+  o.pres = 0;
+  o.members = 0;
+  o.pod_cnt = 0;
+  o.ovf = false;
+  for (int32_t g = g0; g < g1; ++g) {
+    const int32_t r = rep[g];
     int64_t k;
     if (mode == 1) {                       // util.go:126-141: count pods until podCnt == minMember
       if (r <= 0) continue;                // Replicas == nil (-1) or an empty loop
-      const int64_t room = (int64_t)mm - pod_cnt;
+      const int64_t room = (int64_t)mm - o.pod_cnt;
       if (room <= 0) continue;
       k = r < room ? r : room;
-      pod_cnt += (int32_t)k;
+      o.pod_cnt += (int32_t)k;
     } else {                               // coscheduling.go:110-111: int32 members wrap like Go
-      members += (uint32_t)r;
+      o.members += (uint32_t)r;
       k = r;
     }
     int64_t side[D] = {0, 0, 0, 0}, initmax[D] = {0, 0, 0, 0}, main_[D] = {0, 0, 0, 0}, over[D] = {0, 0, 0, 0};
     uint32_t pp = 0;
-    for (int32_t c = group_cont_off[g]; c < group_cont_off[g + 1]; ++c) {
-      const uint32_t fl = cont_flags[c];
-      const uint32_t kind = (fl >> 4) & 3u;
+    for (int32_t c = gco[g]; c < gco[g + 1]; ++c) {
+      const uint32_t f = fl[c];
+      const uint32_t kind = (f >> 4) & 3u;
       if (mode == 1 && kind != 0) continue;  // v1 ignores init containers and overhead
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        if (!(fl & (1u << d))) continue;
-        const int64_t v = cont_req[(int64_t)c * D + d];
+        if (!(f & (1u << d))) continue;
+        const int64_t v = req[(int64_t)c * D + d];
         pp |= 1u << d;
-        if (kind == 0) ovf |= add_ovf(main_[d], v, &main_[d]);
-        else if (kind == 2) ovf |= add_ovf(side[d], v, &side[d]);
-        else if (kind == 3) ovf |= add_ovf(over[d], v, &over[d]);
+        if (kind == 0) o.ovf |= add_ovf(main_[d], v, &main_[d]);
+        else if (kind == 2) o.ovf |= add_ovf(side[d], v, &side[d]);
+        else if (kind == 3) o.ovf |= add_ovf(over[d], v, &over[d]);
         else {                               // kueue: init_i + sidecars declared before it
           int64_t u;
-          ovf |= add_ovf(side[d], v, &u);
+          o.ovf |= add_ovf(side[d], v, &u);
           initmax[d] = u > initmax[d] ? u : initmax[d];
         }
       }
@@ -79,19 +86,91 @@ __global__ __launch_bounds__(256) void pg_min_resources_kernel(
     for (int d = 0; d < D; ++d) {
       if (!(pp & (1u << d))) continue;
       int64_t pod, t;
-      ovf |= add_ovf(side[d], main_[d], &pod);          // v1: side/initmax/over are all 0
+      o.ovf |= add_ovf(side[d], main_[d], &pod);          // v1: side/initmax/over are all 0
       pod = initmax[d] > pod ? initmax[d] : pod;
-      ovf |= add_ovf(pod, over[d], &pod);
-      ovf |= mul_ovf(pod, k, &t);
-      ovf |= add_ovf(acc[d], t, &acc[d]);
+      o.ovf |= add_ovf(pod, over[d], &pod);
+      o.ovf |= mul_ovf(pod, k, &t);
+      o.ovf |= add_ovf(o.acc[d], t, &o.acc[d]);
     }
-    pres |= pp;
+    o.pres |= pp;
   }
+  return o;
+}
+
+__global__ __launch_bounds__(256) void pg_min_resources_kernel(
+    int mode, int64_t n_jobs, const int32_t* __restrict__ job_group_off, const int32_t* __restrict__ min_member,
+    const int32_t* __restrict__ group_replicas, const int32_t* __restrict__ group_cont_off,
+    const int64_t* __restrict__ cont_req, const uint8_t* __restrict__ cont_flags, int64_t* __restrict__ out_res,
+    uint8_t* __restrict__ out_present, int32_t* __restrict__ out_members, uint8_t* __restrict__ out_overflow) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  const AggJob o = agg_job(mode, mode == 1 ? min_member[j] : 0, job_group_off[j], job_group_off[j + 1],
+                           group_replicas, group_cont_off, cont_req, cont_flags);
 #pragma unroll
-  for (int d = 0; d < D; ++d) out_res[j * D + d] = ovf ? 0 : acc[d];   // no int64 answer: defined as 0
-  out_present[j] = (uint8_t)pres;
-  out_members[j] = mode == 1 ? pod_cnt : (int32_t)members;
-  out_overflow[j] = ovf ? 1 : 0;
+  for (int d = 0; d < D; ++d) out_res[j * D + d] = o.ovf ? 0 : o.acc[d];   // no int64 answer: defined as 0
+  out_present[j] = (uint8_t)o.pres;
+  out_members[j] = mode == 1 ? o.pod_cnt : (int32_t)o.members;
+  out_overflow[j] = o.ovf ? 1 : 0;
+}
+
+// Segmented form (pe_kernels.h AggSegHdr): block b = segment b.  The segment (<= AGG_SEG_BYTES)
+// comes into LDS with one round of coalesced 16-B loads -- from pinned host memory over PCIe, so a
+// one-job call costs one PCIe round trip for its inputs -- then lane t aggregates job t of the
+// segment from LDS and writes its outputs into the (pinned) output buffer.
+__global__ __launch_bounds__(AGG_SEG_JOBS) void pg_agg_seg_kernel(int mode, const uint8_t* __restrict__ blob,
+                                                                 const int64_t* __restrict__ seg_off, int64_t nbytes0,
+                                                                 uint8_t* __restrict__ out, int64_t J, uint32_t* flag,
+                                                                 uint32_t flag_val) {
+  __shared__ uint4 lds[AGG_SEG_BYTES / 16];
+  int64_t a = 0, e = nbytes0;
+  if (seg_off) {
+    a = seg_off[blockIdx.x];
+    e = seg_off[blockIdx.x + 1];
+  }
+  const uint8_t* seg = blob + a;
+  if (e - a <= AGG_SEG_BYTES) {   // stage in LDS (else read in place: one oversized job)
+    const uint4* src = reinterpret_cast<const uint4*>(seg);
+    const int n16 = (int)((e - a) >> 4);
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) lds[i] = src[i];
+    __syncthreads();
+    seg = reinterpret_cast<const uint8_t*>(lds);
+  }
+  const AggSegHdr h = *reinterpret_cast<const AggSegHdr*>(seg);
+  int64_t off[7];
+  agg_seg_layout(h.nj, h.ng, h.nc, mode == 1, off);
+  const int t = threadIdx.x;
+  if (t < h.nj) {
+    const int32_t* jgo = reinterpret_cast<const int32_t*>(seg + off[0]);
+    const int32_t mm = mode == 1 ? reinterpret_cast<const int32_t*>(seg + off[1])[t] : 0;
+    const AggJob o = agg_job(mode, mm, jgo[t], jgo[t + 1], reinterpret_cast<const int32_t*>(seg + off[2]),
+                             reinterpret_cast<const int32_t*>(seg + off[3]), reinterpret_cast<const int64_t*>(seg + off[4]),
+                             seg + off[5]);
+    int64_t oo[4];
+    agg_out_layout(J, oo);
+    const int64_t j = h.j0 + t;
+    int64_t* res = reinterpret_cast<int64_t*>(out + oo[0]) + j * D;
+    const int64_t z0 = o.ovf ? 0 : o.acc[0], z1 = o.ovf ? 0 : o.acc[1], z2 = o.ovf ? 0 : o.acc[2],
+                  z3 = o.ovf ? 0 : o.acc[3];
+    reinterpret_cast<longlong2*>(res)[0] = longlong2{z0, z1};   // 32 B per lane, two 16-B stores
+    reinterpret_cast<longlong2*>(res)[1] = longlong2{z2, z3};
+    reinterpret_cast<int32_t*>(out + oo[1])[j] = mode == 1 ? o.pod_cnt : (int32_t)o.members;
+    out[oo[2] + j] = (uint8_t)o.pres;
+    out[oo[3] + j] = o.ovf ? 1 : 0;
+  }
+  if (flag) {   // one-segment launch: publish the outputs, then the flag (the host spins on it)
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(flag, flag_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+hipError_t launch_pg_agg_segments(hipStream_t s, int mode, const uint8_t* blob, const int64_t* seg_off, int64_t nseg,
+                                  int64_t nbytes0, uint8_t* out, int64_t J, uint32_t* flag, uint32_t flag_val) {
+  if (nseg <= 0) return hipSuccess;
+  if (flag && nseg != 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pg_agg_seg_kernel, dim3((unsigned)nseg), dim3(AGG_SEG_JOBS), 0, s, mode, blob, seg_off, nbytes0,
+                     out, J, flag, flag_val);
+  return hipGetLastError();
 }
 
 hipError_t launch_pg_min_resources(hipStream_t s, int mode, int64_t n_jobs, const int32_t* job_group_off,

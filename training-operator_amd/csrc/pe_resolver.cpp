@@ -472,7 +472,11 @@ void SeedScorer::compute(const DirtySet& seeds, const GroupCands& gc, const int6
 SeedScorer::~SeedScorer() {
   if (!th_) return;
   stop();
-  state_.store(3, std::memory_order_release);
+  state_.store(3, std::memory_order_seq_cst);
+  {
+    std::lock_guard<std::mutex> lk(park_mu_);
+    park_cv_.notify_one();
+  }
   th_->join();
 }
 
@@ -495,36 +499,59 @@ void SeedScorer::start(const DirtySet* seeds, const std::vector<int32_t>* groups
     gen_ = 1;
   }
   main_wi_.store(0, std::memory_order_relaxed);
-  busy_.store(true, std::memory_order_relaxed);
   if (!th_) {
     th_.reset(new std::thread([this] { loop(); }));
     // The resolver and the helper exchange a few cache lines per group (flags, tops): keep the
     // helper on the CPUs that share the resolver thread's L3 (one CCD), not across the machine.
+#ifndef PE_SEED_TEST_YIELD   // (the handshake test keeps both threads on one CPU)
     cpu_set_t set;
     if (l3_cpus(sched_getcpu(), &set)) (void)pthread_setaffinity_np(th_->native_handle(), sizeof(set), &set);
+#endif
   }
-  state_.store(1, std::memory_order_release);
+  // seq_cst with the helper's parked_ store and predicate load: either it sees 1 before sleeping
+  // or this sees parked_ and wakes it (no lost wake-up)
+  state_.store(1, std::memory_order_seq_cst);
+  if (parked_.load(std::memory_order_seq_cst)) {   // the helper sleeps (long idle): wake it
+    std::lock_guard<std::mutex> lk(park_mu_);
+    park_cv_.notify_one();
+  }
 }
 
+// Handshake (no separate busy flag): stop() moves 1 -> 2 and waits for 0; only the helper moves
+// 2 -> 0, with a CAS, once it has left the window (or never entered it).  A stale read of 2 by the
+// helper cannot acknowledge a later window: the CAS fails on the 1 that start() stored.
 void SeedScorer::stop() {
   if (!th_) return;
   int posted = 1;
-  state_.compare_exchange_strong(posted, 2, std::memory_order_acq_rel);
-  for (int spin = 0; busy_.load(std::memory_order_acquire); ++spin)   // at most one group's work
+  if (!state_.compare_exchange_strong(posted, 2, std::memory_order_acq_rel)) return;   // nothing posted
+  for (int spin = 0; state_.load(std::memory_order_acquire) != 0; ++spin)   // at most one group's work
     if (spin < 4096) _mm_pause();
     else std::this_thread::yield();   // the helper is not running (oversubscribed host)
-  state_.store(0, std::memory_order_release);
 }
 
 void SeedScorer::loop() {
   int idle = 0;
   for (;;) {
     const int st = state_.load(std::memory_order_acquire);
+#ifdef PE_SEED_TEST_YIELD   // tests/cpp/test_feed.cc: widen the gap between reading the state and acting on it
+    std::this_thread::yield();
+#endif
     if (st == 3) return;
+    if (st == 2) {   // cancel seen (window done or never started): acknowledge
+      int c = 2;
+      state_.compare_exchange_strong(c, 0, std::memory_order_acq_rel);
+      continue;
+    }
     if (st != 1) {
-      if (busy_.load(std::memory_order_relaxed) && st == 2) busy_.store(false, std::memory_order_release);
       if (++idle < 4096) _mm_pause();
-      else std::this_thread::yield();   // long idle: let others run
+      else if (idle < kParkAfter) std::this_thread::yield();   // idle: let others run
+      else {   // long idle (e.g. a pe_resolver between ABI calls): sleep until start() or exit
+        std::unique_lock<std::mutex> lk(park_mu_);
+        parked_.store(true, std::memory_order_seq_cst);
+        park_cv_.wait_for(lk, std::chrono::milliseconds(20),
+                          [this] { return state_.load(std::memory_order_seq_cst) != 0; });
+        parked_.store(false, std::memory_order_relaxed);
+      }
       continue;
     }
     idle = 0;
@@ -551,6 +578,9 @@ void SeedScorer::loop() {
         }
         if (!go) break;
       }
+#ifdef PE_SEED_TEST_YIELD
+      std::this_thread::yield();
+#endif
       const int32_t g = (*groups_)[wi];
       try {
         compute(*seeds_, (*cands_)[wi], req_ + (int64_t)g * RD, need_[g], slots_[wi].top, out_, idx_);
@@ -559,11 +589,10 @@ void SeedScorer::loop() {
       }
       slots_[wi].gen.store(gen, std::memory_order_release);
     }
-    // done with the window: wait for stop() (state 2) before going idle
+    // done with the window: wait for stop() (state 2, acknowledged at the top of the loop)
     for (int spin = 0; state_.load(std::memory_order_acquire) == 1; ++spin)
       if (spin < 4096) _mm_pause();
       else std::this_thread::yield();
-    busy_.store(false, std::memory_order_release);
   }
 }
 

@@ -15,6 +15,8 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <memory>
 #include <thread>
 #include <unordered_map>
@@ -305,7 +307,11 @@ class SeedScorer {
   size_t cap_ = 0;
   uint32_t gen_ = 0;                                  // window generation (written before posting)
   std::atomic<size_t> main_wi_{0};
-  std::atomic<bool> busy_{false};
+  // long idle: the helper sleeps on park_cv_ (parked_ set) instead of spinning a core between calls
+  static constexpr int kParkAfter = 1 << 16;
+  std::atomic<bool> parked_{false};
+  std::mutex park_mu_;
+  std::condition_variable park_cv_;
   const DirtySet* seeds_ = nullptr;
   const std::vector<int32_t>* groups_ = nullptr;
   const std::vector<GroupCands>* cands_ = nullptr;
