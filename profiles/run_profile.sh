@@ -21,5 +21,15 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_
   -d $OUT/sq -o sq --output-format csv -- python3 bench.py $BENCH_SMALL "$@" > $OUT/bench_sq.json 2> $OUT/sq.err
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INST_CYCLES_SALU SQ_INSTS_SMEM SQ_BUSY_CU_CYCLES SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_INT32 \
   -d $OUT/sq2 -o sq2 --output-format csv -- python3 bench.py $BENCH_SMALL "$@" > $OUT/bench_sq2.json 2> $OUT/sq2.err
+# greedy walk kernel without the bench's hipEvent passes: warm (as the bench runs) and cold (a 512 MiB
+# buffer rewritten before every walk launch, PE_WALK_FLUSH)
+GREEDY_ONLY="--steps 2 --warmup 1 --no-configs --no-cpu-baseline --no-walk-passes"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/walk_warm -o walk --output-format csv -- \
+  python3 bench.py $GREEDY_ONLY "$@" > $OUT/bench_walk_warm.json 2> $OUT/walk_warm.err
+PE_WALK_FLUSH=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/walk_cold -o walk --output-format csv -- \
+  python3 bench.py $GREEDY_ONLY "$@" > $OUT/bench_walk_cold.json 2> $OUT/walk_cold.err
+# aggregation: the 1M-job call alone
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/agg -o agg --output-format csv -- \
+  python3 tools/agg_calls.py > $OUT/agg.out 2> $OUT/agg.err
 python3 profiles/summarize.py $OUT > $OUT/summary.json
 echo "profile $TAG done"

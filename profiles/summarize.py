@@ -26,10 +26,19 @@ def kname(name: str) -> str:
 def main(d):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = {"source_hash": source_hash(root), "kernels": {}, "pmc": collections.defaultdict(dict)}
-    for f in glob.glob(os.path.join(d, "trace", "*kernel_stats.csv")):
+    for f in glob.glob(os.path.join(d, "trace", "*kernel_stats.csv")):   # the full bench
         for r in csv.DictReader(open(f)):
             out["kernels"][kname(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                                        "total_ns": float(r["TotalDurationNs"])}
+    # the greedy walk passes (warm / cold) and the aggregation pass: their kernel stats apart
+    for sub, key in (("walk_warm", ("greedy", "warm")), ("walk_cold", ("greedy", "cold")), ("agg", ("aggregation", None))):
+        for f in glob.glob(os.path.join(d, sub, "*kernel_stats.csv")):
+            stats = {kname(r["Name"]): {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                        "total_ns": float(r["TotalDurationNs"])} for r in csv.DictReader(open(f))}
+            if key[1]:
+                out.setdefault(key[0], {})[key[1]] = stats
+            else:
+                out[key[0]] = stats
     for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
         acc = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):

@@ -159,6 +159,35 @@ void ncclchk(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) raise(PE_ERCCL, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
+// The communicator is NON-BLOCKING (ncclConfig_t.blocking = 0), so that a rank whose peers never
+// arrive (a wrong comm_id, a dead peer) gets PE_ERCCL after a bounded wait instead of hanging in
+// ncclCommInitRank.  Every RCCL call on it may return ncclInProgress: wait for its completion here
+// (ncclCommGetAsyncError), at most timeout_ms (< 0: no limit).  Returns the final state.
+ncclResult_t nccl_settle(ncclComm_t comm, ncclResult_t r, double timeout_ms) {
+  if (r != ncclInProgress) return r;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spin = 0;; ++spin) {
+    ncclResult_t st = ncclSuccess;
+    const ncclResult_t q = ncclCommGetAsyncError(comm, &st);
+    if (q != ncclSuccess) return q;
+    if (st != ncclInProgress) return st;
+    if (timeout_ms >= 0 &&
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > timeout_ms)
+      return ncclInProgress;
+    if (spin < 1024) _mm_pause();
+    else std::this_thread::yield();
+  }
+}
+
+void nccl_call(ncclComm_t comm, ncclResult_t r, const char* what) { ncclchk(nccl_settle(comm, r, -1.0), what); }
+
+// Bound of the communicator set-up: PE_RCCL_INIT_TIMEOUT_S seconds (default 120).
+double rccl_init_timeout_ms() {
+  const char* e = std::getenv("PE_RCCL_INIT_TIMEOUT_S");
+  const double s = e ? std::atof(e) : 120.0;
+  return (s > 0 ? s : 120.0) * 1e3;
+}
+
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // pe_config.fit_path_mask bits
@@ -208,7 +237,7 @@ struct pe_ctx {
   DevBuf<pe::LdsSpec> lds_spec_d;
   DevBuf<int64_t> lds_vals;
   DevBuf<uint16_t> lds_codes;
-  DevBuf<uint32_t> lds_ranks, lds_aux;
+  DevBuf<uint32_t> lds_ranks, lds_aux, lds_slots;   // lds_slots: the fit kernel's per-job u32 count slots
   int num_cu = 256;
   int fit_path_mask = PATHS_ALL;   // allowed paths (pe_config.fit_path_mask)
   pe::PlaneSpec plane{};
@@ -273,6 +302,7 @@ struct pe_ctx {
   DevBuf<int64_t> w_ovres;
   DevBuf<int32_t> w_ovl, w_ovln;
   DevBuf<uint8_t> w_temp;
+  DevBuf<uint32_t> w_flush;   // PE_WALK_FLUSH: 512 MiB rewritten before each walk (cold-cache diagnostics)
   DevBuf<unsigned long long> w_stat;   // walk counters of the current pe_place_greedy (rounds, overlay)
   pe_stats stats{};
 
@@ -283,7 +313,7 @@ struct pe_ctx {
     fit_jobs.release(); fit_jobs32.release(); res32.release(); mask.release();
     code_vals.release(); code_needs.release(); code_jobs.release(); code_x.release(); counts.release(); h_counts.release();
     planes.release(); plane_jobs.release();
-    lds_spec_d.release(); lds_vals.release(); lds_codes.release(); lds_ranks.release(); lds_aux.release();
+    lds_spec_d.release(); lds_vals.release(); lds_codes.release(); lds_ranks.release(); lds_aux.release(); lds_slots.release();
     a_stage.release(); a_outh.release(); a_segoff.release(); a_flag.release();
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
@@ -296,8 +326,11 @@ struct pe_ctx {
     }
     w_sk.release(); w_kin.release(); w_rmin.release(); w_sr.release(); w_rmax.release(); w_sl.release(); w_pos.release();
     w_ror.release(); w_inovl.release(); w_ovl.release(); w_ovln.release(); w_temp.release();
-    w_ovidx.release(); w_ovlab.release(); w_ovres.release(); w_stat.release();
-    if (comm) (void)ncclCommDestroy(comm);
+    w_ovidx.release(); w_ovlab.release(); w_ovres.release(); w_stat.release(); w_flush.release();
+    if (comm) {
+      (void)nccl_settle(comm, ncclInProgress, 10000.0);   // let a pending operation finish (non-blocking comm)
+      (void)ncclCommDestroy(comm);
+    }
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -552,7 +585,18 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
       if (!cfg->comm_id) raise(PE_EINVAL, "world_size > 1 needs comm_id or an exchange callback");
       ncclUniqueId id;
       std::memcpy(&id, cfg->comm_id, sizeof(id));
-      ncclchk(ncclCommInitRank(&ctx->comm, ctx->world, id, ctx->rank), "ncclCommInitRank");
+      ncclConfig_t conf = NCCL_CONFIG_INITIALIZER;
+      conf.blocking = 0;   // bounded set-up (nccl_settle)
+      ncclResult_t r = ncclCommInitRankConfig(&ctx->comm, ctx->world, id, ctx->rank, &conf);
+      if (ctx->comm) r = nccl_settle(ctx->comm, r, rccl_init_timeout_ms());
+      if (r != ncclSuccess) {
+        if (ctx->comm) (void)ncclCommAbort(ctx->comm);
+        ctx->comm = nullptr;
+        if (r == ncclInProgress)
+          raise(PE_ERCCL, "ncclCommInitRank: the " + std::to_string(ctx->world) + " ranks did not meet within " +
+                              std::to_string((int)(rccl_init_timeout_ms() / 1e3)) + " s (PE_RCCL_INIT_TIMEOUT_S)");
+        ncclchk(r, "ncclCommInitRank");
+      }
     }
   } catch (const PeError& e) {
     rc = e.code;
@@ -718,7 +762,7 @@ int pe_comm_ranks(const pe_ctx* ctx, int32_t* nranks) {
   *nranks = 0;
   if (!ctx->comm) return PE_OK;
   int n = 0;
-  if (ncclCommCount(ctx->comm, &n) != ncclSuccess) return PE_ERCCL;
+  if (nccl_settle(ctx->comm, ncclCommCount(ctx->comm, &n), -1.0) != ncclSuccess) return PE_ERCCL;
   *nranks = n;
   return PE_OK;
 }
@@ -1492,6 +1536,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   ctx->lds_nblk = nblk;
   ctx->lds_R = R;
   ctx->lds_Tpad = Tpad;
+  hipchk(ctx->lds_slots.ensure((size_t)R * 16 * Tpad), "alloc count slots");
   ctx->lds_npad = nblk * S;
   ctx->lds_pitch = nblk * S / 64;
   hipchk(ctx->lds_spec_d.ensure(1), "alloc lds spec");
@@ -1579,7 +1624,7 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
       hipchk(hipStreamSynchronize(ctx->stream), "sync fit jobs");
     }
   }
-  const size_t mask_words = ctx->fit_path == 4   ? (size_t)(n_jobs + 1) * ctx->lds_pitch   // + the scratch row
+  const size_t mask_words = ctx->fit_path == 4   ? (size_t)std::max<int64_t>(n_jobs, 1) * ctx->lds_pitch
                             : ctx->fit_path == 3 ? (size_t)std::max<int64_t>(n_jobs, 1) *
                                                        (ctx->pl_rows ? ctx->pl_pitch : ctx->pl_nblk) * 128
                             : ctx->fit_path == 2 ? (size_t)(ctx->code_Jp / 64) * ctx->node_stride
@@ -1604,6 +1649,8 @@ static void fit_run(pe_ctx* ctx) {
   int64_t tpw = (ctx->Ns + 256 * want_x - 1) / (256 * want_x);
   tpw = std::min<int64_t>(16, std::max<int64_t>(1, tpw));
   if (ctx->fit_path == 4) {
+    hipchk(hipMemsetAsync(ctx->lds_slots.p, 0, (size_t)ctx->lds_R * 16 * ctx->lds_Tpad * 4, ctx->stream),
+           "memset count slots");
     hipchk(pe::launch_node_ranks(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->lds_npad,
                                  ctx->lds_spec_d.p, ctx->lds_vals.p, ctx->lds_ranks.p, ctx->lds_aux.p),
            "launch node_ranks");
@@ -1611,8 +1658,10 @@ static void fit_run(pe_ctx* ctx) {
                                    ctx->lds_ranks.p,
                                    ctx->lds_npad, ctx->lds_aux.p, ctx->lds_nblk, ctx->lds_codes.p, J,
                                    ctx->lds_R, ctx->lds_Tpad, ctx->lds_pitch * 8,
-                                   reinterpret_cast<uint8_t*>(ctx->mask.p), ctx->counts.p),
+                                   reinterpret_cast<uint8_t*>(ctx->mask.p), ctx->lds_slots.p),
            "launch fit_mask_lds");
+    hipchk(pe::launch_lds_counts(ctx->stream, ctx->lds_slots.p, J, ctx->lds_R, ctx->lds_Tpad, ctx->counts.p),
+           "launch lds_counts");
     ctx->stats.fit_runs_lds += 1;
   } else if (ctx->fit_path == 3) {
     // ~16k waves: every 8192-node block times enough job ranges, at least 64 jobs per wave
@@ -1970,6 +2019,12 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // PE_WALK_EVENTS=1: hipEvents around every walk launch, summed into stats.walk_ms (diagnostics:
     // the greedy roofline of bench.py; the events cost a few us of host time per window)
     const bool wev = walk && std::getenv("PE_WALK_EVENTS") != nullptr;
+    // PE_WALK_FLUSH=1 (diagnostics, with PE_WALK_EVENTS: the COLD-cache greedy roofline): before every
+    // walk launch a 512 MiB device buffer is rewritten, evicting the walk index (sorted keys, residual
+    // copy, round summaries: ~50 MB at 1M nodes) from L2 and the 256 MiB Infinity Cache, so the walk
+    // reads come from HBM.  The fill is outside the walk's events.
+    const bool wflush = walk && std::getenv("PE_WALK_FLUSH") != nullptr;
+    if (wflush) hipchk(ctx->w_flush.ensure((size_t)512 << 20), "alloc flush buffer");
     std::vector<std::pair<hipEvent_t, hipEvent_t>> walk_events;
     struct EventsFree {
       std::vector<std::pair<hipEvent_t, hipEvent_t>>& v;
@@ -2083,6 +2138,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (walk) {   // one 64-B request per block: read from pinned host memory, no H2D copy
         if (ctx->w_est > ctx->resort_nodes) walk_resort(ctx);
         std::pair<hipEvent_t, hipEvent_t> evp{nullptr, nullptr};
+        if (wflush) hipchk(hipMemsetD32Async((hipDeviceptr_t)ctx->w_flush.p, ctx->walk_gen, (size_t)128 << 20, s), "flush");
         if (wev) {
           hipchk(hipEventCreate(&evp.first), "event");
           hipchk(hipEventCreate(&evp.second), "event");
@@ -2121,7 +2177,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       } else if (use_exchange) {
         hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
       } else {
-        ncclchk(ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
+        nccl_call(ctx->comm, ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
         if (dev_merge)
           hipchk(pe::launch_merge_shards(s, ctx->g_gath.p, ctx->world, Wg, K, outbufdev(b), gen), "launch merge_shards");
         else

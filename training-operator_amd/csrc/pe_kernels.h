@@ -234,13 +234,16 @@ hipError_t launch_node_ranks(hipStream_t s, const int64_t* res, int64_t stride, 
 // workgroups, wave w of workgroup (blk, r) takes jobs j = r + R (w + 16 t).  codes: LD_CODE u16 per
 // job, job j's at position (r * 16 + w) * Tpad + t (Tpad >= the longest run, a multiple of 16).
 // Mask row-major (PE_MASK_ROWS): row j at mask + j * pitch_bytes, block blk's S/8 bytes at + blk * S/8.
-// counts: [J], per job (zeroed by the caller).  spec: device copy; nplanes = spec->nplanes.
-// shape = {N3, N2, N1}: fields 0 .. N3-1 have 3 digit levels, the next N2 two, the last N1 one.
-// The mask needs J + 1 rows: row J is the scratch row of the last, partial 16-job batches.
+// slots: [R * 16 * Tpad] u32 count slots (zeroed by the caller), job j = r + R (w + 16 t) in slot
+// (r * 16 + w) * Tpad + t; launch_lds_counts turns them into per-job u64 counts.  spec: device copy;
+// nplanes = spec->nplanes.  shape = {N3, N2, N1}: fields 0 .. N3-1 have 3 digit levels, the next N2
+// two, the last N1 one.  The mask has J rows.
 hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[3], const LdsSpec* spec, int nplanes,
                                const uint32_t* ranks, int64_t npad, const uint32_t* aux, int64_t nblk,
                                const uint16_t* codes, int64_t J, int64_t R, int64_t Tpad, int64_t pitch_bytes,
-                               uint8_t* mask, unsigned long long* counts);
+                               uint8_t* mask, uint32_t* slots);
+hipError_t launch_lds_counts(hipStream_t s, const uint32_t* slots, int64_t J, int64_t R, int64_t Tpad,
+                             unsigned long long* counts);
 
 // kn / lo: the node-only score terms of prep_nodes (K(n) = (S(n) << 24) | gid, lo20(r1), lo24(r3)),
 // kept current by apply; see pe_kernels.hip node_prep for the exactness argument.

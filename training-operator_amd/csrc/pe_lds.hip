@@ -56,7 +56,7 @@ hipError_t launch_node_ranks(hipStream_t s, const int64_t* res, int64_t stride, 
 hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[3], const LdsSpec* spec, int nplanes,
                                const uint32_t* ranks, int64_t npad, const uint32_t* aux, int64_t nblk,
                                const uint16_t* codes, int64_t J, int64_t R, int64_t Tpad, int64_t pitch_bytes,
-                               uint8_t* mask, unsigned long long* counts) {
+                               uint8_t* mask, uint32_t* slots) {
   if (J <= 0 || nblk <= 0 || R <= 0) return hipSuccess;
   const size_t lds = (size_t)nplanes * 2048 * W / 8;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
@@ -69,9 +69,26 @@ hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[3], const L
   if (e != hipSuccess) return e;
   const uint2* c = reinterpret_cast<const uint2*>(codes);
   void* args[] = {(void*)&spec, (void*)&ranks, (void*)&npad, (void*)&aux,         (void*)&nblk,   (void*)&c,
-                  (void*)&J,    (void*)&R,     (void*)&Tpad, (void*)&pitch_bytes, (void*)&mask,   (void*)&counts};
+                  (void*)&J,    (void*)&R,     (void*)&Tpad, (void*)&pitch_bytes, (void*)&mask,   (void*)&slots};
   e = hipLaunchKernel(fn, dim3((unsigned)(nblk * R)), dim3(LD_THREADS), args, lds, s);
   if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+// Per-job counts from the fit kernel's count slots: job j = r + R (w + 16 t) sits in slot
+// (r * 16 + w) * Tpad + t (the t-major run of wave w of phase r).
+__global__ __launch_bounds__(256) void lds_counts_kernel(const uint32_t* __restrict__ slots, int64_t J, int64_t R,
+                                                         int64_t Tpad, unsigned long long* __restrict__ counts) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= J) return;
+  const int64_t r = j % R, q = j / R;
+  counts[j] = slots[(r * 16 + q % 16) * Tpad + q / 16];
+}
+
+hipError_t launch_lds_counts(hipStream_t s, const uint32_t* slots, int64_t J, int64_t R, int64_t Tpad,
+                             unsigned long long* counts) {
+  if (J <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lds_counts_kernel, dim3((unsigned)((J + 255) / 256)), dim3(256), 0, s, slots, J, R, Tpad, counts);
   return hipGetLastError();
 }
 

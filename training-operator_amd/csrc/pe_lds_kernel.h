@@ -34,8 +34,11 @@ __device__ __forceinline__ typename LdVec<W>::T plane_rd(const uint32_t* lds, ui
 //     need planes by wave ballots (label test AND the folded dimensions);
 //  3. waves stream jobs r + R (w + 16 t): per job the need plane AND, per field, the last level's
 //     plane, then GE_k(c + 1) | (GE_k(c) & acc) per higher level; the slice is stored, its popcount
-//     joins a 16-job batch that one column sum (reduce16x64) turns into 16 per-job atomics.  A batch
-//     is always 16 jobs: past the wave's last job the slices go to the scratch row J.
+//     joins a 16-job batch that one column sum (reduce16x64) turns into 16 per-job counts, added by ONE
+//     atomic instruction into 16 CONSECUTIVE u32 count slots (the wave's t-major run, like its codes:
+//     one 64-B request per batch instead of 16 scattered 8-B atomics -- at W = 1 those were ~12 % of
+//     the kernel's HBM traffic); lds_counts_kernel maps the slots back to jobs.  Past the wave's last
+//     job the batch's slices are not stored (uniform branch).
 template <int W, int N3, int N2, int N1>
 __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec* __restrict__ spp,
                                                                   const uint32_t* __restrict__ ranks, int64_t npad,
@@ -43,7 +46,7 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
                                                                   const uint2* __restrict__ codes, int64_t J,
                                                                   int64_t R, int64_t Tpad, int64_t pitch_bytes,
                                                                   uint8_t* __restrict__ mask,
-                                                                  unsigned long long* __restrict__ counts) {
+                                                                  uint32_t* __restrict__ slots) {
   typedef typename LdVec<W>::T V;
   constexpr int S = 2048 * W;                 // nodes per block
   constexpr int WPP = S / 32;                 // u32 words per plane
@@ -106,6 +109,7 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
   const int64_t T = j0 < J ? (J - j0 + step - 1) / step : 0;
   uint8_t* const col = mask + blk * (S / 8) + lane * (4 * W);
   const uint2* const cb = codes + (r * 16 + wave) * Tpad * (LD_CODE / 4);
+  uint32_t* const sl = slots + (r * 16 + wave) * Tpad;
   uint32_t sigma;
   {
     uint32_t probe[16];
@@ -121,7 +125,7 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
     uint32_t p[16];
 #pragma unroll
     for (int K = 0; K < 16; ++K) {
-      const int64_t j = K < n ? j0 + step * (t0 + K) : J;           // past the run: the scratch row
+      const int64_t j = j0 + step * (t0 + K);
       auto entry = [&](int e) -> uint32_t {                           // u16 entry e of job K
         const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)((e & 2) ? cur.y : cur.x), 4 * K + e / 4);
         return (e & 1) ? d >> 16 : d & 0xFFFFu;
@@ -147,12 +151,11 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
       }
 #pragma unroll
       for (int fi = N3 + N2; fi < N3 + N2 + N1; ++fi) f &= plane_rd<W>(lds, entry(3 * fi), lane);
-      *reinterpret_cast<V*>(col + j * pitch_bytes) = f;
+      if (K < n) *reinterpret_cast<V*>(col + j * pitch_bytes) = f;   // n is wave-uniform
       p[K] = popc_vec<W>(f);
     }
     const uint32_t F = reduce16x64(p, lane);
-    if ((lane & 3) == 0 && sigma < (uint32_t)n && F)
-      atomicAdd(&counts[j0 + step * (t0 + sigma)], (unsigned long long)F);
+    if ((lane & 3) == 0 && sigma < (uint32_t)n && F) atomicAdd(&sl[t0 + sigma], F);
   }
 }
 
