@@ -85,6 +85,11 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def progress(msg: str):
+    """One line on stderr per bench stage (a long GPU run stays visibly alive)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -440,6 +445,7 @@ def main(argv=None):
         wall = allmax(t1 - t0)        # from the common start to the last rank's finish
         return wall, ev.elapsed_ms(e0, e1) / steps, fit_path_of(eng.stats(), st0, blocks), feas
 
+    progress("fit headline")
     elapsed, kern_ms, fit_path, feasible = time_fit(req, need, args.steps, args.warmup, "headline")
     value = float(N) * J * args.steps / elapsed
     alg = fit_bytes(Ns, J)
@@ -522,6 +528,7 @@ def main(argv=None):
         areq, aneed = synth.make_fit_jobs_worst(J, synth.SEED["cfg5"], (0, 1, 3))
         cases.append(("fit_adversarial", "cfg5 batch, cpu, memory and ephemeral each unique per job", areq, aneed))
         for key, what, rq, nd in cases:
+            progress(key)
             wt, wms, wpath, wfeas = time_fit(rq, nd, max(2, args.steps // 2), 1, key)
             pairs = {f"distinct_{n}": int(len(np.unique(rq[:, d]))) for d, n in enumerate(("cpu", "mem", "gpu", "eph"))}
             out[key] = {"workload": what, **pairs, "kernel_ms": wms, "ms_per_step": wt / max(2, args.steps // 2) * 1e3,
@@ -537,6 +544,7 @@ def main(argv=None):
         # J = 1 / 16 / 256 is the figure that decides whether the drop-in beats the code it replaces;
         # the 1M-job batch is the throughput line.  Jobs are independent: at N > 1 every rank
         # aggregates its contiguous slice of the batch.
+        progress("aggregation")
         agg = synth.make_pg_batch(args.agg_jobs, synth.SEED["cfg3"])
         lat = {}
         call0 = eng.lib.pe_abi_version
@@ -606,6 +614,7 @@ def main(argv=None):
                     "ms_per_call = max over ranks"}
 
     if not args.no_greedy:
+        progress("greedy")
         batch = synth.make_jobs(args.greedy_jobs, synth.SEED["cfg3"], "mixed")
         eng.reset_residuals()
         eng.place_batch(batch)                      # warm-up pass (allocations, code paths)
@@ -691,6 +700,7 @@ def main(argv=None):
                  "x 8/M GPUs co-located on one node; 1/4 multi-node gangs of 2-4 whole-node pods), all-or-nothing"),
                 ("cfg4_gang8", "gang8", 100_000, 10_000, 1.0,
                  "100k 8-GPU nodes x 10k gangs of 1-16 whole-node pods x 8 GPUs, label-constrained, all-or-nothing")):
+            progress(cfg)
             cinv = synth.make_inventory(n_nodes, synth.SEED[cfg[:4]], gpu_frac)
             cb = synth.make_jobs(n_jobs, synth.SEED[cfg[:4]], mix)
             ce = Engine(device, rank=rank, world_size=world, comm=new_comm(), exchange=exchange, max_nodes=n_nodes,
@@ -719,6 +729,7 @@ def main(argv=None):
             ce.close()
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("cpu baseline")
         import oracle
         from placement import Resolver
         nthreads = cpu_share()

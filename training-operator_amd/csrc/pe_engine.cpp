@@ -25,6 +25,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <numeric>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -195,6 +196,13 @@ constexpr int PATH_I64 = 1, PATH_I32 = 2, PATH_CODED = 4, PATH_NO_THERM = 8, PAT
               PATH_LDS = 64;
 constexpr int PATHS_ALL = PATH_I64 | PATH_I32 | PATH_CODED | PATH_PLANES | PATH_LDS;
 
+// One segment of the packed aggregation batch (pe_kernels.h AggSegHdr).
+struct AggSeg {
+  int64_t j0;
+  int32_t nj, ng, nc;
+  int64_t bytes;
+};
+
 }  // namespace
 
 struct pe_ctx {
@@ -238,6 +246,7 @@ struct pe_ctx {
   DevBuf<int64_t> lds_vals;
   DevBuf<uint16_t> lds_codes;
   DevBuf<uint32_t> lds_ranks, lds_aux, lds_slots;   // lds_slots: the fit kernel's per-job u32 count slots
+  DevBuf<uint32_t> lds_rows;                         // the job (mask row) of each count slot, ~0 = none
   int num_cu = 256;
   int fit_path_mask = PATHS_ALL;   // allowed paths (pe_config.fit_path_mask)
   pe::PlaneSpec plane{};
@@ -272,6 +281,8 @@ struct pe_ctx {
   HostBuf<int64_t> a_segoff;
   HostBuf<uint32_t> a_flag;
   uint32_t agg_gen = 0;
+  std::vector<std::vector<AggSeg>> agg_segs;   // per planning range, reused across calls (no allocation per call)
+  std::vector<AggSeg> agg_all;                 // all segments in order
   DevBuf<int32_t> a_jgo, a_mm, a_rep, a_gco, a_mem;
   DevBuf<int64_t> a_req, a_out;
   DevBuf<uint8_t> a_fl, a_pres, a_ovf;
@@ -313,7 +324,7 @@ struct pe_ctx {
     fit_jobs.release(); fit_jobs32.release(); res32.release(); mask.release();
     code_vals.release(); code_needs.release(); code_jobs.release(); code_x.release(); counts.release(); h_counts.release();
     planes.release(); plane_jobs.release();
-    lds_spec_d.release(); lds_vals.release(); lds_codes.release(); lds_ranks.release(); lds_aux.release(); lds_slots.release();
+    lds_spec_d.release(); lds_vals.release(); lds_codes.release(); lds_ranks.release(); lds_aux.release(); lds_slots.release(); lds_rows.release();
     a_stage.release(); a_outh.release(); a_segoff.release(); a_flag.release();
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
@@ -590,7 +601,10 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
       ncclResult_t r = ncclCommInitRankConfig(&ctx->comm, ctx->world, id, ctx->rank, &conf);
       if (ctx->comm) r = nccl_settle(ctx->comm, r, rccl_init_timeout_ms());
       if (r != ncclSuccess) {
-        if (ctx->comm) (void)ncclCommAbort(ctx->comm);
+        // a set-up that never completed is left behind, not aborted: ncclCommAbort joins the
+        // bootstrap, which waits for the missing peers without a timeout of its own
+        // (PE_RCCL_TIMEOUT_ABORT=1 aborts it anyway)
+        if (ctx->comm && (r != ncclInProgress || std::getenv("PE_RCCL_TIMEOUT_ABORT"))) (void)ncclCommAbort(ctx->comm);
         ctx->comm = nullptr;
         if (r == ncclInProgress)
           raise(PE_ERCCL, "ncclCommInitRank: the " + std::to_string(ctx->world) + " ranks did not meet within " +
@@ -784,13 +798,6 @@ int pe_read_residuals(pe_ctx* ctx, int64_t* res_out) {
 
 namespace {
 
-// One segment of the packed aggregation batch (pe_kernels.h AggSegHdr).
-struct AggSeg {
-  int64_t j0;
-  int32_t nj, ng, nc;
-  int64_t bytes;
-};
-
 // Wait for the one-segment aggregation kernel's flag (pinned host memory, written after its outputs).
 // The stream is polled now and then: a faulted kernel surfaces as its HIP error, a kernel that ended
 // without the flag as PE_EHIP.
@@ -896,11 +903,12 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       const int32_t* gco = G > 0 ? group_cont_off : nullptr;
       // 1. segments, per job range (one range below 32k jobs; segments never span ranges)
       const int T = n_jobs < 32768 ? 1 : 8;
-      std::vector<std::vector<AggSeg>> segs((size_t)T);
+      auto& segs = ctx->agg_segs;
+      if (segs.size() < (size_t)T) segs.resize((size_t)T);
       auto plan = [&](int t) {
         const int64_t ja = n_jobs * t / T, jb = n_jobs * (t + 1) / T;
         auto& out = segs[(size_t)t];
-        out.reserve((size_t)((jb - ja) / pe::AGG_SEG_JOBS + 1));
+        out.clear();
         int64_t off[7];
         for (int64_t j = ja; j < jb;) {
           AggSeg sg{j, 0, 0, 0, 0};
@@ -920,7 +928,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       };
       if (T == 1) plan(0);
       else PlanPool::get().run(T, plan);
-      std::vector<size_t> first((size_t)T + 1, 0);
+      size_t first[9] = {0};
       for (int t = 0; t < T; ++t) first[t + 1] = first[t] + segs[t].size();
       const int64_t nseg = (int64_t)first[T];
       ensure_pinned(ctx->a_segoff, (size_t)nseg + 1, "alloc pinned segment offsets");
@@ -935,12 +943,16 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       ensure_pinned(ctx->a_stage, (size_t)total, "alloc pinned aggregation batch");
       ensure_pinned(ctx->a_outh, (size_t)out_bytes, "alloc pinned aggregation outputs");
       if (!ctx->a_flag.p) hipchk(ctx->a_flag.ensure(16, kZeroCopy), "alloc pinned flag");
-      // 2. pack (and the negative-request check, on the copied values)
-      std::vector<int64_t> bad((size_t)T, INT64_MAX);
-      auto pack = [&](int t) {
-        size_t k = first[t];
-        for (const AggSeg& sg : segs[t]) {
-          uint8_t* b = ctx->a_stage.p + so[k++];
+      // 2. pack (and the negative-request check, on the copied values); 3. launch
+      auto& all = ctx->agg_all;
+      all.clear();
+      for (int t = 0; t < T; ++t) all.insert(all.end(), segs[t].begin(), segs[t].end());
+      int64_t bad[8];
+      std::fill(bad, bad + 8, INT64_MAX);
+      auto pack = [&](int64_t s0, int64_t s1, int64_t& badv) {
+        for (int64_t k = s0; k < s1; ++k) {
+          const AggSeg& sg = all[(size_t)k];
+          uint8_t* b = ctx->a_stage.p + so[k];
           pe::AggSegHdr h{};
           h.j0 = sg.j0;
           h.nj = sg.nj;
@@ -965,10 +977,10 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
               std::memcpy(b + off[5], cont_flags + c0, (size_t)sg.nc);
               int64_t any = 0;
               for (int64_t i = 0; i < nq; ++i) any |= q[i];
-              if (any < 0 && bad[t] == INT64_MAX)
+              if (any < 0 && badv == INT64_MAX)
                 for (int64_t i = 0; i < nq; ++i)
                   if (q[i] < 0) {
-                    bad[t] = (int64_t)c0 * pe::D + i;
+                    badv = (int64_t)c0 * pe::D + i;
                     break;
                   }
             }
@@ -977,24 +989,37 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
           }
         }
       };
-      if (T == 1) pack(0);
-      else PlanPool::get().run(T, pack);
-      const int64_t first_neg = *std::min_element(bad.begin(), bad.end());
-      if (first_neg != INT64_MAX) raise(PE_EINVAL, "cont_req: negative request at index " + std::to_string(first_neg));
-      // 3. one launch; 4. outputs
       uint8_t* const od = ctx->a_outh.dev;
+      int64_t first_neg = INT64_MAX;
       if (nseg == 1) {
-        if (++ctx->agg_gen == 0) ++ctx->agg_gen;
-        hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, nullptr, 1, total, od, n_jobs,
-                                          ctx->a_flag.dev, ctx->agg_gen),
-               "launch pg_agg_segments");
-        agg_wait_flag(ctx, ctx->agg_gen);
+        pack(0, 1, bad[0]);
+        first_neg = bad[0];
+        if (first_neg == INT64_MAX) {
+          if (++ctx->agg_gen == 0) ++ctx->agg_gen;
+          hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, nullptr, 1, total, od, n_jobs,
+                                            ctx->a_flag.dev, ctx->agg_gen),
+                 "launch pg_agg_segments");
+          agg_wait_flag(ctx, ctx->agg_gen);
+        }
       } else {
-        hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, ctx->a_segoff.dev, nseg, 0, od, n_jobs,
-                                          nullptr, 0),
-               "launch pg_agg_segments");
-        hipchk(hipStreamSynchronize(ctx->stream), "sync pg_agg_segments");
+        // chunks of segments, each packed by the planning pool and launched at once: the kernel of
+        // chunk k reads its segments over PCIe while the host packs chunk k + 1
+        const int64_t C = T == 1 ? 1 : 8;
+        for (int64_t c = 0; c < C && first_neg == INT64_MAX; ++c) {
+          const int64_t s0 = nseg * c / C, s1 = nseg * (c + 1) / C;
+          if (s1 == s0) continue;
+          if (T == 1) pack(s0, s1, bad[0]);
+          else PlanPool::get().run(T, [&](int t) { pack(s0 + (s1 - s0) * t / T, s0 + (s1 - s0) * (t + 1) / T, bad[t]); });
+          first_neg = *std::min_element(bad, bad + T);
+          if (first_neg == INT64_MAX)
+            hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, ctx->a_segoff.dev + s0, s1 - s0, 0,
+                                              od, n_jobs, nullptr, 0),
+                   "launch pg_agg_segments");
+        }
+        hipchk(hipStreamSynchronize(ctx->stream), "sync pg_agg_segments");   // (also before an EINVAL:
+                                                                             // launched chunks read the batch)
       }
+      if (first_neg != INT64_MAX) raise(PE_EINVAL, "cont_req: negative request at index " + std::to_string(first_neg));
       const uint8_t* oh = ctx->a_outh.p;
       auto unpack = [&](int64_t a, int64_t e) {
         std::memcpy(out_min_res + a * pe::D, oh + oo[0] + a * 32, (size_t)(e - a) * 32);
@@ -1501,12 +1526,11 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   if (const char* ev = std::getenv("PE_LDS_R")) R = std::max<int64_t>(1, std::atoll(ev));
   const int64_t Tmax = ((n_jobs + R - 1) / R + 15) / 16;
   const int64_t Tpad = round_up(std::max<int64_t>(Tmax, 1), 16);
-  // job codes: u16 plane indices at the kernel's slots, stored in the kernel's consumption order
-  std::vector<uint16_t> codes((size_t)(R * 16 * Tpad * pe::LD_CODE), 0);
+  // job codes: u16 plane indices (+ the job's mask row in dword 7), per job first
+  std::vector<uint16_t> jc((size_t)n_jobs * pe::LD_CODE, 0);
   parallel_for(n_jobs, [&](int64_t j0, int64_t j1) {
   for (int64_t j = j0; j < j1; ++j) {
-    const int64_t r = j % R, q = j / R, w = q % 16, t = q / 16;
-    uint16_t* c = codes.data() + (size_t)(((r * 16 + w) * Tpad + t) * pe::LD_CODE);
+    uint16_t* c = jc.data() + (size_t)j * pe::LD_CODE;
     for (int i = 0; i < sp.nf; ++i) {
       const int64_t rank = (int64_t)bd.rank[fdim[i]][j] + 1;
       if (sp.L[i] == 1) {
@@ -1521,8 +1545,51 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
       }
     }
     c[pe::LD_NEED_SLOT] = (uint16_t)(sp.need_pbase + bd.rank[4][j]);
+    c[14] = (uint16_t)(j & 0xFFFF);
+    c[15] = (uint16_t)(j >> 16);
   }
   });
+  // Consumption order: the jobs sorted by the fields' top digits, then the three-level fields'
+  // middle digits (stable: ties keep job order), so consecutive jobs of a wave's run share the plane
+  // pairs the kernel keeps in VGPRs.  LSD counting sorts over the u16 plane indices (the least
+  // significant key first).  PE_LDS_NOSORT=1: job order (A/B).
+  std::vector<uint32_t> order((size_t)n_jobs);
+  std::iota(order.begin(), order.end(), 0u);
+  if (!std::getenv("PE_LDS_NOSORT")) {
+    std::vector<int> keys;   // code entries, most significant first
+    for (int i = 0; i < sp.nf; ++i)
+      if (sp.L[i] >= 2) keys.push_back(3 * i + sp.L[i] - 1);
+    for (int i = 0; i < sp.nf; ++i)
+      if (sp.L[i] == 3) keys.push_back(3 * i + 1);
+    std::vector<uint32_t> tmp((size_t)n_jobs);
+    std::vector<int64_t> cnt((size_t)sp.nplanes + 2);
+    for (int ki = (int)keys.size() - 1; ki >= 0; --ki) {
+      const int e = keys[(size_t)ki];
+      std::fill(cnt.begin(), cnt.end(), 0);
+      for (uint32_t j : order) ++cnt[(size_t)jc[(size_t)j * pe::LD_CODE + e] + 1];
+      for (size_t v = 1; v < cnt.size(); ++v) cnt[v] += cnt[v - 1];
+      for (uint32_t j : order) tmp[(size_t)cnt[(size_t)jc[(size_t)j * pe::LD_CODE + e]]++] = j;
+      order.swap(tmp);
+    }
+  }
+  // runs: wave (r, w) of every block takes T(r, w) consecutive jobs of the order (the kernel derives
+  // T from (J, r, w, R)); slot (r * 16 + w) * Tpad + t, its job's row in lds_rows for the counts
+  std::vector<uint16_t> codes((size_t)(R * 16 * Tpad * pe::LD_CODE), 0);
+  std::vector<uint32_t> rows((size_t)(R * 16 * Tpad), ~0u);
+  {
+    int64_t pos = 0;
+    for (int64_t v = 0; v < R * 16; ++v) {
+      const int64_t r = v / 16, w = v % 16, j0 = r + R * w;
+      const int64_t T = j0 < n_jobs ? (n_jobs - j0 + 16 * R - 1) / (16 * R) : 0;
+      for (int64_t t = 0; t < T; ++t, ++pos) {
+        const uint32_t j = order[(size_t)pos];
+        std::memcpy(codes.data() + (size_t)((v * Tpad + t) * pe::LD_CODE), jc.data() + (size_t)j * pe::LD_CODE,
+                    pe::LD_CODE * 2);
+        rows[(size_t)(v * Tpad + t)] = j;
+      }
+    }
+    if (pos != n_jobs) raise(PE_EINVAL, "lds: run lengths do not cover the batch");
+  }
   if (std::getenv("PE_LDS_DEBUG")) {   // diagnostics: the chosen configuration
     std::fprintf(stderr, "lds: W %d nblk %lld R %lld planes %d need %d fold %d |", W, (long long)nblk, (long long)R,
                  sp.nplanes, sp.nneed, sp.nfold);
@@ -1537,6 +1604,9 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   ctx->lds_R = R;
   ctx->lds_Tpad = Tpad;
   hipchk(ctx->lds_slots.ensure((size_t)R * 16 * Tpad), "alloc count slots");
+  hipchk(ctx->lds_rows.ensure((size_t)R * 16 * Tpad), "alloc count rows");
+  hipchk(hipMemcpyAsync(ctx->lds_rows.p, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, ctx->stream),
+         "H2D lds rows");
   ctx->lds_npad = nblk * S;
   ctx->lds_pitch = nblk * S / 64;
   hipchk(ctx->lds_spec_d.ensure(1), "alloc lds spec");
@@ -1660,7 +1730,8 @@ static void fit_run(pe_ctx* ctx) {
                                    ctx->lds_R, ctx->lds_Tpad, ctx->lds_pitch * 8,
                                    reinterpret_cast<uint8_t*>(ctx->mask.p), ctx->lds_slots.p),
            "launch fit_mask_lds");
-    hipchk(pe::launch_lds_counts(ctx->stream, ctx->lds_slots.p, J, ctx->lds_R, ctx->lds_Tpad, ctx->counts.p),
+    hipchk(pe::launch_lds_counts(ctx->stream, ctx->lds_slots.p, ctx->lds_rows.p, ctx->lds_R * 16 * ctx->lds_Tpad,
+                                 ctx->counts.p),
            "launch lds_counts");
     ctx->stats.fit_runs_lds += 1;
   } else if (ctx->fit_path == 3) {

@@ -204,7 +204,7 @@ hipError_t launch_fit_mask_planes_sets(hipStream_t s, const uint32_t* planes, in
 constexpr int LD_MAXF = 4;        // digit fields (dimensions with >= 2 distinct values)
 constexpr int LD_MAXL = 3;        // digit levels per field
 constexpr int LD_MAXNEED = 64;    // distinct label needs
-constexpr int LD_CODE = 16;       // u16 plane indices per job: field f, level slot k at 3f + k; need at 12
+constexpr int LD_CODE = 16;       // u16 entries per job: field f, level slot k at 3f + k; need at 12; mask row (u32) at 14-15
 constexpr int LD_NEED_SLOT = 12;
 constexpr int LD_THREADS = 1024;  // 16 waves per workgroup, one node block per workgroup
 struct LdsSpec {
@@ -234,15 +234,16 @@ hipError_t launch_node_ranks(hipStream_t s, const int64_t* res, int64_t stride, 
 // workgroups, wave w of workgroup (blk, r) takes jobs j = r + R (w + 16 t).  codes: LD_CODE u16 per
 // job, job j's at position (r * 16 + w) * Tpad + t (Tpad >= the longest run, a multiple of 16).
 // Mask row-major (PE_MASK_ROWS): row j at mask + j * pitch_bytes, block blk's S/8 bytes at + blk * S/8.
-// slots: [R * 16 * Tpad] u32 count slots (zeroed by the caller), job j = r + R (w + 16 t) in slot
-// (r * 16 + w) * Tpad + t; launch_lds_counts turns them into per-job u64 counts.  spec: device copy;
+// slots: [R * 16 * Tpad] u32 count slots (zeroed by the caller), slot (r * 16 + w) * Tpad + t = job t
+// of wave w's run in phase r (the host's order: codes carry each job's mask row in dword 7);
+// launch_lds_counts turns them into per-job u64 counts through the slots' rows.  spec: device copy;
 // nplanes = spec->nplanes.  shape = {N3, N2, N1}: fields 0 .. N3-1 have 3 digit levels, the next N2
 // two, the last N1 one.  The mask has J rows.
 hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[3], const LdsSpec* spec, int nplanes,
                                const uint32_t* ranks, int64_t npad, const uint32_t* aux, int64_t nblk,
                                const uint16_t* codes, int64_t J, int64_t R, int64_t Tpad, int64_t pitch_bytes,
                                uint8_t* mask, uint32_t* slots);
-hipError_t launch_lds_counts(hipStream_t s, const uint32_t* slots, int64_t J, int64_t R, int64_t Tpad,
+hipError_t launch_lds_counts(hipStream_t s, const uint32_t* slots, const uint32_t* rows, int64_t nslots,
                              unsigned long long* counts);
 
 // kn / lo: the node-only score terms of prep_nodes (K(n) = (S(n) << 24) | gid, lo20(r1), lo24(r3)),

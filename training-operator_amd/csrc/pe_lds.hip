@@ -75,20 +75,21 @@ hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[3], const L
   return hipGetLastError();
 }
 
-// Per-job counts from the fit kernel's count slots: job j = r + R (w + 16 t) sits in slot
-// (r * 16 + w) * Tpad + t (the t-major run of wave w of phase r).
-__global__ __launch_bounds__(256) void lds_counts_kernel(const uint32_t* __restrict__ slots, int64_t J, int64_t R,
-                                                         int64_t Tpad, unsigned long long* __restrict__ counts) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= J) return;
-  const int64_t r = j % R, q = j / R;
-  counts[j] = slots[(r * 16 + q % 16) * Tpad + q / 16];
+// Per-job counts from the fit kernel's count slots: slot s holds job rows[s] (~0: an empty slot).
+__global__ __launch_bounds__(256) void lds_counts_kernel(const uint32_t* __restrict__ slots,
+                                                         const uint32_t* __restrict__ rows, int64_t nslots,
+                                                         unsigned long long* __restrict__ counts) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+  const uint32_t j = rows[s];
+  if (j != ~0u) counts[j] = slots[s];
 }
 
-hipError_t launch_lds_counts(hipStream_t s, const uint32_t* slots, int64_t J, int64_t R, int64_t Tpad,
+hipError_t launch_lds_counts(hipStream_t s, const uint32_t* slots, const uint32_t* rows, int64_t nslots,
                              unsigned long long* counts) {
-  if (J <= 0) return hipSuccess;
-  hipLaunchKernelGGL(lds_counts_kernel, dim3((unsigned)((J + 255) / 256)), dim3(256), 0, s, slots, J, R, Tpad, counts);
+  if (nslots <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lds_counts_kernel, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, s, slots, rows, nslots,
+                     counts);
   return hipGetLastError();
 }
 

@@ -20,8 +20,8 @@
 
 namespace pe {
 #ifdef PE_RES_PROF   // section cycle counts for tools/replay_resolver (-DPE_RES_PROF)
-struct ResProf { unsigned long long p1 = 0, p2 = 0, p3 = 0, la = 0, ka = 0, st = 0, seed = 0, keys = 0, skip = 0, place = 0, fin = 0, other = 0; long skips = 0, pods = 0, groups = 0, dirty = 0, scored = 0, sready = 0, slocal = 0, sfull = 0;
-  ~ResProf() { std::fprintf(stderr, "keys split: lookahead %.1fM keys_all %.1fM seed top %.1fM | place split: choose+fetch %.1fM m %.1fM upsert..key %.1fM\n", la / 1e6, ka / 1e6, st / 1e6, p1 / 1e6, p2 / 1e6, p3 / 1e6); std::fprintf(stderr, "cycles seed %.1fM keys %.1fM skip %.1fM place %.1fM fin %.1fM | skips %ld pods %ld | per group: dirty %.0f scored %.1f\n", seed / 1e6, keys / 1e6, skip / 1e6, place / 1e6, fin / 1e6, skips, pods, (double)dirty / groups, (double)scored / groups); std::fprintf(stderr, "seed tops: helper %ld local %ld full %ld\n", sready, slocal, sfull); } };
+struct ResProf { long cgroups = 0, cskip = 0, cdirty = 0; unsigned long long p1 = 0, p2 = 0, p3 = 0, la = 0, ka = 0, st = 0, seed = 0, keys = 0, skip = 0, place = 0, fin = 0, other = 0; long skips = 0, pods = 0, groups = 0, dirty = 0, scored = 0, sready = 0, slocal = 0, sfull = 0;
+  ~ResProf() { std::fprintf(stderr, "keys split: lookahead %.1fM keys_all %.1fM seed top %.1fM | place split: choose+fetch %.1fM m %.1fM upsert..key %.1fM\n", la / 1e6, ka / 1e6, st / 1e6, p1 / 1e6, p2 / 1e6, p3 / 1e6); std::fprintf(stderr, "cycles seed %.1fM keys %.1fM skip %.1fM place %.1fM fin %.1fM | skips %ld pods %ld | per group: dirty %.0f scored %.1f\n", seed / 1e6, keys / 1e6, skip / 1e6, place / 1e6, fin / 1e6, skips, pods, (double)dirty / groups, (double)scored / groups); std::fprintf(stderr, "seed tops: helper %ld local %ld full %ld\n", sready, slocal, sfull); std::fprintf(stderr, "window conflicts: %ld of %ld groups depend on an earlier group of their window (%ld via a skipped list entry, %ld via a chosen changed node)\n", cgroups, groups, cskip, cdirty); } };
 static ResProf rp;
 #define RP_T() __rdtsc()
 #define RP_ADD(f, t) (rp.f += __rdtsc() - (t))
@@ -892,14 +892,23 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     size_t ptr = useS ? std::max(top->head, head_[wi]) : head_[wi];
     size_t pf = ptr;   // clean entries up to pf have been prefetched
     bool failed = false;
+#ifdef PE_RES_PROF
+    // does this group's answer depend on an earlier group of the window (a node changed in this
+    // window: skipped at its list head, or chosen from the dirty set)?  Then resolving the group
+    // apart from its predecessors (speculatively, on another thread) would have to be redone.
+    bool conflict = false;
+    for (size_t i = 0; i < ptr && i < gc.size(); ++i)
+      if (dirty_.contains((int64_t)(gc.key(i) & 0xFFFFFFull))) { conflict = true; rp.cskip++; break; }
+#endif
     if (unit == 2) failed = true;   // an island group whose summed request overflows fits nowhere
     while (!failed && p_ < cnt_[g_]) {
       t_ = RP_T();
       while (ptr < gc.size() && is_dirty((int64_t)(gc.key(ptr) & 0xFFFFFFull))) {
-        ++ptr;
 #ifdef PE_RES_PROF
         rp.skips++;
+        if (!conflict && dirty_.contains((int64_t)(gc.key(ptr) & 0xFFFFFFull))) conflict = true, rp.cskip++;
 #endif
+        ++ptr;
       }
       RP_ADD(skip, t_);
       t_ = RP_T();
@@ -922,6 +931,9 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       if (bkey == kdT) {
         slot = best;
         st = dirty_.get(slot);
+#ifdef PE_RES_PROF
+        if (!conflict && dirty_.touched[slot]) conflict = true, rp.cdirty++;
+#endif
       } else if (bkey == kdS) {   // an unchanged seed: its window-start state is current
         st = seeds_.get(seeds_.find(gid));
         slot = -1;
@@ -985,6 +997,9 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       rp.pods++;
 #endif
     }
+#ifdef PE_RES_PROF
+    rp.cgroups += conflict;
+#endif
     if (!consumed) break;
     if (failed) {
       finish_job(false);
