@@ -29,10 +29,19 @@ def _check(eng, mode, arrs):
 
 
 @pytest.mark.parametrize("mode", [V1, V2])
-@pytest.mark.parametrize("J", [1, 2, 17, 255, 256, 257, 511, 1000, 33000, 70001])
+@pytest.mark.parametrize("J", [1, 2, 17, 32, 33, 255, 256, 257, 511, 1000, 8192, 8193, 33000, 70001])
 def test_agg_segment_sizes(eng, mode, J):
-    """One segment (flag path) up to 256 jobs, then several; 33k+ jobs take the multi-range planner."""
+    """Up to 8192 jobs: 32-job segments in one launch whose last block stores the flag (one block up to
+    32 jobs); above: 256-job segments, chunked, stream sync; 33k+ jobs take the multi-range planner."""
     _check(eng, mode, random_csr(J, 100 + J + mode, big=(J % 2 == 1)))
+
+
+@pytest.mark.parametrize("seg_jobs", ["1", "7", "64", "256"])
+def test_agg_segment_jobs_override(eng, monkeypatch, seg_jobs):
+    """PE_AGG_SEG_JOBS (A/B knob): any segment size gives the same answers, on both call paths."""
+    monkeypatch.setenv("PE_AGG_SEG_JOBS", seg_jobs)
+    for J in (1, 300, 9000):
+        _check(eng, V1, random_csr(J, 700 + J))
 
 
 def _one_job_csr(n_groups, n_cont_per_group, seed):

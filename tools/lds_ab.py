@@ -32,6 +32,9 @@ def main():
     shapes = sys.argv[1:] or ["many", "worst", "adversarial", "cfg5"]
     configs = [dict(), dict(PE_LDS_W="4"), dict(PE_LDS_W="2"), dict(PE_LDS_W="1"), dict(PE_LDS_MAXL="2"),
                dict(PE_LDS_MAXL="3", PE_LDS_W="2")]
+    if os.environ.get("LDS_AB_CONFIGS"):   # JSON list of environment dicts
+        import json
+        configs = json.loads(os.environ["LDS_AB_CONFIGS"])
     inv = synth.make_inventory(N, synth.SEED["cfg5"], gpu_frac=0.2)
     ev = HipEvents()
     a, b = ev.create(), ev.create()
@@ -40,7 +43,7 @@ def main():
         req, need = batch(shape)
         ref = None
         for cfg in configs:
-            for k in ("PE_LDS_W", "PE_LDS_MAXL"):
+            for k in ("PE_LDS_W", "PE_LDS_MAXL", "PE_LDS_NOSORT", "PE_LDS_R"):
                 os.environ.pop(k, None)
             os.environ.update(cfg)
             e = Engine(0, max_nodes=N, fit_path_mask=64 if shape != "cfg5" else 0)
@@ -59,7 +62,8 @@ def main():
             cnt = e.fit_counts()
             ref = cnt if ref is None else ref
             path = "lds" if s["fit_runs_lds"] else ("planes" if s["fit_runs_planes"] else "other")
-            print(f"{shape:<12} {str(cfg):<40} {statistics.median(t):7.3f} ms  path {path}  "
+            lib = os.path.basename(os.environ.get("PE_LIBRARY", "libplacement.so"))
+            print(f"{lib:<16} {shape:<12} {str(cfg):<40} {statistics.median(t):7.3f} ms  path {path}  "
                   f"same {bool(np.array_equal(cnt, ref))}", flush=True)
             e.close()
 

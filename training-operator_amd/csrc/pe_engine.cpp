@@ -280,6 +280,7 @@ struct pe_ctx {
   HostBuf<uint8_t> a_stage, a_outh;
   HostBuf<int64_t> a_segoff;
   HostBuf<uint32_t> a_flag;
+  DevBuf<uint32_t> a_ctr;   // latency launches: blocks done (the last one stores the flag)
   uint32_t agg_gen = 0;
   std::vector<std::vector<AggSeg>> agg_segs;   // per planning range, reused across calls (no allocation per call)
   std::vector<AggSeg> agg_all;                 // all segments in order
@@ -325,7 +326,7 @@ struct pe_ctx {
     code_vals.release(); code_needs.release(); code_jobs.release(); code_x.release(); counts.release(); h_counts.release();
     planes.release(); plane_jobs.release();
     lds_spec_d.release(); lds_vals.release(); lds_codes.release(); lds_ranks.release(); lds_aux.release(); lds_slots.release(); lds_rows.release();
-    a_stage.release(); a_outh.release(); a_segoff.release(); a_flag.release();
+    a_stage.release(); a_outh.release(); a_segoff.release(); a_flag.release(); a_ctr.release();
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
@@ -903,6 +904,13 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       const int32_t* gco = G > 0 ? group_cont_off : nullptr;
       // 1. segments, per job range (one range below 32k jobs; segments never span ranges)
       const int T = n_jobs < 32768 ? 1 : 8;
+      // Segment size: operator-sized calls (<= kLatJobs jobs) take segments of 32 jobs, so a
+      // 256-job call spreads its ~40 KB over 8 CUs (one CU's zero-copy reads come in at a few GB/s:
+      // 41 KB through one block took ~27 us) and waits on the kernel's flag; larger batches take
+      // 256-job segments and the chunked stream path.  PE_AGG_SEG_JOBS overrides (A/B).
+      constexpr int64_t kLatJobs = 8192;
+      int64_t seg_jobs = n_jobs <= kLatJobs ? 32 : pe::AGG_SEG_JOBS;
+      if (const char* e = std::getenv("PE_AGG_SEG_JOBS")) seg_jobs = std::max<int64_t>(1, std::min<int64_t>(pe::AGG_SEG_JOBS, std::atoll(e)));
       auto& segs = ctx->agg_segs;
       if (segs.size() < (size_t)T) segs.resize((size_t)T);
       auto plan = [&](int t) {
@@ -912,7 +920,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
         int64_t off[7];
         for (int64_t j = ja; j < jb;) {
           AggSeg sg{j, 0, 0, 0, 0};
-          while (j < jb && sg.nj < pe::AGG_SEG_JOBS) {
+          while (j < jb && sg.nj < seg_jobs) {
             const int64_t g0 = job_group_off[j], g1 = job_group_off[j + 1];
             const int64_t nc = gco ? (int64_t)gco[g1] - gco[g0] : 0;
             pe::agg_seg_layout(sg.nj + 1, sg.ng + (g1 - g0), sg.nc + nc, v1, off);
@@ -943,6 +951,10 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       ensure_pinned(ctx->a_stage, (size_t)total, "alloc pinned aggregation batch");
       ensure_pinned(ctx->a_outh, (size_t)out_bytes, "alloc pinned aggregation outputs");
       if (!ctx->a_flag.p) hipchk(ctx->a_flag.ensure(16, kZeroCopy), "alloc pinned flag");
+      if (!ctx->a_ctr.p) {
+        hipchk(ctx->a_ctr.ensure(1), "alloc done counter");
+        hipchk(hipMemsetAsync(ctx->a_ctr.p, 0, 4, ctx->stream), "memset done counter");
+      }
       // 2. pack (and the negative-request check, on the copied values); 3. launch
       auto& all = ctx->agg_all;
       all.clear();
@@ -991,13 +1003,13 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       };
       uint8_t* const od = ctx->a_outh.dev;
       int64_t first_neg = INT64_MAX;
-      if (nseg == 1) {
-        pack(0, 1, bad[0]);
+      if (n_jobs <= kLatJobs) {   // latency path: one launch, the host waits on the flag
+        pack(0, nseg, bad[0]);
         first_neg = bad[0];
         if (first_neg == INT64_MAX) {
           if (++ctx->agg_gen == 0) ++ctx->agg_gen;
-          hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, nullptr, 1, total, od, n_jobs,
-                                            ctx->a_flag.dev, ctx->agg_gen),
+          hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, nseg == 1 ? nullptr : ctx->a_segoff.dev,
+                                            nseg, total, od, n_jobs, ctx->a_flag.dev, ctx->agg_gen, ctx->a_ctr.p),
                  "launch pg_agg_segments");
           agg_wait_flag(ctx, ctx->agg_gen);
         }
@@ -1013,7 +1025,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
           first_neg = *std::min_element(bad, bad + T);
           if (first_neg == INT64_MAX)
             hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, ctx->a_segoff.dev + s0, s1 - s0, 0,
-                                              od, n_jobs, nullptr, 0),
+                                              od, n_jobs, nullptr, 0, nullptr),
                    "launch pg_agg_segments");
         }
         hipchk(hipStreamSynchronize(ctx->stream), "sync pg_agg_segments");   // (also before an EINVAL:
@@ -1526,7 +1538,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   if (const char* ev = std::getenv("PE_LDS_R")) R = std::max<int64_t>(1, std::atoll(ev));
   const int64_t Tmax = ((n_jobs + R - 1) / R + 15) / 16;
   const int64_t Tpad = round_up(std::max<int64_t>(Tmax, 1), 16);
-  // job codes: u16 plane indices (+ the job's mask row in dword 7), per job first
+  // job codes: u16 plane indices, per job first
   std::vector<uint16_t> jc((size_t)n_jobs * pe::LD_CODE, 0);
   parallel_for(n_jobs, [&](int64_t j0, int64_t j1) {
   for (int64_t j = j0; j < j1; ++j) {
@@ -1545,35 +1557,10 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
       }
     }
     c[pe::LD_NEED_SLOT] = (uint16_t)(sp.need_pbase + bd.rank[4][j]);
-    c[14] = (uint16_t)(j & 0xFFFF);
-    c[15] = (uint16_t)(j >> 16);
   }
   });
-  // Consumption order: the jobs sorted by the fields' top digits, then the three-level fields'
-  // middle digits (stable: ties keep job order), so consecutive jobs of a wave's run share the plane
-  // pairs the kernel keeps in VGPRs.  LSD counting sorts over the u16 plane indices (the least
-  // significant key first).  PE_LDS_NOSORT=1: job order (A/B).
-  std::vector<uint32_t> order((size_t)n_jobs);
-  std::iota(order.begin(), order.end(), 0u);
-  if (!std::getenv("PE_LDS_NOSORT")) {
-    std::vector<int> keys;   // code entries, most significant first
-    for (int i = 0; i < sp.nf; ++i)
-      if (sp.L[i] >= 2) keys.push_back(3 * i + sp.L[i] - 1);
-    for (int i = 0; i < sp.nf; ++i)
-      if (sp.L[i] == 3) keys.push_back(3 * i + 1);
-    std::vector<uint32_t> tmp((size_t)n_jobs);
-    std::vector<int64_t> cnt((size_t)sp.nplanes + 2);
-    for (int ki = (int)keys.size() - 1; ki >= 0; --ki) {
-      const int e = keys[(size_t)ki];
-      std::fill(cnt.begin(), cnt.end(), 0);
-      for (uint32_t j : order) ++cnt[(size_t)jc[(size_t)j * pe::LD_CODE + e] + 1];
-      for (size_t v = 1; v < cnt.size(); ++v) cnt[v] += cnt[v - 1];
-      for (uint32_t j : order) tmp[(size_t)cnt[(size_t)jc[(size_t)j * pe::LD_CODE + e]]++] = j;
-      order.swap(tmp);
-    }
-  }
-  // runs: wave (r, w) of every block takes T(r, w) consecutive jobs of the order (the kernel derives
-  // T from (J, r, w, R)); slot (r * 16 + w) * Tpad + t, its job's row in lds_rows for the counts
+  // slot (r * 16 + w) * Tpad + t = job r + R (w + 16 t), the t-th of wave w's run in phase r (the
+  // kernel's consumption order); each slot's job in lds_rows for the counts
   std::vector<uint16_t> codes((size_t)(R * 16 * Tpad * pe::LD_CODE), 0);
   std::vector<uint32_t> rows((size_t)(R * 16 * Tpad), ~0u);
   {
@@ -1582,7 +1569,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
       const int64_t r = v / 16, w = v % 16, j0 = r + R * w;
       const int64_t T = j0 < n_jobs ? (n_jobs - j0 + 16 * R - 1) / (16 * R) : 0;
       for (int64_t t = 0; t < T; ++t, ++pos) {
-        const uint32_t j = order[(size_t)pos];
+        const uint32_t j = (uint32_t)(j0 + 16 * R * t);
         std::memcpy(codes.data() + (size_t)((v * Tpad + t) * pe::LD_CODE), jc.data() + (size_t)j * pe::LD_CODE,
                     pe::LD_CODE * 2);
         rows[(size_t)(v * Tpad + t)] = j;

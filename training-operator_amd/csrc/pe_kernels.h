@@ -92,10 +92,12 @@ __host__ __device__ inline void agg_out_layout(int64_t J, int64_t off[4]) {
 // ---- launch wrappers (return hipError_t of the launch)
 // Segmented aggregation: nseg segments; segment s spans blob[seg_off[s], seg_off[s+1]) (seg_off
 // may be NULL for one segment of nbytes0 bytes at blob[0]).  out = output buffer (agg_out_layout,
-// J jobs).  flag != NULL (one segment only): after the outputs are visible system-wide, block 0
-// stores flag_val there (release, system scope) -- the host waits on it instead of the stream.
+// J jobs).  flag != NULL (latency launches): every block publishes its outputs system-wide and counts
+// itself in done_ctr (device memory, 0 between launches; unused for one block); the last one resets
+// it and stores flag_val (release, system scope) -- the host waits on the flag, not on the stream.
 hipError_t launch_pg_agg_segments(hipStream_t s, int mode, const uint8_t* blob, const int64_t* seg_off, int64_t nseg,
-                                  int64_t nbytes0, uint8_t* out, int64_t J, uint32_t* flag, uint32_t flag_val);
+                                  int64_t nbytes0, uint8_t* out, int64_t J, uint32_t* flag, uint32_t flag_val,
+                                  uint32_t* done_ctr);
 hipError_t launch_pg_min_resources(hipStream_t s, int mode, int64_t n_jobs, const int32_t* job_group_off,
                                    const int32_t* min_member, const int32_t* group_replicas,
                                    const int32_t* group_cont_off, const int64_t* cont_req,
@@ -204,7 +206,7 @@ hipError_t launch_fit_mask_planes_sets(hipStream_t s, const uint32_t* planes, in
 constexpr int LD_MAXF = 4;        // digit fields (dimensions with >= 2 distinct values)
 constexpr int LD_MAXL = 3;        // digit levels per field
 constexpr int LD_MAXNEED = 64;    // distinct label needs
-constexpr int LD_CODE = 16;       // u16 entries per job: field f, level slot k at 3f + k; need at 12; mask row (u32) at 14-15
+constexpr int LD_CODE = 16;       // u16 plane indices per job: field f, level slot k at 3f + k; need at 12
 constexpr int LD_NEED_SLOT = 12;
 constexpr int LD_THREADS = 1024;  // 16 waves per workgroup, one node block per workgroup
 struct LdsSpec {
@@ -234,9 +236,8 @@ hipError_t launch_node_ranks(hipStream_t s, const int64_t* res, int64_t stride, 
 // workgroups, wave w of workgroup (blk, r) takes jobs j = r + R (w + 16 t).  codes: LD_CODE u16 per
 // job, job j's at position (r * 16 + w) * Tpad + t (Tpad >= the longest run, a multiple of 16).
 // Mask row-major (PE_MASK_ROWS): row j at mask + j * pitch_bytes, block blk's S/8 bytes at + blk * S/8.
-// slots: [R * 16 * Tpad] u32 count slots (zeroed by the caller), slot (r * 16 + w) * Tpad + t = job t
-// of wave w's run in phase r (the host's order: codes carry each job's mask row in dword 7);
-// launch_lds_counts turns them into per-job u64 counts through the slots' rows.  spec: device copy;
+// slots: [R * 16 * Tpad] u32 count slots (zeroed by the caller), slot (r * 16 + w) * Tpad + t = job
+// r + R (w + 16 t); launch_lds_counts turns them into per-job u64 counts through the slots' rows.  spec: device copy;
 // nplanes = spec->nplanes.  shape = {N3, N2, N1}: fields 0 .. N3-1 have 3 digit levels, the next N2
 // two, the last N1 one.  The mask has J rows.
 hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[3], const LdsSpec* spec, int nplanes,

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void pg_min_resources_kernel(
 __global__ __launch_bounds__(AGG_SEG_JOBS) void pg_agg_seg_kernel(int mode, const uint8_t* __restrict__ blob,
                                                                  const int64_t* __restrict__ seg_off, int64_t nbytes0,
                                                                  uint8_t* __restrict__ out, int64_t J, uint32_t* flag,
-                                                                 uint32_t flag_val) {
+                                                                 uint32_t flag_val, uint32_t* done_ctr) {
   __shared__ uint4 lds[AGG_SEG_BYTES / 16];
   int64_t a = 0, e = nbytes0;
   if (seg_off) {
@@ -171,19 +171,28 @@ __global__ __launch_bounds__(AGG_SEG_JOBS) void pg_agg_seg_kernel(int mode, cons
     out[oo[2] + j] = (uint8_t)o.pres;
     out[oo[3] + j] = o.ovf ? 1 : 0;
   }
-  if (flag) {   // one-segment launch: publish the outputs, then the flag (the host spins on it)
+  if (flag) {   // latency launch: publish the outputs; the LAST block to finish stores the flag
     __threadfence_system();
     __syncthreads();
-    if (t == 0) __hip_atomic_store(flag, flag_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == 0) {
+      const uint32_t nb = gridDim.x;
+      const uint32_t done = nb == 1 ? 0u
+                                    : __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (done == nb - 1) {
+        if (nb > 1) __hip_atomic_store(done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next call
+        __hip_atomic_store(flag, flag_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
 }
 
 hipError_t launch_pg_agg_segments(hipStream_t s, int mode, const uint8_t* blob, const int64_t* seg_off, int64_t nseg,
-                                  int64_t nbytes0, uint8_t* out, int64_t J, uint32_t* flag, uint32_t flag_val) {
+                                  int64_t nbytes0, uint8_t* out, int64_t J, uint32_t* flag, uint32_t flag_val,
+                                  uint32_t* done_ctr) {
   if (nseg <= 0) return hipSuccess;
-  if (flag && nseg != 1) return hipErrorInvalidValue;
+  if ((!seg_off && nseg != 1) || (flag && nseg > 1 && !done_ctr)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(pg_agg_seg_kernel, dim3((unsigned)nseg), dim3(AGG_SEG_JOBS), 0, s, mode, blob, seg_off, nbytes0,
-                     out, J, flag, flag_val);
+                     out, J, flag, flag_val, done_ctr);
   return hipGetLastError();
 }
 

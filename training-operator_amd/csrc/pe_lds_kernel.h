@@ -32,12 +32,8 @@ __device__ __forceinline__ typename LdVec<W>::T plane_rd(const uint32_t* lds, ui
 //     digit -- work items are (field, level, u32 word column), so no two threads write one word;
 //  2. suffix OR per (field, level): GE(v) = E(v) | GE(v + 1), turning equality into threshold planes;
 //     need planes by wave ballots (label test AND the folded dimensions);
-//  3. waves stream their run of jobs (slot (r, w, t); the job's mask row travels in its code, dword 7):
-//     per job the need plane AND, per field, the last level's plane, then GE_k(c + 1) | (GE_k(c) & acc)
-//     per higher level.  The host sorts the batch by the fields' top (then middle) digits, so
-//     consecutive jobs of a run mostly share them: the pair (GE_k(c), GE_k(c + 1)) of a field's top and
-//     middle level stays in VGPRs and is re-read from LDS only when the job's digit changes (a
-//     wave-uniform branch) -- LDS bandwidth is what bounds this kernel at W = 1.  The slice is stored, its popcount
+//  3. waves stream jobs r + R (w + 16 t): per job the need plane AND, per field, the last level's
+//     plane, then GE_k(c + 1) | (GE_k(c) & acc) per higher level; the slice is stored, its popcount
 //     joins a 16-job batch that one column sum (reduce16x64) turns into 16 per-job counts, added by ONE
 //     atomic instruction into 16 CONSECUTIVE u32 count slots (the wave's t-major run, like its codes:
 //     one 64-B request per batch instead of 16 scattered 8-B atomics -- at W = 1 those were ~12 % of
@@ -109,8 +105,13 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
   // 3. the jobs of this wave: j = r + R (wave + 16 t), t < T.  Their codes are contiguous (the t-major
   //    run of wave (r, wave), padded to 16 jobs): a 16-job batch is 512 B, one 8-B load per lane
   //    issued a batch ahead; lane 4K + i holds dwords 2i, 2i + 1 of batch job K (v_readlane).
+  //    (Round-3 A/B, profiles/r10_lds_ab.txt: scalar loads of the codes instead of the readlanes were
+  //    35 % slower -- they share lgkmcnt with the LDS reads -- and sorting the batch by digits so that
+  //    consecutive jobs reuse plane pairs kept in VGPRs saved 3.6 % on the adversarial batch but cost
+  //    7-8 % elsewhere: the sorted jobs' rows scatter the mask stores, which this job interleave keeps
+  //    in one sweeping window.)
   const int64_t j0 = r + R * wave, step = 16 * R;
-  const int64_t T = j0 < J ? (J - j0 + step - 1) / step : 0;   // (the run's length; its jobs are the host's choice)
+  const int64_t T = j0 < J ? (J - j0 + step - 1) / step : 0;
   uint8_t* const col = mask + blk * (S / 8) + lane * (4 * W);
   const uint2* const cb = codes + (r * 16 + wave) * Tpad * (LD_CODE / 4);
   uint32_t* const sl = slots + (r * 16 + wave) * Tpad;
@@ -122,14 +123,6 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
     sigma = reduce16x64(probe, lane);
   }
   uint2 cv = T > 0 ? cb[lane] : make_uint2(0u, 0u);
-  // plane-pair caches: top level of the N3 + N2 fields, middle level of the N3 fields
-  constexpr int NT = N3 + N2 > 0 ? N3 + N2 : 1, NM = N3 > 0 ? N3 : 1;
-  uint32_t ct[NT], cm[NM];
-  V tg[NT], th[NT], mg[NM], mh[NM];
-#pragma unroll
-  for (int i = 0; i < NT; ++i) ct[i] = ~0u;
-#pragma unroll
-  for (int i = 0; i < NM; ++i) cm[i] = ~0u;
   for (int64_t t0 = 0; t0 < T; t0 += 16) {
     const int n = (int)min<int64_t>(16, T - t0);
     const uint2 cur = cv;
@@ -137,45 +130,33 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
     uint32_t p[16];
 #pragma unroll
     for (int K = 0; K < 16; ++K) {
+      const int64_t j = j0 + step * (t0 + K);
       auto entry = [&](int e) -> uint32_t {                           // u16 entry e of job K
         const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)((e & 2) ? cur.y : cur.x), 4 * K + e / 4);
         return (e & 1) ? d >> 16 : d & 0xFFFFu;
       };
-      const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)cur.y, 4 * K + 3);   // dword 7: the mask row
       V f = plane_rd<W>(lds, entry(LD_NEED_SLOT), lane);
 #pragma unroll
       for (int fi = 0; fi < N3; ++fi) {
         const uint32_t p1 = entry(3 * fi + 1), p2 = entry(3 * fi + 2);
         V a = plane_rd<W>(lds, entry(3 * fi), lane);
-        if (p1 != cm[fi]) {
-          mg[fi] = plane_rd<W>(lds, p1, lane);
-          mh[fi] = plane_rd<W>(lds, p1 + 1, lane);
-          cm[fi] = p1;
-        }
-        if (p2 != ct[fi]) {
-          tg[fi] = plane_rd<W>(lds, p2, lane);
-          th[fi] = plane_rd<W>(lds, p2 + 1, lane);
-          ct[fi] = p2;
-        }
-        a = mh[fi] | (mg[fi] & a);
-        a = th[fi] | (tg[fi] & a);
+        const V g1 = plane_rd<W>(lds, p1, lane), h1 = plane_rd<W>(lds, p1 + 1, lane);
+        const V g2 = plane_rd<W>(lds, p2, lane), h2 = plane_rd<W>(lds, p2 + 1, lane);
+        a = h1 | (g1 & a);
+        a = h2 | (g2 & a);
         f &= a;
       }
 #pragma unroll
       for (int fi = N3; fi < N3 + N2; ++fi) {
         const uint32_t p1 = entry(3 * fi + 1);
         V a = plane_rd<W>(lds, entry(3 * fi), lane);
-        if (p1 != ct[fi]) {
-          tg[fi] = plane_rd<W>(lds, p1, lane);
-          th[fi] = plane_rd<W>(lds, p1 + 1, lane);
-          ct[fi] = p1;
-        }
-        a = th[fi] | (tg[fi] & a);
+        const V g1 = plane_rd<W>(lds, p1, lane), h1 = plane_rd<W>(lds, p1 + 1, lane);
+        a = h1 | (g1 & a);
         f &= a;
       }
 #pragma unroll
       for (int fi = N3 + N2; fi < N3 + N2 + N1; ++fi) f &= plane_rd<W>(lds, entry(3 * fi), lane);
-      if (K < n) *reinterpret_cast<V*>(col + (int64_t)row * pitch_bytes) = f;   // n is wave-uniform
+      if (K < n) *reinterpret_cast<V*>(col + j * pitch_bytes) = f;   // n is wave-uniform
       p[K] = popc_vec<W>(f);
     }
     const uint32_t F = reduce16x64(p, lane);
