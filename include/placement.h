@@ -187,7 +187,9 @@ int pe_read_residuals(pe_ctx* ctx, int64_t* res_out /* [4][end-begin] of this sh
  * Outputs per job: out_min_res[j][4], out_present[j] (bit d = key d present), out_members[j],
  * out_overflow[j] (1 = int64 overflow: the reference would have switched to inf.Dec; that job's
  * out_min_res values are then defined as 0, its presence bits and members are still exact).
- * Returns PE_EOVERFLOW if any job overflowed (outputs still written). */
+ * Returns PE_EOVERFLOW if any job overflowed (outputs still written).  A negative request is
+ * PE_EINVAL (the first offending index in pe_last_error); a large batch streams to the device in
+ * chunks, so the outputs of jobs before the offending chunk may then be written. */
 int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t* job_group_off,
                         const int32_t* min_member, const int32_t* group_replicas, const int32_t* group_cont_off,
                         const int64_t* cont_req, const uint8_t* cont_flags, int64_t* out_min_res,

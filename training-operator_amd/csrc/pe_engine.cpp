@@ -160,33 +160,50 @@ void ncclchk(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) raise(PE_ERCCL, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-// The communicator is NON-BLOCKING (ncclConfig_t.blocking = 0), so that a rank whose peers never
-// arrive (a wrong comm_id, a dead peer) gets PE_ERCCL after a bounded wait instead of hanging in
-// ncclCommInitRank.  Every RCCL call on it may return ncclInProgress: wait for its completion here
-// (ncclCommGetAsyncError), at most timeout_ms (< 0: no limit).  Returns the final state.
-ncclResult_t nccl_settle(ncclComm_t comm, ncclResult_t r, double timeout_ms) {
-  if (r != ncclInProgress) return r;
-  const auto t0 = std::chrono::steady_clock::now();
-  for (int spin = 0;; ++spin) {
-    ncclResult_t st = ncclSuccess;
-    const ncclResult_t q = ncclCommGetAsyncError(comm, &st);
-    if (q != ncclSuccess) return q;
-    if (st != ncclInProgress) return st;
-    if (timeout_ms >= 0 &&
-        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > timeout_ms)
-      return ncclInProgress;
-    if (spin < 1024) _mm_pause();
-    else std::this_thread::yield();
-  }
-}
-
-void nccl_call(ncclComm_t comm, ncclResult_t r, const char* what) { ncclchk(nccl_settle(comm, r, -1.0), what); }
-
 // Bound of the communicator set-up: PE_RCCL_INIT_TIMEOUT_S seconds (default 120).
 double rccl_init_timeout_ms() {
   const char* e = std::getenv("PE_RCCL_INIT_TIMEOUT_S");
   const double s = e ? std::atof(e) : 120.0;
   return (s > 0 ? s : 120.0) * 1e3;
+}
+
+// ncclCommInitRank with a time bound: a rank whose peers never arrive (a wrong comm_id, a dead
+// peer) gets PE_ERCCL instead of hanging in the bootstrap, which has no timeout of its own.  The
+// blocking call runs on a helper thread; past the bound the call is abandoned: the thread stays
+// behind (detached) and destroys the communicator itself if the peers ever do arrive.  (A
+// non-blocking communicator, ncclConfig_t.blocking = 0, still blocked in the bootstrap on this
+// RCCL, and ncclCommAbort of a set-up in progress waits for it: profiles/r10_rccl_init.txt.)
+ncclComm_t comm_init_bounded(int device, int world, const ncclUniqueId& id, int rank, double timeout_ms) {
+  struct State {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    ncclResult_t r = ncclSuccess;
+    ncclComm_t comm = nullptr;
+  };
+  auto st = std::make_shared<State>();
+  std::thread([st, device, world, id, rank] {
+    (void)hipSetDevice(device);   // the current device is per thread
+    ncclComm_t c = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&c, world, id, rank);
+    std::lock_guard<std::mutex> lk(st->m);
+    if (st->abandoned) {
+      if (r == ncclSuccess && c) (void)ncclCommDestroy(c);
+      return;
+    }
+    st->r = r;
+    st->comm = c;
+    st->done = true;
+    st->cv.notify_all();
+  }).detach();
+  std::unique_lock<std::mutex> lk(st->m);
+  if (!st->cv.wait_for(lk, std::chrono::duration<double, std::milli>(timeout_ms), [&] { return st->done; })) {
+    st->abandoned = true;
+    raise(PE_ERCCL, "ncclCommInitRank: the " + std::to_string(world) + " ranks did not meet within " +
+                        std::to_string((int)(timeout_ms / 1e3)) + " s (PE_RCCL_INIT_TIMEOUT_S)");
+  }
+  ncclchk(st->r, "ncclCommInitRank");
+  return st->comm;
 }
 
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
@@ -280,6 +297,7 @@ struct pe_ctx {
   HostBuf<uint8_t> a_stage, a_outh;
   HostBuf<int64_t> a_segoff;
   HostBuf<uint32_t> a_flag;
+  std::vector<hipEvent_t> a_ev;   // large batches: one per chunk (its outputs are copied out when it is done)
   DevBuf<uint32_t> a_ctr;   // latency launches: blocks done (the last one stores the flag)
   uint32_t agg_gen = 0;
   std::vector<std::vector<AggSeg>> agg_segs;   // per planning range, reused across calls (no allocation per call)
@@ -327,6 +345,7 @@ struct pe_ctx {
     planes.release(); plane_jobs.release();
     lds_spec_d.release(); lds_vals.release(); lds_codes.release(); lds_ranks.release(); lds_aux.release(); lds_slots.release(); lds_rows.release();
     a_stage.release(); a_outh.release(); a_segoff.release(); a_flag.release(); a_ctr.release();
+    for (hipEvent_t e : a_ev) (void)hipEventDestroy(e);
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
@@ -339,10 +358,7 @@ struct pe_ctx {
     w_sk.release(); w_kin.release(); w_rmin.release(); w_sr.release(); w_rmax.release(); w_sl.release(); w_pos.release();
     w_ror.release(); w_inovl.release(); w_ovl.release(); w_ovln.release(); w_temp.release();
     w_ovidx.release(); w_ovlab.release(); w_ovres.release(); w_stat.release(); w_flush.release();
-    if (comm) {
-      (void)nccl_settle(comm, ncclInProgress, 10000.0);   // let a pending operation finish (non-blocking comm)
-      (void)ncclCommDestroy(comm);
-    }
+    if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -597,21 +613,7 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
       if (!cfg->comm_id) raise(PE_EINVAL, "world_size > 1 needs comm_id or an exchange callback");
       ncclUniqueId id;
       std::memcpy(&id, cfg->comm_id, sizeof(id));
-      ncclConfig_t conf = NCCL_CONFIG_INITIALIZER;
-      conf.blocking = 0;   // bounded set-up (nccl_settle)
-      ncclResult_t r = ncclCommInitRankConfig(&ctx->comm, ctx->world, id, ctx->rank, &conf);
-      if (ctx->comm) r = nccl_settle(ctx->comm, r, rccl_init_timeout_ms());
-      if (r != ncclSuccess) {
-        // a set-up that never completed is left behind, not aborted: ncclCommAbort joins the
-        // bootstrap, which waits for the missing peers without a timeout of its own
-        // (PE_RCCL_TIMEOUT_ABORT=1 aborts it anyway)
-        if (ctx->comm && (r != ncclInProgress || std::getenv("PE_RCCL_TIMEOUT_ABORT"))) (void)ncclCommAbort(ctx->comm);
-        ctx->comm = nullptr;
-        if (r == ncclInProgress)
-          raise(PE_ERCCL, "ncclCommInitRank: the " + std::to_string(ctx->world) + " ranks did not meet within " +
-                              std::to_string((int)(rccl_init_timeout_ms() / 1e3)) + " s (PE_RCCL_INIT_TIMEOUT_S)");
-        ncclchk(r, "ncclCommInitRank");
-      }
+      ctx->comm = comm_init_bounded(ctx->device, ctx->world, id, ctx->rank, rccl_init_timeout_ms());
     }
   } catch (const PeError& e) {
     rc = e.code;
@@ -777,7 +779,7 @@ int pe_comm_ranks(const pe_ctx* ctx, int32_t* nranks) {
   *nranks = 0;
   if (!ctx->comm) return PE_OK;
   int n = 0;
-  if (nccl_settle(ctx->comm, ncclCommCount(ctx->comm, &n), -1.0) != ncclSuccess) return PE_ERCCL;
+  if (ncclCommCount(ctx->comm, &n) != ncclSuccess) return PE_ERCCL;
   *nranks = n;
   return PE_OK;
 }
@@ -902,14 +904,20 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
     } else {
       const bool v1 = mode == PE_MODE_V1;
       const int32_t* gco = G > 0 ? group_cont_off : nullptr;
+      // PE_AGG_TRACE=1: phase times of the call on stderr (diagnostics)
+      const bool trace = std::getenv("PE_AGG_TRACE") != nullptr;
+      auto now = [] { return std::chrono::steady_clock::now(); };
+      const auto tt0 = now();
+      double t_pack = 0;
       // 1. segments, per job range (one range below 32k jobs; segments never span ranges)
       const int T = n_jobs < 32768 ? 1 : 8;
-      // Segment size: operator-sized calls (<= kLatJobs jobs) take segments of 32 jobs, so a
-      // 256-job call spreads its ~40 KB over 8 CUs (one CU's zero-copy reads come in at a few GB/s:
-      // 41 KB through one block took ~27 us) and waits on the kernel's flag; larger batches take
-      // 256-job segments and the chunked stream path.  PE_AGG_SEG_JOBS overrides (A/B).
+      // Calls of <= kLatJobs jobs are one launch the host waits on through the kernel's flag; up to
+      // 2048 jobs with segments of 32 jobs, so a 256-job call spreads its ~40 KB over 8 CUs (one
+      // CU's zero-copy reads come in at a few GB/s: 41 KB through one block took ~27 us, 8 blocks
+      // 19 us); larger batches take 256-job segments, above kLatJobs in chunks with a stream sync.
+      // PE_AGG_SEG_JOBS overrides the segment size (A/B, profiles/r10_agg_latency.txt).
       constexpr int64_t kLatJobs = 8192;
-      int64_t seg_jobs = n_jobs <= kLatJobs ? 32 : pe::AGG_SEG_JOBS;
+      int64_t seg_jobs = n_jobs <= 2048 ? 32 : pe::AGG_SEG_JOBS;   // (8192 jobs: 94 us with 256, 112 with 32)
       if (const char* e = std::getenv("PE_AGG_SEG_JOBS")) seg_jobs = std::max<int64_t>(1, std::min<int64_t>(pe::AGG_SEG_JOBS, std::atoll(e)));
       auto& segs = ctx->agg_segs;
       if (segs.size() < (size_t)T) segs.resize((size_t)T);
@@ -955,6 +963,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
         hipchk(ctx->a_ctr.ensure(1), "alloc done counter");
         hipchk(hipMemsetAsync(ctx->a_ctr.p, 0, 4, ctx->stream), "memset done counter");
       }
+      const auto tt1 = now();
       // 2. pack (and the negative-request check, on the copied values); 3. launch
       auto& all = ctx->agg_all;
       all.clear();
@@ -1002,6 +1011,14 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
         }
       };
       uint8_t* const od = ctx->a_outh.dev;
+      const uint8_t* oh = ctx->a_outh.p;
+      auto unpack = [&](int64_t a, int64_t e) {   // outputs of jobs [a, e) into the caller's arrays
+        std::memcpy(out_min_res + a * pe::D, oh + oo[0] + a * 32, (size_t)(e - a) * 32);
+        std::memcpy(out_members + a, oh + oo[1] + a * 4, (size_t)(e - a) * 4);
+        std::memcpy(out_present + a, oh + oo[2] + a, (size_t)(e - a));
+        std::memcpy(out_overflow + a, oh + oo[3] + a, (size_t)(e - a));
+      };
+      int64_t unpacked = 0;   // jobs [0, unpacked) already copied out
       int64_t first_neg = INT64_MAX;
       if (n_jobs <= kLatJobs) {   // latency path: one launch, the host waits on the flag
         pack(0, nseg, bad[0]);
@@ -1015,32 +1032,52 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
         }
       } else {
         // chunks of segments, each packed by the planning pool and launched at once: the kernel of
-        // chunk k reads its segments over PCIe while the host packs chunk k + 1
+        // chunk k reads its segments over PCIe while the host packs chunk k + 1, and chunk k - 1's
+        // outputs are copied out once its kernel is done (an event per chunk)
         const int64_t C = T == 1 ? 1 : 8;
+        while ((int64_t)ctx->a_ev.size() < C) {
+          hipEvent_t e;
+          hipchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+          ctx->a_ev.push_back(e);
+        }
+        int64_t prev_s0 = -1, prev_s1 = -1;
+        auto job_end = [&](int64_t s1) { return all[(size_t)s1 - 1].j0 + all[(size_t)s1 - 1].nj; };
         for (int64_t c = 0; c < C && first_neg == INT64_MAX; ++c) {
           const int64_t s0 = nseg * c / C, s1 = nseg * (c + 1) / C;
           if (s1 == s0) continue;
+          const auto tp = now();
           if (T == 1) pack(s0, s1, bad[0]);
           else PlanPool::get().run(T, [&](int t) { pack(s0 + (s1 - s0) * t / T, s0 + (s1 - s0) * (t + 1) / T, bad[t]); });
+          t_pack += std::chrono::duration<double, std::milli>(now() - tp).count();
           first_neg = *std::min_element(bad, bad + T);
-          if (first_neg == INT64_MAX)
-            hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, ctx->a_segoff.dev + s0, s1 - s0, 0,
-                                              od, n_jobs, nullptr, 0, nullptr),
-                   "launch pg_agg_segments");
+          if (first_neg != INT64_MAX) break;
+          hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, ctx->a_segoff.dev + s0, s1 - s0, 0, od,
+                                            n_jobs, nullptr, 0, nullptr),
+                 "launch pg_agg_segments");
+          hipchk(hipEventRecord(ctx->a_ev[(size_t)c], ctx->stream), "event record");
+          if (prev_s1 > prev_s0) {   // the previous chunk's outputs, while this chunk runs
+            hipchk(hipEventSynchronize(ctx->a_ev[(size_t)c - 1]), "event sync");
+            const int64_t ja = all[(size_t)prev_s0].j0, jb = job_end(prev_s1);
+            parallel_for(jb - ja, [&](int64_t a, int64_t e) { unpack(ja + a, ja + e); });
+            unpacked = jb;
+          }
+          prev_s0 = s0;
+          prev_s1 = s1;
         }
         hipchk(hipStreamSynchronize(ctx->stream), "sync pg_agg_segments");   // (also before an EINVAL:
                                                                              // launched chunks read the batch)
       }
       if (first_neg != INT64_MAX) raise(PE_EINVAL, "cont_req: negative request at index " + std::to_string(first_neg));
-      const uint8_t* oh = ctx->a_outh.p;
-      auto unpack = [&](int64_t a, int64_t e) {
-        std::memcpy(out_min_res + a * pe::D, oh + oo[0] + a * 32, (size_t)(e - a) * 32);
-        std::memcpy(out_members + a, oh + oo[1] + a * 4, (size_t)(e - a) * 4);
-        std::memcpy(out_present + a, oh + oo[2] + a, (size_t)(e - a));
-        std::memcpy(out_overflow + a, oh + oo[3] + a, (size_t)(e - a));
-      };
-      if (T == 1) unpack(0, n_jobs);
-      else parallel_for(n_jobs, unpack);
+      const auto tt2 = now();
+      if (T == 1) unpack(unpacked, n_jobs);
+      else parallel_for(n_jobs - unpacked, [&](int64_t a, int64_t e) { unpack(unpacked + a, unpacked + e); });
+      if (trace) {
+        const auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+          return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        std::fprintf(stderr, "agg: J %lld segs %lld bytes %lld | plan %.3f ms, pack %.3f ms, pack+launch+wait %.3f ms, unpack %.3f ms\n",
+                     (long long)n_jobs, (long long)nseg, (long long)total, ms(tt0, tt1), t_pack, ms(tt1, tt2), ms(tt2, now()));
+      }
     }
     const void* o1 = std::memchr(out_overflow, 1, (size_t)n_jobs);
     if (o1) {
@@ -2235,7 +2272,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       } else if (use_exchange) {
         hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
       } else {
-        nccl_call(ctx->comm, ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
+        ncclchk(ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
         if (dev_merge)
           hipchk(pe::launch_merge_shards(s, ctx->g_gath.p, ctx->world, Wg, K, outbufdev(b), gen), "launch merge_shards");
         else
