@@ -1020,15 +1020,22 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       };
       int64_t unpacked = 0;   // jobs [0, unpacked) already copied out
       int64_t first_neg = INT64_MAX;
+      double t_launch = 0, t_wait = 0;
       if (n_jobs <= kLatJobs) {   // latency path: one launch, the host waits on the flag
+        const auto tp = now();
         pack(0, nseg, bad[0]);
         first_neg = bad[0];
+        t_pack = std::chrono::duration<double, std::milli>(now() - tp).count();
         if (first_neg == INT64_MAX) {
           if (++ctx->agg_gen == 0) ++ctx->agg_gen;
+          const auto tl = now();
           hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, nseg == 1 ? nullptr : ctx->a_segoff.dev,
                                             nseg, total, od, n_jobs, ctx->a_flag.dev, ctx->agg_gen, ctx->a_ctr.p),
                  "launch pg_agg_segments");
+          const auto tw = now();
           agg_wait_flag(ctx, ctx->agg_gen);
+          t_launch = std::chrono::duration<double, std::milli>(tw - tl).count();
+          t_wait = std::chrono::duration<double, std::milli>(now() - tw).count();
         }
       } else {
         // chunks of segments, each packed by the planning pool and launched at once: the kernel of
@@ -1075,8 +1082,10 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
         const auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
           return std::chrono::duration<double, std::milli>(b - a).count();
         };
-        std::fprintf(stderr, "agg: J %lld segs %lld bytes %lld | plan %.3f ms, pack %.3f ms, pack+launch+wait %.3f ms, unpack %.3f ms\n",
-                     (long long)n_jobs, (long long)nseg, (long long)total, ms(tt0, tt1), t_pack, ms(tt1, tt2), ms(tt2, now()));
+        std::fprintf(stderr, "agg: J %lld segs %lld bytes %lld | plan %.4f ms, pack %.4f ms, pack+launch+wait %.4f ms "
+                             "(launch call %.4f, flag wait %.4f), unpack %.4f ms\n",
+                     (long long)n_jobs, (long long)nseg, (long long)total, ms(tt0, tt1), t_pack, ms(tt1, tt2), t_launch,
+                     t_wait, ms(tt2, now()));
       }
     }
     const void* o1 = std::memchr(out_overflow, 1, (size_t)n_jobs);
