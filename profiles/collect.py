@@ -9,7 +9,7 @@ import os
 import shutil
 import sys
 
-KEEP = ("fit_mask", "encode_", "walk_kernel", "apply_kernel", "node_ranks")
+KEEP = ("fit_mask", "encode_", "walk_kernel", "apply_kernel", "node_ranks", "pg_agg_seg")
 
 
 def main(src, name, latest):
@@ -19,6 +19,14 @@ def main(src, name, latest):
     shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     shutil.copy(os.path.join(src, "bench_trace.json"), os.path.join(dst, "bench_trace.json"))
     shutil.copy(os.path.join(src, "summary.json"), os.path.join(dst, "summary.json"))
+    # the greedy walk passes (warm / cold, PE_WALK_FLUSH) and the aggregation pass: kernel stats + bench lines
+    for sub, stem in (("walk_warm", "walk"), ("walk_cold", "walk"), ("agg", "agg")):
+        f = os.path.join(src, sub, f"{stem}_kernel_stats.csv")
+        if os.path.exists(f):
+            shutil.copy(f, os.path.join(dst, f"kernel_stats_{sub}.csv"))
+    for f in ("bench_walk_warm.json", "bench_walk_cold.json", "agg.out"):
+        if os.path.exists(os.path.join(src, f)):
+            shutil.copy(os.path.join(src, f), os.path.join(dst, f))
     for pas in ("fetch", "write", "sq", "sq2"):
         f = os.path.join(src, pas, f"{pas}_counter_collection.csv")
         if not os.path.exists(f):

@@ -1029,9 +1029,18 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
         if (first_neg == INT64_MAX) {
           if (++ctx->agg_gen == 0) ++ctx->agg_gen;
           const auto tl = now();
-          hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, nseg == 1 ? nullptr : ctx->a_segoff.dev,
-                                            nseg, total, od, n_jobs, ctx->a_flag.dev, ctx->agg_gen, ctx->a_ctr.p),
-                 "launch pg_agg_segments");
+          if (nseg == 1 && total <= pe::AGG_KARG_BYTES && !std::getenv("PE_AGG_NO_KARG")) {
+            // the segment in the kernel arguments (no zero-copy read; PE_AGG_NO_KARG=1: A/B)
+            static thread_local pe::AggKarg karg;
+            std::memcpy(karg.b, ctx->a_stage.p, (size_t)total);
+            hipchk(pe::launch_pg_agg_karg(ctx->stream, mode, karg, total, od, n_jobs, ctx->a_flag.dev, ctx->agg_gen),
+                   "launch pg_agg_karg");
+          } else {
+            hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev,
+                                              nseg == 1 ? nullptr : ctx->a_segoff.dev, nseg, total, od, n_jobs,
+                                              ctx->a_flag.dev, ctx->agg_gen, ctx->a_ctr.p),
+                   "launch pg_agg_segments");
+          }
           const auto tw = now();
           agg_wait_flag(ctx, ctx->agg_gen);
           t_launch = std::chrono::duration<double, std::milli>(tw - tl).count();

@@ -98,6 +98,13 @@ __host__ __device__ inline void agg_out_layout(int64_t J, int64_t off[4]) {
 hipError_t launch_pg_agg_segments(hipStream_t s, int mode, const uint8_t* blob, const int64_t* seg_off, int64_t nseg,
                                   int64_t nbytes0, uint8_t* out, int64_t J, uint32_t* flag, uint32_t flag_val,
                                   uint32_t* done_ctr);
+// One segment of <= AGG_KARG_BYTES (a multiple of 16) passed by value in the kernel arguments.
+constexpr int64_t AGG_KARG_BYTES = 3072;
+struct AggKarg {
+  alignas(16) uint8_t b[AGG_KARG_BYTES];
+};
+hipError_t launch_pg_agg_karg(hipStream_t s, int mode, const AggKarg& blob, int64_t nbytes, uint8_t* out, int64_t J,
+                              uint32_t* flag, uint32_t flag_val);
 hipError_t launch_pg_min_resources(hipStream_t s, int mode, int64_t n_jobs, const int32_t* job_group_off,
                                    const int32_t* min_member, const int32_t* group_replicas,
                                    const int32_t* group_cont_off, const int64_t* cont_req,

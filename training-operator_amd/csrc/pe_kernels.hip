@@ -117,21 +117,15 @@ __global__ __launch_bounds__(256) void pg_min_resources_kernel(
 // comes into LDS with one round of coalesced 16-B loads -- from pinned host memory over PCIe, so a
 // one-job call costs one PCIe round trip for its inputs -- then lane t aggregates job t of the
 // segment from LDS and writes its outputs into the (pinned) output buffer.
-__global__ __launch_bounds__(AGG_SEG_JOBS) void pg_agg_seg_kernel(int mode, const uint8_t* __restrict__ blob,
-                                                                 const int64_t* __restrict__ seg_off, int64_t nbytes0,
-                                                                 uint8_t* __restrict__ out, int64_t J, uint32_t* flag,
-                                                                 uint32_t flag_val, uint32_t* done_ctr) {
-  __shared__ uint4 lds[AGG_SEG_BYTES / 16];
-  int64_t a = 0, e = nbytes0;
-  if (seg_off) {
-    a = seg_off[blockIdx.x];
-    e = seg_off[blockIdx.x + 1];
-  }
-  const uint8_t* seg = blob + a;
-  if (e - a <= AGG_SEG_BYTES) {   // stage in LDS (else read in place: one oversized job)
+// One segment: stage [seg, seg + bytes) into LDS (8 16-B loads in flight per lane before the LDS
+// stores: a 48 KB segment is 2 PCIe round trips, not 12), lane t aggregates job t from LDS and writes
+// its outputs into `out`; with a flag, the last block to finish publishes the launch.
+__device__ __forceinline__ void agg_segment(int mode, const uint8_t* seg, int64_t bytes, uint4* lds,
+                                            uint8_t* __restrict__ out, int64_t J, uint32_t* flag, uint32_t flag_val,
+                                            uint32_t* done_ctr) {
+  if (bytes <= AGG_SEG_BYTES) {   // stage in LDS (else read in place: one oversized job)
     const uint4* src = reinterpret_cast<const uint4*>(seg);
-    const int n16 = (int)((e - a) >> 4);
-    // 8 loads in flight per lane before the LDS stores: a 48 KB segment is 2 PCIe round trips, not 12
+    const int n16 = (int)(bytes >> 4);
     constexpr int U = 8;
     for (int i0 = 0; i0 < n16; i0 += U * AGG_SEG_JOBS) {
       uint4 v[U];
@@ -184,6 +178,39 @@ __global__ __launch_bounds__(AGG_SEG_JOBS) void pg_agg_seg_kernel(int mode, cons
       }
     }
   }
+}
+
+
+__global__ __launch_bounds__(AGG_SEG_JOBS) void pg_agg_seg_kernel(int mode, const uint8_t* __restrict__ blob,
+                                                                 const int64_t* __restrict__ seg_off, int64_t nbytes0,
+                                                                 uint8_t* __restrict__ out, int64_t J, uint32_t* flag,
+                                                                 uint32_t flag_val, uint32_t* done_ctr) {
+  __shared__ uint4 lds[AGG_SEG_BYTES / 16];
+  int64_t a = 0, e = nbytes0;
+  if (seg_off) {
+    a = seg_off[blockIdx.x];
+    e = seg_off[blockIdx.x + 1];
+  }
+  agg_segment(mode, blob + a, e - a, lds, out, J, flag, flag_val, done_ctr);
+}
+
+// A one-segment call of <= AGG_KARG_BYTES travels IN the kernel arguments (the blob is the first
+// argument, so it sits at offset 0 of the kernarg segment): no zero-copy read of host memory, i.e.
+// one PCIe round trip less on the operator's one-job call.
+__global__ __launch_bounds__(AGG_SEG_JOBS) void pg_agg_karg_kernel(AggKarg blob, int mode, int64_t nbytes,
+                                                                  uint8_t* __restrict__ out, int64_t J, uint32_t* flag,
+                                                                  uint32_t flag_val) {
+  __shared__ uint4 lds[AGG_KARG_BYTES / 16];
+  const uint8_t* kp = (const uint8_t*)__builtin_amdgcn_kernarg_segment_ptr();   // (address space 4 -> generic)
+  (void)blob;
+  agg_segment(mode, kp, nbytes, lds, out, J, flag, flag_val, nullptr);
+}
+
+hipError_t launch_pg_agg_karg(hipStream_t s, int mode, const AggKarg& blob, int64_t nbytes, uint8_t* out, int64_t J,
+                              uint32_t* flag, uint32_t flag_val) {
+  if (nbytes <= 0 || nbytes > AGG_KARG_BYTES || (nbytes & 15) || !flag) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pg_agg_karg_kernel, dim3(1), dim3(AGG_SEG_JOBS), 0, s, blob, mode, nbytes, out, J, flag, flag_val);
+  return hipGetLastError();
 }
 
 hipError_t launch_pg_agg_segments(hipStream_t s, int mode, const uint8_t* blob, const int64_t* seg_off, int64_t nseg,
