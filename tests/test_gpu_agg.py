@@ -102,13 +102,13 @@ def test_agg_device_path_ab(eng, monkeypatch):
 
 @pytest.mark.parametrize("no_karg", ["", "1"])
 def test_agg_small_calls_both_paths(eng, monkeypatch, no_karg):
-    """A one-segment call of <= 3 KB travels in the kernel arguments (pg_agg_karg_kernel); with
+    """A one-segment call of <= 512 B travels in the kernel arguments (pg_agg_karg_kernel); with
     PE_AGG_NO_KARG=1 it is staged from pinned memory.  Both agree with the oracle, including a
-    segment just under and just over the 3 KB argument limit."""
+    segment just under and just over the argument limit (one job of 12 / 13 containers)."""
     if no_karg:
         monkeypatch.setenv("PE_AGG_NO_KARG", "1")
     for J in (1, 2, 5, 13, 20, 32):
         for mode in (V1, V2):
             _check(eng, mode, random_csr(J, 300 + J + mode))
-    for n_cont in (10, 60, 90, 100):   # one job, n_cont containers x 33 B around the limit
+    for n_cont in (1, 10, 12, 13, 60):   # one job, n_cont containers x 33 B around the limit
         _check(eng, V1, _one_job_csr(1, n_cont, n_cont))

@@ -855,6 +855,26 @@ void agg_device_path(pe_ctx* ctx, int32_t mode, int64_t n_jobs, int64_t G, int64
   hipchk(hipStreamSynchronize(s), "sync pg_min_resources");
 }
 
+// dst[0, n) = src[0, n) and the OR of all values (its sign says whether any is negative), in one
+// pass: the aggregation's request records are validated while they are packed.
+__attribute__((target("avx2"))) int64_t copy_or_i64(int64_t* dst, const int64_t* src, int64_t n) {
+  __m256i acc = _mm256_setzero_si256();
+  int64_t i = 0;
+  for (; i + 4 <= n; i += 4) {
+    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+    _mm256_storeu_si256(reinterpret_cast<__m256i*>(dst + i), v);
+    acc = _mm256_or_si256(acc, v);
+  }
+  alignas(32) int64_t lanes[4];
+  _mm256_store_si256(reinterpret_cast<__m256i*>(lanes), acc);
+  int64_t any = lanes[0] | lanes[1] | lanes[2] | lanes[3];
+  for (; i < n; ++i) {
+    dst[i] = src[i];
+    any |= src[i];
+  }
+  return any;
+}
+
 // Grow-only pinned buffer (a 1M-job batch needs ~170 MB; hipHostMalloc costs ms, so keep it).
 template <class T>
 void ensure_pinned(HostBuf<T>& b, size_t count, const char* what) {
@@ -994,10 +1014,8 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
             if (sg.nc > 0) {
               const int64_t* q = cont_req + (int64_t)c0 * pe::D;
               const int64_t nq = (int64_t)sg.nc * pe::D;
-              std::memcpy(b + off[4], q, (size_t)nq * 8);
+              const int64_t any = copy_or_i64(reinterpret_cast<int64_t*>(b + off[4]), q, nq);   // one pass
               std::memcpy(b + off[5], cont_flags + c0, (size_t)sg.nc);
-              int64_t any = 0;
-              for (int64_t i = 0; i < nq; ++i) any |= q[i];
               if (any < 0 && badv == INT64_MAX)
                 for (int64_t i = 0; i < nq; ++i)
                   if (q[i] < 0) {
@@ -1031,7 +1049,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
           const auto tl = now();
           if (nseg == 1 && total <= pe::AGG_KARG_BYTES && !std::getenv("PE_AGG_NO_KARG")) {
             // the segment in the kernel arguments (no zero-copy read; PE_AGG_NO_KARG=1: A/B)
-            static thread_local pe::AggKarg karg;
+            static thread_local pe::AggKarg karg;   // (512 B)
             std::memcpy(karg.b, ctx->a_stage.p, (size_t)total);
             hipchk(pe::launch_pg_agg_karg(ctx->stream, mode, karg, total, od, n_jobs, ctx->a_flag.dev, ctx->agg_gen),
                    "launch pg_agg_karg");

@@ -99,7 +99,7 @@ hipError_t launch_pg_agg_segments(hipStream_t s, int mode, const uint8_t* blob, 
                                   int64_t nbytes0, uint8_t* out, int64_t J, uint32_t* flag, uint32_t flag_val,
                                   uint32_t* done_ctr);
 // One segment of <= AGG_KARG_BYTES (a multiple of 16) passed by value in the kernel arguments.
-constexpr int64_t AGG_KARG_BYTES = 3072;
+constexpr int64_t AGG_KARG_BYTES = 512;   // (a 3 KB argument block cost ~1.5 us more per launch call)
 struct AggKarg {
   alignas(16) uint8_t b[AGG_KARG_BYTES];
 };
