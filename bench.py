@@ -146,7 +146,8 @@ def fit_bytes(n_nodes: int, n_jobs: int) -> int:
 
 def agg_bytes(job_group_off, group_cont_off) -> int:
     """SURVEY.md 8(d) aggregation bytes: per job G*(4 + 32 + 1) + 32 + 4 + 1 + 1, with the
-    container records (32 + 1 B each) counted as they are read."""
+    container records (32 + 1 B each) counted as they are read.  Of these, 38 B per job are outputs
+    (res 32 + members 4 + present 1 + overflow 1), the rest inputs."""
     J = len(job_group_off) - 1
     G = int(job_group_off[-1])
     C = int(group_cont_off[-1])
@@ -264,14 +265,37 @@ def profile_check(path: str, n_nodes: int, n_jobs: int, kern_ms: float, src_hash
     return out
 
 
+AGG_PROFILE_CALLS = 7   # tools/agg_calls.py: 1M-job calls in the profile's aggregation pass
+
+
 def agg_profile_ms(src_hash: str):
-    """pg_agg_seg_kernel's average duration (ms) in the committed profile's aggregation pass (the
-    1M-job call, tools/agg_calls.py), when taken on the same engine sources; else None."""
+    """Kernel time of one 1M-job pe_pg_min_resources call (the sum of its chunk launches of
+    pg_agg_seg_kernel) in the committed profile's aggregation pass (tools/agg_calls.py), when taken
+    on the same engine sources; else None."""
     _, summ = profile_summary()
     if summ is None or summ.get("source_hash") != src_hash:
         return None
     k = summ.get("aggregation", {}).get("pe::pg_agg_seg_kernel")
-    return k["avg_ns"] / 1e6 if k else None
+    return k["total_ns"] / AGG_PROFILE_CALLS / 1e6 if k else None
+
+
+def agg_roofline(in_bytes: int, out_bytes: int, events_ms: float, profile_ms, pcie):
+    """Roofline of the 1M-job aggregation call's kernel.  The batch crosses PCIe: the packed batch is
+    read zero-copy (in_bytes, host to device) while the outputs are written into pinned memory
+    (out_bytes, device to host) -- the two directions of a full-duplex link, so peak = the box's
+    measured pinned H2D + D2H rates, and h2d_frac prices the input stream alone.  Kernel time = the
+    committed profile's (the sum of the call's chunk launches) when it matches the sources, else
+    hipEvents around the whole call (which also cover the host packing its first chunk)."""
+    ms = profile_ms if profile_ms else events_ms
+    ach = (in_bytes + out_bytes) / (ms * 1e-3) / 1e9
+    peak = (pcie["h2d_gbs"] + pcie["d2h_gbs"]) if pcie else None
+    return {"bound": "pcie", "kernel": "pe::pg_agg_seg_kernel", "kernel_ms": ms,
+            "time_source": "rocprof profile (sum of the call's chunk launches)" if profile_ms else
+                           "hipEvents around the call (host packing of the first chunk included)",
+            "events_call_ms": events_ms, "profile_kernel_ms": profile_ms, "in_bytes": in_bytes, "out_bytes": out_bytes,
+            "achieved": ach, "unit": "GB/s", "peak": peak, "frac": ach / peak if peak else None,
+            "h2d_frac": in_bytes / (ms * 1e-3) / 1e9 / pcie["h2d_gbs"] if pcie else None,
+            "hbm_frac": ach / HBM_PEAK_GBS}
 
 
 def greedy_profile(src_hash: str):
@@ -598,16 +622,8 @@ def main(argv=None):
             "pcie": pcie,
             "pcie_bound_ms": (mb / pcie["h2d_gbs"] / 1e6) if pcie else None,
             "latency_us": lat, "ctypes_call_us": ctypes_us,
-            "roofline": {"bound": "pcie", "kernel": "pe::pg_agg_seg_kernel", "kernel_ms": kms,
-                         "profile_kernel_ms": agg_profile_ms(source_hash(ROOT)),
-                         "achieved": mb / (kms * 1e-3) / 1e9, "unit": "GB/s",
-                         "peak": pcie["h2d_gbs"] if pcie else None,
-                         "frac": (mb / (kms * 1e-3) / 1e9 / pcie["h2d_gbs"]) if pcie else None,
-                         "hbm_frac": mb / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "note": "kernel_ms = hipEvents around the call on the engine stream (its only device work is "
-                                 "the one launch); the kernel reads the packed batch over PCIe (zero-copy) and writes "
-                                 "the outputs into pinned host memory, so the bound is the link, peak = this box's "
-                                 "measured pinned H2D rate; hbm_frac against 8 TB/s for reference"},
+            "roofline": agg_roofline(mb - 38 * (hi_j - lo_j), 38 * (hi_j - lo_j), kms, agg_profile_ms(source_hash(ROOT)),
+                                     pcie),
             "note": "latency_us: one pe_pg_min_resources call on the first J jobs (median / p90 of 400, ctypes pointers "
                     "built once; ctypes_call_us = the dispatch cost of an empty ABI call, included); r2_path = the "
                     "round-2 call path (PE_AGG_DEVICE=1: six H2D + four D2H copies + stream sync) on the same box; "

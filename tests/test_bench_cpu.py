@@ -102,3 +102,30 @@ def test_aggregation_slices_partition_the_batch():
                  for r in range(world)]
         for k in range(len(want)):
             np.testing.assert_array_equal(np.concatenate([p[k] for p in parts]), want[k])
+
+
+def test_greedy_and_aggregation_profile_lookups(tmp_path, monkeypatch):
+    """greedy_profile / agg_profile_ms read the committed profile's greedy (warm / cold) and
+    aggregation passes only when its sources match; agg_roofline prices the call's kernel time
+    against the box's PCIe rate."""
+    sys.path.insert(0, ROOT)
+    import bench
+    prof = tmp_path / "p"
+    prof.mkdir()
+    (tmp_path / "LATEST").write_text("p\n")
+    summ = {"source_hash": "abc", "kernels": {},
+            "greedy": {"warm": {"pe::walk_kernel": {"avg_ns": 30000.0, "calls": 10, "total_ns": 3e5}},
+                       "cold": {"pe::walk_kernel": {"avg_ns": 45000.0, "calls": 10, "total_ns": 4.5e5}}},
+            "aggregation": {"pe::pg_agg_seg_kernel": {"avg_ns": 1e5, "calls": 56,
+                                                      "total_ns": 2.8e6 * bench.AGG_PROFILE_CALLS}}}
+    (prof / "summary.json").write_text(json.dumps(summ))
+    monkeypatch.setattr(bench, "PROFILES", str(tmp_path))
+    g = bench.greedy_profile("abc")
+    assert g["warm"] == 30000.0 and g["cold"] == 45000.0 and g["profile"].endswith("p/summary.json")
+    assert bench.greedy_profile("other") == {}
+    assert abs(bench.agg_profile_ms("abc") - 2.8) < 1e-9 and bench.agg_profile_ms("other") is None
+    r = bench.agg_roofline(42_000_000, 14_000_000, 4.0, 2.8, {"h2d_gbs": 56.0, "d2h_gbs": 55.0})
+    assert r["bound"] == "pcie" and abs(r["achieved"] - 20.0) < 1e-9 and abs(r["frac"] - 20.0 / 111.0) < 1e-9
+    assert abs(r["h2d_frac"] - 15.0 / 56.0) < 1e-9
+    r = bench.agg_roofline(42_000_000, 14_000_000, 4.0, None, None)
+    assert r["kernel_ms"] == 4.0 and r["frac"] is None and "hipEvents" in r["time_source"]
