@@ -3,7 +3,7 @@
 The path takes every batch that one register plane set cannot hold (more than 32 distinct
 (dimension, value) pairs): per dimension a digit field of 1-3 levels, single-valued dimensions
 folded into the need planes, one plane per distinct need.  Cases cover every block size W (2048,
-4096, 8192 nodes per workgroup), every level count, ragged last blocks, job counts around the
+4096, 8192 nodes per workgroup), every level count (four only at W >= 2), ragged last blocks, job counts around the
 16-job batch and the phase interleave, int64 extremes, negative residuals, many needs, and shards."""
 import os
 
@@ -103,7 +103,7 @@ def test_lds_shapes_vs_oracle(shape, W):
     e.close()
 
 
-@pytest.mark.parametrize("maxl", [1, 2, 3])
+@pytest.mark.parametrize("maxl", [1, 2, 3, 4])
 def test_lds_level_counts(maxl):
     """The same batch through single-level, two-level and three-level digit fields (150 cpu, 150
     memory, 100 ephemeral values: ~410 planes at one level, which only the 2048-node blocks hold)."""
@@ -117,6 +117,30 @@ def test_lds_level_counts(maxl):
     need[:] = (rng.integers(0, 8, J).astype(np.uint32) << 1) | (req[:, 2] > 0)
     e, counts = run(inv, req, need, maxl=maxl)
     check(e, counts, inv, req, need)
+    e.close()
+
+
+@pytest.mark.parametrize("W,dims", [(2, (0, 1, 3)), (4, (0, 1))])
+def test_lds_four_level_fields(W, dims, capfd):
+    """Fields that only four digit levels fit into LDS: 60k values unique per job in each of `dims`
+    (three fields at 4096-node blocks, two at 8192; at three levels they need ~120 planes each, more
+    than the block's budget) -- the four-level kernels, bit-exact, on a ragged last block."""
+    N, J = 6001, 60000
+    inv = inventory(N, 71 + W)
+    rng = np.random.default_rng(73 + W)
+    req, need = synth.make_fit_jobs(J, 73 + W)
+    scale = {0: 1, 1: 1 << 20, 3: 7}
+    for d in dims:
+        req[:, d] = scale[d] * (1 + rng.permutation(J))
+    os.environ["PE_LDS_DEBUG"] = "1"
+    try:
+        e, counts = run(inv, req, need, W=W)
+    finally:
+        os.environ.pop("PE_LDS_DEBUG", None)
+    check(e, counts, inv, req, need)
+    plan = capfd.readouterr().err            # the engine's PE_LDS_DEBUG line: "lds: W w ... L l B b" per field
+    assert f"lds: W {W} " in plan and " L 4 " in plan, plan
+    assert 0 < counts.sum() < N * J
     e.close()
 
 

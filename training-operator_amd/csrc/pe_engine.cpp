@@ -257,7 +257,7 @@ struct pe_ctx {
   // LDS digit-plane path (pe_kernels.h LdsSpec): spec, node-block geometry, codes, ranks
   pe::LdsSpec lds{};
   int lds_W = 4;                          // u32 words per lane per plane: block = 2048 W nodes
-  int lds_shape[3] = {0, 0, 0};           // fields with 3 / 2 / 1 digit levels (kernel template)
+  int lds_shape[4] = {0, 0, 0, 0};        // fields with 4 / 3 / 2 / 1 digit levels (kernel template)
   int64_t lds_nblk = 0, lds_R = 1, lds_Tpad = 0, lds_npad = 0, lds_pitch = 0;   // pitch in u64 words
   DevBuf<pe::LdsSpec> lds_spec_d;
   DevBuf<int64_t> lds_vals;
@@ -1460,7 +1460,7 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd, bool 
 // digit field of L levels (chosen with the node-block size W to minimise plane reads per job within
 // the LDS budget), dimensions with one value folded into the need planes, one plane per distinct
 // need.  Returns false when no configuration fits 160 KiB of LDS (the other paths take the batch).
-// PE_LDS_W=1|2|4 forces the block size, PE_LDS_MAXL=1..3 caps the levels (tuning / tests).
+// PE_LDS_W=1|2|4 forces the block size, PE_LDS_MAXL=1..4 caps the levels (tuning / tests).
 static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   if (n_jobs == 0 || ctx->Ns == 0) return false;
   const std::vector<int64_t>* vals = bd.vals;
@@ -1477,7 +1477,8 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
       fdim[sp.nf++] = d;
     }
   }
-  // planes of a field with m values at L levels (lower levels base B, top level whatever is left)
+  // planes of a field with m values at L levels (lower levels base B, top level whatever is left):
+  // level 0 has B planes, levels 1 .. L-2 B + 1 (their GE(c + 1) is read too), the top m / B^(L-1) + 2
   auto plan = [](int64_t m, int L, int64_t& B) -> int64_t {
     if (L == 1) {
       B = m;
@@ -1485,20 +1486,20 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
     }
     int64_t best = INT64_MAX;
     for (int64_t b = 2; b <= m; ++b) {
-      const int64_t low = L == 2 ? b : b * b;
-      if (L == 3 && b * b > 4 * m + 4) break;
+      int64_t low = 1;
+      for (int k = 1; k < L; ++k) low *= b;
       const int64_t T = m / low + 1;
-      const int64_t p = (T + 1) + (L == 3 ? (b + 1) : 0) + b;
+      const int64_t p = (T + 1) + (L - 2) * (b + 1) + b;
       if (p < best) {
         best = p;
         B = b;
       }
-      if (L == 2 && b * b > 4 * m + 4) break;
+      if (low / b * b * b > 4 * m + 4) break;   // past the square-ish optimum
     }
     return best;
   };
-  int maxl = 3;
-  if (const char* e = std::getenv("PE_LDS_MAXL")) maxl = std::max(1, std::min(3, std::atoi(e)));
+  int maxl = pe::LD_MAXL;
+  if (const char* e = std::getenv("PE_LDS_MAXL")) maxl = std::max(1, std::min(pe::LD_MAXL, std::atoi(e)));
   int forced_w = 0;
   if (const char* e = std::getenv("PE_LDS_W")) forced_w = std::atoi(e);
   const int64_t nneed = (int64_t)needs.size();
@@ -1513,18 +1514,24 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
     for (int cix = 0; cix < combos; ++cix) {
       int L[pe::LD_MAXF];
       int64_t B[pe::LD_MAXF];
-      int64_t planes = nneed, reads = 1;
+      int64_t planes = nneed, reads = 1, entries = 0;
+      bool ok = true;
       for (int i = 0, x = cix; i < sp.nf; ++i, x /= maxl) {
         L[i] = 1 + x % maxl;
         const int64_t m = (int64_t)vals[fdim[i]].size();
         if (L[i] > 1 && m < 4) L[i] = 1;
+        if (L[i] == 4 && W == 1) ok = false;     // four-level kernels exist for W >= 2 only
         planes += plan(m, L[i], B[i]);
         reads += 2 * L[i] - 1;
+        entries += L[i];
       }
-      if (planes > budget || planes > 65535) continue;
-      // LDS cycles per KiB of plane reads (b128 / b64: 4, b32: 8) plus ~60 VALU cycles of fixed work
-      // per job and wave, both per 8192 nodes
-      const double cost = reads * (W == 1 ? 8.0 : 4.0) + 60.0 * 4 / W;
+      if (!ok || entries > pe::LD_NEED_SLOT || planes > budget || planes > 65535) continue;
+      // per job and 8192 nodes, in CU cycles: LDS plane reads (b128 / b64 / read2st64_b64: 4 per KiB,
+      // b32: 8) -- the kernel's bound -- plus its VALU at ~0.6 CU cycles per wave instruction: per
+      // entry a readlane half and an address, ~6 fixed, and the three-input combines (2 per extra level
+      // and word, 4 per 8192 nodes whatever W)
+      const double valu = (4.0 / W) * (1.5 * (double)entries + 6.0) + 4.0 * (double)(reads - 1 - sp.nf + sp.nf / 2);
+      const double cost = reads * (W == 1 ? 8.0 : 4.0) + 0.625 * valu;
       if (cost < bestCost - 1e-9) {
         bestCost = cost;
         bestW = W;
@@ -1553,8 +1560,8 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
       bestB[i] = B2[i];
     }
   }
-  int shape[3] = {0, 0, 0};
-  for (int i = 0; i < sp.nf; ++i) ++shape[3 - bestL[i]];
+  int shape[4] = {0, 0, 0, 0};
+  for (int i = 0; i < sp.nf; ++i) ++shape[4 - bestL[i]];
   // level specs, plane bases
   int32_t p = 0;
   int64_t voff = 0;
@@ -1618,14 +1625,15 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
     uint16_t* c = jc.data() + (size_t)j * pe::LD_CODE;
     for (int i = 0; i < sp.nf; ++i) {
       const int64_t rank = (int64_t)bd.rank[fdim[i]][j] + 1;
+      const int o = pe::lds_field_off(i, shape[0], shape[1], shape[2]);
       if (sp.L[i] == 1) {
-        c[3 * i] = (uint16_t)(sp.pbase[i][0] + rank - 1);
+        c[o] = (uint16_t)(sp.pbase[i][0] + rank - 1);
       } else {
         int64_t x = rank;
         for (int k = 0; k < sp.L[i]; ++k) {
           const int64_t digit = sp.mod[i][k] ? x % sp.mod[i][k] : x;
           x = sp.mod[i][k] ? x / sp.mod[i][k] : 0;
-          c[3 * i + k] = (uint16_t)(sp.pbase[i][k] + digit);
+          c[o + k] = (uint16_t)(sp.pbase[i][k] + digit);
         }
       }
     }
@@ -1659,7 +1667,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   }
   ctx->lds = sp;
   ctx->lds_W = W;
-  for (int i = 0; i < 3; ++i) ctx->lds_shape[i] = shape[i];
+  for (int i = 0; i < 4; ++i) ctx->lds_shape[i] = shape[i];
   ctx->lds_nblk = nblk;
   ctx->lds_R = R;
   ctx->lds_Tpad = Tpad;

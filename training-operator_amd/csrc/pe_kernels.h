@@ -211,10 +211,18 @@ hipError_t launch_fit_mask_planes_sets(hipStream_t s, const uint32_t* planes, in
 // block's planes in LDS (scatter of the equality bits + suffix OR), then streams the jobs: per job
 // a handful of LDS reads, AND/AND-OR combines, one store of the block's slice of the mask row.
 constexpr int LD_MAXF = 4;        // digit fields (dimensions with >= 2 distinct values)
-constexpr int LD_MAXL = 3;        // digit levels per field
+constexpr int LD_MAXL = 4;        // digit levels per field
 constexpr int LD_MAXNEED = 64;    // distinct label needs
-constexpr int LD_CODE = 16;       // u16 plane indices per job: field f, level slot k at 3f + k; need at 12
-constexpr int LD_NEED_SLOT = 12;
+constexpr int LD_CODE = 16;       // u16 plane indices per job: field f's levels at lds_field_off(f) + k; need at 15
+constexpr int LD_NEED_SLOT = 15;
+// First code entry of field fi when the fields are ordered N4 four-level, N3 three-level, N2 two-level,
+// then one-level (the kernel's template shape; the sum of the levels must stay <= LD_NEED_SLOT).
+__host__ __device__ constexpr int lds_field_off(int fi, int n4, int n3, int n2) {
+  return fi <= n4                ? 4 * fi
+         : fi <= n4 + n3         ? 4 * n4 + 3 * (fi - n4)
+         : fi <= n4 + n3 + n2    ? 4 * n4 + 3 * n3 + 2 * (fi - n4 - n3)
+                                 : 4 * n4 + 3 * n3 + 2 * n2 + (fi - n4 - n3 - n2);
+}
 constexpr int LD_THREADS = 1024;  // 16 waves per workgroup, one node block per workgroup
 struct LdsSpec {
   int32_t nf;                       // digit fields
@@ -245,9 +253,9 @@ hipError_t launch_node_ranks(hipStream_t s, const int64_t* res, int64_t stride, 
 // Mask row-major (PE_MASK_ROWS): row j at mask + j * pitch_bytes, block blk's S/8 bytes at + blk * S/8.
 // slots: [R * 16 * Tpad] u32 count slots (zeroed by the caller), slot (r * 16 + w) * Tpad + t = job
 // r + R (w + 16 t); launch_lds_counts turns them into per-job u64 counts through the slots' rows.  spec: device copy;
-// nplanes = spec->nplanes.  shape = {N3, N2, N1}: fields 0 .. N3-1 have 3 digit levels, the next N2
-// two, the last N1 one.  The mask has J rows.
-hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[3], const LdsSpec* spec, int nplanes,
+// nplanes = spec->nplanes.  shape = {N4, N3, N2, N1}: fields 0 .. N4-1 have 4 digit levels (W >= 2
+// only), the next N3 three, then N2 two, the last N1 one.  The mask has J rows.
+hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[4], const LdsSpec* spec, int nplanes,
                                const uint32_t* ranks, int64_t npad, const uint32_t* aux, int64_t nblk,
                                const uint16_t* codes, int64_t J, int64_t R, int64_t Tpad, int64_t pitch_bytes,
                                uint8_t* mask, uint32_t* slots);

@@ -1,8 +1,10 @@
 // The LDS digit-plane fit kernel (pe_kernels.h LdsSpec), templated on the block size W and on the
-// batch's field shape: N3 fields of three digit levels, then N2 of two, then N1 of one (the host
-// orders the fields that way).  With the shape fixed at compile time a job's body is straight-line
-// code -- every plane read issued first, one AND-OR per level, no branches -- so the scheduler can
-// overlap consecutive jobs of the 16-job batch.  Included by pe_lds_w{1,2,4}.hip, one W each.
+// batch's field shape: N4 fields of four digit levels, then N3 of three, N2 of two and N1 of one (the
+// host orders the fields that way).  With the shape fixed at compile time a job's body is
+// straight-line code -- every plane read issued first, one AND-OR per level, no branches -- so the
+// scheduler can overlap consecutive jobs of the 16-job batch.  Included by pe_lds_w{1,2,4}.hip, one W
+// each.  Four-level fields exist for W >= 2 only: they let a 4096-node block (one ds_read_b64 per
+// plane, 256 B/clk of LDS, twice the b32 rate) hold fields that need ~130 planes each at three levels.
 #pragma once
 #include "pe_kernels.h"
 #include "pe_wave.h"
@@ -19,6 +21,28 @@ __device__ __forceinline__ uint32_t popc_vec(typename LdVec<W>::T v) {
   if constexpr (W == 1) return __popc(v);
   else if constexpr (W == 2) return __popc(v.x) + __popc(v.y);
   else return __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+}
+
+// A slice as W separate u32 words and back: the AND / AND-OR combines run on plain u32 values, which
+// the compiler folds into three-input v_bitop3_b32 (on the vector type it emitted one v_and / v_or per
+// word and input: 61 VALU per job at W = 2 instead of ~40).
+template <int W>
+__device__ __forceinline__ void slice_split(typename LdVec<W>::T v, uint32_t (&o)[W]) {
+  if constexpr (W == 1) o[0] = v;
+  else {
+#pragma unroll
+    for (int i = 0; i < W; ++i) o[i] = v[i];
+  }
+}
+template <int W>
+__device__ __forceinline__ typename LdVec<W>::T slice_join(const uint32_t (&o)[W]) {
+  typename LdVec<W>::T v;
+  if constexpr (W == 1) v = o[0];
+  else {
+#pragma unroll
+    for (int i = 0; i < W; ++i) v[i] = o[i];
+  }
+  return v;
 }
 
 // Plane p's slice of lane `lane` (W u32 words: nodes 32 W lane .. +32 W - 1 of the block).
@@ -39,7 +63,7 @@ __device__ __forceinline__ typename LdVec<W>::T plane_rd(const uint32_t* lds, ui
 //     one 64-B request per batch instead of 16 scattered 8-B atomics -- at W = 1 those were ~12 % of
 //     the kernel's HBM traffic); lds_counts_kernel maps the slots back to jobs.  Past the wave's last
 //     job the batch's slices are not stored (uniform branch).
-template <int W, int N3, int N2, int N1>
+template <int W, int N4, int N3, int N2, int N1>
 __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec* __restrict__ spp,
                                                                   const uint32_t* __restrict__ ranks, int64_t npad,
                                                                   const uint32_t* __restrict__ aux, int64_t nblk,
@@ -112,7 +136,8 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
   //    in one sweeping window.)
   const int64_t j0 = r + R * wave, step = 16 * R;
   const int64_t T = j0 < J ? (J - j0 + step - 1) / step : 0;
-  uint8_t* const col = mask + blk * (S / 8) + lane * (4 * W);
+  uint8_t* const col0 = mask + blk * (S / 8);       // this block's column of row 0 (wave-uniform)
+  const uint32_t lane_off = (uint32_t)lane * (4 * W);
   const uint2* const cb = codes + (r * 16 + wave) * Tpad * (LD_CODE / 4);
   uint32_t* const sl = slots + (r * 16 + wave) * Tpad;
   uint32_t sigma;
@@ -122,11 +147,20 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
     for (int k = 0; k < 16; ++k) probe[k] = lane == 0 ? (uint32_t)k : 0u;
     sigma = reduce16x64(probe, lane);
   }
-  uint2 cv = T > 0 ? cb[lane] : make_uint2(0u, 0u);
+  // No branch inside a batch: the next batch's codes are loaded unconditionally (index clamped into the
+  // padded run) and the stores are buffer stores whose resource holds the job's row slice, with 0 bytes
+  // for a job past the wave's last (the hardware drops an out-of-range store: no traffic, no scratch
+  // row).  A batch is then one basic block -- job K + 1's plane reads overlap job K's combines -- and
+  // the compiler's wait for the code load counts exactly the batch's 16 stores behind it (with
+  // conditional stores it drained every store of the batch, vmcnt(0), once per batch).
+  uint2 cv = cb[lane];
+  // (wait for the first batch's codes here, once: left pending into the loop, the header would merge
+  // that pending load with the latch's state and wait vmcnt(0) -- every store drained -- per batch)
+  asm volatile("" : : "v"(cv.x), "v"(cv.y));
   for (int64_t t0 = 0; t0 < T; t0 += 16) {
     const int n = (int)min<int64_t>(16, T - t0);
     const uint2 cur = cv;
-    if (t0 + 16 < T) cv = cb[(t0 + 16) * (LD_CODE / 4) + lane];   // next batch, in flight meanwhile
+    cv = cb[min<int64_t>(t0 + 16, Tpad - 16) * (LD_CODE / 4) + lane];   // next batch, in flight meanwhile
     uint32_t p[16];
 #pragma unroll
     for (int K = 0; K < 16; ++K) {
@@ -135,55 +169,72 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
         const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)((e & 2) ? cur.y : cur.x), 4 * K + e / 4);
         return (e & 1) ? d >> 16 : d & 0xFFFFu;
       };
-      V f = plane_rd<W>(lds, entry(LD_NEED_SLOT), lane);
+      uint32_t f[W];
+      slice_split<W>(plane_rd<W>(lds, entry(LD_NEED_SLOT), lane), f);
 #pragma unroll
-      for (int fi = 0; fi < N3; ++fi) {
-        const uint32_t p1 = entry(3 * fi + 1), p2 = entry(3 * fi + 2);
-        V a = plane_rd<W>(lds, entry(3 * fi), lane);
-        const V g1 = plane_rd<W>(lds, p1, lane), h1 = plane_rd<W>(lds, p1 + 1, lane);
-        const V g2 = plane_rd<W>(lds, p2, lane), h2 = plane_rd<W>(lds, p2 + 1, lane);
-        a = h1 | (g1 & a);
-        a = h2 | (g2 & a);
-        f &= a;
+      for (int fi = 0; fi < N4 + N3 + N2 + N1; ++fi) {          // unrolled: L and the entries are constants
+        const int L = fi < N4 ? 4 : fi < N4 + N3 ? 3 : fi < N4 + N3 + N2 ? 2 : 1;
+        const int o = lds_field_off(fi, N4, N3, N2);
+        uint32_t a[W], g[W], h[W];
+        slice_split<W>(plane_rd<W>(lds, entry(o), lane), a);
+#pragma unroll
+        for (int k = 1; k < L; ++k) {
+          const uint32_t pk = entry(o + k);
+          slice_split<W>(plane_rd<W>(lds, pk, lane), g);
+          slice_split<W>(plane_rd<W>(lds, pk + 1, lane), h);
+#pragma unroll
+          for (int i = 0; i < W; ++i) a[i] = h[i] | (g[i] & a[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < W; ++i) f[i] &= a[i];
       }
-#pragma unroll
-      for (int fi = N3; fi < N3 + N2; ++fi) {
-        const uint32_t p1 = entry(3 * fi + 1);
-        V a = plane_rd<W>(lds, entry(3 * fi), lane);
-        const V g1 = plane_rd<W>(lds, p1, lane), h1 = plane_rd<W>(lds, p1 + 1, lane);
-        a = h1 | (g1 & a);
-        f &= a;
-      }
-#pragma unroll
-      for (int fi = N3 + N2; fi < N3 + N2 + N1; ++fi) f &= plane_rd<W>(lds, entry(3 * fi), lane);
-      if (K < n) *reinterpret_cast<V*>(col + j * pitch_bytes) = f;   // n is wave-uniform
-      p[K] = popc_vec<W>(f);
+      const V fv = slice_join<W>(f);
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(col0 + j * pitch_bytes), 0, K < n ? 256 * W : 0, 0x00020000);
+      if constexpr (W == 1) __builtin_amdgcn_raw_buffer_store_b32(fv, rs, lane_off, 0, 0);
+      else if constexpr (W == 2) __builtin_amdgcn_raw_buffer_store_b64(fv, rs, lane_off, 0, 0);
+      else __builtin_amdgcn_raw_buffer_store_b128(fv, rs, lane_off, 0, 0);
+      p[K] = popc_vec<W>(fv);
     }
     const uint32_t F = reduce16x64(p, lane);
     if ((lane & 3) == 0 && sigma < (uint32_t)n && F) atomicAdd(&sl[t0 + sigma], F);
   }
 }
 
-// Every field shape (N3, N2, N1) with N3 + N2 + N1 <= LD_MAXF.
-#define PE_LDS_SHAPES(X, W)                                                                               \
-  X(W, 0, 0, 0) X(W, 0, 0, 1) X(W, 0, 1, 0) X(W, 1, 0, 0) X(W, 0, 0, 2) X(W, 0, 1, 1) X(W, 0, 2, 0)         \
-  X(W, 1, 0, 1) X(W, 1, 1, 0) X(W, 2, 0, 0) X(W, 0, 0, 3) X(W, 0, 1, 2) X(W, 0, 2, 1) X(W, 0, 3, 0)         \
-  X(W, 1, 0, 2) X(W, 1, 1, 1) X(W, 1, 2, 0) X(W, 2, 0, 1) X(W, 2, 1, 0) X(W, 3, 0, 0) X(W, 0, 0, 4)         \
-  X(W, 0, 1, 3) X(W, 0, 2, 2) X(W, 0, 3, 1) X(W, 0, 4, 0) X(W, 1, 0, 3) X(W, 1, 1, 2) X(W, 1, 2, 1)         \
-  X(W, 1, 3, 0) X(W, 2, 0, 2) X(W, 2, 1, 1) X(W, 2, 2, 0) X(W, 3, 0, 1) X(W, 3, 1, 0) X(W, 4, 0, 0)
+// Every field shape (N4, N3, N2, N1) with N4 + N3 + N2 + N1 <= LD_MAXF whose entries fit the code
+// (4 N4 + 3 N3 + 2 N2 + N1 <= LD_NEED_SLOT): 35 without four-level fields, 34 with.
+#define PE_LDS_SHAPES3(X, W)                                                                             \
+  X(W, 0, 0, 0, 0) X(W, 0, 0, 0, 1) X(W, 0, 0, 0, 2) X(W, 0, 0, 0, 3) X(W, 0, 0, 0, 4) X(W, 0, 0, 1, 0)  \
+  X(W, 0, 0, 1, 1) X(W, 0, 0, 1, 2) X(W, 0, 0, 1, 3) X(W, 0, 0, 2, 0) X(W, 0, 0, 2, 1) X(W, 0, 0, 2, 2)  \
+  X(W, 0, 0, 3, 0) X(W, 0, 0, 3, 1) X(W, 0, 0, 4, 0) X(W, 0, 1, 0, 0) X(W, 0, 1, 0, 1) X(W, 0, 1, 0, 2)  \
+  X(W, 0, 1, 0, 3) X(W, 0, 1, 1, 0) X(W, 0, 1, 1, 1) X(W, 0, 1, 1, 2) X(W, 0, 1, 2, 0) X(W, 0, 1, 2, 1)  \
+  X(W, 0, 1, 3, 0) X(W, 0, 2, 0, 0) X(W, 0, 2, 0, 1) X(W, 0, 2, 0, 2) X(W, 0, 2, 1, 0) X(W, 0, 2, 1, 1)  \
+  X(W, 0, 2, 2, 0) X(W, 0, 3, 0, 0) X(W, 0, 3, 0, 1) X(W, 0, 3, 1, 0) X(W, 0, 4, 0, 0)
 
-// The kernel of block size W for shape (n3, n2, n1); nullptr for a shape outside the table.
+#define PE_LDS_SHAPES4(X, W)                                                                             \
+  X(W, 1, 0, 0, 0) X(W, 1, 0, 0, 1) X(W, 1, 0, 0, 2) X(W, 1, 0, 0, 3) X(W, 1, 0, 1, 0) X(W, 1, 0, 1, 1)  \
+  X(W, 1, 0, 1, 2) X(W, 1, 0, 2, 0) X(W, 1, 0, 2, 1) X(W, 1, 0, 3, 0) X(W, 1, 1, 0, 0) X(W, 1, 1, 0, 1)  \
+  X(W, 1, 1, 0, 2) X(W, 1, 1, 1, 0) X(W, 1, 1, 1, 1) X(W, 1, 1, 2, 0) X(W, 1, 2, 0, 0) X(W, 1, 2, 0, 1)  \
+  X(W, 1, 2, 1, 0) X(W, 1, 3, 0, 0) X(W, 2, 0, 0, 0) X(W, 2, 0, 0, 1) X(W, 2, 0, 0, 2) X(W, 2, 0, 1, 0)  \
+  X(W, 2, 0, 1, 1) X(W, 2, 0, 2, 0) X(W, 2, 1, 0, 0) X(W, 2, 1, 0, 1) X(W, 2, 1, 1, 0) X(W, 2, 2, 0, 0)  \
+  X(W, 3, 0, 0, 0) X(W, 3, 0, 0, 1) X(W, 3, 0, 1, 0) X(W, 3, 1, 0, 0)
+
+// The kernel of block size W for shape (n4, n3, n2, n1); nullptr for a shape outside the table
+// (four-level shapes are built for W >= 2 only).
 template <int W>
-const void* lds_kernel_for(int n3, int n2, int n1) {
-#define PE_LDS_PICK(W_, a, b, c) \
-  if (n3 == a && n2 == b && n1 == c) return (const void*)fit_mask_lds_kernel<W_, a, b, c>;
-  PE_LDS_SHAPES(PE_LDS_PICK, W)
+const void* lds_kernel_for(int n4, int n3, int n2, int n1) {
+#define PE_LDS_PICK(W_, a, b, c, d) \
+  if (n4 == a && n3 == b && n2 == c && n1 == d) return (const void*)fit_mask_lds_kernel<W_, a, b, c, d>;
+  PE_LDS_SHAPES3(PE_LDS_PICK, W)
+  if constexpr (W >= 2) {
+    PE_LDS_SHAPES4(PE_LDS_PICK, W)
+  }
 #undef PE_LDS_PICK
   return nullptr;
 }
 
-const void* lds_kernel_w1(int n3, int n2, int n1);
-const void* lds_kernel_w2(int n3, int n2, int n1);
-const void* lds_kernel_w4(int n3, int n2, int n1);
+const void* lds_kernel_w1(int n4, int n3, int n2, int n1);
+const void* lds_kernel_w2(int n4, int n3, int n2, int n1);
+const void* lds_kernel_w4(int n4, int n3, int n2, int n1);
 
 }  // namespace pe
