@@ -400,7 +400,7 @@ void need_ptr(const void* p, const char* name) {
 // PE_NO_POOL=1: a thread per task instead (A/B).
 class PlanPool {
  public:
-  static constexpr int kMax = 8;
+  static constexpr int kMax = 16;
   static PlanPool& get() {
     static PlanPool* p = new PlanPool();   // never destroyed: its threads may still wait at exit
     return *p;
@@ -930,7 +930,12 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       const auto tt0 = now();
       double t_pack = 0;
       // 1. segments, per job range (one range below 32k jobs; segments never span ranges)
-      const int T = n_jobs < 32768 ? 1 : 8;
+      // PE_AGG_THREADS (1..16, default 8): host threads planning / packing / copying out a large batch
+      static const int kAggT = [] {
+        const char* e = std::getenv("PE_AGG_THREADS");
+        return e ? std::max(1, std::min(PlanPool::kMax, std::atoi(e))) : 8;
+      }();
+      const int T = n_jobs < 32768 ? 1 : kAggT;
       // Calls of <= kLatJobs jobs are one launch the host waits on through the kernel's flag; up to
       // 2048 jobs with segments of 32 jobs, so a 256-job call spreads its ~40 KB over 8 CUs (one
       // CU's zero-copy reads come in at a few GB/s: 41 KB through one block took ~27 us, 8 blocks
@@ -964,7 +969,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       };
       if (T == 1) plan(0);
       else PlanPool::get().run(T, plan);
-      size_t first[9] = {0};
+      size_t first[PlanPool::kMax + 1] = {0};
       for (int t = 0; t < T; ++t) first[t + 1] = first[t] + segs[t].size();
       const int64_t nseg = (int64_t)first[T];
       ensure_pinned(ctx->a_segoff, (size_t)nseg + 1, "alloc pinned segment offsets");
@@ -988,8 +993,8 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       auto& all = ctx->agg_all;
       all.clear();
       for (int t = 0; t < T; ++t) all.insert(all.end(), segs[t].begin(), segs[t].end());
-      int64_t bad[8];
-      std::fill(bad, bad + 8, INT64_MAX);
+      int64_t bad[PlanPool::kMax];
+      std::fill(bad, bad + PlanPool::kMax, INT64_MAX);
       auto pack = [&](int64_t s0, int64_t s1, int64_t& badv) {
         for (int64_t k = s0; k < s1; ++k) {
           const AggSeg& sg = all[(size_t)k];
@@ -1068,7 +1073,11 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
         // chunks of segments, each packed by the planning pool and launched at once: the kernel of
         // chunk k reads its segments over PCIe while the host packs chunk k + 1, and chunk k - 1's
         // outputs are copied out once its kernel is done (an event per chunk)
-        const int64_t C = T == 1 ? 1 : 8;
+        static const int64_t kChunks = [] {   // PE_AGG_CHUNKS (1..64, default 8): pipeline depth
+          const char* e = std::getenv("PE_AGG_CHUNKS");
+          return e ? std::max<int64_t>(1, std::min<int64_t>(64, std::atoll(e))) : 8;
+        }();
+        const int64_t C = T == 1 ? 1 : kChunks;
         while ((int64_t)ctx->a_ev.size() < C) {
           hipEvent_t e;
           hipchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");

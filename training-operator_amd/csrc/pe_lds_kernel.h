@@ -180,8 +180,14 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
 #pragma unroll
         for (int k = 1; k < L; ++k) {
           const uint32_t pk = entry(o + k);
+          uint32_t ph = pk + 1;
+          // W = 2: the compiler would fuse the two reads into one ds_read2st64_b64, which the LDS serves
+          // at half the rate of two ds_read_b64 (8 vs 2 x 2 cycles: 128 vs 256 B/clk -- counted, the
+          // fused form put the LDS array at 74 cycles per job instead of 42); an opaque index keeps them
+          // apart for one extra address add
+          if constexpr (W == 2) asm("" : "+s"(ph));
           slice_split<W>(plane_rd<W>(lds, pk, lane), g);
-          slice_split<W>(plane_rd<W>(lds, pk + 1, lane), h);
+          slice_split<W>(plane_rd<W>(lds, ph, lane), h);
 #pragma unroll
           for (int i = 0; i < W; ++i) a[i] = h[i] | (g[i] & a[i]);
         }
