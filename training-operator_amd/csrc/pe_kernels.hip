@@ -1350,12 +1350,51 @@ __device__ void hist_cut(TopkShared& s, int need) {
 // smallest, a second 256-bin histogram inside that bin narrows it, and the C keys up to the
 // narrowed cut (C ~ K + 1 + a sub-bin) are placed by rank -- each thread counts the selected keys
 // below its own (keys are unique: the node id is in the low bits) -- instead of a bitonic sort
-// with ~50 block barriers.  Small T, or a cut that still holds > MG_SEL keys, falls back to the
-// bitonic sort of all T.  T <= MG_CAP.  Starts and ends with a block barrier.
+// with ~50 block barriers.  T <= 2(K+1) keys are rank-placed directly; a cut that still holds
+// > MG_SEL keys falls back to the bitonic sort of all T.  T <= MG_CAP.  Starts and ends with a
+// block barrier.
+// Rank placement: the C unique keys of s.sel, each thread t < C counts the keys below its own and
+// writes it to s.keys[rank] if rank <= K.  The count loop reads 16 keys per step (every lane the same
+// address: LDS broadcast) before comparing, so 16 reads are in flight instead of one read latency per
+// key (the one-at-a-time loop was ~11 us of the walk's ~30 us per group at C ~ 300).
+__device__ __forceinline__ void rank_place(TopkShared& s, int C, int K) {
+  for (int t = threadIdx.x; t < C; t += MG_THREADS) {
+    const uint64_t k = s.sel[t];
+    int rank = 0, j = 0;
+    for (; j + 16 <= C; j += 16) {
+      uint64_t v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = s.sel[j + u];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) rank += v[u] < k;
+    }
+    for (; j < C; ++j) rank += s.sel[j] < k;
+    if (rank <= K) s.keys[rank] = k;
+  }
+}
+
+#ifdef PE_WALK_PROF   // topk_sort breakdown (diagnostics build): calls, T, C, bitonic fallbacks, phase ticks
+__device__ unsigned long long topk_prof[8];
+#define TKP(i, v) (threadIdx.x == 0 ? (void)atomicAdd(&topk_prof[i], (unsigned long long)(v)) : (void)0)
+#define TKT(n) unsigned long long tkt##n = wall_clock64()
+#else
+#define TKP(i, v)
+#define TKT(n)
+#endif
 __device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   __syncthreads();
-  if (T > 2 * (K + 1) && K + 1 <= MG_SEL) {
+  TKT(0);
+  TKP(0, 1);
+  TKP(1, T);
+  if (T <= 2 * (K + 1) && T <= MG_SEL) {   // few keys: rank-place them all (no histogram, no bitonic)
+    for (int i = tid; i < T; i += MG_THREADS) s.sel[i] = s.keys[i];
+    __syncthreads();
+    rank_place(s, T, K);
+    __syncthreads();
+    return s.keys;
+  }
+  if (K + 1 <= MG_SEL) {
     uint64_t mn = NO_KEY, mx = 0;
     for (int i = tid; i < T; i += MG_THREADS) {
       mn = umin64(mn, s.keys[i]);
@@ -1412,19 +1451,19 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
     }
     __syncthreads();
     const int C = s.sel_n;
+    TKT(1);
+    TKP(3, C);
+    TKP(4, tkt1 - tkt0);
     if (C <= MG_SEL) {
-      // rank placement into s.keys (its old contents are no longer needed)
-      for (int t = tid; t < C; t += MG_THREADS) {
-        const uint64_t k = s.sel[t];
-        int rank = 0;
-        for (int j = 0; j < C; ++j) rank += s.sel[j] < k;
-        if (rank <= K) s.keys[rank] = k;
-      }
+      rank_place(s, C, K);                 // into s.keys (its old contents are no longer needed)
       __syncthreads();
+      TKT(2);
+      TKP(5, tkt2 - tkt1);
       return s.keys;
     }
   }
   // bitonic sort of all T keys
+  TKP(2, 1);
   uint64_t* sk = s.keys;
   int P = 2;
   while (P < T) P <<= 1;
@@ -1889,6 +1928,11 @@ hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const
             p[3] / n / us, p[4] / n / us, p[6] / n, p[7] / n, p[8] / n);
     fprintf(stderr, "walk prof max: block %.2f us setup %.2f overlay %.2f walk %.2f sort %.2f | rounds %llu T %llu\n",
             p[9] / us, p[15] / us, p[10] / us, p[11] / us, p[12] / us, p[13], p[14]);
+    unsigned long long t[8];
+    (void)hipMemcpyFromSymbol(t, HIP_SYMBOL(topk_prof), sizeof(t));
+    const double c = (double)t[0];
+    fprintf(stderr, "topk_sort: %.0f calls, T %.0f, C %.0f, bitonic %.0f, hist+select %.2f us, rank %.2f us per call\n",
+            c, t[1] / c, t[3] / c, (double)t[2], t[4] / c / us, t[5] / c / us);
   }
 #endif
   return hipGetLastError();
