@@ -397,7 +397,20 @@ def main(argv=None):
             dist.broadcast_object_list(ids, src=0)
             return ids[0]
 
-        cid = new_comm()
+        # a gloo group beside the RCCL one: the fallback exchange and the fallback vote must not
+        # depend on the transport whose set-up failed
+        gloo = dist.new_group(backend="gloo")
+
+        def gloo_exchange(blob: bytes) -> bytes:
+            parts = [None] * world
+            dist.all_gather_object(parts, blob, group=gloo)
+            return b"".join(parts)
+
+        def first_error(err):
+            """Every rank's set-up error (None = fine) -> the first one, on every rank."""
+            errs = [None] * world
+            dist.all_gather_object(errs, err, group=gloo)
+            return next((e for e in errs if e is not None), None)
 
         def barrier():
             dist.barrier()
@@ -423,6 +436,9 @@ def main(argv=None):
         def barrier():
             pass
 
+        def first_error(err):
+            return err
+
         def allmax(x):
             return x
 
@@ -432,12 +448,35 @@ def main(argv=None):
         def allgather(x):
             return [x]
 
+    fallbacks = []
+
+    def make_engine(**kw):
+        """An engine on this rank's GPU with a fresh RCCL communicator (world > 1).  If the RCCL set-up
+        fails on any rank (pe_create returns PE_ERCCL within PE_RCCL_INIT_TIMEOUT_S), every rank builds
+        its engine with a gloo all-gather of the candidate blobs instead -- the same sharded greedy,
+        windows exchanged through host memory (not pipelined) -- and the JSON line says so."""
+        err = None
+        try:
+            if world > 1 and rank == world - 1 and os.environ.get("PE_BENCH_SIMULATE_RCCL_FAIL"):   # (test hook)
+                new_comm()
+                raise RuntimeError("simulated RCCL set-up failure (PE_BENCH_SIMULATE_RCCL_FAIL)")
+            e = Engine(device, rank=rank, world_size=world, comm=new_comm(), exchange=exchange, **kw)
+        except Exception as ex:   # noqa: BLE001 -- any set-up failure takes the fallback
+            e, err = None, f"rank {rank}: {type(ex).__name__}: {ex}"
+        err = first_error(err)
+        if err is None:
+            return e
+        if e is not None:
+            e.close()
+        fallbacks.append(err)
+        return Engine(device, rank=rank, world_size=world, comm=None, exchange=gloo_exchange, **kw)
+
     N = args.nodes
     J = args.fit_jobs * (world if args.scaling == "weak" else 1)
     inv = synth.make_inventory(N, synth.SEED["cfg5"], gpu_frac=0.2)
-    eng = Engine(device, rank=rank, world_size=world, comm=cid, exchange=exchange, max_nodes=N, topk=args.topk,
-                 window_groups=args.window_groups, window_pods=args.window_pods, fit_path_mask=args.fit_path_mask,
-                 greedy_flags=args.greedy_flags, resort_nodes=args.resort_nodes)
+    eng = make_engine(max_nodes=N, topk=args.topk, window_groups=args.window_groups, window_pods=args.window_pods,
+                      fit_path_mask=args.fit_path_mask, greedy_flags=args.greedy_flags,
+                      resort_nodes=args.resort_nodes)
     eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     b, e = eng.shard_range()
     Ns = e - b
@@ -493,7 +532,11 @@ def main(argv=None):
                    "shard_nodes": Ns, "shard_nodes_per_rank": shards, "rccl_ranks": rccl,
                    "parallelism": f"node-shard x{world}" + (" (host exchange rehearsal)" if host_exchange and world > 1
                                                             else ""),
-                   "feasible_pairs": feasible},
+                   "feasible_pairs": feasible,
+                   "greedy_exchange": ("none (one GPU)" if world == 1
+                                       else f"gloo host exchange: RCCL set-up failed ({fallbacks[0]})" if fallbacks
+                                       else "gloo host exchange (rehearsal)" if host_exchange
+                                       else "RCCL all-gather + device merge")},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": prof["traffic"],
                      "traffic_source": prof["traffic_source"], "kernel_ms": kern_ms,
@@ -719,9 +762,9 @@ def main(argv=None):
             progress(cfg)
             cinv = synth.make_inventory(n_nodes, synth.SEED[cfg[:4]], gpu_frac)
             cb = synth.make_jobs(n_jobs, synth.SEED[cfg[:4]], mix)
-            ce = Engine(device, rank=rank, world_size=world, comm=new_comm(), exchange=exchange, max_nodes=n_nodes,
-                        topk=args.topk, window_groups=args.window_groups, window_pods=args.window_pods,
-                        greedy_flags=args.greedy_flags, resort_nodes=args.resort_nodes)
+            ce = make_engine(max_nodes=n_nodes, topk=args.topk, window_groups=args.window_groups,
+                             window_pods=args.window_pods, greedy_flags=args.greedy_flags,
+                             resort_nodes=args.resort_nodes)
             ce.load_nodes(cinv.cap, cinv.used, cinv.labels, cinv.island)
             ce.place_batch(cb)                       # warm-up
             ce.reset_stats()

@@ -5,7 +5,9 @@ multi-rank bench runs).
    through torch.distributed.run; both ranks share this box's one GPU and exchange the greedy
    windows' candidate lists over gloo (PE_BENCH_EXCHANGE=host).  Its results must equal the
    one-rank run of the same workload: feasible pairs of the fit mask, placed jobs of every greedy
-   line, and the node shards must partition the inventory.
+   line, and the node shards must partition the inventory.  The last rank's engine set-up is made to
+   fail (PE_BENCH_SIMULATE_RCCL_FAIL): the ranks vote over gloo and all rebuild their engines with the
+   gloo exchange, which the JSON line reports (config.greedy_exchange).
 2. A communicator whose peers never arrive returns PE_ERCCL after PE_RCCL_INIT_TIMEOUT_S instead of
    blocking in ncclCommInitRank (non-blocking RCCL set-up, pe_engine.cpp nccl_settle)."""
 import json
@@ -54,8 +56,11 @@ def _bench(gpus, extra_env):
 @pytest.mark.timeout(900)
 def test_bench_two_ranks_matches_one():
     one = _bench(1, {})
-    two = _bench(2, {"PE_BENCH_EXCHANGE": "host"})
+    # the last rank's engine set-up fails (simulated): every rank falls back to the gloo exchange
+    two = _bench(2, {"PE_BENCH_EXCHANGE": "host", "PE_BENCH_SIMULATE_RCCL_FAIL": "1"})
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert one["config"]["greedy_exchange"] == "none (one GPU)"
+    assert "RCCL set-up failed" in two["config"]["greedy_exchange"] and "simulated" in two["config"]["greedy_exchange"]
     cfg1, cfg2 = one["config"], two["config"]
     assert sum(cfg2["shard_nodes_per_rank"]) == cfg2["nodes"] == 100000 and len(cfg2["shard_nodes_per_rank"]) == 2
     assert cfg2["feasible_pairs"] == cfg1["feasible_pairs"] > 0

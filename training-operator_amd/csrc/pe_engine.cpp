@@ -1004,18 +1004,19 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
           h.nj = sg.nj;
           h.ng = sg.ng;
           h.nc = sg.nc;
+          const int32_t g0 = job_group_off[sg.j0];
+          h.g0 = g0;
+          h.c0 = sg.ng > 0 ? gco[g0] : 0;
           std::memcpy(b, &h, sizeof(h));
           int64_t off[7];
           pe::agg_seg_layout(sg.nj, sg.ng, sg.nc, v1, off);
-          const int32_t g0 = job_group_off[sg.j0];
-          int32_t* jl = reinterpret_cast<int32_t*>(b + off[0]);
-          for (int32_t i = 0; i <= sg.nj; ++i) jl[i] = job_group_off[sg.j0 + i] - g0;
+          // offsets copied as they are (the kernel rebases by h.g0 / h.c0): every section is a memcpy
+          std::memcpy(b + off[0], job_group_off + sg.j0, (size_t)(sg.nj + 1) * 4);
           if (v1) std::memcpy(b + off[1], min_member + sg.j0, (size_t)sg.nj * 4);
           if (sg.ng > 0) {
             std::memcpy(b + off[2], group_replicas + g0, (size_t)sg.ng * 4);
-            const int32_t c0 = gco[g0];
-            int32_t* gl = reinterpret_cast<int32_t*>(b + off[3]);
-            for (int32_t i = 0; i <= sg.ng; ++i) gl[i] = gco[g0 + i] - c0;
+            const int32_t c0 = h.c0;
+            std::memcpy(b + off[3], gco + g0, (size_t)(sg.ng + 1) * 4);
             if (sg.nc > 0) {
               const int64_t* q = cont_req + (int64_t)c0 * pe::D;
               const int64_t nq = (int64_t)sg.nc * pe::D;
@@ -1029,7 +1030,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
                   }
             }
           } else {
-            reinterpret_cast<int32_t*>(b + off[3])[0] = 0;
+            reinterpret_cast<int32_t*>(b + off[3])[0] = 0;   // (h.c0 = 0)
           }
         }
       };

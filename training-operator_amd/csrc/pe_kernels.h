@@ -65,12 +65,15 @@ constexpr int64_t AGG_SEG_BYTES = 48 * 1024;
 struct AggSegHdr {
   int64_t j0;            // first job of the segment (index in the call's batch)
   int32_t nj, ng, nc;    // jobs, groups, containers
-  int32_t pad_[3];
+  int32_t g0, c0;        // the segment's first group / container: its jgo / gco sections hold the caller's
+                         // absolute offsets (copied as they are), the kernel rebases
+  int32_t pad_;
 };
 static_assert(sizeof(AggSegHdr) == 32, "AggSegHdr must be 32 B");
 __host__ __device__ inline int64_t agg_r16(int64_t x) { return (x + 15) & ~int64_t(15); }
-// byte offsets of the sections in a segment: [0] jgo (nj+1 i32), [1] min_member (nj i32, V1 only),
-// [2] replicas (ng i32), [3] gco (ng+1 i32), [4] req (nc x 4 i64), [5] flags (nc u8), [6] = size
+// byte offsets of the sections in a segment: [0] jgo (nj+1 i32, absolute group ids), [1] min_member
+// (nj i32, V1 only), [2] replicas (ng i32), [3] gco (ng+1 i32, absolute container ids), [4] req
+// (nc x 4 i64), [5] flags (nc u8), [6] = size
 __host__ __device__ inline void agg_seg_layout(int64_t nj, int64_t ng, int64_t nc, bool v1, int64_t off[7]) {
   off[0] = (int64_t)sizeof(AggSegHdr);
   off[1] = off[0] + agg_r16((nj + 1) * 4);

@@ -150,9 +150,10 @@ __device__ __forceinline__ void agg_segment(int mode, const uint8_t* seg, int64_
   if (t < h.nj) {
     const int32_t* jgo = reinterpret_cast<const int32_t*>(seg + off[0]);
     const int32_t mm = mode == 1 ? reinterpret_cast<const int32_t*>(seg + off[1])[t] : 0;
-    const AggJob o = agg_job(mode, mm, jgo[t], jgo[t + 1], reinterpret_cast<const int32_t*>(seg + off[2]),
-                             reinterpret_cast<const int32_t*>(seg + off[3]), reinterpret_cast<const int64_t*>(seg + off[4]),
-                             seg + off[5]);
+    // the offsets are the caller's (absolute): rebase the group and container sections instead
+    const AggJob o = agg_job(mode, mm, jgo[t] - h.g0, jgo[t + 1] - h.g0, reinterpret_cast<const int32_t*>(seg + off[2]),
+                             reinterpret_cast<const int32_t*>(seg + off[3]),
+                             reinterpret_cast<const int64_t*>(seg + off[4]) - (int64_t)h.c0 * D, seg + off[5] - h.c0);
     int64_t oo[4];
     agg_out_layout(J, oo);
     const int64_t j = h.j0 + t;
