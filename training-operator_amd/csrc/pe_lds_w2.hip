@@ -3,6 +3,8 @@
 
 namespace pe {
 
-const void* lds_kernel_w2(int n4, int n3, int n2, int n1) { return lds_kernel_for<2>(n4, n3, n2, n1); }
+const void* lds_kernel_w2(int n4, int n3, int n2, int n1, bool sa) {
+  return lds_kernel_for<2>(n4, n3, n2, n1, sa);
+}
 
 }  // namespace pe
