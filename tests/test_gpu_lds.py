@@ -56,14 +56,12 @@ def inventory(N, seed, gpu_frac=0.4):
     return inv
 
 
-def run(inv, req, need, W=None, maxl=None, fit_path_mask=LDS_ONLY, rank=0, world=1, sorted_field=None):
+def run(inv, req, need, W=None, maxl=None, fit_path_mask=LDS_ONLY, rank=0, world=1):
     env = {}
     if W is not None:
         env["PE_LDS_W"] = str(W)
     if maxl is not None:
         env["PE_LDS_MAXL"] = str(maxl)
-    if sorted_field is not None:
-        env["PE_LDS_SORTED"] = "1" if sorted_field else "0"
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -119,25 +117,6 @@ def test_lds_level_counts(maxl):
     need[:] = (rng.integers(0, 8, J).astype(np.uint32) << 1) | (req[:, 2] > 0)
     e, counts = run(inv, req, need, maxl=maxl)
     check(e, counts, inv, req, need)
-    e.close()
-
-
-@pytest.mark.parametrize("W", [1, 2, 4])
-@pytest.mark.parametrize("shape", ["cpu400", "unique_mem", "wide", "adversarial", "needs", "extremes"])
-def test_lds_sorted_field_vs_oracle(shape, W, capfd):
-    """The sorted-field kernels (PE_LDS_SORTED=1): the field with the most values has no digit planes --
-    the jobs run in ascending threshold of it and each wave lowers one register plane -- same bits as
-    the oracle, on ragged blocks, with job rows read from the codes (the mask stays in job order)."""
-    N, J = 20011, 1500
-    inv = inventory(N, 91 + W)
-    req, need = batch(shape, J, 93 + W)
-    os.environ["PE_LDS_DEBUG"] = "1"
-    try:
-        e, counts = run(inv, req, need, W=W, sorted_field=True)
-    finally:
-        os.environ.pop("PE_LDS_DEBUG", None)
-    check(e, counts, inv, req, need)
-    assert " sorted |" in capfd.readouterr().err
     e.close()
 
 

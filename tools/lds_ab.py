@@ -43,7 +43,7 @@ def main():
         req, need = batch(shape)
         ref = None
         for cfg in configs:
-            for k in ("PE_LDS_W", "PE_LDS_MAXL", "PE_LDS_NOSORT", "PE_LDS_R"):
+            for k in ("PE_LDS_W", "PE_LDS_MAXL", "PE_LDS_NOSORT", "PE_LDS_R", "PE_LDS_SORTED"):
                 os.environ.pop(k, None)
             os.environ.update(cfg)
             e = Engine(0, max_nodes=N, fit_path_mask=64 if shape != "cfg5" else 0)

@@ -257,7 +257,7 @@ struct pe_ctx {
   // LDS digit-plane path (pe_kernels.h LdsSpec): spec, node-block geometry, codes, ranks
   pe::LdsSpec lds{};
   int lds_W = 4;                          // u32 words per lane per plane: block = 2048 W nodes
-  int lds_shape[5] = {0, 0, 0, 0, 0};     // fields with 4 / 3 / 2 / 1 digit levels, sorted field (kernel template)
+  int lds_shape[4] = {0, 0, 0, 0};        // fields with 4 / 3 / 2 / 1 digit levels (kernel template)
   int64_t lds_nblk = 0, lds_R = 1, lds_Tpad = 0, lds_npad = 0, lds_pitch = 0;   // pitch in u64 words
   DevBuf<pe::LdsSpec> lds_spec_d;
   DevBuf<int64_t> lds_vals;
@@ -1513,35 +1513,20 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   int forced_w = 0;
   if (const char* e = std::getenv("PE_LDS_W")) forced_w = std::atoi(e);
   const int64_t nneed = (int64_t)needs.size();
-  // Sorted field (PE_LDS_SORTED=1, study knob): the field with the most values gets no digit planes; the
-  // jobs are sorted by its threshold and each wave lowers one VGPR plane of it as the thresholds rise
-  // (pe_lds_kernel.h, SA).  It moves to the end of fdim; nd = the digit fields.
-  int nd = sp.nf;
-  bool sa = false;
-  if (const char* e = std::getenv("PE_LDS_SORTED"); e && std::atoi(e) == 1 && sp.nf >= 1) {
-    int a = 0;
-    for (int i = 1; i < sp.nf; ++i)
-      if (vals[fdim[i]].size() > vals[fdim[a]].size()) a = i;
-    if (vals[fdim[a]].size() >= 16 && vals[fdim[a]].size() < (1u << 19)) {   // rank + 1 < 2^(32 - log2 S)
-      std::swap(fdim[a], fdim[sp.nf - 1]);
-      nd = sp.nf - 1;
-      sa = true;
-    }
-  }
   int bestW = 0, bestL[pe::LD_MAXF] = {1, 1, 1, 1};
   int64_t bestB[pe::LD_MAXF] = {0, 0, 0, 0};
   double bestCost = 1e300;
   for (int W : {4, 2, 1}) {
     if (forced_w && W != forced_w) continue;
-    const int64_t budget = (163840 - (sa ? 2048 * W * 4 : 0)) / (256 * W);   // (SA: the node list)
+    const int64_t budget = 163840 / (256 * W);
     int combos = 1;
-    for (int i = 0; i < nd; ++i) combos *= maxl;
+    for (int i = 0; i < sp.nf; ++i) combos *= maxl;
     for (int cix = 0; cix < combos; ++cix) {
       int L[pe::LD_MAXF];
       int64_t B[pe::LD_MAXF];
       int64_t planes = nneed, reads = 1, entries = 0;
       bool ok = true;
-      for (int i = 0, x = cix; i < nd; ++i, x /= maxl) {
+      for (int i = 0, x = cix; i < sp.nf; ++i, x /= maxl) {
         L[i] = 1 + x % maxl;
         const int64_t m = (int64_t)vals[fdim[i]].size();
         if (L[i] > 1 && m < 4) L[i] = 1;
@@ -1550,17 +1535,17 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
         reads += 2 * L[i] - 1;
         entries += L[i];
       }
-      if (!ok || entries > (sa ? pe::LD_SA_MAXE : pe::LD_NEED_SLOT) || planes > budget || planes > 65535) continue;
+      if (!ok || entries > pe::LD_NEED_SLOT || planes > budget || planes > 65535) continue;
       // per job and 8192 nodes, in CU cycles: LDS plane reads (b128 / b64 / read2st64_b64: 4 per KiB,
       // b32: 8) -- the kernel's bound -- plus its VALU at ~0.6 CU cycles per wave instruction: per
       // entry a readlane half and an address, ~6 fixed, and the three-input combines (2 per extra level
       // and word, 4 per 8192 nodes whatever W)
-      const double valu = (4.0 / W) * (1.5 * (double)entries + 6.0) + 4.0 * (double)(reads - 1 - nd + nd / 2);
+      const double valu = (4.0 / W) * (1.5 * (double)entries + 6.0) + 4.0 * (double)(reads - 1 - sp.nf + sp.nf / 2);
       const double cost = reads * (W == 1 ? 8.0 : 4.0) + 0.625 * valu;
       if (cost < bestCost - 1e-9) {
         bestCost = cost;
         bestW = W;
-        for (int i = 0; i < nd; ++i) {
+        for (int i = 0; i < sp.nf; ++i) {
           bestL[i] = L[i];
           bestB[i] = B[i];
         }
@@ -1568,26 +1553,25 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
     }
   }
   if (!bestW) return false;
-  if (sa) bestL[nd] = 0;   // the sorted field: no digit levels, last
-  // digit fields in the kernel's order: four-level first, then three-, two-, single-level
+  // fields in the kernel's order: three-level first, then two-level, then single-level
   {
     int ord[pe::LD_MAXF] = {0, 1, 2, 3};
-    std::stable_sort(ord, ord + nd, [&](int x, int y) { return bestL[x] > bestL[y]; });
+    std::stable_sort(ord, ord + sp.nf, [&](int x, int y) { return bestL[x] > bestL[y]; });
     int d2[pe::LD_MAXF], L2[pe::LD_MAXF];
     int64_t B2[pe::LD_MAXF];
-    for (int i = 0; i < nd; ++i) {
+    for (int i = 0; i < sp.nf; ++i) {
       d2[i] = fdim[ord[i]];
       L2[i] = bestL[ord[i]];
       B2[i] = bestB[ord[i]];
     }
-    for (int i = 0; i < nd; ++i) {
+    for (int i = 0; i < sp.nf; ++i) {
       fdim[i] = d2[i];
       bestL[i] = L2[i];
       bestB[i] = B2[i];
     }
   }
-  int shape[5] = {0, 0, 0, 0, sa ? 1 : 0};
-  for (int i = 0; i < nd; ++i) ++shape[4 - bestL[i]];
+  int shape[4] = {0, 0, 0, 0};
+  for (int i = 0; i < sp.nf; ++i) ++shape[4 - bestL[i]];
   // level specs, plane bases
   int32_t p = 0;
   int64_t voff = 0;
@@ -1626,7 +1610,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   const int W = bestW;
   const int64_t S = 2048 * W;
   const int64_t nblk = (ctx->Ns + S - 1) / S;
-  const int64_t lds_bytes = (int64_t)sp.nplanes * S / 8 + (sa ? S * 4 : 0);
+  const int64_t lds_bytes = (int64_t)sp.nplanes * S / 8;
   const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(2, 163840 / std::max<int64_t>(lds_bytes, 1)));
   const int64_t slots = (int64_t)ctx->num_cu * per_cu;
   // job phases R: every workgroup builds its block's planes before its share (1/R) of the jobs, so
@@ -1664,21 +1648,8 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
       }
     }
     c[pe::LD_NEED_SLOT] = (uint16_t)(sp.need_pbase + bd.rank[4][j]);
-    if (sa) {   // the sorted field's threshold (u32 dword LD_SA_C) and the job's mask row (dword LD_SA_ROW)
-      const uint32_t cA = bd.rank[fdim[nd]][j] + 1, row = (uint32_t)j;
-      std::memcpy(c + 2 * pe::LD_SA_C, &cA, 4);
-      std::memcpy(c + 2 * pe::LD_SA_ROW, &row, 4);
-    }
   }
   });
-  // SA: the kernel's job order is ascending threshold of the sorted field (virtual index v -> job ord[v])
-  std::vector<uint32_t> ordv;
-  if (sa) {
-    ordv.resize((size_t)n_jobs);
-    std::iota(ordv.begin(), ordv.end(), 0u);
-    const std::vector<uint32_t>& rk = bd.rank[fdim[nd]];
-    std::stable_sort(ordv.begin(), ordv.end(), [&](uint32_t x, uint32_t y) { return rk[x] < rk[y]; });
-  }
   // slot (r * 16 + w) * Tpad + t = job r + R (w + 16 t), the t-th of wave w's run in phase r (the
   // kernel's consumption order); each slot's job in lds_rows for the counts
   std::vector<uint16_t> codes((size_t)(R * 16 * Tpad * pe::LD_CODE), 0);
@@ -1689,7 +1660,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
       const int64_t r = v / 16, w = v % 16, j0 = r + R * w;
       const int64_t T = j0 < n_jobs ? (n_jobs - j0 + 16 * R - 1) / (16 * R) : 0;
       for (int64_t t = 0; t < T; ++t, ++pos) {
-        const uint32_t j = sa ? ordv[(size_t)(j0 + 16 * R * t)] : (uint32_t)(j0 + 16 * R * t);
+        const uint32_t j = (uint32_t)(j0 + 16 * R * t);
         std::memcpy(codes.data() + (size_t)((v * Tpad + t) * pe::LD_CODE), jc.data() + (size_t)j * pe::LD_CODE,
                     pe::LD_CODE * 2);
         rows[(size_t)(v * Tpad + t)] = j;
@@ -1698,15 +1669,15 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
     if (pos != n_jobs) raise(PE_EINVAL, "lds: run lengths do not cover the batch");
   }
   if (std::getenv("PE_LDS_DEBUG")) {   // diagnostics: the chosen configuration
-    std::fprintf(stderr, "lds: W %d nblk %lld R %lld planes %d need %d fold %d%s |", W, (long long)nblk, (long long)R,
-                 sp.nplanes, sp.nneed, sp.nfold, sa ? " sorted" : "");
+    std::fprintf(stderr, "lds: W %d nblk %lld R %lld planes %d need %d fold %d |", W, (long long)nblk, (long long)R,
+                 sp.nplanes, sp.nneed, sp.nfold);
     for (int i = 0; i < sp.nf; ++i)
       std::fprintf(stderr, " dim %d m %lld L %d B %u", sp.dim[i], (long long)sp.m[i], sp.L[i], sp.mod[i][0]);
     std::fprintf(stderr, "\n");
   }
   ctx->lds = sp;
   ctx->lds_W = W;
-  for (int i = 0; i < 5; ++i) ctx->lds_shape[i] = shape[i];
+  for (int i = 0; i < 4; ++i) ctx->lds_shape[i] = shape[i];
   ctx->lds_nblk = nblk;
   ctx->lds_R = R;
   ctx->lds_Tpad = Tpad;

@@ -218,11 +218,6 @@ constexpr int LD_MAXL = 4;        // digit levels per field
 constexpr int LD_MAXNEED = 64;    // distinct label needs
 constexpr int LD_CODE = 16;       // u16 plane indices per job: field f's levels at lds_field_off(f) + k; need at 15
 constexpr int LD_NEED_SLOT = 15;
-// Sorted-field batches (fit_mask_lds_kernel<..., SA = true>): the spec's LAST field has no digit planes
-// (L = 0); jobs reach the kernel in ascending threshold of it, each code holding the threshold c (u32 at
-// dword LD_SA_C) and the job's mask row (u32 at dword LD_SA_ROW); the digit fields' entries end before
-// entry 2 LD_SA_C.
-constexpr int LD_SA_C = 5, LD_SA_ROW = 6, LD_SA_MAXE = 2 * LD_SA_C;
 // First code entry of field fi when the fields are ordered N4 four-level, N3 three-level, N2 two-level,
 // then one-level (the kernel's template shape; the sum of the levels must stay <= LD_NEED_SLOT).
 __host__ __device__ constexpr int lds_field_off(int fi, int n4, int n3, int n2) {
@@ -261,10 +256,9 @@ hipError_t launch_node_ranks(hipStream_t s, const int64_t* res, int64_t stride, 
 // Mask row-major (PE_MASK_ROWS): row j at mask + j * pitch_bytes, block blk's S/8 bytes at + blk * S/8.
 // slots: [R * 16 * Tpad] u32 count slots (zeroed by the caller), slot (r * 16 + w) * Tpad + t = job
 // r + R (w + 16 t); launch_lds_counts turns them into per-job u64 counts through the slots' rows.  spec: device copy;
-// nplanes = spec->nplanes.  shape = {N4, N3, N2, N1, SA}: fields 0 .. N4-1 have 4 digit levels (W >= 2
-// only), the next N3 three, then N2 two, then N1 one; SA != 0: the spec's last field is the sorted field
-// (LD_SA_C).  The mask has J rows.
-hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[5], const LdsSpec* spec, int nplanes,
+// nplanes = spec->nplanes.  shape = {N4, N3, N2, N1}: fields 0 .. N4-1 have 4 digit levels (W >= 2
+// only), the next N3 three, then N2 two, the last N1 one.  The mask has J rows.
+hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[4], const LdsSpec* spec, int nplanes,
                                const uint32_t* ranks, int64_t npad, const uint32_t* aux, int64_t nblk,
                                const uint16_t* codes, int64_t J, int64_t R, int64_t Tpad, int64_t pitch_bytes,
                                uint8_t* mask, uint32_t* slots);

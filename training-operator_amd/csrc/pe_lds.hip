@@ -53,17 +53,16 @@ hipError_t launch_node_ranks(hipStream_t s, const int64_t* res, int64_t stride, 
 }
 
 // The fit kernel of the batch's shape and block size (pe_lds_kernel.h, one translation unit per W).
-hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[5], const LdsSpec* spec, int nplanes,
+hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[4], const LdsSpec* spec, int nplanes,
                                const uint32_t* ranks, int64_t npad, const uint32_t* aux, int64_t nblk,
                                const uint16_t* codes, int64_t J, int64_t R, int64_t Tpad, int64_t pitch_bytes,
                                uint8_t* mask, uint32_t* slots) {
   if (J <= 0 || nblk <= 0 || R <= 0) return hipSuccess;
-  const bool sa = shape[4] != 0;   // sorted field: its node list (4 B per node) after the planes
-  const size_t lds = (size_t)nplanes * 2048 * W / 8 + (sa ? (size_t)2048 * W * 4 : 0);
+  const size_t lds = (size_t)nplanes * 2048 * W / 8;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const void* fn = W == 1   ? lds_kernel_w1(shape[0], shape[1], shape[2], shape[3], sa)
-                   : W == 2 ? lds_kernel_w2(shape[0], shape[1], shape[2], shape[3], sa)
-                   : W == 4 ? lds_kernel_w4(shape[0], shape[1], shape[2], shape[3], sa)
+  const void* fn = W == 1   ? lds_kernel_w1(shape[0], shape[1], shape[2], shape[3])
+                   : W == 2 ? lds_kernel_w2(shape[0], shape[1], shape[2], shape[3])
+                   : W == 4 ? lds_kernel_w4(shape[0], shape[1], shape[2], shape[3])
                             : nullptr;
   if (!fn) return hipErrorInvalidValue;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

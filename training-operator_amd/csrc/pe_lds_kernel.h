@@ -63,7 +63,7 @@ __device__ __forceinline__ typename LdVec<W>::T plane_rd(const uint32_t* lds, ui
 //     one 64-B request per batch instead of 16 scattered 8-B atomics -- at W = 1 those were ~12 % of
 //     the kernel's HBM traffic); lds_counts_kernel maps the slots back to jobs.  Past the wave's last
 //     job the batch's slices are not stored (uniform branch).
-template <int W, int N4, int N3, int N2, int N1, bool SA>
+template <int W, int N4, int N3, int N2, int N1>
 __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec* __restrict__ spp,
                                                                   const uint32_t* __restrict__ ranks, int64_t npad,
                                                                   const uint32_t* __restrict__ aux, int64_t nblk,
@@ -124,30 +124,6 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
       if (lane == 0) *reinterpret_cast<uint64_t*>(lds + (sp.need_pbase + i) * WPP + 2 * g) = b;
     }
   }
-  // SA (sorted field, the spec's last field, no digit planes): the block's nodes as (rank << NB) | node
-  // after the planes, sorted ascending in LDS (bitonic, unique keys) -- each wave walks this list as its
-  // jobs' thresholds rise (below)
-  constexpr int NB = W == 1 ? 11 : W == 2 ? 12 : 13;   // log2(S)
-  uint32_t* const lst = lds + sp.nplanes * WPP;
-  if constexpr (SA) {
-    const uint32_t* rkA = ranks + (int64_t)(sp.nf - 1) * npad + n0;
-    for (int i = tid; i < S; i += LD_THREADS) lst[i] = (rkA[i] << NB) | (uint32_t)i;
-    __syncthreads();
-    for (int k = 2; k <= S; k <<= 1)
-      for (int jj = k >> 1; jj > 0; jj >>= 1) {
-        for (int i = tid; i < S; i += LD_THREADS) {
-          const int ixj = i ^ jj;
-          if (ixj > i) {
-            const uint32_t a = lst[i], b = lst[ixj];
-            if ((a > b) == ((i & k) == 0)) {
-              lst[i] = b;
-              lst[ixj] = a;
-            }
-          }
-        }
-        __syncthreads();
-      }
-  }
   __syncthreads();
 
   // 3. the jobs of this wave: j = r + R (wave + 16 t), t < T.  Their codes are contiguous (the t-major
@@ -177,14 +153,6 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
   // row).  A batch is then one basic block -- job K + 1's plane reads overlap job K's combines -- and
   // the compiler's wait for the code load counts exactly the batch's 16 stores behind it (with
   // conditional stores it drained every store of the batch, vmcnt(0), once per batch).
-  // SA: this wave's jobs come in ascending threshold c of the sorted field, so its plane GE(c) is kept in
-  // VGPRs and only lowered: before each job the list's nodes of rank < c are cleared (each node once per
-  // wave: <= S clears over the whole run) -- the field costs no plane reads per job
-  uint32_t run[W];
-#pragma unroll
-  for (int i = 0; i < W; ++i) run[i] = ~0u;
-  int ptr = 0;
-  uint32_t nx = SA ? (uint32_t)__builtin_amdgcn_readfirstlane((int)lst[0]) : 0u;
   uint2 cv = cb[lane];
   // (wait for the first batch's codes here, once: left pending into the loop, the header would merge
   // that pending load with the latch's state and wait vmcnt(0) -- every store drained -- per batch)
@@ -194,41 +162,15 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
     const uint2 cur = cv;
     cv = cb[min<int64_t>(t0 + 16, Tpad - 16) * (LD_CODE / 4) + lane];   // next batch, in flight meanwhile
     uint32_t p[16];
-    // SA, first the batch's 16 sorted-field planes (the only branches of a batch: a uniform loop per job
-    // that runs ~S / (jobs of the wave) times on average), then the branch-free job bodies
-    uint32_t runs[SA ? 16 : 1][W];
-    if constexpr (SA) {
-#pragma unroll
-      for (int K = 0; K < 16; ++K) {
-        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cur.y, 4 * K + LD_SA_C / 2);   // dword 5
-        while ((nx >> NB) < c) {
-          const uint32_t node = nx & (S - 1);
-          if (lane == (int)(node / (32 * W))) {
-#pragma unroll
-            for (int i = 0; i < W; ++i)
-              if (i == (int)((node >> 5) % W)) run[i] &= ~(1u << (node & 31));
-          }
-          ++ptr;
-          nx = ptr < S ? (uint32_t)__builtin_amdgcn_readfirstlane((int)lst[ptr]) : ~0u;
-        }
-#pragma unroll
-        for (int i = 0; i < W; ++i) runs[K][i] = run[i];
-      }
-    }
 #pragma unroll
     for (int K = 0; K < 16; ++K) {
-      const int64_t j = SA ? (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)cur.x, 4 * K + LD_SA_ROW / 2)   // dword 6
-                           : j0 + step * (t0 + K);
+      const int64_t j = j0 + step * (t0 + K);
       auto entry = [&](int e) -> uint32_t {                           // u16 entry e of job K
         const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)((e & 2) ? cur.y : cur.x), 4 * K + e / 4);
         return (e & 1) ? d >> 16 : d & 0xFFFFu;
       };
       uint32_t f[W];
       slice_split<W>(plane_rd<W>(lds, entry(LD_NEED_SLOT), lane), f);
-      if constexpr (SA) {
-#pragma unroll
-        for (int i = 0; i < W; ++i) f[i] &= runs[K][i];
-      }
 #pragma unroll
       for (int fi = 0; fi < N4 + N3 + N2 + N1; ++fi) {          // unrolled: L and the entries are constants
         const int L = fi < N4 ? 4 : fi < N4 + N3 ? 3 : fi < N4 + N3 + N2 ? 2 : 1;
@@ -266,8 +208,7 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
 }
 
 // Every field shape (N4, N3, N2, N1) with N4 + N3 + N2 + N1 <= LD_MAXF whose entries fit the code
-// (4 N4 + 3 N3 + 2 N2 + N1 <= LD_NEED_SLOT): 35 without four-level fields, 34 with.  Sorted-field
-// kernels (SA) for the shapes of <= 3 digit fields whose entries end before LD_SA_MAXE: 20 + 13.
+// (4 N4 + 3 N3 + 2 N2 + N1 <= LD_NEED_SLOT): 35 without four-level fields, 34 with.
 #define PE_LDS_SHAPES3(X, W)                                                                             \
   X(W, 0, 0, 0, 0) X(W, 0, 0, 0, 1) X(W, 0, 0, 0, 2) X(W, 0, 0, 0, 3) X(W, 0, 0, 0, 4) X(W, 0, 0, 1, 0)  \
   X(W, 0, 0, 1, 1) X(W, 0, 0, 1, 2) X(W, 0, 0, 1, 3) X(W, 0, 0, 2, 0) X(W, 0, 0, 2, 1) X(W, 0, 0, 2, 2)  \
@@ -284,38 +225,22 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
   X(W, 2, 0, 1, 1) X(W, 2, 0, 2, 0) X(W, 2, 1, 0, 0) X(W, 2, 1, 0, 1) X(W, 2, 1, 1, 0) X(W, 2, 2, 0, 0)  \
   X(W, 3, 0, 0, 0) X(W, 3, 0, 0, 1) X(W, 3, 0, 1, 0) X(W, 3, 1, 0, 0)
 
-#define PE_LDS_SA_SHAPES3(X, W)                                                                          \
-  X(W, 0, 0, 0, 0) X(W, 0, 0, 0, 1) X(W, 0, 0, 0, 2) X(W, 0, 0, 0, 3) X(W, 0, 0, 1, 0) X(W, 0, 0, 1, 1)  \
-  X(W, 0, 0, 1, 2) X(W, 0, 0, 2, 0) X(W, 0, 0, 2, 1) X(W, 0, 0, 3, 0) X(W, 0, 1, 0, 0) X(W, 0, 1, 0, 1)  \
-  X(W, 0, 1, 0, 2) X(W, 0, 1, 1, 0) X(W, 0, 1, 1, 1) X(W, 0, 1, 2, 0) X(W, 0, 2, 0, 0) X(W, 0, 2, 0, 1)  \
-  X(W, 0, 2, 1, 0) X(W, 0, 3, 0, 0)
-
-#define PE_LDS_SA_SHAPES4(X, W)                                                                          \
-  X(W, 1, 0, 0, 0) X(W, 1, 0, 0, 1) X(W, 1, 0, 0, 2) X(W, 1, 0, 1, 0) X(W, 1, 0, 1, 1) X(W, 1, 0, 2, 0)  \
-  X(W, 1, 1, 0, 0) X(W, 1, 1, 0, 1) X(W, 1, 1, 1, 0) X(W, 1, 2, 0, 0) X(W, 2, 0, 0, 0) X(W, 2, 0, 0, 1)  \
-  X(W, 2, 0, 1, 0)
-
-// The kernel of block size W for shape (n4, n3, n2, n1) and sorted field sa; nullptr for a shape outside
-// the tables (four-level shapes are built for W >= 2 only).
+// The kernel of block size W for shape (n4, n3, n2, n1); nullptr for a shape outside the table
+// (four-level shapes are built for W >= 2 only).
 template <int W>
-const void* lds_kernel_for(int n4, int n3, int n2, int n1, bool sa) {
+const void* lds_kernel_for(int n4, int n3, int n2, int n1) {
 #define PE_LDS_PICK(W_, a, b, c, d) \
-  if (!sa && n4 == a && n3 == b && n2 == c && n1 == d) return (const void*)fit_mask_lds_kernel<W_, a, b, c, d, false>;
-#define PE_LDS_PICK_SA(W_, a, b, c, d) \
-  if (sa && n4 == a && n3 == b && n2 == c && n1 == d) return (const void*)fit_mask_lds_kernel<W_, a, b, c, d, true>;
+  if (n4 == a && n3 == b && n2 == c && n1 == d) return (const void*)fit_mask_lds_kernel<W_, a, b, c, d>;
   PE_LDS_SHAPES3(PE_LDS_PICK, W)
-  PE_LDS_SA_SHAPES3(PE_LDS_PICK_SA, W)
   if constexpr (W >= 2) {
     PE_LDS_SHAPES4(PE_LDS_PICK, W)
-    PE_LDS_SA_SHAPES4(PE_LDS_PICK_SA, W)
   }
 #undef PE_LDS_PICK
-#undef PE_LDS_PICK_SA
   return nullptr;
 }
 
-const void* lds_kernel_w1(int n4, int n3, int n2, int n1, bool sa);
-const void* lds_kernel_w2(int n4, int n3, int n2, int n1, bool sa);
-const void* lds_kernel_w4(int n4, int n3, int n2, int n1, bool sa);
+const void* lds_kernel_w1(int n4, int n3, int n2, int n1);
+const void* lds_kernel_w2(int n4, int n3, int n2, int n1);
+const void* lds_kernel_w4(int n4, int n3, int n2, int n1);
 
 }  // namespace pe

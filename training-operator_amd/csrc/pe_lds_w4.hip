@@ -3,8 +3,6 @@
 
 namespace pe {
 
-const void* lds_kernel_w4(int n4, int n3, int n2, int n1, bool sa) {
-  return lds_kernel_for<4>(n4, n3, n2, n1, sa);
-}
+const void* lds_kernel_w4(int n4, int n3, int n2, int n1) { return lds_kernel_for<4>(n4, n3, n2, n1); }
 
 }  // namespace pe
