@@ -49,7 +49,7 @@ constexpr int SC_M = 16;       // scan: nodes per lane (wave span 1024 nodes)
 constexpr int SC_GT = 4;       // scan: groups per wave (top-2 state in registers)
 constexpr int SC_SPAN = 64 * SC_M;
 constexpr int SC_WPB = 16;     // scan: waves (group tiles) per block, all on one node span
-constexpr int MG_CAP = 8192;   // merge: LDS candidate capacity per group
+constexpr int MG_CAP = 16384;  // merge / walk: LDS candidate capacity per group (128 KiB of keys)
 constexpr int MG_THREADS = 1024;
 constexpr int MG_SEL = 1024;   // merge: keys kept after the histogram cut (sorted instead of all)
 

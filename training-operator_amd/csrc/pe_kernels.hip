@@ -1382,7 +1382,8 @@ __device__ unsigned long long topk_prof[8];
 #define TKP(i, v)
 #define TKT(n)
 #endif
-__device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
+// bound: keys >= bound can be ignored (the caller knows >= K + 1 keys lie below it; NO_KEY = none)
+__device__ uint64_t* topk_sort(TopkShared& s, int T, int K, uint64_t bound = NO_KEY) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   __syncthreads();
   TKT(0);
@@ -1398,8 +1399,11 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
   if (K + 1 <= MG_SEL) {
     uint64_t mn = NO_KEY, mx = 0;
     for (int i = tid; i < T; i += MG_THREADS) {
-      mn = umin64(mn, s.keys[i]);
-      mx = umax64(mx, s.keys[i]);
+      const uint64_t k = s.keys[i];
+      if (k < bound) {
+        mn = umin64(mn, k);
+        mx = umax64(mx, k);
+      }
     }
     mn = wave_min_u64(mn);
     mx = wave_max_u64(mx);
@@ -1417,7 +1421,10 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
     }
     const int bits = 64 - __clzll((long long)((kmax - kmin) | 1));
     const int sh = bits > 8 ? bits - 8 : 0;
-    for (int i = tid; i < T; i += MG_THREADS) atomicAdd(&s.hist[(int)((s.keys[i] - kmin) >> sh)], 1);
+    for (int i = tid; i < T; i += MG_THREADS) {
+      const uint64_t k = s.keys[i];
+      if (k < bound) atomicAdd(&s.hist[(int)((k - kmin) >> sh)], 1);
+    }
     __syncthreads();
     hist_cut(s, K + 1);
     const int cb = s.sel_bin;
@@ -1432,7 +1439,7 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
       __syncthreads();
       for (int i = tid; i < T; i += MG_THREADS) {
         const uint64_t k = s.keys[i];
-        if ((int)((k - kmin) >> sh) == cb) atomicAdd(&s.hist[(int)((k - base) >> sh2)], 1);
+        if (k < bound && (int)((k - kmin) >> sh) == cb) atomicAdd(&s.hist[(int)((k - base) >> sh2)], 1);
       }
       __syncthreads();
       hist_cut(s, K + 1 - before);
@@ -1444,7 +1451,7 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K) {
     __syncthreads();
     for (int i = tid; i < T; i += MG_THREADS) {
       const uint64_t k = s.keys[i];
-      const int b1 = (int)((k - kmin) >> sh);
+      const int b1 = k < bound ? (int)((k - kmin) >> sh) : 256;
       if (b1 < cb || (b1 == cb && (int)((k - base) >> sh2) <= cb2)) {
         const int pos = atomicAdd(&s.sel_n, 1);
         if (pos < MG_SEL) s.sel[pos] = k;
@@ -1769,7 +1776,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   static_assert(WK_ROUND == MG_THREADS, "the walk uses the merge's block-wide selection");
   __shared__ TopkShared s;
   __shared__ uint32_t cbits[WK_MAXR / 32];
-  __shared__ int start_cnt, below;
+  __shared__ int start_cnt, below[2];
   const int g = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   WPT(0);
@@ -1789,6 +1796,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   if (tid == 0) {
     s.total = 0;
     start_cnt = 0;
+    below[0] = below[1] = 0;
   }
   __syncthreads();
   if (walk) {
@@ -1804,16 +1812,24 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   }
   WPT(1);
   // overlay: every node changed since the sort (and the saturating ones), current values
+  // OV entries per thread between barriers (the overlay holds up to resort_nodes = 16k entries: one
+  // barrier, append and compaction check per 4096 instead of per 1024)
+  constexpr int OV = 4;
   const int no = *w.ovl_n;
-  for (int i0 = 0; i0 < no; i0 += WK_ROUND) {
-    const int i = i0 + tid;
-    uint64_t k = NO_KEY;
-    if (i < no)   // the overlay keeps its own state copy: independent, coalesced loads
-      k = node_key(w.ovl_res[i], w.ovl_res[w.sstride + i], w.ovl_res[2 * w.sstride + i], w.ovl_res[3 * w.sstride + i],
-                   w.ovl_lab[i], q0, q1, q2, q3, need, id_base + (uint64_t)w.ovl[i]);
-    topk_append(s, k, k != NO_KEY);
+  for (int i0 = 0; i0 < no; i0 += OV * WK_ROUND) {
+    uint64_t k[OV];
+#pragma unroll
+    for (int u = 0; u < OV; ++u) {
+      const int i = i0 + u * WK_ROUND + tid;
+      k[u] = NO_KEY;
+      if (i < no)   // the overlay keeps its own state copy: independent, coalesced loads
+        k[u] = node_key(w.ovl_res[i], w.ovl_res[w.sstride + i], w.ovl_res[2 * w.sstride + i],
+                        w.ovl_res[3 * w.sstride + i], w.ovl_lab[i], q0, q1, q2, q3, need, id_base + (uint64_t)w.ovl[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < OV; ++u) topk_append(s, k[u], k[u] != NO_KEY);
     __syncthreads();
-    if (s.total > MG_CAP - WK_ROUND) {     // keep the K + 1 smallest (the rest can never matter)
+    if (s.total > MG_CAP - OV * WK_ROUND) {   // keep the K + 1 smallest (the rest can never matter)
       const int T = s.total;
       const uint64_t* sk = topk_sort(s, T, K);
       const int m = T < K + 1 ? T : K + 1;
@@ -1840,6 +1856,8 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
     return wi * 32 + __ffs(bits) - 1;
   };
   if (!done) r = next_round(r);
+  uint64_t xstop = NO_KEY;
+  int tests = 0;
   while (!done && r < nr) {
     const int T = s.total;
     if (T >= K + 1) {                      // stop once K + 1 keys lie below every unvisited key
@@ -1848,11 +1866,17 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
       int c = 0;
       for (int i = tid; i < T; i += WK_ROUND) c += s.keys[i] < X;
       for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
-      if (tid == 0) below = 0;
+      // two counters used in turn: the one for the next test is zeroed after this test's barrier (every
+      // thread read it at the previous test, and an append barrier lies between) -- one barrier per test
+      if (lane == 0 && c) atomicAdd(&below[tests & 1], c);
       __syncthreads();
-      if (lane == 0 && c) atomicAdd(&below, c);
-      __syncthreads();
-      if (below >= K + 1) break;
+      const int nb = below[tests & 1];
+      if (tid == 0) below[(tests + 1) & 1] = 0;
+      ++tests;
+      if (nb >= K + 1) {
+        xstop = X;                         // >= K + 1 collected keys lie below it: the rest never matter
+        break;
+      }
     }
     const int64_t i = r * WK_ROUND + tid;
     uint64_t k = NO_KEY;
@@ -1879,7 +1903,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   }
   WPT(3);
   const int T = s.total;
-  const uint64_t* sk = topk_sort(s, T, K);
+  const uint64_t* sk = topk_sort(s, T, K, xstop);
   WPT(4);
   write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : NO_KEY, K, g, out, gen);
   if (tid == 0 && w.stat) {
