@@ -9,5 +9,5 @@ g++ -O3 -march=x86-64-v3 -std=c++17 -DPE_RES_PROF -I"$(dirname "$src")" -Itraini
   tools/replay_resolver.cc "$src" -o /tmp/rp/rp -lpthread
 g++ -O3 -march=x86-64-v3 -std=c++17 -I"$(dirname "$src")" -Itraining-operator_amd/csrc -Iinclude \
   tools/replay_resolver.cc "$src" -o /tmp/rp/r -lpthread
-taskset -c 2,3 /tmp/rp/r /tmp/rp/d.bin 5 2>&1 | tail -2
-taskset -c 2,3 /tmp/rp/rp /tmp/rp/d.bin 3 2>&1 | tail -8
+taskset -c 2,3 /tmp/rp/r /tmp/rp/d.bin 5 2>&1 | grep -v "^rep"
+taskset -c 2,3 /tmp/rp/rp /tmp/rp/d.bin 3 2>&1 | grep -v "^rep"
