@@ -2,7 +2,8 @@
 
 The path takes every batch that one register plane set cannot hold (more than 32 distinct
 (dimension, value) pairs): per dimension a digit field of 1-3 levels, single-valued dimensions
-folded into the need planes, one plane per distinct need.  Cases cover every block size W (2048,
+folded into the need planes, one plane per distinct need (or per need and crossed single-level
+field values).  Cases cover every block size W (2048,
 4096, 8192 nodes per workgroup), every level count (four only at W >= 2), ragged last blocks, job counts around the
 16-job batch and the phase interleave, int64 extremes, negative residuals, many needs, and shards."""
 import os
@@ -56,8 +57,8 @@ def inventory(N, seed, gpu_frac=0.4):
     return inv
 
 
-def run(inv, req, need, W=None, maxl=None, fit_path_mask=LDS_ONLY, rank=0, world=1):
-    env = {}
+def run(inv, req, need, W=None, maxl=None, fit_path_mask=LDS_ONLY, rank=0, world=1, env=None):
+    env = dict(env or {})
     if W is not None:
         env["PE_LDS_W"] = str(W)
     if maxl is not None:
@@ -140,6 +141,33 @@ def test_lds_four_level_fields(W, dims, capfd):
     check(e, counts, inv, req, need)
     plan = capfd.readouterr().err            # the engine's PE_LDS_DEBUG line: "lds: W w ... L l B b" per field
     assert f"lds: W {W} " in plan and " L 4 " in plan, plan
+    assert 0 < counts.sum() < N * J
+    e.close()
+
+
+@pytest.mark.parametrize("cross", ["1", "0"])
+@pytest.mark.parametrize("case", ["gpu_eph", "three", "many_needs"])
+def test_lds_crossed_fields(case, cross, capfd):
+    """Single-level fields crossed into the need planes (one plane per need and crossed values, so a
+    job reads one plane for its labels and those fields) -- and the same batch with nothing crossed
+    (PE_LDS_CROSS=0): both bit-exact, and the plan says how many fields were crossed."""
+    N, J = 12289, 2000
+    inv = inventory(N, 81)
+    rng = np.random.default_rng(83)
+    req, need = synth.make_fit_jobs(J, 83)
+    req[:, 0] = 500 + (np.arange(J) % 300) * 11                  # a digit field
+    req[:, 2] = rng.choice([0, 1, 2, 4, 8], J)                    # 5 values
+    req[:, 3] = rng.choice([0, 10, 50, 100], J) * (1 << 30)       # 4 values
+    need[:] = (rng.integers(0, 3, J).astype(np.uint32) << 1) | (req[:, 2] > 0)
+    if case == "three":                                           # memory too: 3 values
+        req[:, 1] = rng.choice([1, 8, 64], J) * (1 << 30)
+    elif case == "many_needs":                                    # 24 needs x the crossed values
+        need[:] = (rng.integers(0, 12, J).astype(np.uint32) << 1) | (req[:, 2] > 0)
+    e, counts = run(inv, req, need, env={"PE_LDS_CROSS": cross, "PE_LDS_DEBUG": "1"})
+    check(e, counts, inv, req, need)
+    plan = capfd.readouterr().err
+    ncross = int(plan.split(" cross ")[1].split()[0])
+    assert (ncross >= 1) if cross == "1" else (ncross == 0), plan
     assert 0 < counts.sum() < N * J
     e.close()
 

@@ -1469,8 +1469,10 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd, bool 
 // LDS digit planes of one batch (pe_kernels.h LdsSpec): per dimension with >= 2 distinct values a
 // digit field of L levels (chosen with the node-block size W to minimise plane reads per job within
 // the LDS budget), dimensions with one value folded into the need planes, one plane per distinct
-// need.  Returns false when no configuration fits 160 KiB of LDS (the other paths take the batch).
-// PE_LDS_W=1|2|4 forces the block size, PE_LDS_MAXL=1..4 caps the levels (tuning / tests).
+// need -- or, with single-level fields crossed into them, one per (need, crossed values): a job then
+// reads one plane for its labels and those fields.  Returns false when no configuration fits 160 KiB
+// of LDS (the other paths take the batch).  PE_LDS_W=1|2|4 forces the block size, PE_LDS_MAXL=1..4
+// caps the levels, PE_LDS_CROSS=0 crosses nothing (tuning / tests).
 static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   if (n_jobs == 0 || ctx->Ns == 0) return false;
   const std::vector<int64_t>* vals = bd.vals;
@@ -1513,7 +1515,9 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   int forced_w = 0;
   if (const char* e = std::getenv("PE_LDS_W")) forced_w = std::atoi(e);
   const int64_t nneed = (int64_t)needs.size();
-  int bestW = 0, bestL[pe::LD_MAXF] = {1, 1, 1, 1};
+  bool cross = true;
+  if (const char* e = std::getenv("PE_LDS_CROSS")) cross = std::atoi(e) != 0;
+  int bestW = 0, bestL[pe::LD_MAXF] = {1, 1, 1, 1}, bestX = 0;   // bestX: bit i = field i crossed
   int64_t bestB[pe::LD_MAXF] = {0, 0, 0, 0};
   double bestCost = 1e300;
   for (int W : {4, 2, 1}) {
@@ -1523,40 +1527,63 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
     for (int i = 0; i < sp.nf; ++i) combos *= maxl;
     for (int cix = 0; cix < combos; ++cix) {
       int L[pe::LD_MAXF];
-      int64_t B[pe::LD_MAXF];
-      int64_t planes = nneed, reads = 1, entries = 0;
+      int64_t B[pe::LD_MAXF], P[pe::LD_MAXF];
       bool ok = true;
       for (int i = 0, x = cix; i < sp.nf; ++i, x /= maxl) {
         L[i] = 1 + x % maxl;
         const int64_t m = (int64_t)vals[fdim[i]].size();
         if (L[i] > 1 && m < 4) L[i] = 1;
         if (L[i] == 4 && W == 1) ok = false;     // four-level kernels exist for W >= 2 only
-        planes += plan(m, L[i], B[i]);
-        reads += 2 * L[i] - 1;
-        entries += L[i];
+        P[i] = plan(m, L[i], B[i]);
       }
-      if (!ok || entries > pe::LD_NEED_SLOT || planes > budget || planes > 65535) continue;
-      // per job and 8192 nodes, in CU cycles: LDS plane reads (b128 / b64 / read2st64_b64: 4 per KiB,
-      // b32: 8) -- the kernel's bound -- plus its VALU at ~0.6 CU cycles per wave instruction: per
-      // entry a readlane half and an address, ~6 fixed, and the three-input combines (2 per extra level
-      // and word, 4 per 8192 nodes whatever W)
-      const double valu = (4.0 / W) * (1.5 * (double)entries + 6.0) + 4.0 * (double)(reads - 1 - sp.nf + sp.nf / 2);
-      const double cost = reads * (W == 1 ? 8.0 : 4.0) + 0.625 * valu;
-      if (cost < bestCost - 1e-9) {
-        bestCost = cost;
-        bestW = W;
+      if (!ok) continue;
+      // crossed sets: the k single-level fields with the fewest values, k = 0 .. all of them
+      int one[pe::LD_MAXF], n1 = 0;
+      for (int i = 0; i < sp.nf; ++i)
+        if (L[i] == 1) one[n1++] = i;
+      std::sort(one, one + n1, [&](int a, int b) { return vals[fdim[a]].size() < vals[fdim[b]].size(); });
+      for (int k = 0; k <= (cross ? n1 : 0); ++k) {
+        int xs = 0;
+        int64_t xprod = 1;
+        for (int t = 0; t < k; ++t) {
+          xs |= 1 << one[t];
+          xprod *= (int64_t)vals[fdim[one[t]]].size();
+        }
+        int64_t planes = nneed * xprod, reads = 1, entries = 0, nfk = 0;
         for (int i = 0; i < sp.nf; ++i) {
-          bestL[i] = L[i];
-          bestB[i] = B[i];
+          if (xs >> i & 1) continue;
+          planes += P[i];
+          reads += 2 * L[i] - 1;
+          entries += L[i];
+          ++nfk;
+        }
+        if (entries > pe::LD_NEED_SLOT || planes > budget || planes > 65535) continue;
+        // per job and 8192 nodes, in CU cycles: LDS plane reads (b128 / b64 / read2st64_b64: 4 per
+        // KiB, b32: 8) -- the kernel's bound -- plus its VALU at ~0.6 CU cycles per wave instruction:
+        // per entry a readlane half and an address, ~6 fixed, and the three-input combines (2 per
+        // extra level and word, 4 per 8192 nodes whatever W)
+        const double valu = (4.0 / W) * (1.5 * (double)entries + 6.0) + 4.0 * (double)(reads - 1 - nfk + nfk / 2);
+        const double cost = reads * (W == 1 ? 8.0 : 4.0) + 0.625 * valu;
+        if (cost < bestCost - 1e-9) {
+          bestCost = cost;
+          bestW = W;
+          bestX = xs;
+          for (int i = 0; i < sp.nf; ++i) {
+            bestL[i] = L[i];
+            bestB[i] = B[i];
+          }
         }
       }
     }
   }
   if (!bestW) return false;
-  // fields in the kernel's order: three-level first, then two-level, then single-level
+  // fields in the kernel's order: four-level first, then three-, two- and single-level; the crossed
+  // fields last (they keep a rank row but no digit planes)
+  const int nx = __builtin_popcount(bestX);
   {
     int ord[pe::LD_MAXF] = {0, 1, 2, 3};
-    std::stable_sort(ord, ord + sp.nf, [&](int x, int y) { return bestL[x] > bestL[y]; });
+    auto key = [&](int x) { return (bestX >> x & 1) ? 0 : bestL[x]; };
+    std::stable_sort(ord, ord + sp.nf, [&](int x, int y) { return key(x) > key(y); });
     int d2[pe::LD_MAXF], L2[pe::LD_MAXF];
     int64_t B2[pe::LD_MAXF];
     for (int i = 0; i < sp.nf; ++i) {
@@ -1570,6 +1597,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
       bestB[i] = B2[i];
     }
   }
+  sp.nf -= nx;
   int shape[4] = {0, 0, 0, 0};
   for (int i = 0; i < sp.nf; ++i) ++shape[4 - bestL[i]];
   // level specs, plane bases
@@ -1602,10 +1630,24 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
       p += sp.nv[i][k];
     }
   }
+  sp.nx = nx;
+  sp.xprod = 1;
+  for (int x = 0; x < nx; ++x) {   // crossed fields: rank rows and values after the digit fields
+    const int i = sp.nf + x;
+    const int64_t m = (int64_t)vals[fdim[i]].size();
+    sp.dim[i] = fdim[i];
+    sp.L[i] = 1;
+    sp.voff[i] = voff;
+    sp.m[i] = m;
+    allv.insert(allv.end(), vals[fdim[i]].begin(), vals[fdim[i]].end());
+    voff += m;
+    sp.xstride[x] = sp.xprod;
+    sp.xprod *= (int32_t)m;
+  }
   sp.need_pbase = p;
   sp.nneed = (int32_t)nneed;
   for (int64_t i = 0; i < nneed; ++i) sp.needs[i] = needs[i];
-  sp.nplanes = p + (int32_t)nneed;
+  sp.nplanes = p + (int32_t)(nneed * sp.xprod);
   // geometry: W words per lane, blocks of 2048 W nodes, R job phases for an even spread over the CUs
   const int W = bestW;
   const int64_t S = 2048 * W;
@@ -1647,7 +1689,9 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
         }
       }
     }
-    c[pe::LD_NEED_SLOT] = (uint16_t)(sp.need_pbase + bd.rank[4][j]);
+    int64_t xc = 0;   // the job's crossed values (0-based value index: the node's rank must exceed it)
+    for (int x = 0; x < sp.nx; ++x) xc += (int64_t)bd.rank[fdim[sp.nf + x]][j] * sp.xstride[x];
+    c[pe::LD_NEED_SLOT] = (uint16_t)(sp.need_pbase + bd.rank[4][j] * sp.xprod + xc);
   }
   });
   // slot (r * 16 + w) * Tpad + t = job r + R (w + 16 t), the t-th of wave w's run in phase r (the
@@ -1669,8 +1713,8 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
     if (pos != n_jobs) raise(PE_EINVAL, "lds: run lengths do not cover the batch");
   }
   if (std::getenv("PE_LDS_DEBUG")) {   // diagnostics: the chosen configuration
-    std::fprintf(stderr, "lds: W %d nblk %lld R %lld planes %d need %d fold %d |", W, (long long)nblk, (long long)R,
-                 sp.nplanes, sp.nneed, sp.nfold);
+    std::fprintf(stderr, "lds: W %d nblk %lld R %lld planes %d need %d fold %d cross %d x %d |", W, (long long)nblk,
+                 (long long)R, sp.nplanes, sp.nneed, sp.nfold, sp.nx, sp.xprod);
     for (int i = 0; i < sp.nf; ++i)
       std::fprintf(stderr, " dim %d m %lld L %d B %u", sp.dim[i], (long long)sp.m[i], sp.L[i], sp.mod[i][0]);
     std::fprintf(stderr, "\n");
@@ -1690,7 +1734,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   hipchk(ctx->lds_spec_d.ensure(1), "alloc lds spec");
   hipchk(ctx->lds_vals.ensure(std::max<size_t>(allv.size(), 1)), "alloc lds vals");
   hipchk(ctx->lds_codes.ensure(codes.size()), "alloc lds codes");
-  hipchk(ctx->lds_ranks.ensure((size_t)std::max(sp.nf, 1) * ctx->lds_npad), "alloc lds ranks");
+  hipchk(ctx->lds_ranks.ensure((size_t)std::max(sp.nf + sp.nx, 1) * ctx->lds_npad), "alloc lds ranks");
   hipchk(ctx->lds_aux.ensure((size_t)2 * ctx->lds_npad), "alloc lds aux");
   hipchk(hipMemcpyAsync(ctx->lds_spec_d.p, &ctx->lds, sizeof(pe::LdsSpec), hipMemcpyHostToDevice, ctx->stream),
          "H2D lds spec");

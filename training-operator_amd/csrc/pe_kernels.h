@@ -210,7 +210,9 @@ hipError_t launch_fit_mask_planes_sets(hipStream_t s, const uint32_t* planes, in
 //     [R >= c] = GE_top(c_top + 1) | (GE_top(c_top) & ( ... GE_0(c_0) ... ))
 // so a field of m values costs L digit levels (m^(1/L)-ish planes each) and 2L - 1 plane reads per
 // job; a single-level field is one plane per value.  Label needs are one plane each, and
-// dimensions with a single requested value are folded into those.  The workgroup builds its node
+// dimensions with a single requested value are folded into those.  Single-level fields may be
+// CROSSED with the needs instead: one plane per (need, value of each crossed field), the AND of the
+// label test and the crossed thresholds, so the job reads one plane for all of them.  The workgroup builds its node
 // block's planes in LDS (scatter of the equality bits + suffix OR), then streams the jobs: per job
 // a handful of LDS reads, AND/AND-OR combines, one store of the block's slice of the mask row.
 constexpr int LD_MAXF = 4;        // digit fields (dimensions with >= 2 distinct values)
@@ -239,13 +241,17 @@ struct LdsSpec {
   int32_t vlo[LD_MAXF][LD_MAXL];
   int32_t nv[LD_MAXF][LD_MAXL];
   int32_t nneed, need_pbase, nplanes, nfold;
+  // crossed single-level fields (ranks rows nf .. nf + nx - 1, dim / voff / m at nf + i): need plane
+  // need_pbase + i * xprod + sum_f c_f * xstride[f] = need i AND rank_f >= c_f + 1 for every crossed f
+  int32_t nx, xprod;
+  int32_t xstride[LD_MAXF];
   uint32_t needs[LD_MAXNEED];
   int32_t fold_dim[D];              // single-valued dimensions folded into the need planes:
   int64_t fold_val[D];              // a node passes them iff res[fold_dim] >= fold_val
   int64_t voff[LD_MAXF];            // field f's sorted distinct values at vals[voff[f] .. voff[f] + m[f])
   int64_t m[LD_MAXF];
 };
-// ranks: [nf][npad] u32 (npad = node blocks x S, padding nodes 0); aux: [2][npad] u32, row 0 = 1 for
+// ranks: [nf + nx][npad] u32 (npad = node blocks x S, padding nodes 0); aux: [2][npad] u32, row 0 = 1 for
 // a shard node passing the folded dimensions (else 0), row 1 = its labels (0 for padding).
 // spec: device copy.
 hipError_t launch_node_ranks(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,

@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void node_ranks_kernel(const int64_t* __restri
   for (int i = 0; i < sp.nfold; ++i) ok &= real && res[sp.fold_dim[i] * stride + n] >= sp.fold_val[i];
   aux[n] = ok;
   aux[npad + n] = real ? labels[n] : 0u;
-  for (int f = 0; f < sp.nf; ++f) {
+  for (int f = 0; f < sp.nf + sp.nx; ++f) {   // digit fields, then the crossed ones
     uint32_t R = 0;
     if (real) {
       const int64_t x = res[sp.dim[f] * stride + n];

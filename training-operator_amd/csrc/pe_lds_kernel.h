@@ -55,7 +55,8 @@ __device__ __forceinline__ typename LdVec<W>::T plane_rd(const uint32_t* lds, ui
 //  1. zero the digit planes; scatter one equality bit per (node, field, level) into the plane of its
 //     digit -- work items are (field, level, u32 word column), so no two threads write one word;
 //  2. suffix OR per (field, level): GE(v) = E(v) | GE(v + 1), turning equality into threshold planes;
-//     need planes by wave ballots (label test AND the folded dimensions);
+//     need planes by wave ballots (label test AND the folded dimensions AND, per crossed single-level
+//     field, the plane's threshold of it);
 //  3. waves stream jobs r + R (w + 16 t): per job the need plane AND, per field, the last level's
 //     plane, then GE_k(c + 1) | (GE_k(c) & acc) per higher level; the slice is stored, its popcount
 //     joins a 16-job batch that one column sum (reduce16x64) turns into 16 per-job counts, added by ONE
@@ -119,9 +120,26 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
     const int64_t n = n0 + 64 * g + lane;
     const bool ok = aux[n] != 0u;
     const uint32_t lab = aux[npad + n];
+    uint32_t xr[LD_MAXF];                     // the crossed fields' ranks of this node
+#pragma unroll
+    for (int x = 0; x < LD_MAXF; ++x) xr[x] = x < sp.nx ? ranks[(sp.nf + x) * npad + n] : 0u;
     for (int i = 0; i < sp.nneed; ++i) {
-      const uint64_t b = __ballot(ok && (lab & sp.needs[i]) == sp.needs[i]);
-      if (lane == 0) *reinterpret_cast<uint64_t*>(lds + (sp.need_pbase + i) * WPP + 2 * g) = b;
+      const bool li = ok && (lab & sp.needs[i]) == sp.needs[i];
+      uint32_t dig[LD_MAXF] = {0u, 0u, 0u, 0u};   // plane (i, c)'s value index per crossed field
+      for (int c = 0; c < sp.xprod; ++c) {
+        bool pass = li;
+#pragma unroll
+        for (int x = 0; x < LD_MAXF; ++x) pass = pass && (x >= sp.nx || xr[x] > dig[x]);
+        const uint64_t b = __ballot(pass);
+        if (lane == 0) *reinterpret_cast<uint64_t*>(lds + (sp.need_pbase + i * sp.xprod + c) * WPP + 2 * g) = b;
+        bool carry = true;                    // next c: the crossed values count up, field 0 fastest
+#pragma unroll
+        for (int x = 0; x < LD_MAXF; ++x)
+          if (carry && x < sp.nx) {
+            carry = ++dig[x] == (uint32_t)sp.m[sp.nf + x];
+            if (carry) dig[x] = 0u;
+          }
+      }
     }
   }
   __syncthreads();
