@@ -630,26 +630,36 @@ def main(argv=None):
                             "alg_bytes": agg_bytes(sub[0], sub[3])}
         lo_j, hi_j = rank * args.agg_jobs // world, (rank + 1) * args.agg_jobs // world
         mine = pg_slice(agg, lo_j, hi_j)
-        eng.pg_min_resources(1, *mine)
+        # the C call with caller-owned outputs allocated once (the ABI's contract, like the latency
+        # lines); the Python wrapper, which allocates fresh zeroed outputs per call (38 B per job of
+        # first-touch page faults), is timed beside it as wrapper_ms_per_call
+        mcall, _ = agg_raw_call(eng.lib.pe_pg_min_resources, (eng.h,), 1, mine)
+        assert mcall() in (0, -2)
         e0, e1 = ev.create(), ev.create()
         ts, ks = [], []
         for _ in range(5):
             barrier()
             t0 = time.perf_counter()
             ev.record(e0, stream)
-            eng.pg_min_resources(1, *mine)
+            mcall()
             ev.record(e1, stream)
             ts.append(allmax(time.perf_counter() - t0))
             ks.append(ev.elapsed_ms(e0, e1))
         at = float(np.median(ts))
         kms = float(np.median(ks))
+        wts = []
+        for _ in range(3):
+            barrier()
+            t0 = time.perf_counter()
+            eng.pg_min_resources(1, *mine)
+            wts.append(allmax(time.perf_counter() - t0))
         os.environ["PE_AGG_DEVICE"] = "1"
         try:
             dts = []
             for _ in range(3):
                 barrier()
                 t0 = time.perf_counter()
-                eng.pg_min_resources(1, *mine)
+                mcall()
                 dts.append(allmax(time.perf_counter() - t0))
         finally:
             del os.environ["PE_AGG_DEVICE"]
@@ -662,6 +672,7 @@ def main(argv=None):
                         + (f", split over {world} ranks ({hi_j - lo_j} jobs on rank {rank})" if world > 1 else ""),
             "jobs_per_s": args.agg_jobs / at, "ms_per_call": at * 1e3, "alg_bytes": ab,
             "achieved_gbs": ab / at / 1e9, "r2_path_ms_per_call": float(np.median(dts)) * 1e3,
+            "wrapper_ms_per_call": float(np.median(wts)) * 1e3,
             "pcie": pcie,
             "pcie_bound_ms": (mb / pcie["h2d_gbs"] / 1e6) if pcie else None,
             "latency_us": lat, "ctypes_call_us": ctypes_us,
@@ -670,7 +681,8 @@ def main(argv=None):
             "note": "latency_us: one pe_pg_min_resources call on the first J jobs (median / p90 of 400, ctypes pointers "
                     "built once; ctypes_call_us = the dispatch cost of an empty ABI call, included); r2_path = the "
                     "round-2 call path (PE_AGG_DEVICE=1: six H2D + four D2H copies + stream sync) on the same box; "
-                    "ms_per_call = max over ranks"}
+                    "ms_per_call = the C call on caller-owned input and output arrays (allocated once), max over ranks; "
+                    "wrapper_ms_per_call = the Python wrapper, which allocates fresh zeroed outputs every call"}
 
     if not args.no_greedy:
         progress("greedy")

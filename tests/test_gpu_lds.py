@@ -167,7 +167,10 @@ def test_lds_crossed_fields(case, cross, capfd):
     check(e, counts, inv, req, need)
     plan = capfd.readouterr().err
     ncross = int(plan.split(" cross ")[1].split()[0])
-    assert (ncross >= 1) if cross == "1" else (ncross == 0), plan
+    if cross == "0":
+        assert ncross == 0, plan
+    elif case != "many_needs":    # (24 needs: crossing would cost the second workgroup per CU -> planner's call)
+        assert ncross >= 1, plan
     assert 0 < counts.sum() < N * J
     e.close()
 

@@ -1542,6 +1542,12 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
       for (int i = 0; i < sp.nf; ++i)
         if (L[i] == 1) one[n1++] = i;
       std::sort(one, one + n1, [&](int a, int b) { return vals[fdim[a]].size() < vals[fdim[b]].size(); });
+      // a crossing must not cost the second workgroup per CU (LDS <= 80 KiB) the uncrossed plan has:
+      // store-bound batches need the waves more than the plane read they save ("many": R 4 -> 2, 90 KB,
+      // 2.32 -> 2.68 ms when crossing pushed the LDS past half the CU's)
+      int64_t planes0 = nneed;
+      for (int i = 0; i < sp.nf; ++i) planes0 += P[i];
+      const int64_t half = 81920 / (256 * W);
       for (int k = 0; k <= (cross ? n1 : 0); ++k) {
         int xs = 0;
         int64_t xprod = 1;
@@ -1558,6 +1564,7 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
           ++nfk;
         }
         if (entries > pe::LD_NEED_SLOT || planes > budget || planes > 65535) continue;
+        if (k > 0 && planes > half && planes0 <= half) continue;
         // per job and 8192 nodes, in CU cycles: LDS plane reads (b128 / b64 / read2st64_b64: 4 per
         // KiB, b32: 8) -- the kernel's bound -- plus its VALU at ~0.6 CU cycles per wave instruction:
         // per entry a readlane half and an address, ~6 fixed, and the three-input combines (2 per
