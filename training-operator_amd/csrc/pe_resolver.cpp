@@ -171,7 +171,8 @@ void DirtySet::keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vec
 }
 
 // keys_all, 8 dirty nodes per AVX-512 step: the K(n) range test, the Appendix-B fit and key (the
-// arithmetic of key_bf), the fitting slots compressed into idx and the running minimum.
+// arithmetic of key_bf), the fitting slots compressed into idx and the running minimum.  Only the
+// fitting slots' keys are stored: callers read out[] at the slots listed in idx.
 __attribute__((target("avx512f,avx512dq,avx512vl,avx512bw"))) static uint64_t keys_avx512(
     size_t n, const uint64_t* kn, const int64_t* x0p, const int64_t* x1p, const int64_t* x2p, const int64_t* x3p,
     const uint32_t* lab, const int64_t* gid, const int64_t q[RD], uint32_t need, uint64_t lo, uint64_t span,
@@ -188,10 +189,7 @@ __attribute__((target("avx512f,avx512dq,avx512vl,avx512bw"))) static uint64_t ke
     const __mmask8 m = n - i >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << (n - i)) - 1);
     const __m512i k = _mm512_maskz_loadu_epi64(m, kn + i);
     __mmask8 fit = m & (_mm512_cmplt_epu64_mask(_mm512_sub_epi64(k, vlo), vspan) | _mm512_cmpeq_epi64_mask(k, ones));
-    if (!fit) {
-      _mm512_mask_storeu_epi64(out + i, m, ones);
-      continue;
-    }
+    if (!fit) continue;   // (out is read at the slots listed in idx only)
     const __m512i x0 = _mm512_maskz_loadu_epi64(m, x0p + i), x1 = _mm512_maskz_loadu_epi64(m, x1p + i),
                   x2 = _mm512_maskz_loadu_epi64(m, x2p + i), x3 = _mm512_maskz_loadu_epi64(m, x3p + i);
     const __m512i l = _mm512_cvtepu32_epi64(_mm256_maskz_loadu_epi32(m, lab + i));
@@ -206,7 +204,7 @@ __attribute__((target("avx512f,avx512dq,avx512vl,avx512bw"))) static uint64_t ke
     const __m512i score = _mm512_mask_mov_epi64(sum, big, smax);
     const __m512i key = _mm512_mask_mov_epi64(
         ones, fit, _mm512_or_si512(_mm512_slli_epi64(score, 24), _mm512_maskz_loadu_epi64(m, gid + i)));
-    _mm512_mask_storeu_epi64(out + i, m, key);
+    _mm512_mask_storeu_epi64(out + i, fit, key);
     vmin = _mm512_min_epu64(vmin, key);
     _mm256_mask_compressstoreu_epi32(idx + ni, fit, _mm256_add_epi32(lane, _mm256_set1_epi32((int32_t)i)));
     ni += (size_t)__builtin_popcount(fit);
@@ -681,7 +679,10 @@ void Resolver::finish_job(bool ok) {
         --pods_placed_;
       }
     }
-    for (const auto& kv : jn_) dirty_.mark(dirty_.upsert(kv.first, kv.second));
+    for (const auto& kv : jn_) {
+      dirty_.mark(dirty_.upsert(kv.first, kv.second));
+      any_set(kv.first);
+    }
     job_status_[j] = 1;
     ++jobs_failed_;
   }
@@ -777,10 +778,11 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       }
     }
     scorer_.start(&seeds_, &groups, &cands, qeff_.data(), need_, feed);
+    for (int64_t g : seeds_.gid) any_set(g);
   }
   if (feed) feed->advance();
   auto have = [&](size_t w) { return !feed || w < feed->parsed(); };   // list of group w is there
-  auto is_dirty = [&](int64_t gid) { return dirty_.contains(gid) || (useS && seeds_.contains(gid)); };
+  auto is_dirty = [&](int64_t gid) { return any_has(gid); };   // dirty_.contains || (useS && seeds_.contains)
   RP_ADD(seed, t_);
   for (int32_t g : groups) {   // the window's group records (scattered over the batch arrays)
     __builtin_prefetch(req_ + (int64_t)g * RD);
@@ -977,6 +979,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       t3_ = RP_T();
       if (slot < 0) {
         slot = dirty_.upsert(gid, st);
+        any_set(gid);
         if (dk.size() <= (size_t)slot) dk.resize((size_t)slot + 1);
         dki.push_back(slot);
       } else {
@@ -1021,6 +1024,9 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     u.labels = st.labels;
     updates.push_back(u);
   }
+  for (int64_t g : dirty_.gid) any_[(size_t)g >> 6] = 0;   // (clears whole words: every bit set is listed)
+  if (useS)
+    for (int64_t g : seeds_.gid) any_[(size_t)g >> 6] = 0;
   prev_.clear();               // (last window's changes, or the seeds taken over from them)
   std::swap(prev_, dirty_);    // kept: the next window's seeds if it is pipelined on this one
   prev_ok_ = true;

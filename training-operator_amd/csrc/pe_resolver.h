@@ -236,9 +236,10 @@ class DirtySet {
   // `idx` receives the slots that were scored (the rest are NO_KEY in out).
   void keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
             std::vector<int32_t>& idx) const;
-  // every slot's key for (q, need) -> out[0..size()) (NO_KEY where it does not fit or where the
-  // K(n) range test above rules out a key < limit); returns the smallest.  AVX-512 where the CPU
-  // has it (8 nodes per step, no index list), else keys() + a scalar pass.
+  // the fitting slots' keys for (q, need): their slots -> idx, their keys -> out at those slots
+  // (out elsewhere is left as it was; the K(n) range test above leaves out nodes that cannot have a
+  // key < limit); returns the smallest.  AVX-512 where the CPU has it (8 nodes per step), else
+  // keys() + a scalar pass.
   uint64_t keys_all(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
                     std::vector<int32_t>& idx) const;
   uint64_t key_at(int32_t i, const int64_t q[RD], uint32_t need) const;
@@ -388,6 +389,18 @@ class Resolver {
   // window's seeds are exactly those updates, so the set is taken over as is (no re-insertion)
   DirtySet prev_;
   bool prev_ok_ = false;
+  // dirty_ OR seeds_ during a resolve, one bitmap: the list-skip test (every list entry the resolver
+  // looks at) is one bit instead of a bit in each set; cleared entry by entry when the resolve ends
+  std::vector<uint64_t> any_;
+  void any_set(int64_t g) {
+    const size_t w = (size_t)g >> 6;
+    if (w >= any_.size()) any_.resize(std::max(w + 1, 2 * any_.size()), 0);
+    any_[w] |= 1ull << (g & 63);
+  }
+  bool any_has(int64_t g) const {
+    const size_t w = (size_t)g >> 6;
+    return w < any_.size() && (any_[w] >> (g & 63) & 1);
+  }
   std::vector<uint64_t> sk_out_;
   std::vector<int32_t> sk_idx_;
   std::vector<uint64_t> sfull_;      // a group's every seed key below the limit (truncated top)
