@@ -146,7 +146,7 @@ def test_lds_four_level_fields(W, dims, capfd):
 
 
 @pytest.mark.parametrize("cross", ["1", "0"])
-@pytest.mark.parametrize("case", ["gpu_eph", "three", "many_needs"])
+@pytest.mark.parametrize("case", ["gpu_eph", "three", "many_needs", "all_crossed"])
 def test_lds_crossed_fields(case, cross, capfd):
     """Single-level fields crossed into the need planes (one plane per need and crossed values, so a
     job reads one plane for its labels and those fields) -- and the same batch with nothing crossed
@@ -163,6 +163,9 @@ def test_lds_crossed_fields(case, cross, capfd):
         req[:, 1] = rng.choice([1, 8, 64], J) * (1 << 30)
     elif case == "many_needs":                                    # 24 needs x the crossed values
         need[:] = (rng.integers(0, 12, J).astype(np.uint32) << 1) | (req[:, 2] > 0)
+    elif case == "all_crossed":                                   # no digit field left (shape 0,0,0,0)
+        req[:, 0] = 1500
+        req[:, 1] = 4 << 30
     e, counts = run(inv, req, need, env={"PE_LDS_CROSS": cross, "PE_LDS_DEBUG": "1"})
     check(e, counts, inv, req, need)
     plan = capfd.readouterr().err
