@@ -239,11 +239,14 @@ def test_lds_sharded_columns():
     np.testing.assert_array_equal(total, o_counts)
 
 
-def test_lds_full_size_worst_case():
-    """cfg5 at full size (1M nodes x 100k jobs) with memory unique per job: sampled rows exact vs the
-    oracle, counts == popcount(rows), the whole count vector equal to the int64 compare path's."""
+@pytest.mark.parametrize("unique", [(1,), (0, 1, 3)])
+def test_lds_full_size_worst_case(unique):
+    """cfg5 at full size (1M nodes x 100k jobs) with memory unique per job (the bench's worst batch) or
+    cpu, memory and ephemeral-storage unique per job (its adversarial batch: four-level fields and a
+    crossed gpu field): sampled rows exact vs the oracle, counts == popcount(rows), the whole count
+    vector equal to the int64 compare path's."""
     inv = synth.make_inventory(1_000_000, synth.SEED["cfg5"], 0.2)
-    req, need = synth.make_fit_jobs_worst(100_000, synth.SEED["cfg5"], (1,))
+    req, need = synth.make_fit_jobs_worst(100_000, synth.SEED["cfg5"], unique)
     e, counts = run(inv, req, need, fit_path_mask=0)
     assert e.stats()["fit_runs_lds"] == 1
     rng = np.random.default_rng(3)
