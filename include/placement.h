@@ -113,7 +113,7 @@ typedef struct {
                                     bit1 set = every window scans all nodes of the shard (scan +
                                     merge kernels) instead of the sorted walk */
   int32_t resort_nodes;          /* sorted walk: rebuild the sorted index once this many node updates
-                                    were applied since the last build (0 = 16384) */
+                                    were applied since the last build (0 = 20480) */
 } pe_config;
 
 typedef struct {

@@ -11,7 +11,7 @@ sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "
 from placement import Engine, synth  # noqa: E402
 
 KEYS = {"wg": "window_groups", "wp": "window_pods", "k": "topk", "rs": "resort_nodes", "gf": "greedy_flags"}
-ENVS = {"d": "PE_PIPE_DEPTH"}   # environment settings read per pe_place_greedy call
+ENVS = {"d": "PE_PIPE_DEPTH", "ar": "PE_ASYNC_RESORT"}   # environment settings read per pe_place_greedy call
 
 
 def parse(spec):

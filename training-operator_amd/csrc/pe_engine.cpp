@@ -324,13 +324,28 @@ struct pe_ctx {
   HostBuf<int64_t> h_upd;
   // greedy sorted walk (pe_kernels.h WalkIndex; the default window path, greedy_flags bit1 = full scan)
   bool walk = true;
-  int64_t resort_nodes = 16384;  // re-sort once this many applied updates joined the overlay
+  int64_t resort_nodes = 20480;  // re-sort once this many applied updates joined the overlay
   int64_t w_est = 0;             // updates applied since the last sort (>= overlay size)
-  DevBuf<uint64_t> w_sk, w_kin, w_rmin;
-  DevBuf<int64_t> w_sr, w_rmax;
-  DevBuf<uint32_t> w_sl, w_pos, w_ror, w_inovl, w_ovidx, w_ovlab;
-  DevBuf<int64_t> w_ovres;
-  DevBuf<int32_t> w_ovl, w_ovln;
+  // two index sets: the walks read ws[w_cur]; the next one is rebuilt on the side stream w_s2
+  // (lowest priority) while the walks go on (walk_resort_async), then taken over (walk_switch)
+  struct WalkSet {
+    DevBuf<uint64_t> sk, rmin;
+    DevBuf<int64_t> sr, rmax;
+    DevBuf<uint32_t> sl, pos, ror, inovl, ovidx, ovlab;
+    DevBuf<int64_t> ovres;
+    DevBuf<int32_t> ovl, ovln;
+    void release() {
+      sk.release(); rmin.release(); sr.release(); rmax.release(); sl.release(); pos.release(); ror.release();
+      inovl.release(); ovidx.release(); ovlab.release(); ovres.release(); ovl.release(); ovln.release();
+    }
+  } ws[2];
+  int w_cur = 0;
+  bool w_pending = false;        // ws[1 - w_cur] is being rebuilt on w_s2
+  int64_t w_pend_est = 0;        // updates applied since that rebuild's snapshot
+  hipStream_t w_s2 = nullptr;
+  hipEvent_t w_ev_snap = nullptr, w_ev_done = nullptr;
+  DevBuf<uint64_t> w_kin;
+  DevBuf<uint32_t> w_slow;       // saturating nodes of the side-stream rebuild (walk_switch adds them)
   DevBuf<uint8_t> w_temp;
   DevBuf<uint32_t> w_flush;   // PE_WALK_FLUSH: 512 MiB rewritten before each walk (cold-cache diagnostics)
   DevBuf<unsigned long long> w_stat;   // walk counters of the current pe_place_greedy (rounds, overlay)
@@ -355,9 +370,12 @@ struct pe_ctx {
       h_outx[i].release();
       h_updx[i].release();
     }
-    w_sk.release(); w_kin.release(); w_rmin.release(); w_sr.release(); w_rmax.release(); w_sl.release(); w_pos.release();
-    w_ror.release(); w_inovl.release(); w_ovl.release(); w_ovln.release(); w_temp.release();
-    w_ovidx.release(); w_ovlab.release(); w_ovres.release(); w_stat.release(); w_flush.release();
+    if (w_s2) (void)hipStreamSynchronize(w_s2);
+    for (auto& x : ws) x.release();
+    w_kin.release(); w_slow.release(); w_temp.release(); w_stat.release(); w_flush.release();
+    if (w_ev_snap) (void)hipEventDestroy(w_ev_snap);
+    if (w_ev_done) (void)hipEventDestroy(w_ev_done);
+    if (w_s2) (void)hipStreamDestroy(w_s2);
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -597,7 +615,7 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   // the walk's block holds K + 1 <= WK_ROUND selected keys; larger K takes the full scan + merge
   ctx->walk = (cfg->greedy_flags & 2) == 0 && ctx->topk + 1 <= pe::WK_ROUND;
   if (cfg->resort_nodes < 0) raise(PE_EINVAL, "resort_nodes < 0");
-  ctx->resort_nodes = cfg->resort_nodes > 0 ? cfg->resort_nodes : 16384;
+  ctx->resort_nodes = cfg->resort_nodes > 0 ? cfg->resort_nodes : 20480;   // (profiles/r12_async_resort.txt)
   if (!(ctx->fit_path_mask & PATHS_ALL)) ctx->fit_path_mask |= PATHS_ALL;   // no kernel bits = all kernels
   ctx->fit_path_mask |= PATH_I64;                                           // always available
   int rc = PE_OK;
@@ -2045,59 +2063,126 @@ int pe_fit_mask(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const uint32_t*
 // The sorted-walk index of the shard over the current residuals (g_kn must be current): sort the
 // walkable nodes by K(n), gather the sorted SoA copy and the round summaries, empty the overlay
 // (then holding only the saturating nodes).
-static pe::WalkIndex walk_index(pe_ctx* ctx) {
+static pe::WalkIndex walk_index(pe_ctx* ctx, int set) {
+  pe_ctx::WalkSet& x = ctx->ws[set];
   pe::WalkIndex w{};
-  w.sk = ctx->w_sk.p;
-  w.sr = ctx->w_sr.p;
-  w.sl = ctx->w_sl.p;
-  w.pos = ctx->w_pos.p;
-  w.rmin = ctx->w_rmin.p;
-  w.rmax = ctx->w_rmax.p;
-  w.ror = ctx->w_ror.p;
-  w.ovl = ctx->w_ovl.p;
-  w.ovl_n = ctx->w_ovln.p;
-  w.in_ovl = ctx->w_inovl.p;
-  w.ovl_idx = ctx->w_ovidx.p;
-  w.ovl_res = ctx->w_ovres.p;
-  w.ovl_lab = ctx->w_ovlab.p;
+  w.sk = x.sk.p;
+  w.sr = x.sr.p;
+  w.sl = x.sl.p;
+  w.pos = x.pos.p;
+  w.rmin = x.rmin.p;
+  w.rmax = x.rmax.p;
+  w.ror = x.ror.p;
+  w.ovl = x.ovl.p;
+  w.ovl_n = x.ovln.p;
+  w.in_ovl = x.inovl.p;
+  w.ovl_idx = x.ovidx.p;
+  w.ovl_res = x.ovres.p;
+  w.ovl_lab = x.ovlab.p;
   w.stat = ctx->w_stat.p;
   w.sstride = ctx->stride;
   w.nr = (ctx->Ns + pe::WK_ROUND - 1) / pe::WK_ROUND;
   return w;
 }
+static pe::WalkIndex walk_index(pe_ctx* ctx) { return walk_index(ctx, ctx->w_cur); }
 
-static void walk_resort(pe_ctx* ctx) {
-  hipStream_t s = ctx->stream;
+// Index set `set` allocated and its overlay / pos cleared on stream s; returns the sort scratch size.
+static size_t walk_set_prepare(pe_ctx* ctx, int set, hipStream_t s) {
   const int64_t Ns = ctx->Ns, st = std::max<int64_t>(ctx->stride, 1);
   const int64_t nr = std::max<int64_t>(1, (Ns + pe::WK_ROUND - 1) / pe::WK_ROUND);
   if (nr > pe::WK_MAXR) raise(PE_EINVAL, "shard too large for the sorted walk");
-  hipchk(ctx->w_sk.ensure(st), "alloc walk keys");
+  pe_ctx::WalkSet& x = ctx->ws[set];
+  hipchk(x.sk.ensure(st), "alloc walk keys");
   hipchk(ctx->w_kin.ensure(st), "alloc walk keys");
-  hipchk(ctx->w_sr.ensure((size_t)pe::D * st), "alloc walk residuals");
-  hipchk(ctx->w_sl.ensure(st), "alloc walk labels");
-  hipchk(ctx->w_pos.ensure(st), "alloc walk pos");
-  hipchk(ctx->w_rmin.ensure(nr), "alloc walk rounds");
-  hipchk(ctx->w_rmax.ensure((size_t)pe::D * nr), "alloc walk rounds");
-  hipchk(ctx->w_ror.ensure(nr), "alloc walk rounds");
-  hipchk(ctx->w_ovl.ensure(st), "alloc overlay");
-  hipchk(ctx->w_ovln.ensure(1), "alloc overlay");
-  hipchk(ctx->w_inovl.ensure(st), "alloc overlay");
-  hipchk(ctx->w_ovidx.ensure(st), "alloc overlay");
-  hipchk(ctx->w_ovlab.ensure(st), "alloc overlay");
-  hipchk(ctx->w_ovres.ensure((size_t)pe::D * st), "alloc overlay");
+  hipchk(x.sr.ensure((size_t)pe::D * st), "alloc walk residuals");
+  hipchk(x.sl.ensure(st), "alloc walk labels");
+  hipchk(x.pos.ensure(st), "alloc walk pos");
+  hipchk(x.rmin.ensure(nr), "alloc walk rounds");
+  hipchk(x.rmax.ensure((size_t)pe::D * nr), "alloc walk rounds");
+  hipchk(x.ror.ensure(nr), "alloc walk rounds");
+  hipchk(x.ovl.ensure(st), "alloc overlay");
+  hipchk(x.ovln.ensure(1), "alloc overlay");
+  hipchk(x.inovl.ensure(st), "alloc overlay");
+  hipchk(x.ovidx.ensure(st), "alloc overlay");
+  hipchk(x.ovlab.ensure(st), "alloc overlay");
+  hipchk(x.ovres.ensure((size_t)pe::D * st), "alloc overlay");
   size_t tb = 0;
-  hipchk(pe::sort_keys_u64(nullptr, &tb, ctx->w_kin.p, ctx->w_sk.p, Ns, s), "sort size");
+  hipchk(pe::sort_keys_u64(nullptr, &tb, ctx->w_kin.p, x.sk.p, Ns, s), "sort size");
   hipchk(ctx->w_temp.ensure(tb), "alloc sort scratch");
+  hipchk(hipMemsetAsync(x.ovln.p, 0, sizeof(int32_t), s), "memset overlay");
+  hipchk(hipMemsetAsync(x.inovl.p, 0, (size_t)st * 4, s), "memset overlay");
+  hipchk(hipMemsetAsync(x.pos.p, 0xFF, (size_t)st * 4, s), "memset pos");
+  return tb;
+}
+
+// A side-stream rebuild still running is waited for and dropped (the caller rebuilds in line).
+static void walk_drop_pending(pe_ctx* ctx) {
+  if (!ctx->w_pending) return;
+  hipchk(hipStreamSynchronize(ctx->w_s2), "sync walk rebuild");
+  ctx->w_pending = false;
+}
+
+// In-line rebuild of the current set on the main stream (the walks after it wait for it).
+static void walk_resort(pe_ctx* ctx) {
+  walk_drop_pending(ctx);
+  hipStream_t s = ctx->stream;
+  const int64_t Ns = ctx->Ns;
+  size_t tb = walk_set_prepare(ctx, ctx->w_cur, s);
   const pe::WalkIndex w = walk_index(ctx);
-  hipchk(hipMemsetAsync(ctx->w_ovln.p, 0, sizeof(int32_t), s), "memset overlay");
-  hipchk(hipMemsetAsync(ctx->w_inovl.p, 0, (size_t)st * 4, s), "memset overlay");
-  hipchk(hipMemsetAsync(ctx->w_pos.p, 0xFF, (size_t)st * 4, s), "memset pos");
   hipchk(pe::launch_walk_prep(s, ctx->res.p, ctx->stride, Ns, ctx->g_kn.p, ctx->labels.p, ctx->w_kin.p, w),
          "launch walk_prep");
-  hipchk(pe::sort_keys_u64(ctx->w_temp.p, &tb, ctx->w_kin.p, ctx->w_sk.p, Ns, s), "sort walk keys");
+  hipchk(pe::sort_keys_u64(ctx->w_temp.p, &tb, ctx->w_kin.p, w.sk, Ns, s), "sort walk keys");
   hipchk(pe::launch_walk_build(s, ctx->res.p, ctx->stride, ctx->labels.p, Ns, (uint64_t)ctx->begin, w),
          "launch walk_build");
   ctx->w_est = 0;
+  ctx->stats.resorts += 1;
+}
+
+// Rebuild the other set on the side stream from the residuals as of now (the main stream's point
+// `snap`), while the main stream's walks keep using the current set: the applies after `snap`
+// update both overlays (apply_kernel nx), and walk_switch drops their nodes' possibly torn sorted
+// entries from the new set once it is built.  The side stream has the lowest priority, so the
+// walks' blocks are dispatched first.  Correct for the same reason as the in-line rebuild: every
+// node changed after the snapshot is in the new overlay with its current state, every other node's
+// sorted entry and round summaries are exact (a torn entry only widens its round's summary).
+static void walk_resort_async(pe_ctx* ctx) {
+  if (!ctx->w_s2) {
+    int least = 0, greatest = 0;
+    hipchk(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priorities");
+    hipchk(hipStreamCreateWithPriority(&ctx->w_s2, hipStreamNonBlocking, least), "side stream");
+    hipchk(hipEventCreateWithFlags(&ctx->w_ev_snap, hipEventDisableTiming), "event");
+    hipchk(hipEventCreateWithFlags(&ctx->w_ev_done, hipEventDisableTiming), "event");
+  }
+  hipStream_t s = ctx->stream, s2 = ctx->w_s2;
+  const int nx = 1 - ctx->w_cur;
+  const int64_t Ns = ctx->Ns;
+  size_t tb = walk_set_prepare(ctx, nx, s);   // (cleared on the main stream: before any apply that writes it)
+  hipchk(ctx->w_slow.ensure((size_t)std::max<int64_t>(ctx->stride, 1)), "alloc walk slow flags");
+  hipchk(hipMemsetAsync(ctx->w_slow.p, 0, (size_t)std::max<int64_t>(ctx->stride, 1) * 4, s), "memset slow flags");
+  hipchk(hipEventRecord(ctx->w_ev_snap, s), "event record");
+  hipchk(hipStreamWaitEvent(s2, ctx->w_ev_snap, 0), "stream wait");
+  const pe::WalkIndex w = walk_index(ctx, nx);
+  hipchk(pe::launch_walk_prep(s2, ctx->res.p, ctx->stride, Ns, ctx->g_kn.p, ctx->labels.p, ctx->w_kin.p, w,
+                              ctx->w_slow.p),
+         "launch walk_prep");
+  hipchk(pe::sort_keys_u64(ctx->w_temp.p, &tb, ctx->w_kin.p, w.sk, Ns, s2), "sort walk keys");
+  hipchk(pe::launch_walk_build(s2, ctx->res.p, ctx->stride, ctx->labels.p, Ns, (uint64_t)ctx->begin, w),
+         "launch walk_build");
+  hipchk(hipEventRecord(ctx->w_ev_done, s2), "event record");
+  ctx->w_pending = true;
+  ctx->w_pend_est = 0;
+}
+
+// Take over the side-stream rebuild (the main stream waits for it if it is not done yet).
+static void walk_switch(pe_ctx* ctx) {
+  hipStream_t s = ctx->stream;
+  const int nx = 1 - ctx->w_cur;
+  hipchk(hipStreamWaitEvent(s, ctx->w_ev_done, 0), "stream wait");
+  hipchk(pe::launch_walk_switch(s, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->w_slow.p, walk_index(ctx, nx)),
+         "launch walk_switch");
+  ctx->w_cur = nx;
+  ctx->w_pending = false;
+  ctx->w_est = ctx->w_pend_est;
   ctx->stats.resorts += 1;
 }
 
@@ -2138,6 +2223,12 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
                                  ctx->g_lo.p),
            "launch prep_nodes");
     const bool walk = ctx->walk && ctx->Ns > 0;
+    // PE_ASYNC_RESORT=0: rebuild the walk index in line, on the main stream (A/B; read per call).
+    // Otherwise the rebuild starts kResortEarly updates before the threshold on the side stream and
+    // is taken over once done -- or waited for past kResortLate updates over the threshold.
+    const bool async_resort = walk && !(std::getenv("PE_ASYNC_RESORT") && std::atoi(std::getenv("PE_ASYNC_RESORT")) == 0);
+    const int64_t kResortEarly = std::min<int64_t>(4096, ctx->resort_nodes / 4);
+    const int64_t kResortLate = std::max<int64_t>(1, ctx->resort_nodes / 2);
     hipchk(ctx->w_stat.ensure(2), "alloc walk counters");
     hipchk(hipMemsetAsync(ctx->w_stat.p, 0, 2 * sizeof(unsigned long long), ctx->stream), "memset walk counters");
     if (walk) walk_resort(ctx);
@@ -2336,7 +2427,13 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       buf_gen[b] = gen;
       if (walk) {   // one 64-B request per block: read from pinned host memory, no H2D copy
-        if (ctx->w_est > ctx->resort_nodes) walk_resort(ctx);
+        if (ctx->w_pending &&
+            (hipEventQuery(ctx->w_ev_done) == hipSuccess || ctx->w_est > ctx->resort_nodes + kResortLate))
+          walk_switch(ctx);
+        if (!ctx->w_pending) {
+          if (async_resort && ctx->w_est > ctx->resort_nodes - kResortEarly) walk_resort_async(ctx);
+          else if (ctx->w_est > ctx->resort_nodes) walk_resort(ctx);
+        }
         std::pair<hipEvent_t, hipEvent_t> evp{nullptr, nullptr};
         if (wflush) hipchk(hipMemsetD32Async((hipDeviceptr_t)ctx->w_flush.p, ctx->walk_gen, (size_t)128 << 20, s), "flush");
         if (wev) {
@@ -2439,10 +2536,13 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       if (nu > 0) {   // the kernel reads the pinned records directly (no H2D copy)
         const pe::WalkIndex w = walk_index(ctx);
+        const pe::WalkIndex wn = walk_index(ctx, 1 - ctx->w_cur);   // (read only while a rebuild is pending)
         hipchk(pe::launch_apply(s, ctx->res.p, ctx->stride, hu.dev, nu, (uint64_t)ctx->begin, ctx->g_kn.p,
-                                ctx->g_lo.p, ctx->labels.p, walk ? &w : nullptr),
+                                ctx->g_lo.p, ctx->labels.p, walk ? &w : nullptr,
+                                walk && ctx->w_pending ? &wn : nullptr),
                "launch apply");
         ctx->w_est += nu;
+        if (ctx->w_pending) ctx->w_pend_est += nu;
       }
     };
     auto timed_resolve = [&](const std::vector<int32_t>& groups, std::vector<pe::Update>& updates,
@@ -2582,6 +2682,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       restart();
     }
     hipchk(hipStreamSynchronize(s), "sync greedy");
+    walk_drop_pending(ctx);   // (the next call rebuilds in line anyway)
     if (walk) {
       unsigned long long wc[2] = {0, 0};
       hipchk(hipMemcpy(wc, ctx->w_stat.p, sizeof(wc), hipMemcpyDeviceToHost), "D2H walk counters");

@@ -311,9 +311,17 @@ struct WalkIndex {
   int64_t sstride, nr;
 };
 // kin[n] = K(n) of a walkable node (no negative residual, not saturating), else WK_INVALID; the
-// saturating ones are appended to the overlay (cleared by the caller beforehand).
+// saturating ones are appended to the overlay (cleared by the caller beforehand) -- or, with `slow`
+// (a rebuild on the side stream, whose overlay only the main stream's applies write), flagged in
+// slow[n] for walk_switch to add.
 hipError_t launch_walk_prep(hipStream_t s, const int64_t* res, int64_t stride, int64_t Ns, const uint64_t* kn,
-                            const uint32_t* labels, uint64_t* kin, const WalkIndex& w);
+                            const uint32_t* labels, uint64_t* kin, const WalkIndex& w, uint32_t* slow = nullptr);
+// Takes over an index rebuilt on the side stream (pe_engine walk_resort_async), on the main stream
+// once the rebuild is done: every node an apply moved into nx's overlay while it was rebuilt leaves
+// nx's sorted walk (its entry may hold a state read mid-update), and the flagged saturating nodes
+// join nx's overlay with their current state.
+hipError_t launch_walk_switch(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
+                              const uint32_t* slow, const WalkIndex& nx);
 // hipcub radix sort of n u64 keys (temp == nullptr: *temp_bytes = the scratch size needed).
 hipError_t sort_keys_u64(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int64_t n, hipStream_t s);
 // Sorted SoA copy, pos[], round summaries from the sorted keys w.sk.
@@ -332,9 +340,11 @@ hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const
 
 // upd: [n] records {local node (i64), res[4]} -> res[d][node] = value (absolute)
 // (kn, lo nullable: refreshed for the updated nodes when given; w nullable: the updated nodes
-// leave the sorted walk and join its overlay)
+// leave the sorted walk and join its overlay; nx nullable: an index being rebuilt on the side
+// stream -- the updated nodes join its overlay too, its sorted entries are left to walk_switch)
 hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n, uint64_t id_base,
-                        uint64_t* kn, uint32_t* lo, const uint32_t* labels, const WalkIndex* w);
+                        uint64_t* kn, uint32_t* lo, const uint32_t* labels, const WalkIndex* w,
+                        const WalkIndex* nx = nullptr);
 
 // Inventory delta for one slot of this shard (pe_update_nodes): residual written to both the
 // live and the reset copy, labels and island replaced.  Slots are unique within a launch.

@@ -1671,7 +1671,7 @@ __device__ __forceinline__ void overlay_add(const WalkIndex& w, int64_t n, const
 __global__ __launch_bounds__(256) void walk_prep_kernel(const int64_t* __restrict__ res, int64_t stride, int64_t Ns,
                                                         const uint64_t* __restrict__ kn,
                                                         const uint32_t* __restrict__ labels, uint64_t* __restrict__ kin,
-                                                        WalkIndex w) {
+                                                        WalkIndex w, uint32_t* __restrict__ slow) {
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= Ns) return;
   const int64_t r[D] = {res[n], res[stride + n], res[2 * stride + n], res[3 * stride + n]};
@@ -1682,17 +1682,47 @@ __global__ __launch_bounds__(256) void walk_prep_kernel(const int64_t* __restric
     k = WK_INVALID;                  // fits nothing
   } else if (K == KEY_SLOW) {
     k = WK_INVALID;                  // saturating terms: evaluated in full through the overlay
-    w.in_ovl[n] = 1u;
-    overlay_add(w, n, r, labels[n]);
+    if (slow) {
+      slow[n] = 1u;                  // (side-stream rebuild: walk_switch adds it)
+    } else {
+      w.in_ovl[n] = 1u;
+      overlay_add(w, n, r, labels[n]);
+    }
   }
   kin[n] = k;
 }
 
 hipError_t launch_walk_prep(hipStream_t s, const int64_t* res, int64_t stride, int64_t Ns, const uint64_t* kn,
-                            const uint32_t* labels, uint64_t* kin, const WalkIndex& w) {
+                            const uint32_t* labels, uint64_t* kin, const WalkIndex& w, uint32_t* slow) {
   if (Ns <= 0) return hipSuccess;
   hipLaunchKernelGGL(walk_prep_kernel, dim3((unsigned)((Ns + 255) / 256)), dim3(256), 0, s, res, stride, Ns, kn, labels,
-                     kin, w);
+                     kin, w, slow);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void walk_switch_kernel(const int64_t* __restrict__ res, int64_t stride,
+                                                          const uint32_t* __restrict__ labels, int64_t Ns,
+                                                          const uint32_t* __restrict__ slow, WalkIndex nx) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= Ns) return;
+  if (nx.in_ovl[n]) {                // updated during the rebuild: its overlay entry is current
+    const uint32_t p = nx.pos[n];
+    if (p != ~0u) {
+      nx.sk[p] = WK_INVALID;
+      nx.pos[n] = ~0u;
+    }
+  } else if (slow[n]) {
+    const int64_t r[D] = {res[n], res[stride + n], res[2 * stride + n], res[3 * stride + n]};
+    nx.in_ovl[n] = 1u;
+    overlay_add(nx, n, r, labels[n]);
+  }
+}
+
+hipError_t launch_walk_switch(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels, int64_t Ns,
+                              const uint32_t* slow, const WalkIndex& nx) {
+  if (Ns <= 0) return hipSuccess;
+  hipLaunchKernelGGL(walk_switch_kernel, dim3((unsigned)((Ns + 255) / 256)), dim3(256), 0, s, res, stride, labels, Ns,
+                     slow, nx);
   return hipGetLastError();
 }
 
@@ -1968,7 +1998,8 @@ hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const
 __global__ __launch_bounds__(256) void apply_kernel(int64_t* __restrict__ res, int64_t stride,
                                                     const int64_t* __restrict__ upd, int64_t n, uint64_t id_base,
                                                     uint64_t* __restrict__ kn, uint32_t* __restrict__ lo,
-                                                    const uint32_t* __restrict__ labels, WalkIndex w, int walk) {
+                                                    const uint32_t* __restrict__ labels, WalkIndex w, int walk,
+                                                    WalkIndex nx, int pend) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t* u = upd + i * (D + 1);
@@ -1997,15 +2028,25 @@ __global__ __launch_bounds__(256) void apply_kernel(int64_t* __restrict__ res, i
 #pragma unroll
       for (int d = 0; d < D; ++d) w.ovl_res[d * w.sstride + i] = r[d];
     }
+    if (pend) {                               // the index being rebuilt: overlay only (walk_switch
+      if (atomicExch(&nx.in_ovl[node], 1u) == 0u) {   // drops its sorted entry)
+        overlay_add(nx, node, r, labels[node]);
+      } else {
+        const uint32_t i = nx.ovl_idx[node];
+#pragma unroll
+        for (int d = 0; d < D; ++d) nx.ovl_res[d * nx.sstride + i] = r[d];
+      }
+    }
   }
 }
 
 hipError_t launch_apply(hipStream_t s, int64_t* res, int64_t stride, const int64_t* upd, int64_t n, uint64_t id_base,
-                        uint64_t* kn, uint32_t* lo, const uint32_t* labels, const WalkIndex* w) {
+                        uint64_t* kn, uint32_t* lo, const uint32_t* labels, const WalkIndex* w,
+                        const WalkIndex* nx) {
   if (n <= 0) return hipSuccess;
   const WalkIndex none{};
   hipLaunchKernelGGL(apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, res, stride, upd, n, id_base,
-                     kn, lo, labels, w ? *w : none, w ? 1 : 0);
+                     kn, lo, labels, w ? *w : none, w ? 1 : 0, (w && nx) ? *nx : none, (w && nx) ? 1 : 0);
   return hipGetLastError();
 }
 
