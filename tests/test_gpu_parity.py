@@ -571,6 +571,27 @@ def test_greedy_walk_and_full_scan(flags, resort, mix, N, J, gpu_frac, topk, wg)
     e.close()
 
 
+@pytest.mark.parametrize("resort", [1, 16, 64])
+@pytest.mark.parametrize("mix,N,J,gpu_frac", [("mixed", 6000, 600, 0.3), ("island8", 1500, 400, 0.7)])
+def test_greedy_walk_rebuild_in_line_and_side_stream(resort, mix, N, J, gpu_frac):
+    """The walk index rebuilt in line (PE_ASYNC_RESORT=0) and on the side stream while the walks go on
+    (default): both exact vs the oracle, identical placements, and the side-stream rebuilds taken over
+    during the batch (resorts > 1)."""
+    inv = synth.make_inventory(N, 91 + N, gpu_frac)
+    batch = synth.make_jobs(J, 93 + J, mix)
+    out = {}
+    for mode in ("0", "1"):
+        os.environ["PE_ASYNC_RESORT"] = mode
+        try:
+            e = Engine(0, topk=16, window_groups=16, resort_nodes=resort)
+            out[mode] = check_greedy(e, inv, batch)
+            assert e.stats()["resorts"] > 1
+            e.close()
+        finally:
+            os.environ.pop("PE_ASYNC_RESORT", None)
+    np.testing.assert_array_equal(out["0"], out["1"])
+
+
 def test_greedy_walk_overlay_compaction():
     """Overlay larger than the LDS candidate buffer (every node updated, resort never triggers):
     the walk's in-loop compaction to the K + 1 smallest keeps the lists exact."""
