@@ -146,6 +146,13 @@ typedef struct {
 int pe_abi_version(void);
 /* RCCL unique id for a sharded context (call on rank 0, broadcast the bytes to every rank). */
 int pe_comm_id(uint8_t out[PE_COMM_ID_BYTES]);
+/* With a comm_id, pe_create waits for the RCCL communicator at most PE_RCCL_INIT_TIMEOUT_S seconds
+ * (environment, default 120) and returns PE_ERCCL past that bound.  The abandoned set-up keeps
+ * running on a detached thread (RCCL's bootstrap cannot be cancelled), so peers that arrive late may
+ * still get a communicator whose collectives would hang.  PE_ERCCL on ANY rank is therefore a
+ * collective decision: every rank must destroy its context (and, if it goes on, create a new one
+ * with a host `exchange` or a fresh comm_id), as bench.py does through its gloo vote.  A process
+ * that abandoned a set-up should leave with _exit(). */
 int pe_create(const pe_config* cfg, pe_ctx** out);
 void pe_destroy(pe_ctx* ctx);
 const char* pe_last_error(const pe_ctx* ctx); /* valid until the next call on ctx */

@@ -1001,7 +1001,13 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       const int64_t out_bytes = oo[3] + pe::agg_r16(n_jobs);
       ensure_pinned(ctx->a_stage, (size_t)total, "alloc pinned aggregation batch");
       ensure_pinned(ctx->a_outh, (size_t)out_bytes, "alloc pinned aggregation outputs");
-      if (!ctx->a_flag.p) hipchk(ctx->a_flag.ensure(16, kZeroCopy), "alloc pinned flag");
+      if (!ctx->a_flag.p) {
+        hipchk(ctx->a_flag.ensure(16, kZeroCopy), "alloc pinned flag");
+        // pinned memory may come back recycled (e.g. the flag of an engine destroyed earlier): clear
+        // it, and start the generations past whatever it held, so no stale value matches a wait
+        __atomic_store_n(ctx->a_flag.p, 0u, __ATOMIC_RELEASE);
+        ctx->agg_gen = 0;
+      }
       if (!ctx->a_ctr.p) {
         hipchk(ctx->a_ctr.ensure(1), "alloc done counter");
         hipchk(hipMemsetAsync(ctx->a_ctr.p, 0, 4, ctx->stream), "memset done counter");
@@ -1102,7 +1108,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
           hipchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
           ctx->a_ev.push_back(e);
         }
-        int64_t prev_s0 = -1, prev_s1 = -1;
+        int64_t prev_s0 = -1, prev_s1 = -1, prev_c = -1;   // prev_c: event of the last launched chunk
         auto job_end = [&](int64_t s1) { return all[(size_t)s1 - 1].j0 + all[(size_t)s1 - 1].nj; };
         for (int64_t c = 0; c < C && first_neg == INT64_MAX; ++c) {
           const int64_t s0 = nseg * c / C, s1 = nseg * (c + 1) / C;
@@ -1118,13 +1124,14 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
                  "launch pg_agg_segments");
           hipchk(hipEventRecord(ctx->a_ev[(size_t)c], ctx->stream), "event record");
           if (prev_s1 > prev_s0) {   // the previous chunk's outputs, while this chunk runs
-            hipchk(hipEventSynchronize(ctx->a_ev[(size_t)c - 1]), "event sync");
+            hipchk(hipEventSynchronize(ctx->a_ev[(size_t)prev_c]), "event sync");
             const int64_t ja = all[(size_t)prev_s0].j0, jb = job_end(prev_s1);
             parallel_for(jb - ja, [&](int64_t a, int64_t e) { unpack(ja + a, ja + e); });
             unpacked = jb;
           }
           prev_s0 = s0;
           prev_s1 = s1;
+          prev_c = c;
         }
         hipchk(hipStreamSynchronize(ctx->stream), "sync pg_agg_segments");   // (also before an EINVAL:
                                                                              // launched chunks read the batch)

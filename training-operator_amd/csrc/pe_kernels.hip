@@ -1842,8 +1842,9 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   }
   WPT(1);
   // overlay: every node changed since the sort (and the saturating ones), current values
-  // OV entries per thread between barriers (the overlay holds up to resort_nodes = 16k entries: one
-  // barrier, append and compaction check per 4096 instead of per 1024)
+  // OV entries per thread between barriers (the overlay holds up to resort_nodes entries, and up to
+  // ~1.5 x resort_nodes while a side-stream rebuild is pending: one barrier, append and compaction
+  // check per 4096 instead of per 1024)
   constexpr int OV = 4;
   const int no = *w.ovl_n;
   for (int i0 = 0; i0 < no; i0 += OV * WK_ROUND) {
