@@ -358,7 +358,7 @@ def main(argv=None):
     sys.path[:0] = [p for p in (ROOT, os.path.join(ROOT, "training-operator_amd"), PROFILES) if p not in sys.path]
     import numpy as np
 
-    from placement import Engine, comm_id, synth
+    from placement import Engine, HostExchange, comm_id, synth
     from provenance import source_hash
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -369,21 +369,26 @@ def main(argv=None):
         sys.exit(2)
     dist = None
     cid, exchange, device = None, None, local
-    host_exchange = os.environ.get("PE_BENCH_EXCHANGE", "rccl") == "host"
+    # PE_BENCH_EXCHANGE: "rccl" (default), "host" (rehearsal on one node, e.g. a 1-GPU box: the native
+    # shared-memory all-gather pe_host_exchange), "gloo" (rehearsal through a Python gloo callback)
+    xmode = os.environ.get("PE_BENCH_EXCHANGE", "rccl")
+    host_exchange = xmode in ("host", "gloo")
     if world > 1:
         import torch
         import torch.distributed as dist
         if host_exchange:
-            # rehearsal mode for a 1-GPU box: every rank on one device, candidate blobs exchanged
-            # over gloo instead of RCCL (the driver's multi-GPU runs use the RCCL default)
+            # rehearsal mode for a 1-GPU box: every rank on one device (RCCL cannot put two ranks on
+            # one GPU), candidate blobs exchanged through host memory instead of RCCL (the driver's
+            # multi-GPU runs use the RCCL default)
             dist.init_process_group("gloo")
             device = int(os.environ.get("PE_BENCH_DEVICE", "0"))
             tdev = "cpu"
 
-            def exchange(blob: bytes) -> bytes:
-                parts = [None] * world
-                dist.all_gather_object(parts, blob)
-                return b"".join(parts)
+            if xmode == "gloo":
+                def exchange(blob: bytes) -> bytes:
+                    parts = [None] * world
+                    dist.all_gather_object(parts, blob)
+                    return b"".join(parts)
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -401,10 +406,19 @@ def main(argv=None):
         # depend on the transport whose set-up failed
         gloo = dist.new_group(backend="gloo")
 
-        def gloo_exchange(blob: bytes) -> bytes:
-            parts = [None] * world
-            dist.all_gather_object(parts, blob, group=gloo)
-            return b"".join(parts)
+        hx = []
+
+        def shm_exchange():
+            """One pe_host_exchange per process (the ranks of this node; shared by every engine of the
+            bench, which all make their calls in the same order on every rank)."""
+            if not hx:
+                names = [f"/pe_bench_{os.getpid()}_{time.time_ns() & 0xFFFFFFFF:x}" if rank == 0 else None]
+                dist.broadcast_object_list(names, src=0, group=gloo)
+                wg = args.window_groups or 128
+                k = args.topk or 256
+                hx.append(HostExchange(names[0], rank, world, wg * (16 + 8 * k)))
+                dist.barrier(group=gloo)
+            return hx[0]
 
         def first_error(err):
             """Every rank's set-up error (None = fine) -> the first one, on every rank."""
@@ -433,6 +447,9 @@ def main(argv=None):
         def new_comm():
             return None
 
+        def shm_exchange():
+            return None
+
         def barrier():
             pass
 
@@ -449,12 +466,15 @@ def main(argv=None):
             return [x]
 
     fallbacks = []
+    if world > 1 and xmode == "host":
+        exchange = shm_exchange()
 
     def make_engine(**kw):
         """An engine on this rank's GPU with a fresh RCCL communicator (world > 1).  If the RCCL set-up
         fails on any rank (pe_create returns PE_ERCCL within PE_RCCL_INIT_TIMEOUT_S), every rank builds
-        its engine with a gloo all-gather of the candidate blobs instead -- the same sharded greedy,
-        windows exchanged through host memory (not pipelined) -- and the JSON line says so."""
+        its engine with the node's shared-memory all-gather instead (pe_host_exchange: the same
+        sharded, pipelined and per-group signalled greedy with another transport); the JSON line says
+        so at its top level ("degraded") and in config.greedy_exchange."""
         err = None
         try:
             if world > 1 and rank == world - 1 and os.environ.get("PE_BENCH_SIMULATE_RCCL_FAIL"):   # (test hook)
@@ -469,7 +489,7 @@ def main(argv=None):
         if e is not None:
             e.close()
         fallbacks.append(err)
-        return Engine(device, rank=rank, world_size=world, comm=None, exchange=gloo_exchange, **kw)
+        return Engine(device, rank=rank, world_size=world, comm=None, exchange=shm_exchange(), **kw)
 
     N = args.nodes
     J = args.fit_jobs * (world if args.scaling == "weak" else 1)
@@ -534,8 +554,10 @@ def main(argv=None):
                                                             else ""),
                    "feasible_pairs": feasible,
                    "greedy_exchange": ("none (one GPU)" if world == 1
-                                       else f"gloo host exchange: RCCL set-up failed ({fallbacks[0]})" if fallbacks
-                                       else "gloo host exchange (rehearsal)" if host_exchange
+                                       else f"host shared-memory exchange: RCCL set-up failed ({fallbacks[0]})"
+                                       if fallbacks
+                                       else "gloo host exchange (rehearsal)" if xmode == "gloo"
+                                       else "host shared-memory exchange (rehearsal)" if host_exchange
                                        else "RCCL all-gather + device merge")},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": prof["traffic"],
@@ -875,6 +897,12 @@ def main(argv=None):
                           "inventory", "jobs_placed": int((gst == 0).sum()),
                 "naive_gang_placements_per_s": 40 / cn,
                 "naive_sample": "naive per-pod argmin over all nodes (oracle.c orc_place_greedy), first 40 jobs"}
+    if world > 1:
+        # an RCCL set-up failure on any rank moved every engine to the host exchange: same results,
+        # another transport -- said at the top level, not only in config.greedy_exchange
+        out["degraded"] = bool(fallbacks)
+        if fallbacks:
+            out["degraded_reason"] = f"{len(fallbacks)} engine(s) without RCCL: {fallbacks[0]}"
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

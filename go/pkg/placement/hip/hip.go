@@ -21,7 +21,8 @@ package hip
 #include "placement.h"
 
 // The Go side cannot hand a Go func to C as a pe_allgather_fn; sharded contexts use RCCL
-// (comm_id), which needs no callback.
+// (comm_id), which needs no callback, or the library's own shared-memory all-gather (HostExchange).
+static pe_allgather_fn hx_allgather_fn(void) { return pe_host_exchange_allgather; }
 */
 import "C"
 
@@ -99,6 +100,53 @@ type Config struct {
 	FitPathMask     int32
 	GreedyFlags     int32
 	ResortNodes     int32
+	// HostExchange replaces RCCL for ranks of one node (e.g. when the communicator set-up failed on
+	// some rank: PE_ERCCL there means every rank drops its engine and creates a new one).
+	HostExchange *HostExchange
+}
+
+// HostExchange is pe_host_exchange: an all-gather through a POSIX shared-memory segment, for the
+// ranks of one node.  Every rank opens the same name ("/..."); rank 0 creates the segment.
+type HostExchange struct {
+	h    *C.pe_host_exchange
+	rank int32
+	size int32
+}
+
+// OpenHostExchange opens (rank 0: creates) the segment; maxBytes bounds one rank's block per call
+// (WindowGroups x (16 + 8 x TopK) for the greedy windows).
+func OpenHostExchange(name string, rank, world int32, maxBytes int) (*HostExchange, error) {
+	cn := C.CString(name)
+	defer C.free(unsafe.Pointer(cn))
+	x := &HostExchange{rank: rank, size: world}
+	if rc := C.pe_host_exchange_open(cn, C.int32_t(rank), C.int32_t(world), C.size_t(maxBytes), &x.h); rc != C.PE_OK {
+		return nil, fmt.Errorf("placement: pe_host_exchange_open: %d", int(rc))
+	}
+	runtime.SetFinalizer(x, (*HostExchange).Close)
+	return x, nil
+}
+
+// Allgather gathers every rank's send block into recv (world x len(send) bytes, rank order).
+func (x *HostExchange) Allgather(send, recv []byte) error {
+	if len(recv) < int(x.size)*len(send) {
+		return errors.New("placement: HostExchange.Allgather: recv too small")
+	}
+	var sp, rp unsafe.Pointer
+	if len(send) > 0 {
+		sp, rp = unsafe.Pointer(&send[0]), unsafe.Pointer(&recv[0])
+	}
+	if rc := C.pe_host_exchange_allgather(unsafe.Pointer(x.h), sp, rp, C.size_t(len(send))); rc != C.PE_OK {
+		return fmt.Errorf("placement: pe_host_exchange_allgather: %d", int(rc))
+	}
+	return nil
+}
+
+// Close unmaps the segment.  Idempotent; the engines using it must be closed first.
+func (x *HostExchange) Close() {
+	if x.h != nil {
+		C.pe_host_exchange_close(x.h)
+		x.h = nil
+	}
 }
 
 // Engine is one pe_ctx: a GPU, an inventory shard, a stream.  Safe for concurrent use (the
@@ -186,6 +234,10 @@ func New(cfg Config) (*Engine, error) {
 	c.fit_path_mask = C.int32_t(cfg.FitPathMask)
 	c.greedy_flags = C.int32_t(cfg.GreedyFlags)
 	c.resort_nodes = C.int32_t(cfg.ResortNodes)
+	if cfg.HostExchange != nil {
+		c.exchange = C.hx_allgather_fn()
+		c.exchange_user = unsafe.Pointer(cfg.HostExchange.h)
+	}
 	rc := C.pe_create(&c, &e.ctx)
 	if rc != C.PE_OK {
 		C.free(unsafe.Pointer(e.name))

@@ -83,6 +83,18 @@ enum { PE_KIND_CONTAINER = 0, PE_KIND_INIT = 1, PE_KIND_SIDECAR = 2, PE_KIND_OVE
  * gather `bytes` from every rank into recv[rank * bytes]; return 0 on success. */
 typedef int (*pe_allgather_fn)(void* user, const void* send, void* recv, size_t bytes);
 
+/* Intra-node host exchange (no reference counterpart: the transport of the sharded greedy when the
+ * ranks share one node and RCCL cannot be set up, e.g. several ranks on one GPU).  An all-gather
+ * through a POSIX shared-memory segment `name` ("/..."), one barrier per call; rank 0 creates it,
+ * the other ranks wait for it (PE_HX_TIMEOUT_S, default 300 s) and the last rank to attach unlinks
+ * the name.  Use as pe_config.exchange = pe_host_exchange_allgather, exchange_user = the handle;
+ * every rank must make the same sequence of calls with the same byte counts (<= max_bytes).  A peer
+ * that does not arrive within PE_HX_TIMEOUT_S makes the call return PE_ERCCL. */
+typedef struct pe_host_exchange pe_host_exchange;
+int pe_host_exchange_open(const char* name, int32_t rank, int32_t world, size_t max_bytes, pe_host_exchange** out);
+int pe_host_exchange_allgather(void* user, const void* send, void* recv, size_t bytes);
+void pe_host_exchange_close(pe_host_exchange* hx);
+
 typedef struct pe_ctx pe_ctx;
 
 typedef struct {

@@ -2,7 +2,10 @@
 the engine on device 0, exchanging the per-window candidate blobs with the other ranks over gloo
 (the pe_config.exchange hook -- RCCL's role on a multi-GPU node).  Writes its results to out_dir.
 
-    python tests/mp_shard_worker.py <rank> <world> <port> <mix> <n_nodes> <n_jobs> <out_dir>
+    python tests/mp_shard_worker.py <rank> <world> <port> <mix> <n_nodes> <n_jobs> <out_dir> [gloo|shm]
+
+Transport "shm": the native shared-memory all-gather (pe_host_exchange) instead of the Python gloo
+callback; gloo then only broadcasts the segment name.
 """
 import os
 import sys
@@ -15,10 +18,11 @@ for p in (ROOT, os.path.join(ROOT, "training-operator_amd")):
 def main():
     rank, world, port = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
     mix, n_nodes, n_jobs, out_dir = sys.argv[4], int(sys.argv[5]), int(sys.argv[6]), sys.argv[7]
+    transport = sys.argv[8] if len(sys.argv) > 8 else "gloo"
     import numpy as np
     import torch.distributed as dist
 
-    from placement import Engine, synth
+    from placement import Engine, HostExchange, synth
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -27,6 +31,12 @@ def main():
         parts = [None] * world
         dist.all_gather_object(parts, blob)
         return b"".join(parts)
+
+    if transport == "shm":
+        names = [f"/pe_mp_{port}_{os.getpid()}" if rank == 0 else None]
+        dist.broadcast_object_list(names, src=0)
+        exchange = HostExchange(names[0], rank, world, 128 * (16 + 8 * 256))
+        dist.barrier()
 
     inv = synth.make_inventory(n_nodes, 3, 0.2 if mix != "gang8" else 1.0)
     batch = synth.make_jobs(n_jobs, 3, mix)

@@ -27,12 +27,17 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("world,mix,n_nodes,n_jobs,host_merge", [(2, "mixed", 20000, 600, False),
-                                                                 (3, "gang8", 9000, 300, False),
-                                                                 (2, "island8", 6000, 300, True)])
-def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, host_merge):
+@pytest.mark.parametrize("world,mix,n_nodes,n_jobs,host_merge,transport", [(2, "mixed", 20000, 600, False, "gloo"),
+                                                                           (3, "gang8", 9000, 300, False, "gloo"),
+                                                                           (2, "island8", 6000, 300, True, "gloo"),
+                                                                           (2, "mixed", 20000, 600, False, "shm"),
+                                                                           (3, "island8", 9000, 300, False, "shm"),
+                                                                           (2, "gang8", 6000, 300, True, "shm")])
+def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, host_merge, transport):
     """host_merge False: the gathered shard lists are merged on the device (merge_shards, the
-    default); True: PE_HOST_MERGE=1, the host's lazy k-way merge."""
+    default); True: PE_HOST_MERGE=1, the host's lazy k-way merge.  transport: the Python gloo
+    callback, or the native shared-memory all-gather (pe_host_exchange).  Either way the windows are
+    pipelined (the launch helper runs the exchange while the host resolves)."""
     port = free_port()
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PE_HOST_MERGE"):
@@ -40,7 +45,7 @@ def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, 
     if host_merge:
         env["PE_HOST_MERGE"] = "1"
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "mp_shard_worker.py"), str(r), str(world), str(port),
-                               mix, str(n_nodes), str(n_jobs), str(tmp_path)], env=env, stdout=subprocess.PIPE,
+                               mix, str(n_nodes), str(n_jobs), str(tmp_path), transport], env=env, stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(world)]
     outs = []
     try:

@@ -7,7 +7,10 @@ multi-rank bench runs).
    one-rank run of the same workload: feasible pairs of the fit mask, placed jobs of every greedy
    line, and the node shards must partition the inventory.  The last rank's engine set-up is made to
    fail (PE_BENCH_SIMULATE_RCCL_FAIL): the ranks vote over gloo and all rebuild their engines with the
-   gloo exchange, which the JSON line reports (config.greedy_exchange).
+   node's shared-memory exchange (pe_host_exchange), which the JSON line reports at its top level
+   ("degraded") and in config.greedy_exchange.  That fallback runs the production loop (pipelined
+   windows, device merge signalled per group), so the 2-rank cfg3 batch must stay within 2x of the
+   1-rank one (round 3's synchronous gloo fallback was 20x).
 2. A communicator whose peers never arrive returns PE_ERCCL after PE_RCCL_INIT_TIMEOUT_S instead of
    blocking in ncclCommInitRank (non-blocking RCCL set-up, pe_engine.cpp nccl_settle)."""
 import json
@@ -61,6 +64,8 @@ def test_bench_two_ranks_matches_one():
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     assert one["config"]["greedy_exchange"] == "none (one GPU)"
     assert "RCCL set-up failed" in two["config"]["greedy_exchange"] and "simulated" in two["config"]["greedy_exchange"]
+    assert "shared-memory" in two["config"]["greedy_exchange"]
+    assert two["degraded"] is True and "simulated" in two["degraded_reason"] and "degraded" not in one
     cfg1, cfg2 = one["config"], two["config"]
     assert sum(cfg2["shard_nodes_per_rank"]) == cfg2["nodes"] == 100000 and len(cfg2["shard_nodes_per_rank"]) == 2
     assert cfg2["feasible_pairs"] == cfg1["feasible_pairs"] > 0
@@ -70,6 +75,10 @@ def test_bench_two_ranks_matches_one():
     for k in ("fit_many_values", "fit_worst_case", "fit_adversarial"):
         assert two[k]["feasible_pairs"] == one[k]["feasible_pairs"], k
     assert two["value"] > 0 and two["fit_weak_scaling"]["value"] > 0
+    # no throughput cliff on the fallback transport (both ranks share this box's one GPU)
+    for k in ("cfg3", "cfg4"):
+        assert two["configs"][k]["ms_per_batch"] <= 2.0 * one["configs"][k]["ms_per_batch"], \
+            (k, two["configs"][k], one["configs"][k])
 
 
 _INIT = r"""

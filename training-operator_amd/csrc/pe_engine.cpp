@@ -321,6 +321,7 @@ struct pe_ctx {
   int pin_cpu = -2;                       // greedy thread pinning at world > 1: a CPU of this rank's L3 (-2: not chosen yet)
   HostBuf<uint8_t> h_out, h_out2, h_own;   // h_out2: the pipelined loop's second blob buffer (h_outx: 3rd, 4th)
   HostBuf<uint8_t> h_merged;                // host-exchange windows: the device-merged lists
+  HostBuf<uint8_t> h_xg[4];                 // pipelined host exchange: the gathered lists of blob buffer b
   HostBuf<int64_t> h_upd;
   // greedy sorted walk (pe_kernels.h WalkIndex; the default window path, greedy_flags bit1 = full scan)
   bool walk = true;
@@ -365,6 +366,7 @@ struct pe_ctx {
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
     g_upd.release(); g_kn.release(); g_lo.release(); h_groups.release(); h_groups2.release(); h_out.release(); h_out2.release(); h_own.release(); h_merged.release(); h_upd.release();
+    for (auto& x : h_xg) x.release();
     for (int i = 0; i < 2; ++i) {
       h_groupsx[i].release();
       h_outx[i].release();
@@ -2337,8 +2339,10 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     std::vector<pe::GroupCands> cands;
     hipStream_t s = ctx->stream;
     const bool use_exchange = ctx->exchange && !(ctx->world == 1 && !ctx->comm);
-    // The host exchange is a synchronous callback: it cannot sit behind queued device work.
-    const bool pipelined = ctx->pipeline && !use_exchange;
+    // The host exchange is a synchronous callback.  Pipelined, the launch helper runs it: after it
+    // issued window w+1's scan it waits for the own lists, exchanges them and launches the device
+    // merge, signalled per group like an RCCL window -- all while the host resolves window w.
+    const bool pipelined = ctx->pipeline;
     // ---- one window on the device: group requests H2D, scan, merge, (RCCL all-gather), blob D2H
     int cb = 0;   // the blob buffer of the window being resolved
     std::unique_ptr<SpinWorker> worker;
@@ -2398,7 +2402,11 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     auto hgroups = [&](int b) -> HostBuf<ReqRec>& {
       return !signalled || b == 0 ? ctx->h_groups : b == 1 ? ctx->h_groups2 : ctx->h_groupsx[b - 2];
     };
-    if (dev_merge && use_exchange) hipchk(ctx->h_merged.ensure((size_t)Wmax * gb, kZeroCopy), "alloc pinned merged");
+    if (dev_merge && use_exchange && !pipelined)
+      hipchk(ctx->h_merged.ensure((size_t)Wmax * gb, kZeroCopy), "alloc pinned merged");
+    if (dev_merge && use_exchange && pipelined)
+      for (int b = 0; b <= std::max(depth, 1); ++b)
+        hipchk(ctx->h_xg[b].ensure((size_t)Wmax * gb * ctx->world, kZeroCopy), "alloc pinned gathered");
     const uint8_t* last_blob = nullptr;   // the parsed blob of the window being resolved (one list per group
                                           // unless the shards are merged on the host)
     uint32_t buf_gen[4] = {0, 0, 0, 0};
@@ -2480,6 +2488,14 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         // written in place
       } else if (use_exchange) {
         hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
+        if (pipelined) {   // (the launch helper, or the main thread at a restart) exchange now
+          hipchk(hipStreamSynchronize(s), "sync own cands");
+          if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, dev_merge ? ctx->h_xg[b].p : outbuf(b), bytes) != 0)
+            raise(PE_ERCCL, "exchange callback failed");
+          if (dev_merge)   // the gathered lists (pinned) merged on the device, signalled per group
+            hipchk(pe::launch_merge_shards(s, ctx->h_xg[b].dev, ctx->world, Wg, K, outbufdev(b), gen),
+                   "launch merge_shards");
+        }
       } else {
         ncclchk(ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
         if (dev_merge)
@@ -2509,7 +2525,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       hipchk(hipStreamSynchronize(s), "sync window");
       last_blob = outbuf(b);
-      if (use_exchange) {
+      if (use_exchange && !pipelined) {
         if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, outbuf(b), bytes) != 0)
           raise(PE_ERCCL, "exchange callback failed");
         if (dev_merge) {   // the gathered blob (pinned) merged by the device into h_merged

@@ -21,7 +21,7 @@ from ._abi import (PE_JOB_PLACED, PE_JOB_UNSCHEDULABLE, PE_KIND_CONTAINER, PE_KI
 
 V1, V2 = PE_MODE_V1, PE_MODE_V2
 
-__all__ = ["Engine", "Resolver", "PlacementError", "V1", "V2", "PE_JOB_PLACED", "PE_JOB_UNSCHEDULABLE",
+__all__ = ["Engine", "HostExchange", "Resolver", "PlacementError", "V1", "V2", "PE_JOB_PLACED", "PE_JOB_UNSCHEDULABLE",
            "PE_KIND_CONTAINER", "PE_KIND_INIT", "PE_KIND_SIDECAR", "PE_KIND_OVERHEAD", "PE_KIND_SHIFT", "comm_id",
            "PE_NODE_SET", "PE_NODE_REMOVE"]
 
@@ -48,6 +48,41 @@ def comm_id() -> bytes:
     return bytes(buf)
 
 
+class HostExchange:
+    """pe_host_exchange: the native shared-memory all-gather of one node's ranks (the sharded greedy's
+    transport when RCCL cannot be set up).  Every rank opens the same `name` ("/..."); rank 0 creates
+    the segment.  Pass it as Engine(..., exchange=hx): the engine calls the C function directly (no
+    Python on the window path)."""
+
+    def __init__(self, name: str, rank: int, world: int, max_bytes: int):
+        self.lib = _abi.load()
+        h = ctypes.c_void_p()
+        rc = self.lib.pe_host_exchange_open(name.encode(), rank, world, max_bytes, ctypes.byref(h))
+        if rc != 0:
+            raise PlacementError(rc, f"pe_host_exchange_open({name!r}, rank {rank} of {world})")
+        self.h = h
+        self.rank, self.world = rank, world
+        self.fn = ctypes.cast(self.lib.pe_host_exchange_allgather, _abi.ALLGATHER_FN)
+
+    def allgather(self, blob: bytes) -> bytes:
+        out = ctypes.create_string_buffer(len(blob) * self.world)
+        rc = self.lib.pe_host_exchange_allgather(self.h, blob, out, len(blob))
+        if rc != 0:
+            raise PlacementError(rc, "pe_host_exchange_allgather")
+        return out.raw
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pe_host_exchange_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
 class Engine:
     """One pe_ctx: a GPU, a node-inventory shard, a stream."""
 
@@ -65,7 +100,11 @@ class Engine:
             cbuf = ctypes.create_string_buffer(bytes(comm), _abi.PE_COMM_ID_BYTES)
             self._keep.append(cbuf)
             cfg.comm_id = ctypes.cast(cbuf, ctypes.c_void_p)
-        if exchange is not None:
+        if isinstance(exchange, HostExchange):   # the native transport: C function + handle
+            self._keep.append(exchange)
+            cfg.exchange = exchange.fn
+            cfg.exchange_user = exchange.h
+        elif exchange is not None:
             # exchange(send: bytes) -> bytes (all ranks' blocks concatenated)
             def _cb(user, send, recv, nbytes):
                 try:

@@ -90,6 +90,9 @@ SIGNATURES = {
     "pe_stream": (P, [P]),
     "pe_get_stats": (ctypes.c_int, [P, ctypes.POINTER(PeStats)]),
     "pe_reset_stats": (ctypes.c_int, [P]),
+    "pe_host_exchange_open": (ctypes.c_int, [ctypes.c_char_p, i32, i32, ctypes.c_size_t, ctypes.POINTER(P)]),
+    "pe_host_exchange_allgather": (ctypes.c_int, [P, P, P, ctypes.c_size_t]),
+    "pe_host_exchange_close": (None, [P]),
 }
 
 _lib = None
