@@ -3,6 +3,8 @@
 // and dirty seeds, sequential or pipelined) and times it on this CPU: the exact host work of the run.
 //   g++ -O3 -march=x86-64-v3 -std=c++17 -Itraining-operator_amd/csrc -Iinclude tools/replay_resolver.cc \
 //       training-operator_amd/csrc/pe_resolver.cpp -o tools/replay_resolver && tools/replay_resolver dump.bin [reps]
+#include <time.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -64,14 +66,21 @@ int main(int argc, char** argv) {
     R.set_mirror(pe::Mirror{mirror.data(), N});
     std::vector<pe::GroupCands> cands;
     std::vector<pe::Update> upd;
-    double t_resolve = 0;
+    double t_resolve = 0, t_cpu = 0;
+    auto cpu_ms = [] {   // this thread's CPU time (excludes time the host took the vCPU away, where accounted)
+      timespec ts;
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+      return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+    };
     size_t wi = 0;
     for (; wi < wins.size(); ++wi) {       // the resolve calls of the run, in order
       const Win& w = wins[wi];
       pe::parse_window_keys(w.blob.data(), 1, (int)w.groups.size(), K, cands);
       upd.clear();
       const auto a = std::chrono::steady_clock::now();
+      const double c0 = cpu_ms();
       R.resolve(w.groups, cands, upd, w.seed.empty() ? nullptr : &w.seed);
+      t_cpu += cpu_ms() - c0;
       for (const pe::Update& u : upd)
         for (int d = 0; d < 4; ++d) mirror[u.gid].res[d] = u.res[d];
       t_resolve += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
@@ -82,8 +91,8 @@ int main(int argc, char** argv) {
     uint64_t h = 1469598103934665603ull;   // FNV-1a over the placements and job states (A/B exactness)
     for (int32_t v : R.pod_node()) h = (h ^ (uint32_t)v) * 1099511628211ull;
     for (int32_t v : R.job_status()) h = (h ^ (uint32_t)v) * 1099511628211ull;
-    std::printf("rep %d: %.3f ms total, %.3f ms in resolve, %zu windows, %lld pods placed, %lld rescans, result %016llx\n",
-                r, ms, t_resolve, wi, (long long)R.pods_placed(), (long long)R.rescans(), (unsigned long long)h);
+    std::printf("rep %d: %.3f ms total, %.3f ms in resolve, %.3f ms cpu, %zu windows, %lld pods placed, %lld rescans, result %016llx\n",
+                r, ms, t_resolve, t_cpu, wi, (long long)R.pods_placed(), (long long)R.rescans(), (unsigned long long)h);
   }
   std::printf("best %.3f ms\n", best);
   return 0;

@@ -637,28 +637,15 @@ void Resolver::advance_group() {
   }
 }
 
-// The current job's nodes: a linear search over the few ids (a job touches at most its pod count
-// of nodes, usually < 20), the hash map only past kJobLinear of them.
-int32_t Resolver::job_find(int64_t gid) const {
-  if (jn_.size() > kJobLinear) return jslot_.find(gid);
-  const int64_t* ids = jn_ids_.data();
-  for (size_t i = 0; i < jn_ids_.size(); ++i)
-    if (ids[i] == gid) return (int32_t)i;
-  return -1;
-}
-
-NodeState& Resolver::job_node(int64_t gid) {
-  int32_t i = job_find(gid);
-  if (i < 0) {
-    i = (int32_t)jn_.size();
-    jn_.emplace_back(gid, NodeState{});
-    jn_ids_.push_back(gid);
-    if (jn_.size() == kJobLinear + 1)   // switch to the map: enter every id so far
-      for (size_t k = 0; k < jn_ids_.size(); ++k) jslot_.insert(jn_ids_[k], (int32_t)k);
-    else if (jn_.size() > kJobLinear + 1)
-      jslot_.insert(gid, i);
-  }
-  return jn_[i].second;
+// A node the current job placed pods on: in the window's dirty set if this window changed it,
+// else its state as of the end of the window that last changed it (mirror, or changed_).
+NodeState Resolver::current_state(int64_t gid) const {
+  const int32_t i = dirty_.find(gid);
+  if (i >= 0) return dirty_.get(i);
+  if (mirror_.nodes) return mirror_.nodes[gid];
+  const int32_t c = changed_slot_.find(gid);
+  if (c < 0) throw std::logic_error("resolver: rollback of a node with no known state");
+  return changed_[(size_t)c];
 }
 
 void Resolver::finish_job(bool ok) {
@@ -673,22 +660,17 @@ void Resolver::finish_job(bool ok) {
       for (int32_t p = 0; p < cnt_[g]; ++p) {
         int32_t& slot = pod_node_[pod_off_[g] + p];
         if (slot < 0) continue;
-        NodeState& st = jn_[job_find(slot)].second;
+        NodeState st = current_state(slot);
         for (int d = 0; d < RD; ++d) st.res[d] += q[d];
+        dirty_.mark(dirty_.upsert(slot, st));
+        any_set(slot);
         slot = -1;
         --pods_placed_;
       }
     }
-    for (const auto& kv : jn_) {
-      dirty_.mark(dirty_.upsert(kv.first, kv.second));
-      any_set(kv.first);
-    }
     job_status_[j] = 1;
     ++jobs_failed_;
   }
-  if (jn_.size() > kJobLinear) jslot_.clear(jn_ids_.begin(), jn_ids_.end());
-  jn_ids_.clear();
-  jn_.clear();
   ++oi_;
   p_ = 0;
   if (!done()) g_ = jgo_[order_[oi_]];
@@ -986,7 +968,6 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         dirty_.set(slot, st);
       }
       dirty_.mark(slot);
-      job_node(gid) = st;
       std::fill_n(pod_node_.begin() + pod_off_[g_] + p_, m, (int32_t)gid);
       p_ += (int32_t)m;
       pods_placed_ += m;
@@ -1023,6 +1004,11 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     for (int d = 0; d < RD; ++d) u.res[d] = st.res[d];
     u.labels = st.labels;
     updates.push_back(u);
+    if (!mirror_.nodes) {   // (record-form lists: the resolver keeps the states it gave for rollbacks)
+      const int32_t c = changed_slot_.insert(u.gid, (int32_t)changed_.size());
+      if (c == (int32_t)changed_.size()) changed_.push_back(st);
+      else changed_[(size_t)c] = st;
+    }
   }
   for (int64_t g : dirty_.gid) any_[(size_t)g >> 6] = 0;   // (clears whole words: every bit set is listed)
   if (useS)

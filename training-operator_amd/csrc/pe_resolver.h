@@ -405,14 +405,13 @@ class Resolver {
   std::vector<int32_t> sk_idx_;
   std::vector<uint64_t> sfull_;      // a group's every seed key below the limit (truncated top)
   SeedScorer scorer_;                // declared after what its thread reads: stopped first
-  // nodes touched by the current job (exact current residuals, survive window flushes)
-  // gid -> index into jn_ (reset per job): no allocation per pod
-  static constexpr size_t kJobLinear = 32;
-  IdMap jslot_;                    // gid -> index into jn_, only for jobs with > kJobLinear nodes
-  std::vector<std::pair<int64_t, NodeState>> jn_;
-  std::vector<int64_t> jn_ids_;    // the ids of jn_, in order
-  NodeState& job_node(int64_t gid);
-  int32_t job_find(int64_t gid) const;
+  // A failed job's nodes are restored from their CURRENT states, looked up only then (rollbacks are
+  // rare; no per-placement bookkeeping): the window's dirty set, else the mirror (which follows every
+  // resolved window), else -- record-form lists without a mirror (pe_resolver_* ABI) -- the last state
+  // this resolver gave the node in an earlier window (changed_).
+  NodeState current_state(int64_t gid) const;
+  IdMap changed_slot_;
+  std::vector<NodeState> changed_;
   int64_t jobs_placed_ = 0, jobs_failed_ = 0, pods_placed_ = 0, rescans_ = 0;
 };
 
