@@ -164,6 +164,7 @@ def pg_slice(agg, a: int, b: int):
 
 
 AGG_LATENCY_JOBS = (1, 16, 256)
+AGG_CROSSOVER_JOBS = (1, 16, 256, 512, 1024, 1536, 2048, 3072, 4096, 6144, 8192, 16384)
 
 
 def agg_raw_call(fn, head, mode, sub):
@@ -310,6 +311,11 @@ def greedy_profile(src_hash: str):
         k = g.get(mode, {}).get("pe::walk_kernel")
         if k:
             out[mode] = k["avg_ns"]
+    p = g.get("pmc", {}).get("pe::walk_kernel", {})
+    if "hbm_traffic_bytes" in p:   # per walk launch (FETCH_SIZE x 2 per the gfx950 note + WRITE_SIZE)
+        out["traffic_per_launch"] = p["hbm_traffic_bytes"]
+        out["read_per_launch"] = p["hbm_read_bytes_corrected"]
+        out["write_per_launch"] = p["hbm_write_bytes"]
     return out
 
 
@@ -776,6 +782,16 @@ def main(argv=None):
                               "hbm_frac": walked / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
                 if mode in ev_ms:
                     roof[mode]["events_walk_ms_per_batch"] = ev_ms[mode]
+            if "traffic_per_launch" in gprof:
+                # counted HBM-side traffic (L2 misses + writes) of the walk, per batch = per launch x launches,
+                # from the profile's greedy PMC passes; traffic_ratio = counted / algorithmic bytes
+                roof["traffic"] = gprof["traffic_per_launch"] * launches
+                roof["traffic_read"] = gprof["read_per_launch"] * launches
+                roof["traffic_write"] = gprof["write_per_launch"] * launches
+                roof["traffic_ratio"] = roof["traffic"] / walked if walked else None
+                roof["traffic_source"] = f"{gprof['profile']} greedy PMC passes (FETCH_SIZE x2 + WRITE_SIZE per walk launch)"
+            else:
+                roof["traffic"] = None
             roof["note"] = ("latency-bound, not bandwidth-bound: one 1024-thread block per group walks 1-7 rounds of 1024 "
                             "sorted nodes; warm peak = the Infinity Cache's measured random-row read rate "
                             "(MI355X_MICROARCH.md: 38 MB table, 8.6 TB/s), cold peak = HBM 8 TB/s")
@@ -870,6 +886,28 @@ def main(argv=None):
                 reps.append(time.perf_counter() - c0)
             gout = eng.pg_min_resources(1, *agg)
             same &= all(np.array_equal(a, b) for a, b in zip(couts, gout))
+            # the crossover: the smallest batch (jobs per call) where one engine call beats the same
+            # arithmetic on one CPU core, both timed here on the same CSR prefixes (outputs checked equal)
+            sweep, crossover = [], None
+            for Jn in AGG_CROSSOVER_JOBS:
+                sub = pg_slice(agg, 0, Jn)
+                ccall, couts = agg_raw_call(ol.orc_pg_min_resources, (), 1, sub)
+                gcall, gouts = agg_raw_call(eng.lib.pe_pg_min_resources, (eng.h,), 1, sub)
+                ccall()
+                gcall()
+                same &= all(np.array_equal(a, b) for a, b in zip(couts, gouts))
+                n = 200 if Jn <= 2048 else 60
+                g_us, c_us = time_calls(gcall, n)[0], time_calls(ccall, n)[0]
+                sweep.append({"jobs": Jn, "gpu_us": g_us, "cpu_us": c_us})
+                if crossover is None and g_us < c_us:
+                    crossover = Jn
+            if "aggregation" in out:
+                out["aggregation"]["crossover_jobs"] = crossover
+                out["aggregation"]["crossover_sweep"] = sweep
+                out["aggregation"]["crossover_note"] = (
+                    "smallest jobs-per-call of the sweep where pe_pg_min_resources (median of the C call) beats "
+                    "cpu_baseline.aggregation's rule (oracle.c, one core) on the same jobs; below it the operator's "
+                    "per-reconcile call (J = 1) is cheaper on its own CPU")
             out["cpu_baseline"]["aggregation"] = {
                 "jobs_per_s": args.agg_jobs / float(np.median(reps)), "ms_per_call": float(np.median(reps)) * 1e3,
                 "cores": 1, "kind": "port", "latency_us": clat, "outputs_match_gpu": bool(same),

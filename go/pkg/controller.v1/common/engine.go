@@ -108,3 +108,46 @@ func CalcPGMinResourcesEngine(eng *hip.Engine, gpuName string) func(int32, map[a
 		return &rl
 	}
 }
+
+// PGRequest is one CalcPGMinResources call of a batch (the arguments of util.go:108).
+type PGRequest struct {
+	MinMember int32
+	Replicas  map[apiv1.ReplicaType]*apiv1.ReplicaSpec
+	PcGetFunc PriorityClassGetFunc
+}
+
+// PGMinResourcesBatch is CalcPGMinResources for many jobs at once -- a resync of every job's
+// PodGroup (job.go:455-457 called in a loop) -- with ONE engine call for all the jobs the tensor path
+// holds; the others (and any overflowed job) take the reference's CalcPGMinResources.  out[i] is the
+// answer for reqs[i], exactly the reference's.  The engine pays off above hip.BatchCrossoverJobs jobs.
+func PGMinResourcesBatch(eng *hip.Engine, gpuName string, reqs []PGRequest) []*v1.ResourceList {
+	out := make([]*v1.ResourceList, len(reqs))
+	batch := &hip.CSR{}
+	idx := make([]int, 0, len(reqs))          // batch job -> request
+	formats := make([]*hip.FormatAcc, 0, len(reqs))
+	for i, r := range reqs {
+		csr, f, err := flattenV1(r.MinMember, r.Replicas, r.PcGetFunc, gpuName)
+		if err != nil {
+			rl := CalcPGMinResources(r.MinMember, r.Replicas, r.PcGetFunc) // exact reference path
+			out[i] = rl
+			continue
+		}
+		batch.AppendJobs(csr)
+		idx = append(idx, i)
+		formats = append(formats, f)
+	}
+	if len(idx) == 0 {
+		return out
+	}
+	agg, err := eng.PGMinResources(hip.ModeV1, batch)
+	for j, i := range idx {
+		r := reqs[i]
+		if err != nil || agg.Overflow[j] != 0 {
+			out[i] = CalcPGMinResources(r.MinMember, r.Replicas, r.PcGetFunc)
+			continue
+		}
+		rl := agg.Unflatten(j, gpuName, formats[j].Formats())
+		out[i] = &rl
+	}
+	return out
+}

@@ -172,3 +172,39 @@ func (a *FormatAcc) Formats() *[Dims]resource.Format {
 	}
 	return &out
 }
+
+// AppendJobs appends every job of o (a CSR built for other jobs, e.g. one flattenV1 / flattenInfo
+// result per object) to b, rebasing o's offsets: a resync of many PodGroups becomes ONE
+// pe_pg_min_resources call.  Job j of o becomes job len(b.MinMember) + j of b.
+func (b *CSR) AppendJobs(o *CSR) {
+	if len(o.JobGroupOff) < 2 {
+		return
+	}
+	if len(b.JobGroupOff) == 0 {
+		b.JobGroupOff = append(b.JobGroupOff, 0)
+	}
+	if len(b.GroupContOff) == 0 {
+		b.GroupContOff = append(b.GroupContOff, 0)
+	}
+	g0 := int32(len(b.GroupReplicas))
+	c0 := int32(len(b.ContFlags))
+	for _, v := range o.JobGroupOff[1:] {
+		b.JobGroupOff = append(b.JobGroupOff, g0+v)
+	}
+	if len(o.GroupContOff) > 1 {
+		for _, v := range o.GroupContOff[1:] {
+			b.GroupContOff = append(b.GroupContOff, c0+v)
+		}
+	}
+	b.MinMember = append(b.MinMember, o.MinMember...)
+	b.GroupReplicas = append(b.GroupReplicas, o.GroupReplicas...)
+	b.ContReq = append(b.ContReq, o.ContReq...)
+	b.ContFlags = append(b.ContFlags, o.ContFlags...)
+}
+
+// BatchCrossoverJobs is the batch size above which one engine call beats the same arithmetic on
+// one CPU core (bench.py `aggregation.crossover_jobs`, measured on the MI355X box: see
+// INTEGRATION.md).  Below it a per-object call costs a kernel round trip over PCIe (~12 us) for
+// work the CPU does in well under a microsecond, so callers with few objects keep the reference
+// path; the batch entry points below take the engine for any size (the caller decides).
+const BatchCrossoverJobs = 2048

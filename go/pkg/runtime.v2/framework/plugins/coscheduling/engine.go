@@ -113,6 +113,50 @@ func (c *EngineCoScheduling) Build(ctx context.Context, obj client.Object, info 
 	return c.CoScheduling.buildPodGroup(ctx, info, trainJob, agg.Members[0], unflatten(agg, c.gpuName, formats))
 }
 
+// BuildBatch is Build for many TrainJobs at once (a resync of every TrainJob's PodGroup): ONE engine
+// call aggregates every (info, trainJob) pair the tensor path holds, the PodGroups are then emitted
+// one by one exactly as Build emits them; pairs the tensor path refuses or that overflow take the
+// reference's Build.  objs[i] / errs[i] answer (infos[i], trainJobs[i]).  The engine pays off above
+// hip.BatchCrossoverJobs pairs; the C++ mirror's kf::CoScheduling::BuildBatch is the same loop.
+func (c *EngineCoScheduling) BuildBatch(ctx context.Context, infos []*runtime.Info,
+	trainJobs []*kubeflowv2.TrainJob) ([]client.Object, []error) {
+	objs := make([]client.Object, len(infos))
+	errs := make([]error, len(infos))
+	batch := &hip.CSR{}
+	idx := make([]int, 0, len(infos))
+	formats := make([]*hip.FormatAcc, 0, len(infos))
+	for i, info := range infos {
+		if info == nil || info.RuntimePolicy.PodGroupPolicy == nil || info.RuntimePolicy.PodGroupPolicy.Coscheduling == nil ||
+			trainJobs[i] == nil {
+			continue // (nil, nil), as Build
+		}
+		csr, f, err := flattenInfo(info, c.gpuName)
+		if err != nil {
+			objs[i], errs[i] = c.CoScheduling.Build(ctx, nil, info, trainJobs[i])
+			continue
+		}
+		batch.AppendJobs(csr)
+		idx = append(idx, i)
+		formats = append(formats, f)
+	}
+	if len(idx) == 0 {
+		return objs, errs
+	}
+	agg, err := c.eng.PGMinResources(hip.ModeV2, batch)
+	for j, i := range idx {
+		switch {
+		case err != nil:
+			errs[i] = err
+		case agg.Overflow[j] != 0:
+			objs[i], errs[i] = c.CoScheduling.Build(ctx, nil, infos[i], trainJobs[i])
+		default:
+			objs[i], errs[i] = c.CoScheduling.buildPodGroup(ctx, infos[i], trainJobs[i], agg.Members[j],
+				agg.Unflatten(j, c.gpuName, formats[j].Formats()))
+		}
+	}
+	return objs, errs
+}
+
 // buildPodGroup is the PodGroup emission of coscheduling.go:119-147 -- the object, its controller
 // reference, the existing object's Get and needsCreateOrUpdate (:150-153) -- factored out of Build so
 // that one copy serves both plugins.  The reference's Build ends in it after its own aggregation

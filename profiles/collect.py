@@ -27,7 +27,7 @@ def main(src, name, latest):
     for f in ("bench_walk_warm.json", "bench_walk_cold.json", "agg.out"):
         if os.path.exists(os.path.join(src, f)):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f))
-    for pas in ("fetch", "write", "sq", "sq2"):
+    for pas in ("fetch", "write", "sq", "sq2", "walk_fetch", "walk_write"):
         f = os.path.join(src, pas, f"{pas}_counter_collection.csv")
         if not os.path.exists(f):
             continue

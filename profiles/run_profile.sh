@@ -28,6 +28,11 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/walk_warm -o walk --o
   python3 bench.py $GREEDY_ONLY "$@" > $OUT/bench_walk_warm.json 2> $OUT/walk_warm.err
 PE_WALK_FLUSH=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/walk_cold -o walk --output-format csv -- \
   python3 bench.py $GREEDY_ONLY "$@" > $OUT/bench_walk_cold.json 2> $OUT/walk_cold.err
+# HBM-side traffic of the greedy passes (FETCH_SIZE / WRITE_SIZE per walk launch, separate passes)
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/walk_fetch -o walk_fetch --output-format csv -- \
+  python3 bench.py $GREEDY_ONLY "$@" > $OUT/bench_walk_fetch.json 2> $OUT/walk_fetch.err
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/walk_write -o walk_write --output-format csv -- \
+  python3 bench.py $GREEDY_ONLY "$@" > $OUT/bench_walk_write.json 2> $OUT/walk_write.err
 # aggregation: the 1M-job call alone
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/agg -o agg --output-format csv -- \
   python3 tools/agg_calls.py > $OUT/agg.out 2> $OUT/agg.err

@@ -39,19 +39,27 @@ def main(d):
                 out.setdefault(key[0], {})[key[1]] = stats
             else:
                 out[key[0]] = stats
+    # PMC passes: the fit passes into "pmc", the greedy passes (walk_fetch / walk_write) into
+    # greedy.pmc -- per-launch averages of each kernel
+    gpmc = collections.defaultdict(dict)
     for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
+        dest = gpmc if os.path.basename(os.path.dirname(f)).startswith("walk_") else out["pmc"]
         acc = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
             acc[(kname(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
         for (k, c), v in acc.items():
-            out["pmc"][k][c] = sum(v) / len(v)
-    for k, p in out["pmc"].items():
-        if "FETCH_SIZE" in p:
-            p["hbm_read_bytes_corrected"] = p["FETCH_SIZE"] * 1024 * 2
-        if "WRITE_SIZE" in p:
-            p["hbm_write_bytes"] = p["WRITE_SIZE"] * 1024
-        if "FETCH_SIZE" in p and "WRITE_SIZE" in p:
-            p["hbm_traffic_bytes"] = p["hbm_read_bytes_corrected"] + p["hbm_write_bytes"]
+            dest[k][c] = sum(v) / len(v)
+            dest[k][c + "_launches"] = len(v)
+    for pm in (out["pmc"], gpmc):
+        for k, p in pm.items():
+            if "FETCH_SIZE" in p:
+                p["hbm_read_bytes_corrected"] = p["FETCH_SIZE"] * 1024 * 2
+            if "WRITE_SIZE" in p:
+                p["hbm_write_bytes"] = p["WRITE_SIZE"] * 1024
+            if "FETCH_SIZE" in p and "WRITE_SIZE" in p:
+                p["hbm_traffic_bytes"] = p["hbm_read_bytes_corrected"] + p["hbm_write_bytes"]
+    if gpmc:
+        out.setdefault("greedy", {})["pmc"] = gpmc
     # the workload the passes ran (bench.py's JSON line under the kernel trace)
     for f in glob.glob(os.path.join(d, "bench_trace.json")):
         lines = [ln for ln in open(f) if ln.startswith("{")]

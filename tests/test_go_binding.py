@@ -94,13 +94,17 @@ def test_cgo_preamble_and_package():
                   # the PodGroup emission (coscheduling.go:119-147) exists once, as a helper both Builds call
                   "func (c *CoScheduling) buildPodGroup(", "return c.CoScheduling.buildPodGroup(ctx, info, trainJob",
                   # print formats of the reference's Build sums (first nonzero quantity x replicas per key)
-                  "acc.AddList(trr.PodRequests, gpuName, int64(trr.Replicas))", "formats.Formats()"]),
+                  "acc.AddList(trr.PodRequests, gpuName, int64(trr.Replicas))", "formats.Formats()",
+                  # batch entry point (a resync of many TrainJobs): one engine call, emission per object
+                  "func (c *EngineCoScheduling) BuildBatch(", "batch.AppendJobs(csr)",
+                  "c.CoScheduling.buildPodGroup(ctx, infos[i], trainJobs[i], agg.Members[j]"]),
     (V1_GO, ["package common", "func flattenV1(", "func CalcPGMinResourcesEngine(", "PGMinResources(hip.ModeV1",
              "c.Resources.Limits", "CalcPGMinResources(minMember, replicas, pcGetFunc)", "pc.Value",
              # print formats of AddResourceList's sums, replayed over the counted pods (util.go:79-104,126-141)
-             "acc.AddList(effectiveList(c), gpuName, 1)", "agg.Unflatten(0, gpuName, formats.Formats())"]),
+             "acc.AddList(effectiveList(c), gpuName, 1)", "agg.Unflatten(0, gpuName, formats.Formats())",
+             "func PGMinResourcesBatch(", "batch.AppendJobs(csr)", "agg.Unflatten(j, gpuName, formats[j].Formats())"]),
     (FLATTEN_GO, ["type FormatAcc struct", "func (a *FormatAcc) Add(", "func (a *FormatAcc) Formats()",
-                  "if !a.nonzero[d] {"]),
+                  "if !a.nonzero[d] {", "func (b *CSR) AppendJobs(o *CSR)", "BatchCrossoverJobs"]),
 ])
 def test_adapters(path, needles):
     text = open(path).read()

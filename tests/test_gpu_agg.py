@@ -112,3 +112,22 @@ def test_agg_small_calls_both_paths(eng, monkeypatch, no_karg):
             _check(eng, mode, random_csr(J, 300 + J + mode))
     for n_cont in (1, 10, 12, 13, 60):   # one job, n_cont containers x 33 B around the limit
         _check(eng, V1, _one_job_csr(1, n_cont, n_cont))
+
+
+@pytest.mark.parametrize("mode", [V1, V2])
+def test_agg_resync_batch_equals_per_object_calls(eng, mode):
+    """The adapters' batch entry points (Go PGMinResourcesBatch / EngineCoScheduling.BuildBatch, C++
+    kf::CalcPGMinResourcesBatch / CoScheduling::BuildBatch): one-object CSRs appended back to back
+    (hip.CSR.AppendJobs; _concat here) and aggregated in ONE call give, job for job, what the
+    per-object calls (J = 1, the reconcile path) and the oracle give.  3000 objects: above the
+    crossover (bench aggregation.crossover_jobs)."""
+    parts = [random_csr(1, 5000 + i + 17 * mode, big=(i % 7 == 0)) for i in range(3000)]
+    batch = _concat(parts)
+    got = eng.pg_min_resources(mode, *batch)
+    want = oracle.pg_min_resources(mode, *batch)
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+    for i in range(0, 3000, 97):   # the per-object calls agree job for job
+        one = eng.pg_min_resources(mode, *parts[i])
+        for a, b in zip(one, got):
+            np.testing.assert_array_equal(a[0], b[i])
