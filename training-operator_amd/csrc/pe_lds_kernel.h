@@ -198,6 +198,7 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
 #pragma unroll
         for (int k = 1; k < L; ++k) {
           const uint32_t pk = entry(o + k);
+#ifdef PE_LDS_OPAQUE_PAIR
           uint32_t ph = pk + 1;
           // W = 2: the compiler would fuse the two reads into one ds_read2st64_b64, which the LDS serves
           // at half the rate of two ds_read_b64 (8 vs 2 x 2 cycles: 128 vs 256 B/clk -- counted, the
@@ -206,6 +207,16 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
           if constexpr (W == 2) asm("" : "+s"(ph));
           slice_split<W>(plane_rd<W>(lds, pk, lane), g);
           slice_split<W>(plane_rd<W>(lds, ph, lane), h);
+#else
+          // W = 2: one address for the pair, GE(c + 1) read through the immediate offset (+512 B).  The
+          // compiler would fuse the two reads into one ds_read2st64_b64, which the LDS serves at half
+          // the rate of two ds_read_b64 (8 vs 2 x 2 cycles -- counted, the fused form put the LDS array at
+          // 74 cycles per job instead of 42): a scheduling barrier that lets every instruction cross
+          // (mask 0x7FF) sits between them, which the load/store merger does not merge across
+          slice_split<W>(plane_rd<W>(lds, pk, lane), g);
+          if constexpr (W == 2) __builtin_amdgcn_sched_barrier(0x7FF);
+          slice_split<W>(plane_rd<W>(lds, pk + 1, lane), h);
+#endif
 #pragma unroll
           for (int i = 0; i < W; ++i) a[i] = h[i] | (g[i] & a[i]);
         }
