@@ -1725,7 +1725,8 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
     }
     int64_t xc = 0;   // the job's crossed values (0-based value index: the node's rank must exceed it)
     for (int x = 0; x < sp.nx; ++x) xc += (int64_t)bd.rank[fdim[sp.nf + x]][j] * sp.xstride[x];
-    c[pe::LD_NEED_SLOT] = (uint16_t)(sp.need_pbase + bd.rank[4][j] * sp.xprod + xc);
+    c[pe::lds_need_slot(shape[0], shape[1], shape[2], shape[3])] =
+        (uint16_t)(sp.need_pbase + bd.rank[4][j] * sp.xprod + xc);
   }
   });
   // slot (r * 16 + w) * Tpad + t = job r + R (w + 16 t), the t-th of wave w's run in phase r (the

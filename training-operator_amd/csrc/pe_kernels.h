@@ -218,8 +218,9 @@ hipError_t launch_fit_mask_planes_sets(hipStream_t s, const uint32_t* planes, in
 constexpr int LD_MAXF = 4;        // digit fields (dimensions with >= 2 distinct values)
 constexpr int LD_MAXL = 4;        // digit levels per field
 constexpr int LD_MAXNEED = 64;    // distinct label needs
-constexpr int LD_CODE = 16;       // u16 plane indices per job: field f's levels at lds_field_off(f) + k; need at 15
-constexpr int LD_NEED_SLOT = 15;
+constexpr int LD_CODE = 16;       // u16 plane indices per job: field f's levels at lds_field_off(f) + k, then
+                                  // the need plane at lds_need_slot (right after the fields: one readlane fewer)
+constexpr int LD_NEED_SLOT = 15;  // the last slot: at most 15 field entries
 // First code entry of field fi when the fields are ordered N4 four-level, N3 three-level, N2 two-level,
 // then one-level (the kernel's template shape; the sum of the levels must stay <= LD_NEED_SLOT).
 __host__ __device__ constexpr int lds_field_off(int fi, int n4, int n3, int n2) {
@@ -227,6 +228,11 @@ __host__ __device__ constexpr int lds_field_off(int fi, int n4, int n3, int n2) 
          : fi <= n4 + n3         ? 4 * n4 + 3 * (fi - n4)
          : fi <= n4 + n3 + n2    ? 4 * n4 + 3 * n3 + 2 * (fi - n4 - n3)
                                  : 4 * n4 + 3 * n3 + 2 * n2 + (fi - n4 - n3 - n2);
+}
+// The need plane's code entry: the first one after the fields, so that it shares the last field's
+// dword (the kernel reads one dword per readlane) instead of sitting alone in the code's last dword.
+__host__ __device__ constexpr int lds_need_slot(int n4, int n3, int n2, int n1) {
+  return 4 * n4 + 3 * n3 + 2 * n2 + n1;
 }
 constexpr int LD_THREADS = 1024;  // 16 waves per workgroup, one node block per workgroup
 struct LdsSpec {

@@ -176,7 +176,9 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
   // that pending load with the latch's state and wait vmcnt(0) -- every store drained -- per batch)
   asm volatile("" : : "v"(cv.x), "v"(cv.y));
   for (int64_t t0 = 0; t0 < T; t0 += 16) {
-    const int n = (int)min<int64_t>(16, T - t0);
+    // (a 32-bit wave-uniform count: the per-job `K < n` tests of the store sizes stay scalar compares;
+    // as a 64-bit value they were 15 v_cmp_gt_u64 per batch)
+    const int n = __builtin_amdgcn_readfirstlane((int)min<int64_t>(16, T - t0));
     const uint2 cur = cv;
     cv = cb[min<int64_t>(t0 + 16, Tpad - 16) * (LD_CODE / 4) + lane];   // next batch, in flight meanwhile
     uint32_t p[16];
@@ -188,7 +190,7 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
         return (e & 1) ? d >> 16 : d & 0xFFFFu;
       };
       uint32_t f[W];
-      slice_split<W>(plane_rd<W>(lds, entry(LD_NEED_SLOT), lane), f);
+      slice_split<W>(plane_rd<W>(lds, entry(lds_need_slot(N4, N3, N2, N1)), lane), f);
 #pragma unroll
       for (int fi = 0; fi < N4 + N3 + N2 + N1; ++fi) {          // unrolled: L and the entries are constants
         const int L = fi < N4 ? 4 : fi < N4 + N3 ? 3 : fi < N4 + N3 + N2 ? 2 : 1;
