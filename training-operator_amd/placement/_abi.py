@@ -107,7 +107,12 @@ def load(path: str = LIB_PATH):
         raise ImportError(f"libplacement.so not built at {path}: run `make -C training-operator_amd/csrc` "
                           "(the engine has no CPU fallback)")
     lib = ctypes.CDLL(path)
+    # an A/B build named by PE_LIBRARY may predate entry points added since (its callers do not use
+    # them); the in-tree library must export every one
+    lenient = path != os.path.join(PKG_ROOT, "libplacement.so")
     for name, (res, args) in SIGNATURES.items():
+        if lenient and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
