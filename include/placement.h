@@ -153,6 +153,8 @@ typedef struct {
   int64_t walk_groups;   /* greedy sorted walk: group blocks launched */
   int64_t walk_prepass;  /* greedy sorted walk: round summaries read (rounds x groups) */
   double walk_ms;        /* walk kernel time by hipEvents, only when PE_WALK_EVENTS=1 in the environment */
+  int64_t walk_pend_updates; /* greedy sorted walk: node updates applied while a side-stream index rebuild
+                                was pending (written into both index sets' overlays) */
 } pe_stats;
 
 int pe_abi_version(void);

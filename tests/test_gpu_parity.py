@@ -575,21 +575,30 @@ def test_greedy_walk_and_full_scan(flags, resort, mix, N, J, gpu_frac, topk, wg)
 @pytest.mark.parametrize("mix,N,J,gpu_frac", [("mixed", 6000, 600, 0.3), ("island8", 1500, 400, 0.7)])
 def test_greedy_walk_rebuild_in_line_and_side_stream(resort, mix, N, J, gpu_frac):
     """The walk index rebuilt in line (PE_ASYNC_RESORT=0) and on the side stream while the walks go on
-    (default): both exact vs the oracle, identical placements, and the side-stream rebuilds taken over
-    during the batch (resorts > 1)."""
+    (default; and with the takeover held back 3 windows, PE_WALK_SWITCH_DELAY=3, so that updates are
+    applied while a rebuild is pending -- the dual overlay writes and the switch's drop of the changed
+    nodes' sorted entries): all exact vs the oracle, identical placements, the side-stream rebuilds
+    taken over during the batch (resorts > 1), and with the delay, updates applied while pending."""
     inv = synth.make_inventory(N, 91 + N, gpu_frac)
     batch = synth.make_jobs(J, 93 + J, mix)
     out = {}
-    for mode in ("0", "1"):
+    for mode, delay in (("0", None), ("1", None), ("1", "3")):
         os.environ["PE_ASYNC_RESORT"] = mode
+        if delay:
+            os.environ["PE_WALK_SWITCH_DELAY"] = delay
         try:
             e = Engine(0, topk=16, window_groups=16, resort_nodes=resort)
-            out[mode] = check_greedy(e, inv, batch)
-            assert e.stats()["resorts"] > 1
+            out[(mode, delay)] = check_greedy(e, inv, batch)
+            s = e.stats()
+            assert s["resorts"] > 1
+            if delay:
+                assert s["walk_pend_updates"] > 0, s
             e.close()
         finally:
             os.environ.pop("PE_ASYNC_RESORT", None)
-    np.testing.assert_array_equal(out["0"], out["1"])
+            os.environ.pop("PE_WALK_SWITCH_DELAY", None)
+    np.testing.assert_array_equal(out[("0", None)], out[("1", None)])
+    np.testing.assert_array_equal(out[("0", None)], out[("1", "3")])
 
 
 def test_greedy_walk_overlay_compaction():

@@ -79,6 +79,9 @@ struct HostBuf {
     p = dev = nullptr;
     n = 0;
     hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T), flags);
+    // zeroed: several of these buffers carry completion flags (signalled groups, the aggregation
+    // flag) that a recycled allocation could otherwise hold from an earlier engine's generations
+    if (e == hipSuccess) std::memset((void*)p, 0, std::max<size_t>(count, 1) * sizeof(T));
     if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&dev, p, 0);
     if (e == hipSuccess) n = count;
     return e;
@@ -343,6 +346,7 @@ struct pe_ctx {
   int w_cur = 0;
   bool w_pending = false;        // ws[1 - w_cur] is being rebuilt on w_s2
   int64_t w_pend_est = 0;        // updates applied since that rebuild's snapshot
+  int64_t w_pend_windows = 0;    // windows launched while that rebuild was pending
   hipStream_t w_s2 = nullptr;
   hipEvent_t w_ev_snap = nullptr, w_ev_done = nullptr;
   DevBuf<uint64_t> w_kin;
@@ -2181,6 +2185,7 @@ static void walk_resort_async(pe_ctx* ctx) {
   hipchk(hipEventRecord(ctx->w_ev_done, s2), "event record");
   ctx->w_pending = true;
   ctx->w_pend_est = 0;
+  ctx->w_pend_windows = 0;
 }
 
 // Take over the side-stream rebuild (the main stream waits for it if it is not done yet).
@@ -2239,6 +2244,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     const bool async_resort = walk && !(std::getenv("PE_ASYNC_RESORT") && std::atoi(std::getenv("PE_ASYNC_RESORT")) == 0);
     const int64_t kResortEarly = std::min<int64_t>(4096, ctx->resort_nodes / 4);
     const int64_t kResortLate = std::max<int64_t>(1, ctx->resort_nodes / 2);
+    const int64_t switch_delay = std::getenv("PE_WALK_SWITCH_DELAY") ? std::atoll(std::getenv("PE_WALK_SWITCH_DELAY")) : 0;
     hipchk(ctx->w_stat.ensure(2), "alloc walk counters");
     hipchk(hipMemsetAsync(ctx->w_stat.p, 0, 2 * sizeof(unsigned long long), ctx->stream), "memset walk counters");
     if (walk) walk_resort(ctx);
@@ -2315,7 +2321,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     if (ctx->pipeline) hipchk(ctx->h_out2.ensure((size_t)Wmax * gb * ctx->world, kZeroCopy), "alloc pinned out");
     if (ctx->world > 1 || ctx->comm) {
       hipchk(ctx->g_gath.ensure((size_t)Wmax * gb * ctx->world), "alloc gather");
-      hipchk(ctx->h_own.ensure((size_t)Wmax * gb), "alloc pinned own");
+      hipchk(ctx->h_own.ensure((size_t)Wmax * gb, kZeroCopy), "alloc pinned own");
     }
     // PE_WALK_EVENTS=1: hipEvents around every walk launch, summed into stats.walk_ms (diagnostics:
     // the greedy roofline of bench.py; the events cost a few us of host time per window)
@@ -2389,11 +2395,13 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // PE_HOST_MERGE=1: the gathered blob is copied and merged lazily on the host instead.
     const bool dev_merge = !direct_out && (int64_t)ctx->world * K <= pe::MG_CAP && !std::getenv("PE_HOST_MERGE");
     const bool signalled = pipelined && !std::getenv("PE_NO_GROUP_SIGNAL") && (direct_out ? walk : dev_merge);
-    // Pipeline depth D (signalled windows; PE_PIPE_DEPTH, 1..3, default 1): windows i+1 .. i+D are
-    // scanned while window i is resolved (D + 1 blob / request buffers, D update staging slots).
-    const int depth = !pipelined ? 0 : !signalled ? 1 : [] {
+    // Pipeline depth D (signalled windows; PE_PIPE_DEPTH, 1..3): windows i+1 .. i+D are scanned
+    // while window i is resolved (D + 1 blob / request buffers, D update staging slots).  Default 1 on
+    // one shard; 2 on several, whose window chain (walk, exchange, device merge) is longer than one
+    // window's resolve.
+    const int depth = !pipelined ? 0 : !signalled ? 1 : [&] {
       const char* e = std::getenv("PE_PIPE_DEPTH");
-      return e ? std::min(3, std::max(1, std::atoi(e))) : 1;
+      return e ? std::min(3, std::max(1, std::atoi(e))) : direct_out ? 1 : 2;
     }();
     if (signalled) hipchk(ctx->h_groups2.ensure(Wpad, kZeroCopy), "alloc pinned groups");
     for (int b = 2; b <= depth; ++b) {
@@ -2434,8 +2442,10 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         const int g = groups[std::min(w, Wg - 1)];
         fill_req(hg.p[w], R.scan_req(g), group_need[g]);   // island groups: count x request
       }
-      // unsharded: the kernel writes the blob straight into pinned host memory (no D2H copy)
-      uint8_t* const dst = direct_out ? outbufdev(b) : ctx->g_out.p;
+      // unsharded: the kernel writes the blob straight into pinned host memory (no D2H copy); so does
+      // a pipelined host exchange's walk (its own lists, signalled per group: no D2H, no stream sync)
+      const bool own_direct = walk && use_exchange && pipelined && signalled;
+      uint8_t* const dst = direct_out ? outbufdev(b) : own_direct ? ctx->h_own.dev : ctx->g_out.p;
       uint32_t gen = 0;   // signalled window: its generation (the walk's or the shard merge's)
       if (signalled) {
         if (++ctx->walk_gen == 0) ++ctx->walk_gen;
@@ -2443,8 +2453,10 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       buf_gen[b] = gen;
       if (walk) {   // one 64-B request per block: read from pinned host memory, no H2D copy
-        if (ctx->w_pending &&
-            (hipEventQuery(ctx->w_ev_done) == hipSuccess || ctx->w_est > ctx->resort_nodes + kResortLate))
+        // PE_WALK_SWITCH_DELAY=n (test knob): take a finished rebuild over only after n windows ran
+        // with it pending, so the dual overlay writes of those windows' applies are exercised
+        if (ctx->w_pending && (ctx->w_est > ctx->resort_nodes + kResortLate ||
+                               (ctx->w_pend_windows++ >= switch_delay && hipEventQuery(ctx->w_ev_done) == hipSuccess)))
           walk_switch(ctx);
         if (!ctx->w_pending) {
           if (async_resort && ctx->w_est > ctx->resort_nodes - kResortEarly) walk_resort_async(ctx);
@@ -2459,7 +2471,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           hipchk(hipEventRecord(evp.first, s), "event record");
         }
         hipchk(pe::launch_walk(s, hg.dev, Wg, K, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns,
-                               (uint64_t)ctx->begin, dst, direct_out ? gen : 0u),
+                               (uint64_t)ctx->begin, dst, direct_out || own_direct ? gen : 0u),
                "launch walk");
         if (wev) hipchk(hipEventRecord(evp.second, s), "event record");
         walk_launch_groups += Wg;
@@ -2488,9 +2500,18 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (direct_out) {
         // written in place
       } else if (use_exchange) {
-        hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
+        if (own_direct && ctx->Ns > 0) {   // every own group signalled: the lists are in h_own
+          pe::WindowFeed own;
+          std::vector<pe::GroupCands> own_cands;
+          own.idle = &StreamIdle::busy;
+          own.idle_user = &stream_idle;
+          own.reset(ctx->h_own.p, Wg, K, gen, &own_cands);
+          own.wait((size_t)Wg - 1);
+        } else {
+          hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
+        }
         if (pipelined) {   // (the launch helper, or the main thread at a restart) exchange now
-          hipchk(hipStreamSynchronize(s), "sync own cands");
+          if (!own_direct || ctx->Ns == 0) hipchk(hipStreamSynchronize(s), "sync own cands");
           if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, dev_merge ? ctx->h_xg[b].p : outbuf(b), bytes) != 0)
             raise(PE_ERCCL, "exchange callback failed");
           if (dev_merge)   // the gathered lists (pinned) merged on the device, signalled per group
@@ -2566,7 +2587,10 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
                                 walk && ctx->w_pending ? &wn : nullptr),
                "launch apply");
         ctx->w_est += nu;
-        if (ctx->w_pending) ctx->w_pend_est += nu;
+        if (ctx->w_pending) {
+          ctx->w_pend_est += nu;
+          ctx->stats.walk_pend_updates += nu;   // applied into both index sets' overlays
+        }
       }
     };
     auto timed_resolve = [&](const std::vector<int32_t>& groups, std::vector<pe::Update>& updates,
