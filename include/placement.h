@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 3
+#define PE_ABI_VERSION 4
 #define PE_DIMS 4
 #define PE_COMM_ID_BYTES 128
 #define PE_MAX_NODES (1LL << 24) /* node ids live in the low 24 bits of the best-fit key */
