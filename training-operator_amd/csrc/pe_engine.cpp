@@ -2393,15 +2393,20 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // on the device into one list per group (merge_shards), written into pinned host memory and
     // signalled like an unsharded walk window -- no D2H of every shard's lists, no host k-way merge.
     // PE_HOST_MERGE=1: the gathered blob is copied and merged lazily on the host instead.
-    const bool dev_merge = !direct_out && (int64_t)ctx->world * K <= pe::MG_CAP && !std::getenv("PE_HOST_MERGE");
+    // A host exchange leaves the gathered lists in host memory: the resolver merges them lazily there
+    // (it reads a few entries of each list) instead of sending them back over PCIe to a merge kernel
+    // and waiting for its signals -- one device round trip less per window (PE_DEV_MERGE=1: the
+    // device merge anyway, A/B).
+    const bool dev_merge = !direct_out && (int64_t)ctx->world * K <= pe::MG_CAP && !std::getenv("PE_HOST_MERGE") &&
+                           (!use_exchange || std::getenv("PE_DEV_MERGE"));
     const bool signalled = pipelined && !std::getenv("PE_NO_GROUP_SIGNAL") && (direct_out ? walk : dev_merge);
-    // Pipeline depth D (signalled windows; PE_PIPE_DEPTH, 1..3): windows i+1 .. i+D are scanned
-    // while window i is resolved (D + 1 blob / request buffers, D update staging slots).  Default 1 on
-    // one shard; 2 on several, whose window chain (walk, exchange, device merge) is longer than one
-    // window's resolve.
+    // Pipeline depth D (signalled windows; PE_PIPE_DEPTH, 1..3, default 1): windows i+1 .. i+D are
+    // scanned while window i is resolved (D + 1 blob / request buffers, D update staging slots).  (2
+    // measured on a 2-rank host-exchange run: 36 vs 22 ms per cfg3 batch -- every dropped speculation
+    // throws away two scans.)
     const int depth = !pipelined ? 0 : !signalled ? 1 : [&] {
       const char* e = std::getenv("PE_PIPE_DEPTH");
-      return e ? std::min(3, std::max(1, std::atoi(e))) : direct_out ? 1 : 2;
+      return e ? std::min(3, std::max(1, std::atoi(e))) : 1;
     }();
     if (signalled) hipchk(ctx->h_groups2.ensure(Wpad, kZeroCopy), "alloc pinned groups");
     for (int b = 2; b <= depth; ++b) {
@@ -2444,10 +2449,10 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       // unsharded: the kernel writes the blob straight into pinned host memory (no D2H copy); so does
       // a pipelined host exchange's walk (its own lists, signalled per group: no D2H, no stream sync)
-      const bool own_direct = walk && use_exchange && pipelined && signalled;
+      const bool own_direct = walk && use_exchange && pipelined;
       uint8_t* const dst = direct_out ? outbufdev(b) : own_direct ? ctx->h_own.dev : ctx->g_out.p;
       uint32_t gen = 0;   // signalled window: its generation (the walk's or the shard merge's)
-      if (signalled) {
+      if (signalled || own_direct) {
         if (++ctx->walk_gen == 0) ++ctx->walk_gen;
         gen = ctx->walk_gen;
       }

@@ -299,6 +299,14 @@ hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt,
 constexpr int WK_ROUND = 1024;          // sorted entries per round = walk threads per group
 constexpr int WK_MAXR = 16384;          // rounds per shard (PE_MAX_NODES / WK_ROUND)
 constexpr uint64_t WK_INVALID = ~0ull;
+// Walk steps: one round at a time for the first WK_MULTI_AFTER rounds (90 % of the groups stop within
+// them), then up to WK_MULTI candidate rounds per step (the long walks that set a launch's length).
+#ifndef WK_MULTI
+#define WK_MULTI 4
+#endif
+#ifndef WK_MULTI_AFTER
+#define WK_MULTI_AFTER 4
+#endif
 struct WalkIndex {
   uint64_t* sk;        // [Ns] sorted keys (WK_INVALID = not walked)
   int64_t* sr;         // [4][sstride] residuals in sorted order

@@ -1909,17 +1909,36 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
         break;
       }
     }
-    const int64_t i = r * WK_ROUND + tid;
-    uint64_t k = NO_KEY;
-    if (i < Ns) {
-      const uint64_t Kn = w.sk[i];
-      if (Kn != WK_INVALID)
-        k = node_key(w.sr[i], w.sr[w.sstride + i], w.sr[2 * w.sstride + i], w.sr[3 * w.sstride + i], w.sl[i], q0, q1,
-                     q2, q3, need, Kn & 0xFFFFFFull);
+    // the rounds of this step: r, and once the walk is long (WK_MULTI_AFTER rounds walked: requests
+    // few nodes fit, the launch's slowest blocks) up to WK_MULTI - 1 more candidate rounds, their loads
+    // all in flight together -- one memory latency and one barrier per step instead of per round.
+    // Walking a round more than needed is harmless (the stop bound only ever needs >= K + 1 keys).
+    int64_t rr[WK_MULTI];
+    int nstep = 1;
+    rr[0] = r;
+    if (rounds >= WK_MULTI_AFTER)
+      for (; nstep < WK_MULTI; ++nstep) {
+        const int64_t nx = next_round(rr[nstep - 1] + 1);
+        if (nx >= nr) break;
+        rr[nstep] = nx;
+      }
+    uint64_t k[WK_MULTI];
+#pragma unroll
+    for (int u = 0; u < WK_MULTI; ++u) {
+      k[u] = NO_KEY;
+      const int64_t i = rr[u < nstep ? u : 0] * WK_ROUND + tid;
+      if (u < nstep && i < Ns) {
+        const uint64_t Kn = w.sk[i];
+        if (Kn != WK_INVALID)
+          k[u] = node_key(w.sr[i], w.sr[w.sstride + i], w.sr[2 * w.sstride + i], w.sr[3 * w.sstride + i], w.sl[i], q0,
+                          q1, q2, q3, need, Kn & 0xFFFFFFull);
+      }
     }
-    topk_append(s, k, k != NO_KEY);
+#pragma unroll
+    for (int u = 0; u < WK_MULTI; ++u)
+      if (u < nstep) topk_append(s, k[u], k[u] != NO_KEY);
     __syncthreads();
-    if (s.total > MG_CAP - WK_ROUND) {
+    if (s.total > MG_CAP - WK_MULTI * WK_ROUND) {   // room for the next step's appends
       const int T2 = s.total;
       const uint64_t* sk = topk_sort(s, T2, K);
       const int m = T2 < K + 1 ? T2 : K + 1;
@@ -1929,8 +1948,8 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
       if (tid == 0) s.total = m;
       __syncthreads();
     }
-    r = next_round(r + 1);
-    ++rounds;
+    r = next_round(rr[nstep - 1] + 1);
+    rounds += nstep;
   }
   WPT(3);
   const int T = s.total;
