@@ -114,6 +114,8 @@ class SpinWorker {
     err_ = nullptr;
     state_.store(1, std::memory_order_release);
   }
+  bool busy() const { return state_.load(std::memory_order_acquire) == 1; }   // a posted task not done yet
+  bool failed() const { return state_.load(std::memory_order_acquire) == 2 && err_ != nullptr; }
   void wait() {   // rethrows what the task threw
     for (int spin = 0; state_.load(std::memory_order_acquire) != 2; ++spin)
       if (spin < 4096) _mm_pause();
@@ -2393,12 +2395,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // on the device into one list per group (merge_shards), written into pinned host memory and
     // signalled like an unsharded walk window -- no D2H of every shard's lists, no host k-way merge.
     // PE_HOST_MERGE=1: the gathered blob is copied and merged lazily on the host instead.
-    // A host exchange leaves the gathered lists in host memory: the resolver merges them lazily there
-    // (it reads a few entries of each list) instead of sending them back over PCIe to a merge kernel
-    // and waiting for its signals -- one device round trip less per window (PE_DEV_MERGE=1: the
-    // device merge anyway, A/B).
-    const bool dev_merge = !direct_out && (int64_t)ctx->world * K <= pe::MG_CAP && !std::getenv("PE_HOST_MERGE") &&
-                           (!use_exchange || std::getenv("PE_DEV_MERGE"));
+    // (PE_HOST_MERGE=1 with a host exchange, measured: the lazy host merge doubled the resolve --
+    // the seed helper cannot pre-skip merged lists -- 20.4 vs 8.9 ms per 2-rank cfg3 batch)
+    const bool dev_merge = !direct_out && (int64_t)ctx->world * K <= pe::MG_CAP && !std::getenv("PE_HOST_MERGE");
     const bool signalled = pipelined && !std::getenv("PE_NO_GROUP_SIGNAL") && (direct_out ? walk : dev_merge);
     // Pipeline depth D (signalled windows; PE_PIPE_DEPTH, 1..3, default 1): windows i+1 .. i+D are
     // scanned while window i is resolved (D + 1 blob / request buffers, D update staging slots).  (2
@@ -2427,19 +2426,74 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     pe::WindowFeed feed;
     struct StreamIdle {
       hipStream_t s;
+      const SpinWorker* x = nullptr;   // the exchange thread (split exchange): a merge it has not launched yet
       // a faulted walk / merge kernel surfaces as its own HIP error (PE_EHIP with the HIP string),
-      // not as the feed's "never signalled"
-      static bool busy(void* u) {
-        const hipError_t e = hipStreamQuery(static_cast<StreamIdle*>(u)->s);
+      // and a failed exchange as its own error, not as the feed's "never signalled"
+      static bool stream_busy(hipStream_t s) {
+        const hipError_t e = hipStreamQuery(s);
         if (e == hipErrorNotReady) return true;
         hipchk(e, "walk window stream");
         return false;
+      }
+      static bool busy(void* u) {
+        auto* t = static_cast<StreamIdle*>(u);
+        if (t->x && t->x->failed()) const_cast<SpinWorker*>(t->x)->wait();   // rethrows the exchange's error
+        return (t->x && t->x->busy()) || stream_busy(t->s);
       }
     } stream_idle{s};
     feed.idle = &StreamIdle::busy;
     feed.idle_user = &stream_idle;
     double feed_spin_seen = 0;   // feed.spin_ms() already counted as device wait
-    auto enqueue_window = [&](const std::vector<int32_t>& groups, int b) {
+    // A pipelined host exchange with device merge runs on its own thread (split_x): the launch helper
+    // only launches window w+1's walk (its lists signalled into pinned memory), the exchange thread
+    // waits for them, exchanges and launches the device merge, while the host resolves window w --
+    // the resolver then waits for the merged groups' signals only, not for the whole chain.
+    const bool split_x = use_exchange && pipelined && signalled && walk && !std::getenv("PE_NO_SPLIT_EXCHANGE");
+    std::unique_ptr<SpinWorker> xworker;
+    if (split_x) {
+      xworker.reset(new SpinWorker(ctx->device));
+      if (pin.on) xworker->pin(pin.l3);
+      stream_idle.x = xworker.get();
+    }
+    struct XWait {   // every exit: the exchange thread's task is over before the buffers it uses go
+      std::unique_ptr<SpinWorker>& w;
+      ~XWait() {
+        if (w) try {
+            w->wait();
+          } catch (...) {
+          }
+      }
+    } xwait_exit{xworker};
+    auto exchange_window = [&](int b, int Wg, uint32_t gen, bool own_direct, const SpinWorker* launcher) {
+      const size_t bytes = (size_t)Wg * gb;
+      if (own_direct && ctx->Ns > 0) {   // every own group signalled: the lists are in h_own
+        struct Idle {   // busy while the launcher has not launched the walk yet, or the stream runs
+          const SpinWorker* l;
+          hipStream_t s;
+          static bool busy(void* u) {
+            auto* x = static_cast<Idle*>(u);
+            return (x->l && x->l->busy()) || StreamIdle::stream_busy(x->s);
+          }
+        } idle{launcher, s};
+        pe::WindowFeed own;
+        std::vector<pe::GroupCands> own_cands;
+        own.idle = &Idle::busy;
+        own.idle_user = &idle;
+        own.reset(ctx->h_own.p, Wg, K, gen, &own_cands);
+        own.wait((size_t)Wg - 1);
+      } else {
+        hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
+        hipchk(hipStreamSynchronize(s), "sync own cands");
+      }
+      if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, dev_merge ? ctx->h_xg[b].p : outbuf(b), bytes) != 0)
+        raise(PE_ERCCL, "exchange callback failed");
+      if (dev_merge)   // the gathered lists (pinned) merged on the device, signalled per group
+        hipchk(pe::launch_merge_shards(s, ctx->h_xg[b].dev, ctx->world, Wg, K, outbufdev(b), gen),
+               "launch merge_shards");
+    };
+    // gen_in: the window's generation assigned by the caller (split exchange: the exchange thread
+    // must know it before the launch); defer_x: leave the exchange to the exchange thread
+    auto enqueue_window = [&](const std::vector<int32_t>& groups, int b, uint32_t gen_in = 0, bool defer_x = false) {
       const int Wg = (int)groups.size();
       const int Wgp = (int)round_up(Wg, pe::SC_GT);
       auto& hg = hgroups(b);
@@ -2452,7 +2506,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       const bool own_direct = walk && use_exchange && pipelined;
       uint8_t* const dst = direct_out ? outbufdev(b) : own_direct ? ctx->h_own.dev : ctx->g_out.p;
       uint32_t gen = 0;   // signalled window: its generation (the walk's or the shard merge's)
-      if (signalled || own_direct) {
+      if (gen_in) {
+        gen = gen_in;
+      } else if (signalled || own_direct) {
         if (++ctx->walk_gen == 0) ++ctx->walk_gen;
         gen = ctx->walk_gen;
       }
@@ -2505,24 +2561,10 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (direct_out) {
         // written in place
       } else if (use_exchange) {
-        if (own_direct && ctx->Ns > 0) {   // every own group signalled: the lists are in h_own
-          pe::WindowFeed own;
-          std::vector<pe::GroupCands> own_cands;
-          own.idle = &StreamIdle::busy;
-          own.idle_user = &stream_idle;
-          own.reset(ctx->h_own.p, Wg, K, gen, &own_cands);
-          own.wait((size_t)Wg - 1);
-        } else {
+        if (!pipelined)
           hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
-        }
-        if (pipelined) {   // (the launch helper, or the main thread at a restart) exchange now
-          if (!own_direct || ctx->Ns == 0) hipchk(hipStreamSynchronize(s), "sync own cands");
-          if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, dev_merge ? ctx->h_xg[b].p : outbuf(b), bytes) != 0)
-            raise(PE_ERCCL, "exchange callback failed");
-          if (dev_merge)   // the gathered lists (pinned) merged on the device, signalled per group
-            hipchk(pe::launch_merge_shards(s, ctx->h_xg[b].dev, ctx->world, Wg, K, outbufdev(b), gen),
-                   "launch merge_shards");
-        }
+        else if (!defer_x)   // (the launch helper, or the main thread at a restart) exchange now
+          exchange_window(b, Wg, gen, own_direct, nullptr);
       } else {
         ncclchk(ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
         if (dev_merge)
@@ -2693,13 +2735,40 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       while ((int)fl.size() < depth + 1)
         if (Flight* f = add_flight(fl.back().end)) to_scan.push_back(f);
         else break;
-      worker->post([&, to_apply, to_scan] {
-        const auto tp = std::chrono::steady_clock::now();
-        if (trace) helper_cpu = sched_getcpu();
-        for (const auto& a : to_apply) enqueue_apply(*a.first, a.second);
-        for (Flight* f : to_scan) enqueue_window(f->groups, f->buf);
-        if (trace) tr_post.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
-      });
+      if (split_x) {
+        // generations assigned here, in launch order: the exchange thread waits for these windows' own
+        // lists (signalled with them) while the launch helper launches the walks
+        struct XWin {
+          int buf, wg;
+          uint32_t gen;
+        };
+        std::vector<XWin> xs;
+        std::vector<std::pair<Flight*, uint32_t>> ws;
+        for (Flight* f : to_scan) {
+          if (++ctx->walk_gen == 0) ++ctx->walk_gen;
+          xs.push_back(XWin{f->buf, (int)f->groups.size(), ctx->walk_gen});
+          ws.emplace_back(f, ctx->walk_gen);
+        }
+        xworker->wait();   // (the previous window's exchange: over once its merged groups were seen)
+        worker->post([&, to_apply, ws] {
+          const auto tp = std::chrono::steady_clock::now();
+          if (trace) helper_cpu = sched_getcpu();
+          for (const auto& a : to_apply) enqueue_apply(*a.first, a.second);
+          for (const auto& w : ws) enqueue_window(w.first->groups, w.first->buf, w.second, true);
+          if (trace) tr_post.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
+        });
+        xworker->post([&, xs] {
+          for (const XWin& x : xs) exchange_window(x.buf, x.wg, x.gen, true, worker.get());
+        });
+      } else {
+        worker->post([&, to_apply, to_scan] {
+          const auto tp = std::chrono::steady_clock::now();
+          if (trace) helper_cpu = sched_getcpu();
+          for (const auto& a : to_apply) enqueue_apply(*a.first, a.second);
+          for (Flight* f : to_scan) enqueue_window(f->groups, f->buf);
+          if (trace) tr_post.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
+        });
+      }
       // seeds: the changes of the windows resolved since cur's scan (later states overwrite)
       seed.clear();
       for (size_t k = cur.ver; k < hist.size(); ++k) seed.insert(seed.end(), hist[k].begin(), hist[k].end());
@@ -2713,6 +2782,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           worker->wait();
         } catch (...) {
         }
+        if (xworker) xworker->wait();   // (a failed exchange is the cause: its error wins)
         throw;
       }
       worker->wait();
@@ -2725,6 +2795,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       // done, or speculation dropped: finish the device work, apply what is left, in order (one
       // launch per window: a node may be in several windows' updates)
+      if (xworker) xworker->wait();   // (its merge launch first: it is stream work too)
       hipchk(hipStreamSynchronize(s), "sync speculative");
       for (; n_app < hist.size(); ++n_app) {   // (depth > 1 only; slot 0 is rewritten after each)
         enqueue_apply(hist[n_app], 0);
@@ -2734,6 +2805,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (R.done()) break;
       restart();
     }
+    if (xworker) xworker->wait();
     hipchk(hipStreamSynchronize(s), "sync greedy");
     walk_drop_pending(ctx);   // (the next call rebuilds in line anyway)
     if (walk) {

@@ -62,20 +62,62 @@ uint64_t key_of(const int64_t res[RD], uint32_t labels, const int64_t q[RD], uin
 
 // ------------------------------------------------------------------ DirtySet
 
+void DirtySet::swap(DirtySet& o) noexcept {
+  std::swap(gid, o.gid);
+  std::swap(r0, o.r0);
+  std::swap(r1, o.r1);
+  std::swap(r2, o.r2);
+  std::swap(r3, o.r3);
+  std::swap(lab, o.lab);
+  std::swap(kn, o.kn);
+  std::swap(n_, o.n_);
+  std::swap(cap_, o.cap_);
+  std::swap(buf_, o.buf_);
+  std::swap(slot_, o.slot_);
+  std::swap(bits_, o.bits_);
+}
+
+void DirtySet::grow() {
+  const size_t cap = std::max<size_t>(1024, 2 * cap_);
+  // one allocation, 64-B aligned columns: five int64, K(n), labels
+  const size_t col = (cap * 8 + 63) / 64 * 64, lcol = (cap * 4 + 63) / 64 * 64;
+  uint8_t* b = static_cast<uint8_t*>(::operator new(6 * col + lcol, std::align_val_t(64)));
+  int64_t* ng = reinterpret_cast<int64_t*>(b);
+  int64_t* n0 = reinterpret_cast<int64_t*>(b + col);
+  int64_t* n1 = reinterpret_cast<int64_t*>(b + 2 * col);
+  int64_t* n2 = reinterpret_cast<int64_t*>(b + 3 * col);
+  int64_t* n3 = reinterpret_cast<int64_t*>(b + 4 * col);
+  uint64_t* nk = reinterpret_cast<uint64_t*>(b + 5 * col);
+  uint32_t* nl = reinterpret_cast<uint32_t*>(b + 6 * col);
+  if (n_) {
+    std::memcpy(ng, gid, n_ * 8);
+    std::memcpy(n0, r0, n_ * 8);
+    std::memcpy(n1, r1, n_ * 8);
+    std::memcpy(n2, r2, n_ * 8);
+    std::memcpy(n3, r3, n_ * 8);
+    std::memcpy(nk, kn, n_ * 8);
+    std::memcpy(nl, lab, n_ * 4);
+  }
+  ::operator delete(buf_, std::align_val_t(64));
+  buf_ = b;
+  gid = ng;
+  r0 = n0;
+  r1 = n1;
+  r2 = n2;
+  r3 = n3;
+  kn = nk;
+  lab = nl;
+  cap_ = cap;
+}
+
 int32_t DirtySet::upsert(int64_t g, const NodeState& st) {
-  int32_t i = slot_.insert(g, (int32_t)gid.size());
-  if (i == (int32_t)gid.size()) {
+  int32_t i = slot_.insert(g, (int32_t)n_);
+  if (i == (int32_t)n_) {
     const size_t w = (size_t)g >> 6;
     if (w >= bits_.size()) bits_.resize(std::max(w + 1, 2 * bits_.size()), 0);
     bits_[w] |= 1ull << (g & 63);
-    gid.push_back(g);
-    r0.push_back(0);
-    r1.push_back(0);
-    r2.push_back(0);
-    r3.push_back(0);
-    lab.push_back(0);
-    kn.push_back(0);
-    touched.push_back(0);
+    if (n_ == cap_) grow();
+    gid[n_++] = g;
   }
   set(i, st);
   return i;
@@ -112,16 +154,9 @@ NodeState DirtySet::get(int32_t i) const {
 }
 
 void DirtySet::clear() {
-  slot_.clear(gid.begin(), gid.end());
-  for (int64_t g : gid) bits_[(size_t)g >> 6] = 0;
-  gid.clear();
-  r0.clear();
-  r1.clear();
-  r2.clear();
-  r3.clear();
-  lab.clear();
-  kn.clear();
-  touched.clear();
+  slot_.clear(gid, gid + n_);
+  for (size_t i = 0; i < n_; ++i) bits_[(size_t)gid[i] >> 6] = 0;
+  n_ = 0;
 }
 
 // Branch-free Appendix-B key (same arithmetic as the device's node_key)
@@ -140,7 +175,7 @@ static inline uint64_t key_bf(int64_t x0, int64_t x1, int64_t x2, int64_t x3, ui
 
 void DirtySet::keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
                     std::vector<int32_t>& idx) const {   // limit: keys >= it may be left out
-  const size_t n = gid.size();
+  const size_t n = n_;
   if (out.size() < n) out.resize(n);   // only the slots listed in idx are read
   idx.clear();
   // [lo, hi): the K(n) that can give a fitting key < limit (s(q) saturated: then nothing but the
@@ -154,7 +189,7 @@ void DirtySet::keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vec
   const uint64_t span = hi > lo ? hi - lo : 0;
   // the range test k - lo < span (unsigned) or k == ~0, four nodes per AVX2 step (signed compare
   // of sign-flipped values); the few hits are scored below
-  const uint64_t* kp = kn.data();
+  const uint64_t* kp = kn;
   const __m256i flip = _mm256_set1_epi64x(INT64_MIN), vlo = _mm256_set1_epi64x((int64_t)lo),
                 vspan = _mm256_set1_epi64x((int64_t)(span ^ (1ull << 63))), ones = _mm256_set1_epi64x(-1);
   size_t i = 0;
@@ -219,7 +254,7 @@ uint64_t DirtySet::keys_all(const int64_t q[RD], uint32_t need, uint64_t limit, 
   static const bool avx512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") &&
                              __builtin_cpu_supports("avx512vl") && __builtin_cpu_supports("avx512bw") &&
                              !std::getenv("PE_NO_AVX512");
-  const size_t n = gid.size();
+  const size_t n = n_;
   if (out.size() < n) out.resize(n);
   if (!avx512) {
     keys(q, need, limit, out, idx);
@@ -244,8 +279,7 @@ uint64_t DirtySet::keys_all(const int64_t q[RD], uint32_t need, uint64_t limit, 
   const uint64_t span = hi > lo ? hi - lo : 0;
   if (idx.size() < n + 16) idx.resize(n + 16);
   size_t ni = 0;
-  const uint64_t mk = keys_avx512(n, kn.data(), r0.data(), r1.data(), r2.data(), r3.data(), lab.data(), gid.data(),
-                                  q, need, lo, span, out.data(), idx.data(), &ni);
+  const uint64_t mk = keys_avx512(n, kn, r0, r1, r2, r3, lab, gid, q, need, lo, span, out.data(), idx.data(), &ni);
   idx.resize(ni);
   return mk;
 }
@@ -662,7 +696,7 @@ void Resolver::finish_job(bool ok) {
         if (slot < 0) continue;
         NodeState st = current_state(slot);
         for (int d = 0; d < RD; ++d) st.res[d] += q[d];
-        dirty_.mark(dirty_.upsert(slot, st));
+        dirty_.upsert(slot, st);
         any_set(slot);
         slot = -1;
         --pods_placed_;
@@ -760,7 +794,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       }
     }
     scorer_.start(&seeds_, &groups, &cands, qeff_.data(), need_, feed);
-    for (int64_t g : seeds_.gid) any_set(g);
+    for (size_t i = 0; i < seeds_.size(); ++i) any_set(seeds_.gid[i]);
   }
   if (feed) feed->advance();
   auto have = [&](size_t w) { return !feed || w < feed->parsed(); };   // list of group w is there
@@ -916,7 +950,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         slot = best;
         st = dirty_.get(slot);
 #ifdef PE_RES_PROF
-        if (!conflict && dirty_.touched[slot]) conflict = true, rp.cdirty++;
+        if (!conflict) conflict = true, rp.cdirty++;   // (every dirty entry is this window's change)
 #endif
       } else if (bkey == kdS) {   // an unchanged seed: its window-start state is current
         st = seeds_.get(seeds_.find(gid));
@@ -967,7 +1001,6 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       } else {
         dirty_.set(slot, st);
       }
-      dirty_.mark(slot);
       std::fill_n(pod_node_.begin() + pod_off_[g_] + p_, m, (int32_t)gid);
       p_ += (int32_t)m;
       pods_placed_ += m;
@@ -996,8 +1029,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     ++wi;
   }
   t_ = RP_T();
-  for (size_t i = 0; i < dirty_.size(); ++i) {
-    if (!dirty_.touched[i]) continue;
+  for (size_t i = 0; i < dirty_.size(); ++i) {   // (every entry: the seeds live apart, in seeds_)
     Update u;
     u.gid = dirty_.gid[i];
     const NodeState st = dirty_.get((int32_t)i);
@@ -1010,9 +1042,9 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
       else changed_[(size_t)c] = st;
     }
   }
-  for (int64_t g : dirty_.gid) any_[(size_t)g >> 6] = 0;   // (clears whole words: every bit set is listed)
+  for (size_t i = 0; i < dirty_.size(); ++i) any_[(size_t)dirty_.gid[i] >> 6] = 0;   // (whole words: every bit set is listed)
   if (useS)
-    for (int64_t g : seeds_.gid) any_[(size_t)g >> 6] = 0;
+    for (size_t i = 0; i < seeds_.size(); ++i) any_[(size_t)seeds_.gid[i] >> 6] = 0;
   prev_.clear();               // (last window's changes, or the seeds taken over from them)
   std::swap(prev_, dirty_);    // kept: the next window's seeds if it is pipelined on this one
   prev_ok_ = true;

@@ -18,6 +18,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <memory>
+#include <new>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -214,9 +215,21 @@ class IdMap {
 };
 
 // Nodes modified since the window's snapshot, as flat struct-of-arrays so the per-group re-score
-// is one branch-free (vectorisable) loop; gid -> slot is a direct-mapped array grown on demand.
+// is one branch-free (vectorisable) loop; gid -> slot is a small hash map.  The columns share one
+// allocation, one count and one capacity: an append is one capacity test and seven stores (seven
+// vector push_backs were seven tests and size updates per placement).
 class DirtySet {
  public:
+  DirtySet() = default;
+  DirtySet(const DirtySet&) = delete;
+  DirtySet& operator=(const DirtySet&) = delete;
+  DirtySet(DirtySet&& o) noexcept { swap(o); }
+  DirtySet& operator=(DirtySet&& o) noexcept {
+    swap(o);
+    return *this;
+  }
+  ~DirtySet() { ::operator delete(buf_, std::align_val_t(64)); }
+  void swap(DirtySet& o) noexcept;
   int32_t find(int64_t gid) const { return slot_.find(gid); }
   // membership only: one bit per node id (128 KiB per 1M ids, cache-resident), the candidate
   // lists' skip test
@@ -226,9 +239,8 @@ class DirtySet {
   }
   int32_t upsert(int64_t gid, const NodeState& st);
   void set(int32_t i, const NodeState& st);
-  void mark(int32_t i) { touched[i] = 1; }
   NodeState get(int32_t i) const;
-  size_t size() const { return gid.size(); }
+  size_t size() const { return n_; }
   void clear();
   // keys of every dirty node for request (q, need) -> out (NO_KEY where it does not fit).  Keys
   // >= `limit` may be reported as NO_KEY: a node whose node-only key K(n) (below) rules out a key
@@ -243,12 +255,15 @@ class DirtySet {
   uint64_t keys_all(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
                     std::vector<int32_t>& idx) const;
   uint64_t key_at(int32_t i, const int64_t q[RD], uint32_t need) const;
-  std::vector<int64_t> gid, r0, r1, r2, r3;
-  std::vector<uint32_t> lab;
-  std::vector<uint64_t> kn;       // K(n) = (S(n) << 24) | gid, or ~0 (saturating / negative: always scored)
-  std::vector<uint8_t> touched;   // changed in this window (seeded entries start untouched)
+  // the columns, size() entries each
+  int64_t *gid = nullptr, *r0 = nullptr, *r1 = nullptr, *r2 = nullptr, *r3 = nullptr;
+  uint32_t* lab = nullptr;
+  uint64_t* kn = nullptr;   // K(n) = (S(n) << 24) | gid, or ~0 (saturating / negative: always scored)
 
  private:
+  void grow();
+  size_t n_ = 0, cap_ = 0;
+  void* buf_ = nullptr;
   IdMap slot_;
   std::vector<uint64_t> bits_;
 };
