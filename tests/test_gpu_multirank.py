@@ -15,6 +15,7 @@ multi-rank bench runs).
    blocking in ncclCommInitRank (non-blocking RCCL set-up, pe_engine.cpp nccl_settle)."""
 import json
 import os
+import signal
 import subprocess
 import sys
 import time
@@ -37,8 +38,9 @@ def _bench(gpus, extra_env):
     log = os.path.join(logdir, f"test_multirank_bench_n{gpus}.log")
     outp = os.path.join(logdir, f"test_multirank_bench_n{gpus}.json")
     with open(log, "w") as err, open(outp, "w") as so:
+        # its own process group: a hung run is killed with its rank processes, not just the launcher
         p = subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", str(gpus)] + ARGS,
-                             stdout=so, stderr=err, text=True, env=env, cwd=ROOT)
+                             stdout=so, stderr=err, text=True, env=env, cwd=ROOT, start_new_session=True)
         t0 = time.time()
         while p.poll() is None:
             try:
@@ -46,8 +48,9 @@ def _bench(gpus, extra_env):
             except subprocess.TimeoutExpired:
                 err.write(f"[test heartbeat] {time.time() - t0:.0f} s\n")
                 err.flush()
-                if time.time() - t0 > 420:
-                    p.kill()
+                if time.time() - t0 > 300:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    p.wait()
                     raise
     out = open(outp).read()
     assert p.returncode == 0, out[-3000:] + open(log).read()[-5000:]

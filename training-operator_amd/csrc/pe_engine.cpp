@@ -112,11 +112,14 @@ class SpinWorker {
   void post(std::function<void()> f) {
     task_ = std::move(f);
     err_ = nullptr;
+    posted_ = true;
     state_.store(1, std::memory_order_release);
   }
   bool busy() const { return state_.load(std::memory_order_acquire) == 1; }   // a posted task not done yet
   bool failed() const { return state_.load(std::memory_order_acquire) == 2 && err_ != nullptr; }
-  void wait() {   // rethrows what the task threw
+  void wait() {   // rethrows what the task threw; returns at once when nothing is posted
+    if (!posted_) return;
+    posted_ = false;
     for (int spin = 0; state_.load(std::memory_order_acquire) != 2; ++spin)
       if (spin < 4096) _mm_pause();
       else std::this_thread::yield();   // the helper is not running (oversubscribed host)
@@ -145,6 +148,7 @@ class SpinWorker {
     }
   }
   std::atomic<int> state_{0};
+  bool posted_ = false;   // (the posting thread's own view: a task posted and not waited for yet)
   std::function<void()> task_;
   std::exception_ptr err_;
   std::thread th_;   // last: starts after the members above exist
