@@ -331,6 +331,8 @@ struct pe_ctx {
   HostBuf<uint8_t> h_out, h_out2, h_own;   // h_out2: the pipelined loop's second blob buffer (h_outx: 3rd, 4th)
   HostBuf<uint8_t> h_merged;                // host-exchange windows: the device-merged lists
   HostBuf<uint8_t> h_xg[4];                 // pipelined host exchange: the gathered lists of blob buffer b
+  std::vector<const uint64_t*> x_lists;     // host merge of the gathered lists (exchange thread scratch)
+  std::vector<int32_t> x_ns, x_hd;
   HostBuf<int64_t> h_upd;
   // greedy sorted walk (pe_kernels.h WalkIndex; the default window path, greedy_flags bit1 = full scan)
   bool walk = true;
@@ -2468,6 +2470,54 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           }
       }
     } xwait_exit{xworker};
+    // The gathered lists of a host exchange are in host memory: the exchange thread merges them there,
+    // group by group, into the window's output, each group signalled as it is written (the resolver
+    // starts on group 0 at once) -- no PCIe read of every rank's lists by a merge kernel, no launch.
+    // PE_XCHG_DEV_MERGE=1: the device merge instead (A/B).  The rule is merge_shards_kernel's: the keys
+    // below the smallest shard limit, the K + 1 smallest of them; limit = the (K+1)-th, else that minimum.
+    const bool xhost_merge = use_exchange && dev_merge && !std::getenv("PE_XCHG_DEV_MERGE");
+    auto host_merge_group = [&](const uint8_t* gath, int Wg, int w, uint8_t* out, uint32_t gen) {
+      const int W = ctx->world;
+      std::vector<const uint64_t*>& lists = ctx->x_lists;
+      std::vector<int32_t>& ns = ctx->x_ns;
+      std::vector<int32_t>& hd = ctx->x_hd;
+      lists.resize((size_t)W);
+      ns.resize((size_t)W);
+      hd.assign((size_t)W, 0);
+      uint64_t L = pe::NO_KEY;
+      for (int r = 0; r < W; ++r) {
+        const uint8_t* g = gath + ((size_t)r * Wg + w) * gb;
+        pe::CandHdr h;
+        std::memcpy(&h, g, sizeof(h));
+        L = std::min(L, h.limit);
+        lists[(size_t)r] = reinterpret_cast<const uint64_t*>(g + sizeof(h));
+        ns[(size_t)r] = std::max(0, std::min(h.n, K));
+      }
+      uint8_t* og = out + (size_t)w * gb;
+      uint64_t* dst = reinterpret_cast<uint64_t*>(og + sizeof(pe::CandHdr));
+      int m = 0;
+      uint64_t lim = L;
+      for (;;) {
+        int br = -1;
+        uint64_t bk = L;   // (only keys below the smallest limit count)
+        for (int r = 0; r < W; ++r)
+          if (hd[(size_t)r] < ns[(size_t)r] && lists[(size_t)r][hd[(size_t)r]] < bk) {
+            bk = lists[(size_t)r][hd[(size_t)r]];
+            br = r;
+          }
+        if (br < 0) break;
+        if (m == K) {   // a (K+1)-th key below the limit: it is the list's limit
+          lim = bk;
+          break;
+        }
+        dst[m++] = bk;
+        ++hd[(size_t)br];
+      }
+      pe::CandHdr* hp = reinterpret_cast<pe::CandHdr*>(og);
+      hp->n = m;
+      hp->limit = lim;
+      __atomic_store_n(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE);   // the group's signal, last
+    };
     auto exchange_window = [&](int b, int Wg, uint32_t gen, bool own_direct, const SpinWorker* launcher) {
       const size_t bytes = (size_t)Wg * gb;
       if (own_direct && ctx->Ns > 0) {   // every own group signalled: the lists are in h_own
@@ -2491,9 +2541,12 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, dev_merge ? ctx->h_xg[b].p : outbuf(b), bytes) != 0)
         raise(PE_ERCCL, "exchange callback failed");
-      if (dev_merge)   // the gathered lists (pinned) merged on the device, signalled per group
+      if (xhost_merge) {
+        for (int w = 0; w < Wg; ++w) host_merge_group(ctx->h_xg[b].p, Wg, w, outbuf(b), gen);
+      } else if (dev_merge) {   // the gathered lists (pinned) merged on the device, signalled per group
         hipchk(pe::launch_merge_shards(s, ctx->h_xg[b].dev, ctx->world, Wg, K, outbufdev(b), gen),
                "launch merge_shards");
+      }
     };
     // gen_in: the window's generation assigned by the caller (split exchange: the exchange thread
     // must know it before the launch); defer_x: leave the exchange to the exchange thread
