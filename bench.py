@@ -560,10 +560,10 @@ def main(argv=None):
                                                             else ""),
                    "feasible_pairs": feasible,
                    "greedy_exchange": ("none (one GPU)" if world == 1
-                                       else f"host shared-memory exchange: RCCL set-up failed ({fallbacks[0]})"
+                                       else f"host shared-memory exchange (zero-copy windows): RCCL set-up failed ({fallbacks[0]})"
                                        if fallbacks
                                        else "gloo host exchange (rehearsal)" if xmode == "gloo"
-                                       else "host shared-memory exchange (rehearsal)" if host_exchange
+                                       else "host shared-memory exchange, zero-copy windows (rehearsal)" if host_exchange
                                        else "RCCL all-gather + device merge")},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": prof["traffic"],
@@ -738,6 +738,7 @@ def main(argv=None):
                          "windows_per_batch": s["windows"] / gs, "rescans_per_batch": s["rescans"] / gs,
                          "device_wait_ms_per_batch": s["greedy_wait_ms"] / gs,
                          "host_resolve_ms_per_batch": s["greedy_host_ms"] / gs,
+                         "zero_copy_exchange_windows_per_batch": s["xchg_zc_windows"] / gs,
                          "naive_pod_x_node_evals_per_s": batch.n_pods * float(N) / gt}
         if s["walk_groups"] > 0:
             # greedy roofline of the walk kernel.  Bytes it reads per batch (engine counters of the timed
@@ -834,7 +835,8 @@ def main(argv=None):
                                    "ms_per_batch": ct * 1e3, "windows_per_batch": cs["windows"] / 3.0,
                                    "rescans_per_batch": cs["rescans"] / 3.0,
                                    "host_resolve_ms_per_batch": cs["greedy_host_ms"] / 3.0,
-                                   "device_wait_ms_per_batch": cs["greedy_wait_ms"] / 3.0}
+                                   "device_wait_ms_per_batch": cs["greedy_wait_ms"] / 3.0,
+                                   "zero_copy_exchange_windows_per_batch": cs["xchg_zc_windows"] / 3.0}
             ce.close()
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -207,4 +207,5 @@ func (b *CSR) AppendJobs(o *CSR) {
 // INTEGRATION.md).  Below it a per-object call costs a kernel round trip over PCIe (~12 us) for
 // work the CPU does in well under a microsecond, so callers with few objects keep the reference
 // path; the batch entry points below take the engine for any size (the caller decides).
-const BatchCrossoverJobs = 2048
+// Round-4 box run: 4096 jobs per call, GPU 51.8 us vs one core 59.6 us (3072: 45.9 vs 42.9).
+const BatchCrossoverJobs = 4096

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 4
+#define PE_ABI_VERSION 5
 #define PE_DIMS 4
 #define PE_COMM_ID_BYTES 128
 #define PE_MAX_NODES (1LL << 24) /* node ids live in the low 24 bits of the best-fit key */
@@ -155,6 +155,8 @@ typedef struct {
   double walk_ms;        /* walk kernel time by hipEvents, only when PE_WALK_EVENTS=1 in the environment */
   int64_t walk_pend_updates; /* greedy sorted walk: node updates applied while a side-stream index rebuild
                                 was pending (written into both index sets' overlays) */
+  int64_t xchg_zc_windows;   /* multi-rank greedy windows exchanged zero-copy through the shared-memory
+                                exchange's registered segment (no host copy, no host barrier) */
 } pe_stats;
 
 int pe_abi_version(void);

@@ -4,8 +4,10 @@ the engine on device 0, exchanging the per-window candidate blobs with the other
 
     python tests/mp_shard_worker.py <rank> <world> <port> <mix> <n_nodes> <n_jobs> <out_dir> [gloo|shm]
 
-Transport "shm": the native shared-memory all-gather (pe_host_exchange) instead of the Python gloo
-callback; gloo then only broadcasts the segment name.
+Transport "shm": the native shared-memory exchange (pe_host_exchange) instead of the Python gloo
+callback -- its zero-copy windows unless PE_NO_ZC_EXCHANGE=1; gloo then only broadcasts the segment
+name.  Transport "shm-stall": both ranks place a small batch, then rank 0 places the test batch while
+the other ranks sleep and exit -- rank 0 must fail with PE_ERCCL within the device timeout (no hang).
 """
 import os
 import sys
@@ -32,7 +34,7 @@ def main():
         dist.all_gather_object(parts, blob)
         return b"".join(parts)
 
-    if transport == "shm":
+    if transport.startswith("shm"):
         names = [f"/pe_mp_{port}_{os.getpid()}" if rank == 0 else None]
         dist.broadcast_object_list(names, src=0)
         exchange = HostExchange(names[0], rank, world, 128 * (16 + 8 * 256))
@@ -43,6 +45,25 @@ def main():
     e = Engine(0, rank=rank, world_size=world, exchange=exchange, max_nodes=n_nodes)
     e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     b, en = e.shard_range()
+    if transport == "shm-stall":
+        import time
+
+        from placement import PlacementError
+        e.place_batch(synth.make_jobs(20, 5, mix))   # (every rank: the zero-copy agreement, a few windows)
+        zc0 = e.stats()["xchg_zc_windows"]
+        if rank != 0:
+            time.sleep(8)
+            e.close()
+            return
+        t0 = time.monotonic()
+        try:
+            e.place_batch(batch)
+            err = "no error"
+        except PlacementError as ex:
+            err = f"{ex.code}:{ex}"
+        np.savez(os.path.join(out_dir, "stall.npz"), err=err, secs=time.monotonic() - t0, zc0=zc0)
+        e.close()
+        return
     pods, st = e.place_batch(batch)
     res = e.read_residuals()
     # a second batch on the updated inventory: every rank's device shard and host mirror stay in step
@@ -51,7 +72,7 @@ def main():
     res2 = e.read_residuals()
     s = e.stats()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), pods=pods, st=st, res=res, pods2=pods2, st2=st2, res2=res2,
-             b=b, e=en, windows=s["windows"])
+             b=b, e=en, windows=s["windows"], zc=s["xchg_zc_windows"])
     e.close()
     dist.destroy_process_group()
 

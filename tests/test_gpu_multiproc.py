@@ -27,26 +27,44 @@ def free_port():
     return p
 
 
+def _spawn(tmp_path, world, mix, n_nodes, n_jobs, transport, env):
+    port = free_port()
+    return [subprocess.Popen([sys.executable, os.path.join(HERE, "mp_shard_worker.py"), str(r), str(world), str(port),
+                              mix, str(n_nodes), str(n_jobs), str(tmp_path), transport], env=env,
+                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
+
+
+def _env(**kv):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PE_HOST_MERGE", "PE_NO_ZC_EXCHANGE", "PE_HX_GPU_TIMEOUT_S", "PE_MERGE_RANKED"):
+        env.pop(k, None)
+    env.update(kv)
+    return env
+
+
 @pytest.mark.parametrize("world,mix,n_nodes,n_jobs,host_merge,transport", [(2, "mixed", 20000, 600, False, "gloo"),
                                                                            (3, "gang8", 9000, 300, False, "gloo"),
                                                                            (2, "island8", 6000, 300, True, "gloo"),
                                                                            (2, "mixed", 20000, 600, False, "shm"),
                                                                            (3, "island8", 9000, 300, False, "shm"),
+                                                                           (2, "mixed", 20000, 600, False, "shm-copy"),
+                                                                           (3, "mixed", 2, 40, False, "shm"),
+                                                                           (2, "mixed", 20000, 600, False, "shm-ranked"),
+                                                                           (3, "island8", 9000, 300, False, "gloo-ranked"),
                                                                            (2, "gang8", 6000, 300, True, "shm")])
 def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, host_merge, transport):
     """host_merge False: the gathered shard lists are merged on the device (merge_shards, the
     default); True: PE_HOST_MERGE=1, the host's lazy k-way merge.  transport: the Python gloo
-    callback, or the native shared-memory all-gather (pe_host_exchange).  Either way the windows are
-    pipelined (the launch helper runs the exchange while the host resolves)."""
-    port = free_port()
-    env = dict(os.environ)
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PE_HOST_MERGE"):
-        env.pop(k, None)
-    if host_merge:
-        env["PE_HOST_MERGE"] = "1"
-    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "mp_shard_worker.py"), str(r), str(world), str(port),
-                               mix, str(n_nodes), str(n_jobs), str(tmp_path), transport], env=env, stdout=subprocess.PIPE,
-                              stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    callback, or the native shared-memory exchange (pe_host_exchange) -- "shm": its zero-copy
+    windows (walk into the registered segment, the merge waits on the device), "shm-copy": the
+    copying all-gather (PE_NO_ZC_EXCHANGE=1); "-ranked": the rank merge kernel (PE_MERGE_RANKED=1).  Either way the windows are pipelined.  (3 ranks over
+    2 nodes: one rank's shard is empty -- its windows are empty lists, signalled.)"""
+    env = _env(**({"PE_HOST_MERGE": "1"} if host_merge else {}), **({"PE_NO_ZC_EXCHANGE": "1"} if transport == "shm-copy" else {}),
+               **({"PE_MERGE_RANKED": "1"} if transport.endswith("-ranked") else {}))
+    transport = transport.split("-")[0] if transport != "shm-copy" else "shm-copy"
+    zc_expected = transport == "shm" and not host_merge
+    transport = "shm" if transport == "shm-copy" else transport
+    procs = _spawn(tmp_path, world, mix, n_nodes, n_jobs, transport, env)
     outs = []
     try:
         for p in procs:
@@ -78,7 +96,31 @@ def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, 
         full2[:, b:e] = d["res2"]
         covered += e - b
         assert int(d["windows"]) > 1
+        assert (int(d["zc"]) > 0) == zc_expected, (r, int(d["zc"]))
     assert covered == n_nodes
     np.testing.assert_array_equal(full, w_res)
     np.testing.assert_array_equal(full2, w_res2)
     assert 0 < (w_st == 0).sum() <= n_jobs
+
+
+def test_zero_copy_exchange_peer_stall_fails_fast(tmp_path):
+    """A rank that stops taking part (it sleeps, then exits) must not hang its peers: their shard
+    merges give up after PE_HX_GPU_TIMEOUT_S on the device and the greedy call fails with PE_ERCCL."""
+    procs = _spawn(tmp_path, 2, "mixed", 20000, 600, "shm-stall", _env(PE_HX_GPU_TIMEOUT_S="3"))
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=100)
+            outs.append(out)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{outs[r][-3000:]}"
+    d = np.load(tmp_path / "stall.npz")
+    assert int(d["zc0"]) > 0                      # the first batch ran zero-copy on both ranks
+    err = str(d["err"])
+    assert err.startswith("-5:"), err              # PE_ERCCL
+    assert "never arrived" in err, err
+    assert float(d["secs"]) < 30, float(d["secs"])

@@ -68,6 +68,9 @@ def test_bench_two_ranks_matches_one():
     assert one["config"]["greedy_exchange"] == "none (one GPU)"
     assert "RCCL set-up failed" in two["config"]["greedy_exchange"] and "simulated" in two["config"]["greedy_exchange"]
     assert "shared-memory" in two["config"]["greedy_exchange"]
+    # the exchange's zero-copy windows ran (walk into the registered segment, merge waits on the device)
+    assert two["configs"]["cfg3"]["zero_copy_exchange_windows_per_batch"] > 0
+    assert one["configs"]["cfg3"]["zero_copy_exchange_windows_per_batch"] == 0
     assert two["degraded"] is True and "simulated" in two["degraded_reason"] and "degraded" not in one
     cfg1, cfg2 = one["config"], two["config"]
     assert sum(cfg2["shard_nodes_per_rank"]) == cfg2["nodes"] == 100000 and len(cfg2["shard_nodes_per_rank"]) == 2

@@ -30,6 +30,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "pe_hostx.h"
 #include "pe_kernels.h"
 #include "pe_resolver.h"
 #include "placement.h"
@@ -238,6 +239,8 @@ struct pe_ctx {
   ncclComm_t comm = nullptr;
   pe_allgather_fn exchange = nullptr;
   void* exchange_user = nullptr;
+  void* zc_hx = nullptr;   // the shared-memory exchange whose zero-copy use the ranks agreed on (zc_ok)
+  bool zc_ok = false;
   int topk = 256, window_groups = 128;
   bool pipeline = true;   // greedy: scan window w+1 while the host resolves window w (greedy_flags bit0 = off)
   int64_t window_pods = 1024;
@@ -362,6 +365,7 @@ struct pe_ctx {
   DevBuf<uint8_t> w_temp;
   DevBuf<uint32_t> w_flush;   // PE_WALK_FLUSH: 512 MiB rewritten before each walk (cold-cache diagnostics)
   DevBuf<unsigned long long> w_stat;   // walk counters of the current pe_place_greedy (rounds, overlay)
+  DevBuf<uint64_t> g_xstatus;          // zero-copy exchange: the window's wait status (launch_xwait)
   pe_stats stats{};
 
   ~pe_ctx() {
@@ -386,7 +390,7 @@ struct pe_ctx {
     }
     if (w_s2) (void)hipStreamSynchronize(w_s2);
     for (auto& x : ws) x.release();
-    w_kin.release(); w_slow.release(); w_temp.release(); w_stat.release(); w_flush.release();
+    w_kin.release(); w_slow.release(); w_temp.release(); w_stat.release(); w_flush.release(); g_xstatus.release();
     if (w_ev_snap) (void)hipEventDestroy(w_ev_snap);
     if (w_ev_done) (void)hipEventDestroy(w_ev_done);
     if (w_s2) (void)hipStreamDestroy(w_s2);
@@ -412,6 +416,9 @@ int guarded(pe_ctx* ctx, F&& body) {
   } catch (const std::bad_alloc&) {
     ctx->err = "host allocation failed";
     return PE_ENOMEM;
+  } catch (const pe::ExchangeError& e) {   // a zero-copy window's peer lists never arrived
+    ctx->err = e.what();
+    return PE_ERCCL;
   } catch (const std::runtime_error& e) {   // pe::WindowFeed: a walk group the device never signalled
     ctx->err = e.what();
     return PE_EHIP;
@@ -2404,6 +2411,10 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // (PE_HOST_MERGE=1 with a host exchange, measured: the lazy host merge doubled the resolve --
     // the seed helper cannot pre-skip merged lists -- 20.4 vs 8.9 ms per 2-rank cfg3 batch)
     const bool dev_merge = !direct_out && (int64_t)ctx->world * K <= pe::MG_CAP && !std::getenv("PE_HOST_MERGE");
+    // the shard merge kernel: PE_MERGE_RANKED=1 the rank merge (256-thread blocks, no sort; A/B)
+    const bool ranked = std::getenv("PE_MERGE_RANKED") && ctx->world <= pe::RM_MAX_WORLD &&
+                        (int64_t)ctx->world * K * 8 <= 64 * 1024;
+    auto* const merge_fn = ranked ? &pe::launch_merge_ranked : &pe::launch_merge_shards;
     const bool signalled = pipelined && !std::getenv("PE_NO_GROUP_SIGNAL") && (direct_out ? walk : dev_merge);
     // Pipeline depth D (signalled windows; PE_PIPE_DEPTH, 1..3, default 1): windows i+1 .. i+D are
     // scanned while window i is resolved (D + 1 blob / request buffers, D update staging slots).  (2
@@ -2454,7 +2465,32 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // only launches window w+1's walk (its lists signalled into pinned memory), the exchange thread
     // waits for them, exchanges and launches the device merge, while the host resolves window w --
     // the resolver then waits for the merged groups' signals only, not for the whole chain.
-    const bool split_x = use_exchange && pipelined && signalled && walk && !std::getenv("PE_NO_SPLIT_EXCHANGE");
+    // Zero-copy shared-memory exchange (pe_hostx.h): each window's walk writes this rank's lists into
+    // its slot of the registered segment and the shard merge, queued behind it, waits on the device
+    // for every rank's signal of its group -- no exchange thread, no host barrier, no copies.  The
+    // ranks agree on it once per context and segment (each says whether it could register the
+    // segment); PE_NO_ZC_EXCHANGE=1 (every rank): the copying exchange below.
+    bool zc = false;
+    pe_host_exchange* const hx = pe::hx_is(ctx->exchange) ? static_cast<pe_host_exchange*>(ctx->exchange_user) : nullptr;
+    if (hx && use_exchange && pipelined && signalled && ctx->walk && !std::getenv("PE_NO_ZC_EXCHANGE")) {
+      if (ctx->zc_hx != hx) {
+        const uint8_t ok = pe::hx_zc_register(hx) && (size_t)Wmax * gb <= pe::hx_slot_bytes(hx) ? 1 : 0;
+        std::vector<uint8_t> all((size_t)ctx->world, 0);
+        if (ctx->exchange(ctx->exchange_user, &ok, all.data(), 1) != 0) raise(PE_ERCCL, "exchange callback failed");
+        ctx->zc_ok = std::all_of(all.begin(), all.end(), [](uint8_t v) { return v == 1; });
+        ctx->zc_hx = hx;
+      }
+      zc = ctx->zc_ok;
+      if (zc) hipchk(ctx->g_xstatus.ensure(1), "alloc exchange status");
+    }
+    // a rank whose peer stalls: its wait gives up after PE_HX_GPU_TIMEOUT_S (default 60) and the
+    // resolver raises (the merged lists come back with n = -1), the GPU is not held
+    const int64_t zc_ticks = [] {
+      const char* e = std::getenv("PE_HX_GPU_TIMEOUT_S");
+      const double t = e ? std::atof(e) : 60.0;
+      return (int64_t)((t > 0 ? t : 60.0) * 1e8);   // wall_clock64: 100 MHz
+    }();
+    const bool split_x = use_exchange && pipelined && signalled && walk && !zc && !std::getenv("PE_NO_SPLIT_EXCHANGE");
     std::unique_ptr<SpinWorker> xworker;
     if (split_x) {
       xworker.reset(new SpinWorker(ctx->device));
@@ -2470,12 +2506,12 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           }
       }
     } xwait_exit{xworker};
-    // The gathered lists of a host exchange are in host memory: the exchange thread merges them there,
-    // group by group, into the window's output, each group signalled as it is written (the resolver
-    // starts on group 0 at once) -- no PCIe read of every rank's lists by a merge kernel, no launch.
-    // PE_XCHG_DEV_MERGE=1: the device merge instead (A/B).  The rule is merge_shards_kernel's: the keys
-    // below the smallest shard limit, the K + 1 smallest of them; limit = the (K+1)-th, else that minimum.
-    const bool xhost_merge = use_exchange && dev_merge && !std::getenv("PE_XCHG_DEV_MERGE");
+    // PE_XCHG_HOST_MERGE=1 (A/B): the exchange thread merges the gathered lists on the host, group by
+    // group, each signalled as written, instead of the device merge -- measured 36.7 vs 18.5 ms per
+    // 2-rank cfg3 batch (the merge of world x K keys per group is host work the resolver waits on).
+    // The rule is merge_shards_kernel's: the keys below the smallest shard limit, the K + 1 smallest
+    // of them; limit = the (K+1)-th, else that minimum.
+    const bool xhost_merge = use_exchange && dev_merge && std::getenv("PE_XCHG_HOST_MERGE");
     auto host_merge_group = [&](const uint8_t* gath, int Wg, int w, uint8_t* out, uint32_t gen) {
       const int W = ctx->world;
       std::vector<const uint64_t*>& lists = ctx->x_lists;
@@ -2544,7 +2580,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (xhost_merge) {
         for (int w = 0; w < Wg; ++w) host_merge_group(ctx->h_xg[b].p, Wg, w, outbuf(b), gen);
       } else if (dev_merge) {   // the gathered lists (pinned) merged on the device, signalled per group
-        hipchk(pe::launch_merge_shards(s, ctx->h_xg[b].dev, ctx->world, Wg, K, outbufdev(b), gen),
+        hipchk(merge_fn(s, ctx->h_xg[b].dev, ctx->world, Wg, K, outbufdev(b), gen, 0, nullptr),
                "launch merge_shards");
       }
     };
@@ -2560,8 +2596,13 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       // unsharded: the kernel writes the blob straight into pinned host memory (no D2H copy); so does
       // a pipelined host exchange's walk (its own lists, signalled per group: no D2H, no stream sync)
-      const bool own_direct = walk && use_exchange && pipelined;
-      uint8_t* const dst = direct_out ? outbufdev(b) : own_direct ? ctx->h_own.dev : ctx->g_out.p;
+      const bool own_direct = walk && use_exchange && pipelined && !zc;
+      pe::HxWindow hw;   // zero-copy: this window's slots and their generation (every rank, every window)
+      if (zc) hw = pe::hx_zc_next(hx);
+      uint8_t* const dst = zc           ? hw.dev + (size_t)ctx->rank * hw.slot
+                           : direct_out ? outbufdev(b)
+                           : own_direct ? ctx->h_own.dev
+                                        : ctx->g_out.p;
       uint32_t gen = 0;   // signalled window: its generation (the walk's or the shard merge's)
       if (gen_in) {
         gen = gen_in;
@@ -2589,7 +2630,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           hipchk(hipEventRecord(evp.first, s), "event record");
         }
         hipchk(pe::launch_walk(s, hg.dev, Wg, K, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns,
-                               (uint64_t)ctx->begin, dst, direct_out || own_direct ? gen : 0u),
+                               (uint64_t)ctx->begin, dst, zc ? hw.gen : direct_out || own_direct ? gen : 0u),
                "launch walk");
         if (wev) hipchk(hipEventRecord(evp.second, s), "event record");
         walk_launch_groups += Wg;
@@ -2601,6 +2642,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
                "launch scan");
         hipchk(pe::launch_merge(s, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p, nwaves, K, dst, Wg),
                "launch merge");
+      } else if (zc) {   // an empty shard: empty lists, signalled in stream order like a walk's
+        hipchk(pe::launch_empty_groups(s, Wg, K, dst, hw.gen), "launch empty groups");
       } else {
         std::vector<uint8_t> empty((size_t)Wg * gb, 0);
         for (int w = 0; w < Wg; ++w) {
@@ -2617,6 +2660,13 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       const size_t bytes = (size_t)Wg * gb;
       if (direct_out) {
         // written in place
+      } else if (zc) {   // merged once every rank's walk signalled every group (pe_hostx.h)
+        ctx->stats.xchg_zc_windows += 1;
+        hipchk(pe::launch_xwait(s, hw.dev, ctx->world, Wg, K, (int64_t)hw.slot, hw.gen, zc_ticks, ctx->g_xstatus.p),
+               "launch exchange wait");
+        hipchk(merge_fn(s, hw.dev, ctx->world, Wg, K, outbufdev(b), gen, (int64_t)hw.slot,
+                                       ctx->g_xstatus.p),
+               "launch merge_shards");
       } else if (use_exchange) {
         if (!pipelined)
           hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
@@ -2625,7 +2675,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       } else {
         ncclchk(ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
         if (dev_merge)
-          hipchk(pe::launch_merge_shards(s, ctx->g_gath.p, ctx->world, Wg, K, outbufdev(b), gen), "launch merge_shards");
+          hipchk(merge_fn(s, ctx->g_gath.p, ctx->world, Wg, K, outbufdev(b), gen, 0, nullptr), "launch merge_shards");
         else
           hipchk(hipMemcpyAsync(outbuf(b), ctx->g_gath.p, bytes * ctx->world, hipMemcpyDeviceToHost, s),
                  "D2H gathered");
@@ -2655,7 +2705,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, outbuf(b), bytes) != 0)
           raise(PE_ERCCL, "exchange callback failed");
         if (dev_merge) {   // the gathered blob (pinned) merged by the device into h_merged
-          hipchk(pe::launch_merge_shards(s, outbufdev(b), ctx->world, Wg, K, ctx->h_merged.dev, 0u),
+          hipchk(merge_fn(s, outbufdev(b), ctx->world, Wg, K, ctx->h_merged.dev, 0u, 0, nullptr),
                  "launch merge_shards");
           hipchk(hipStreamSynchronize(s), "sync merge");
           last_blob = ctx->h_merged.p;

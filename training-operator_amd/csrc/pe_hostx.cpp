@@ -4,11 +4,13 @@
 // loop runs unchanged over it (the helper thread exchanges window w+1 while the host resolves w).
 //
 // Layout of the segment: a 4 KiB header (magic, world, slot bytes, attach count, two arrival
-// counters), then two phases x world slots of `max_bytes`.  Call k of every rank uses phase
+// counters), then four phases x world slots of `max_bytes`: phases 0-1 for the copying all-gather
+// below, 2-3 for the engine's zero-copy windows (pe_hostx.h).  Call k of every rank uses phase
 // p = k & 1: write the own block into slot [p][rank], count the arrival in ctr[p], wait until all
 // world ranks arrived (ctr[p] == world * (k / 2 + 1)), copy the world slots out.  One barrier per
 // call suffices: slot [p][r] is rewritten at call k + 2 only after barrier k + 1, which every rank
 // reaches only after it copied call k's slots.
+#include <hip/hip_runtime.h>
 #include <fcntl.h>
 #include <immintrin.h>
 #include <sched.h>
@@ -24,6 +26,7 @@
 #include <new>
 #include <string>
 
+#include "pe_hostx.h"
 #include "placement.h"
 
 namespace {
@@ -56,6 +59,9 @@ struct pe_host_exchange {
   size_t map_bytes = 0;
   int32_t rank = 0, world = 1;
   uint64_t calls = 0;
+  uint64_t zc_windows = 0;   // zero-copy windows issued (pe_hostx.h)
+  int zc_reg = 0;            // 1: registered with HIP, -1: registration failed
+  uint8_t* zc_dev = nullptr; // device address of the segment's data
   std::string name;
 };
 
@@ -65,7 +71,7 @@ int pe_host_exchange_open(const char* name, int32_t rank, int32_t world, size_t 
   if (!name || !out || name[0] != '/' || world < 1 || rank < 0 || rank >= world || max_bytes == 0) return PE_EINVAL;
   *out = nullptr;
   const size_t slot = (max_bytes + 63) & ~(size_t)63;
-  const size_t total = kHdr + 2 * (size_t)world * slot;
+  const size_t total = kHdr + 4 * (size_t)world * slot;
   int fd = -1;
   const auto t0 = std::chrono::steady_clock::now();
   auto waited = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
@@ -163,9 +169,46 @@ int pe_host_exchange_allgather(void* user, const void* send, void* recv, size_t 
 
 void pe_host_exchange_close(pe_host_exchange* x) {
   if (!x) return;
+  if (x->zc_reg == 1) (void)hipHostUnregister(x->h);
   if (x->rank == 0) shm_unlink(x->name.c_str());   // (ENOENT once every rank attached)
   munmap(x->h, x->map_bytes);
   delete x;
 }
 
 }  // extern "C"
+
+namespace pe {
+
+bool hx_is(pe_allgather_fn fn) { return fn == &pe_host_exchange_allgather; }
+
+bool hx_zc_register(pe_host_exchange* x) {
+  if (!x) return false;
+  if (x->zc_reg == 0) {
+    void* dev = nullptr;
+    x->zc_reg = -1;
+    if (hipHostRegister(x->h, x->map_bytes, hipHostRegisterMapped | hipHostRegisterPortable) == hipSuccess) {
+      if (hipHostGetDevicePointer(&dev, x->h, 0) == hipSuccess && dev) {
+        x->zc_dev = static_cast<uint8_t*>(dev) + kHdr;
+        x->zc_reg = 1;
+      } else {
+        (void)hipHostUnregister(x->h);
+      }
+    }
+    (void)hipGetLastError();   // (a failed registration is an answer, not a sticky error)
+  }
+  return x->zc_reg == 1;
+}
+
+size_t hx_slot_bytes(const pe_host_exchange* x) { return x ? (size_t)x->h->slot_bytes : 0; }
+
+HxWindow hx_zc_next(pe_host_exchange* x) {
+  HxWindow w;
+  const size_t slot = x->h->slot_bytes;
+  const uint64_t k = x->zc_windows++;
+  w.dev = x->zc_dev + (2 + (size_t)(k & 1)) * x->world * slot;
+  w.slot = slot;
+  w.gen = (uint32_t)(k % 0xFFFFFFFFull) + 1;   // (slot headers start zeroed: generation 0 is never current)
+  return w;
+}
+
+}  // namespace pe

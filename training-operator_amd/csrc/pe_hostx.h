@@ -1,0 +1,36 @@
+// Engine-side view of the shared-memory exchange (pe_hostx.cpp): its zero-copy windows.
+//
+// With a pe_host_exchange as the exchange callback, the pipelined multi-rank greedy need not copy
+// the lists through the host at all.  The segment is registered with HIP in every rank; each
+// window's walk writes its rank's lists straight into its slot of the window's phase, signalled
+// per group with the window's generation (the same on every rank: the n-th zero-copy window of
+// the segment), and the rank's shard-merge kernel, queued right behind its walk, waits on the
+// device for every rank's signal of its group before merging.  No host thread, no barrier, no
+// copy: a group's merged list is signalled as soon as the last rank's walk wrote it.
+//
+// Slot reuse needs no barrier either: window k + 2 reuses phase k & 1, and rank r's walk k + 2
+// runs after its merge k + 1 (one stream), which waited for every peer's walk k + 1, which ran
+// after that peer's merge k (its stream) -- the last reader of rank r's window-k slot.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+#include "placement.h"
+
+namespace pe {
+
+struct HxWindow {
+  uint8_t* dev = nullptr;    // device address of the phase's slot 0 (slot r at dev + r * slot)
+  size_t slot = 0;           // bytes between the ranks' slots
+  uint32_t gen = 0;          // the window's signal generation, nonzero, equal on every rank
+};
+
+// is this exchange callback the shared-memory exchange (its user pointer a pe_host_exchange)?
+bool hx_is(pe_allgather_fn fn);
+// registers the segment with HIP (once per process and segment); false when that fails
+bool hx_zc_register(pe_host_exchange* x);
+size_t hx_slot_bytes(const pe_host_exchange* x);
+// the next zero-copy window (every rank calls it once per window, in the same order)
+HxWindow hx_zc_next(pe_host_exchange* x);
+
+}  // namespace pe

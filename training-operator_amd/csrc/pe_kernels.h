@@ -344,7 +344,25 @@ hipError_t launch_walk_build(hipStream_t s, const int64_t* res, int64_t stride, 
 // Multi-rank window: world gathered shard blobs (key lists) -> one list per group (the K smallest
 // keys below the smallest shard limit, limit = the (K+1)-th or that minimum); gen != 0 signals each
 // group as the walk does.  world * K <= MG_CAP.
-hipError_t launch_merge_shards(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen);
+// rank_stride: bytes between the ranks' blocks in gath (0 = Wg x cand_group_bytes(K), back to back; the
+// shared-memory exchange's slots are further apart).  xstatus (zero-copy exchange, device word
+// written by launch_xwait before it on the stream): nonzero = a rank's lists never arrived, every
+// group is written with n = -1 and limit = *xstatus (signalled) instead of a list.
+hipError_t launch_merge_shards(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen,
+                               int64_t rank_stride = 0, const uint64_t* xstatus = nullptr);
+// Zero-copy exchange: one block waits until every rank's header of every group (slot r at gath +
+// r * rank_stride) carries in_gen, at most timeout_ticks of wall_clock64 (100 MHz); *xstatus = 0,
+// or 1 << 63 | rank << 32 | the generation that rank's slot still held.
+constexpr int XW_THREADS = 256;
+hipError_t launch_xwait(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, int64_t rank_stride,
+                        uint32_t in_gen, int64_t timeout_ticks, uint64_t* xstatus);
+// The same merge by rank (merge_ranked_kernel): 256-thread blocks, the lists in LDS (world x K x 8 B
+// of dynamic LDS, at most 64 KiB), no sort
+constexpr int RM_THREADS = 256, RM_MAX_WORLD = 16;
+hipError_t launch_merge_ranked(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen,
+                               int64_t rank_stride = 0, const uint64_t* xstatus = nullptr);
+// Wg empty lists (n = 0, limit = NO_KEY), signalled with gen
+hipError_t launch_empty_groups(hipStream_t s, int Wg, int K, uint8_t* out, uint32_t gen);
 // One block per group: overlay + walk, exact top-K keys and limit, same blob as merge.  gen != 0:
 // each group's header.flags is set to gen after its keys, n and limit are visible to the host
 // (system-scope release; out is pinned host memory the host polls per group).

@@ -1529,7 +1529,11 @@ __device__ void write_group(const uint64_t* sk, int nout, int flags, uint64_t li
   if ((int)(threadIdx.x & ~63u) < nout || threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   __syncthreads();
+#ifdef PE_SIGNAL_RELAXED   // (A/B: no L2 write-back before the flag -- the list went to uncached host memory)
+  if (threadIdx.x == 0) __hip_atomic_store(&hp->flags, (int32_t)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
   if (threadIdx.x == 0) __hip_atomic_store(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
 }
 
 __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __restrict__ cand,
@@ -1615,24 +1619,44 @@ __global__ __launch_bounds__(MG_THREADS) void merge_kernel(const uint64_t* __res
 // limit = the (K+1)-th key, or L -- the unsharded window's blob, signalled (gen) when the host takes
 // groups as they arrive.  world * K <= MG_CAP (the host checks).
 __global__ __launch_bounds__(MG_THREADS) void merge_shards_kernel(const uint8_t* __restrict__ gath, int world, int Wg,
-                                                                  int K, uint8_t* __restrict__ out, uint32_t gen) {
+                                                                  int K, uint8_t* __restrict__ out, uint32_t gen,
+                                                                  int64_t rank_stride,
+                                                                  const uint64_t* __restrict__ xstatus) {
   __shared__ TopkShared s;
   const int g = blockIdx.x;
   const int tid = threadIdx.x;
   const size_t gb = cand_group_bytes(K);
-  const size_t shard_bytes = (size_t)Wg * gb;
-  uint64_t L = NO_KEY;
-  for (int r = 0; r < world; ++r)
-    L = umin64(L, reinterpret_cast<const CandHdr*>(gath + r * shard_bytes + (size_t)g * gb)->limit);
+  const size_t shard_bytes = rank_stride > 0 ? (size_t)rank_stride : (size_t)Wg * gb;
+  if (xstatus && *xstatus != 0) {   // zero-copy exchange: a rank's lists never arrived (xwait_kernel)
+    if (tid == 0) {
+      CandHdr* hp = reinterpret_cast<CandHdr*>(out + (size_t)g * gb);
+      hp->n = -1;   // the host raises on it (pe_resolver.cpp parse_group_keys) and reports the limit
+      hp->limit = *xstatus;
+      __hip_atomic_store(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return;
+  }
+  // The shards' lists may sit in host memory written by other processes' kernels (host exchange):
+  // read them with system-scope loads, which go to memory past the GPU caches (no acquire: that
+  // would invalidate L2 under every kernel on the GPU).  Headers once per block, through LDS.
+  __shared__ uint64_t hl[MG_THREADS / 64];
+  __shared__ int hn[MG_THREADS / 64];
+  if (tid < world) {
+    const CandHdr* h = reinterpret_cast<const CandHdr*>(gath + tid * shard_bytes + (size_t)g * gb);
+    hl[tid] = __hip_atomic_load(&h->limit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    hn[tid] = min(__hip_atomic_load(&h->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), K);
+  }
   if (tid == 0) s.total = 0;
   __syncthreads();
+  uint64_t L = NO_KEY;
+  for (int r = 0; r < world; ++r) L = umin64(L, hl[r]);
   for (int r = 0; r < world; ++r) {
     const uint8_t* base = gath + r * shard_bytes + (size_t)g * gb;
-    const int n = min(reinterpret_cast<const CandHdr*>(base)->n, K);
+    const int n = hn[r];
     const uint64_t* keys = reinterpret_cast<const uint64_t*>(base + sizeof(CandHdr));
     for (int i0 = 0; i0 < n; i0 += MG_THREADS) {   // block-uniform bound: topk_append is wave-collective
       const int i = i0 + tid;
-      const uint64_t k = i < n ? keys[i] : NO_KEY;
+      const uint64_t k = i < n ? __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : NO_KEY;
       topk_append(s, k, k < L);
     }
   }
@@ -1642,10 +1666,158 @@ __global__ __launch_bounds__(MG_THREADS) void merge_shards_kernel(const uint8_t*
   write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : L, K, g, out, gen);
 }
 
-hipError_t launch_merge_shards(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen) {
+hipError_t launch_merge_shards(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen,
+                               int64_t rank_stride, const uint64_t* xstatus) {
   if (Wg <= 0) return hipSuccess;
-  if (world < 1 || K < 1 || (int64_t)world * K > MG_CAP) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(merge_shards_kernel, dim3(Wg), dim3(MG_THREADS), 0, s, gath, world, Wg, K, out, gen);
+  if (world < 1 || world > MG_THREADS / 64 || K < 1 || (int64_t)world * K > MG_CAP) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(merge_shards_kernel, dim3(Wg), dim3(MG_THREADS), 0, s, gath, world, Wg, K, out, gen, rank_stride,
+                     xstatus);
+  return hipGetLastError();
+}
+
+// Zero-copy exchange wait (pe_hostx.h): ONE small block polls every (rank, group) header of the
+// window's slots until it carries in_gen, then the shard merge runs behind it on the stream.  The
+// wait is one block, not the merge's 1024-thread blocks: with several ranks on one GPU, merges that
+// spun while holding a CU's registers each could take every CU a peer's walk needs (a 3-rank run on
+// one card did exactly that).  A peer that never writes: after timeout_ticks of wall_clock64 (100
+// MHz) *xstatus = 1 << 63 | rank << 32 | the generation seen, which the merge reports per group.
+__global__ __launch_bounds__(XW_THREADS) void xwait_kernel(const uint8_t* __restrict__ gath, int world, int Wg, int K,
+                                                           int64_t rank_stride, uint32_t in_gen, int64_t timeout_ticks,
+                                                           uint64_t* __restrict__ xstatus) {
+  __shared__ unsigned long long late;
+  if (threadIdx.x == 0) late = 0;
+  __syncthreads();
+  const size_t gb = cand_group_bytes(K);
+  const long long t0 = wall_clock64();
+  for (int i = threadIdx.x; i < world * Wg; i += XW_THREADS) {
+    const int r = i / Wg, g = i - r * Wg;
+    const CandHdr* h = reinterpret_cast<const CandHdr*>(gath + (size_t)r * rank_stride + (size_t)g * gb);
+    // relaxed system-scope polls: each reads memory, past the caches, without an acquire's cache
+    // invalidation (an acquire per poll invalidated L2 under every kernel of the GPU: the walks
+    // sharing it slowed down ~1.5x).  The merge behind this kernel reads the lists the same way.
+    int32_t f;
+    while ((f = __hip_atomic_load(&h->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != (int32_t)in_gen) {
+      if (__hip_atomic_load(&late, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) break;
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > timeout_ticks) {
+        atomicCAS(&late, 0ull, (1ull << 63) | ((unsigned long long)r << 32) | (uint32_t)f);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *xstatus = late;
+}
+
+hipError_t launch_xwait(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, int64_t rank_stride,
+                        uint32_t in_gen, int64_t timeout_ticks, uint64_t* xstatus) {
+  if (Wg <= 0) return hipSuccess;
+  if (world < 1 || rank_stride < (int64_t)Wg * (int64_t)cand_group_bytes(K) || in_gen == 0 || timeout_ticks <= 0 || !xstatus)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(xwait_kernel, dim3(1), dim3(XW_THREADS), 0, s, gath, world, Wg, K, rank_stride, in_gen,
+                     timeout_ticks, xstatus);
+  return hipGetLastError();
+}
+
+// Rank merge (same output as merge_shards_kernel): one 256-thread block per group holds the shards'
+// lists in LDS (world x K keys) and places every key below L by its rank in the union -- its index
+// in its own list plus, per other shard, the number of that shard's keys below it (binary search;
+// keys are unique across shards: the node id is in their low bits).  Ranks < K are the output, rank
+// K is the limit.  No sort, no histogram: a small block that fits beside a walk's 1024-thread block
+// on one CU, and one pass over host-memory lists.
+__device__ __forceinline__ int lds_lower_bound(const uint64_t* a, int n, uint64_t k) {
+  int lo = 0;
+  while (n > 0) {
+    const int h = n >> 1;
+    if (a[lo + h] < k) {
+      lo += h + 1;
+      n -= h + 1;
+    } else {
+      n = h;
+    }
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(RM_THREADS) void merge_ranked_kernel(const uint8_t* __restrict__ gath, int world, int Wg,
+                                                                  int K, uint8_t* __restrict__ out, uint32_t gen,
+                                                                  int64_t rank_stride,
+                                                                  const uint64_t* __restrict__ xstatus) {
+  extern __shared__ uint64_t lk[];   // shard r's keys at lk[r * K ...]
+  __shared__ uint64_t hl[RM_MAX_WORLD];
+  __shared__ int hn[RM_MAX_WORLD], cnt[RM_MAX_WORLD];
+  __shared__ uint64_t newlim;
+  const int g = blockIdx.x;
+  const int tid = threadIdx.x;
+  const size_t gb = cand_group_bytes(K);
+  const size_t shard_bytes = rank_stride > 0 ? (size_t)rank_stride : (size_t)Wg * gb;
+  uint8_t* og = out + (size_t)g * gb;
+  CandHdr* hp = reinterpret_cast<CandHdr*>(og);
+  if (xstatus && *xstatus != 0) {   // zero-copy exchange: a rank's lists never arrived (xwait_kernel)
+    if (tid == 0) {
+      hp->n = -1;
+      hp->limit = *xstatus;
+      __hip_atomic_store(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return;
+  }
+  if (tid < world) {   // (system-scope loads: see merge_shards_kernel)
+    const CandHdr* h = reinterpret_cast<const CandHdr*>(gath + tid * shard_bytes + (size_t)g * gb);
+    hl[tid] = __hip_atomic_load(&h->limit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    hn[tid] = max(0, min(__hip_atomic_load(&h->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), K));
+  }
+  if (tid == 0) newlim = NO_KEY;
+  __syncthreads();
+  uint64_t L = NO_KEY;
+  for (int r = 0; r < world; ++r) L = umin64(L, hl[r]);
+  for (int r = 0; r < world; ++r) {
+    const uint64_t* keys = reinterpret_cast<const uint64_t*>(gath + r * shard_bytes + (size_t)g * gb + sizeof(CandHdr));
+    for (int i = tid; i < hn[r]; i += RM_THREADS)
+      lk[r * K + i] = __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  if (tid < world) cnt[tid] = lds_lower_bound(lk + tid * K, hn[tid], L);   // keys below L
+  __syncthreads();
+  int T = 0;
+  for (int r = 0; r < world; ++r) T += cnt[r];
+  uint64_t* dst = reinterpret_cast<uint64_t*>(og + sizeof(CandHdr));
+  for (int r = 0; r < world; ++r)
+    for (int i = tid; i < cnt[r]; i += RM_THREADS) {
+      const uint64_t k = lk[r * K + i];
+      int rank = i;
+      for (int r2 = 0; r2 < world; ++r2)
+        if (r2 != r) rank += lds_lower_bound(lk + r2 * K, cnt[r2], k);
+      if (rank < K) dst[rank] = k;
+      else if (rank == K) newlim = k;
+    }
+  __syncthreads();
+  if (tid == 0) {
+    hp->n = T < K ? T : K;
+    hp->limit = T > K ? newlim : L;
+  }
+  // as write_group: every store has left the CU, the block agrees, then the signal (release)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_merge_ranked(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen,
+                               int64_t rank_stride, const uint64_t* xstatus) {
+  if (Wg <= 0) return hipSuccess;
+  if (world < 1 || world > RM_MAX_WORLD || K < 1 || (int64_t)world * K * 8 > 64 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(merge_ranked_kernel, dim3(Wg), dim3(RM_THREADS), (size_t)world * K * 8, s, gath, world, Wg, K, out,
+                     gen, rank_stride, xstatus);
+  return hipGetLastError();
+}
+
+// Empty lists (an empty node shard's window in a zero-copy exchange), signalled like a walk's.
+__global__ __launch_bounds__(64) void empty_groups_kernel(int Wg, int K, uint8_t* __restrict__ out, uint32_t gen) {
+  write_group(nullptr, 0, 0, NO_KEY, K, blockIdx.x, out, gen);
+}
+
+hipError_t launch_empty_groups(hipStream_t s, int Wg, int K, uint8_t* out, uint32_t gen) {
+  if (Wg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(empty_groups_kernel, dim3(Wg), dim3(64), 0, s, Wg, K, out, gen);
   return hipGetLastError();
 }
 

@@ -338,6 +338,10 @@ static void parse_group_keys(const uint8_t* base, GroupCands& gc) {
   uint64_t limit;
   std::memcpy(&n, base, 4);
   std::memcpy(&limit, base + 8, 8);
+  if (n < 0)   // (the zero-copy exchange wait timed out on a peer's list: pe_kernels.h launch_xwait)
+    throw ExchangeError("host exchange: a rank's candidate lists never arrived (peer stalled or failed; rank " +
+                        std::to_string((limit >> 32) & 0x7fffffffu) + "'s slot still held generation " +
+                        std::to_string((uint32_t)limit) + ")");
   gc.keyed = true;
   gc.data = nullptr;
   gc.merged.clear();

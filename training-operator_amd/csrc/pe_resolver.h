@@ -19,6 +19,7 @@
 #include <mutex>
 #include <memory>
 #include <new>
+#include <stdexcept>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -126,6 +127,11 @@ void parse_window_keys(const uint8_t* blob, int n_shards, int n_groups, int K, s
 // arrive, so resolving starts when the first group is done instead of when the slowest one is.
 // Only the resolver thread parses (fills cands[w], then publishes parsed() with release); the
 // seed helper reads groups below parsed() only.
+// A rank's lists never arrived in a zero-copy exchange window (the engine reports PE_ERCCL)
+struct ExchangeError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
 class WindowFeed {
  public:
   void reset(const uint8_t* blob, int n_groups, int K, uint32_t gen, std::vector<GroupCands>* cands);

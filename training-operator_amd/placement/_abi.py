@@ -46,7 +46,8 @@ class PeStats(ctypes.Structure):
                 ("fit_runs_therm", ctypes.c_int64), ("fit_runs_planes", ctypes.c_int64), ("resorts", ctypes.c_int64),
                 ("fit_runs_lds", ctypes.c_int64), ("fit_runs_sets", ctypes.c_int64), ("walk_rounds", ctypes.c_int64),
                 ("walk_overlay", ctypes.c_int64), ("walk_groups", ctypes.c_int64), ("walk_prepass", ctypes.c_int64),
-                ("walk_ms", ctypes.c_double), ("walk_pend_updates", ctypes.c_int64)]
+                ("walk_ms", ctypes.c_double), ("walk_pend_updates", ctypes.c_int64),
+                ("xchg_zc_windows", ctypes.c_int64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
