@@ -36,7 +36,8 @@ def _spawn(tmp_path, world, mix, n_nodes, n_jobs, transport, env):
 
 def _env(**kv):
     env = dict(os.environ)
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PE_HOST_MERGE", "PE_NO_ZC_EXCHANGE", "PE_HX_GPU_TIMEOUT_S", "PE_MERGE_RANKED"):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PE_HOST_MERGE", "PE_NO_ZC_EXCHANGE", "PE_HX_GPU_TIMEOUT_S", "PE_MERGE_RANKED",
+              "PE_ZC_DEV_MERGE", "PE_HX_TIMEOUT_S"):
         env.pop(k, None)
     env.update(kv)
     return env
@@ -50,20 +51,25 @@ def _env(**kv):
                                                                            (2, "mixed", 20000, 600, False, "shm-copy"),
                                                                            (3, "mixed", 2, 40, False, "shm"),
                                                                            (2, "mixed", 20000, 600, False, "shm-ranked"),
+                                                                           (2, "mixed", 20000, 600, False, "shm-devmerge"),
+                                                                           (3, "gang8", 9000, 300, False, "shm-devmerge"),
                                                                            (3, "island8", 9000, 300, False, "gloo-ranked"),
                                                                            (2, "gang8", 6000, 300, True, "shm")])
 def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, host_merge, transport):
     """host_merge False: the gathered shard lists are merged on the device (merge_shards, the
     default); True: PE_HOST_MERGE=1, the host's lazy k-way merge.  transport: the Python gloo
     callback, or the native shared-memory exchange (pe_host_exchange) -- "shm": its zero-copy
-    windows (walk into the registered segment, the merge waits on the device), "shm-copy": the
-    copying all-gather (PE_NO_ZC_EXCHANGE=1); "-ranked": the rank merge kernel (PE_MERGE_RANKED=1).  Either way the windows are pipelined.  (3 ranks over
+    windows (walk into the registered segment, the exchange thread merges each group on the host as
+    every rank signalled it), "shm-devmerge": zero-copy with the device wait + merge kernel
+    (PE_ZC_DEV_MERGE=1), "shm-copy": the copying all-gather (PE_NO_ZC_EXCHANGE=1); "-ranked": the
+    rank merge kernel (PE_MERGE_RANKED=1).  Either way the windows are pipelined.  (3 ranks over
     2 nodes: one rank's shard is empty -- its windows are empty lists, signalled.)"""
-    env = _env(**({"PE_HOST_MERGE": "1"} if host_merge else {}), **({"PE_NO_ZC_EXCHANGE": "1"} if transport == "shm-copy" else {}),
-               **({"PE_MERGE_RANKED": "1"} if transport.endswith("-ranked") else {}))
-    transport = transport.split("-")[0] if transport != "shm-copy" else "shm-copy"
-    zc_expected = transport == "shm" and not host_merge
-    transport = "shm" if transport == "shm-copy" else transport
+    base, _, variant = transport.partition("-")
+    extra = {"copy": {"PE_NO_ZC_EXCHANGE": "1"}, "ranked": {"PE_MERGE_RANKED": "1"},
+             "devmerge": {"PE_ZC_DEV_MERGE": "1"}, "": {}}[variant]
+    env = _env(**({"PE_HOST_MERGE": "1"} if host_merge else {}), **extra)
+    zc_expected = base == "shm" and variant != "copy" and not host_merge
+    transport = base
     procs = _spawn(tmp_path, world, mix, n_nodes, n_jobs, transport, env)
     outs = []
     try:
@@ -103,10 +109,13 @@ def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, 
     assert 0 < (w_st == 0).sum() <= n_jobs
 
 
-def test_zero_copy_exchange_peer_stall_fails_fast(tmp_path):
-    """A rank that stops taking part (it sleeps, then exits) must not hang its peers: their shard
-    merges give up after PE_HX_GPU_TIMEOUT_S on the device and the greedy call fails with PE_ERCCL."""
-    procs = _spawn(tmp_path, 2, "mixed", 20000, 600, "shm-stall", _env(PE_HX_GPU_TIMEOUT_S="3"))
+@pytest.mark.parametrize("dev_merge", [False, True])
+def test_zero_copy_exchange_peer_stall_fails_fast(tmp_path, dev_merge):
+    """A rank that stops taking part (it sleeps, then exits) must not hang its peers: the exchange
+    thread's wait for its lists gives up after PE_HX_TIMEOUT_S (PE_ZC_DEV_MERGE=1: the device wait
+    after PE_HX_GPU_TIMEOUT_S) and the greedy call fails with PE_ERCCL."""
+    env = _env(PE_HX_GPU_TIMEOUT_S="3", PE_HX_TIMEOUT_S="3", **({"PE_ZC_DEV_MERGE": "1"} if dev_merge else {}))
+    procs = _spawn(tmp_path, 2, "mixed", 20000, 600, "shm-stall", env)
     outs = []
     try:
         for p in procs:

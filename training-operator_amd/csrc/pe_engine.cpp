@@ -155,6 +155,128 @@ class SpinWorker {
   std::thread th_;   // last: starts after the members above exist
 };
 
+// A SpinWorker with a queue: post() does not wait for the previous task (up to kCap in flight), the
+// tasks run in order on the thread, wait() waits for all of them.  After a task threw, the rest are
+// skipped and wait() rethrows.  (The host-merged zero-copy exchange: the main thread posts each
+// window's merge as it launches the window, without waiting for the previous merge to finish.)
+class SpinQueue {
+ public:
+  static constexpr unsigned kCap = 8;
+  explicit SpinQueue(int device) : th_([this, device] {
+    (void)hipSetDevice(device);
+    loop();
+  }) {}
+  ~SpinQueue() {
+    while (busy()) _mm_pause();
+    stop_.store(true, std::memory_order_release);
+    th_.join();
+  }
+  void pin(const cpu_set_t& set) { (void)pthread_setaffinity_np(th_.native_handle(), sizeof(set), &set); }
+  void post(std::function<void()> f) {
+    const unsigned t = tail_.load(std::memory_order_relaxed);
+    while (t - head_.load(std::memory_order_acquire) >= kCap) _mm_pause();   // full: the oldest first
+    q_[t % kCap] = std::move(f);
+    tail_.store(t + 1, std::memory_order_release);
+  }
+  bool busy() const { return head_.load(std::memory_order_acquire) != tail_.load(std::memory_order_acquire); }
+  bool failed() const { return failed_.load(std::memory_order_acquire); }
+  void wait() {   // every posted task done; rethrows the first error (once)
+    for (int spin = 0; busy(); ++spin)
+      if (spin < 4096) _mm_pause();
+      else std::this_thread::yield();
+    if (failed_.load(std::memory_order_acquire)) {
+      failed_.store(false, std::memory_order_relaxed);
+      std::exception_ptr e = err_;
+      err_ = nullptr;
+      if (e) std::rethrow_exception(e);
+    }
+  }
+
+ private:
+  void loop() {
+    int idle = 0;
+    for (;;) {
+      const unsigned h = head_.load(std::memory_order_relaxed);
+      if (h == tail_.load(std::memory_order_acquire)) {
+        if (stop_.load(std::memory_order_acquire)) return;
+        if (++idle < 4096) _mm_pause();
+        else std::this_thread::yield();
+        continue;
+      }
+      idle = 0;
+      if (!failed_.load(std::memory_order_relaxed)) {
+        try {
+          q_[h % kCap]();
+        } catch (...) {
+          err_ = std::current_exception();
+          failed_.store(true, std::memory_order_release);
+        }
+      }
+      q_[h % kCap] = nullptr;
+      head_.store(h + 1, std::memory_order_release);
+    }
+  }
+  std::function<void()> q_[kCap];
+  std::atomic<unsigned> head_{0}, tail_{0};
+  std::atomic<bool> failed_{false}, stop_{false};
+  std::exception_ptr err_;
+  std::thread th_;   // last: starts after the members above exist
+};
+
+// Two ascending u64 lists (unique keys) merged: the first `want` keys of their union into out (which
+// holds want rounded up to 8, + 8).  AVX-512 bitonic merge, 8 keys per step (the host-merged
+// zero-copy exchange's two-shard case; the scalar merge is a chain of dependent loads and compares,
+// ~7 cycles per key).
+#define PE_AVX512 __attribute__((target("avx512f")))
+PE_AVX512 static inline __m512i bitonic8(__m512i v) {   // a bitonic 8-vector, sorted ascending
+  const __m512i p4 = _mm512_set_epi64(3, 2, 1, 0, 7, 6, 5, 4), p2 = _mm512_set_epi64(5, 4, 7, 6, 1, 0, 3, 2),
+                p1 = _mm512_set_epi64(6, 7, 4, 5, 2, 3, 0, 1);
+  __m512i q = _mm512_permutexvar_epi64(p4, v);
+  v = _mm512_mask_blend_epi64(0xF0, _mm512_min_epu64(v, q), _mm512_max_epu64(v, q));
+  q = _mm512_permutexvar_epi64(p2, v);
+  v = _mm512_mask_blend_epi64(0xCC, _mm512_min_epu64(v, q), _mm512_max_epu64(v, q));
+  q = _mm512_permutexvar_epi64(p1, v);
+  return _mm512_mask_blend_epi64(0xAA, _mm512_min_epu64(v, q), _mm512_max_epu64(v, q));
+}
+PE_AVX512 static inline void merge16(__m512i& lo, __m512i& hi, __m512i a, __m512i b) {   // a, b sorted
+  const __m512i rev = _mm512_set_epi64(0, 1, 2, 3, 4, 5, 6, 7);
+  const __m512i rb = _mm512_permutexvar_epi64(rev, b);
+  lo = bitonic8(_mm512_min_epu64(a, rb));
+  hi = bitonic8(_mm512_max_epu64(a, rb));
+}
+PE_AVX512 static inline __m512i load8pad(const uint64_t* p, int i, int n) {   // p[i .. i+8), ~0 past n
+  const int k = std::max(0, std::min(8, n - i));
+  return _mm512_mask_loadu_epi64(_mm512_set1_epi64(-1), (__mmask8)((1u << k) - 1u), p + i);
+}
+PE_AVX512 static int merge2_avx512(const uint64_t* a, int na, const uint64_t* b, int nb, int want, uint64_t* out) {
+  __m512i lo, hi;
+  merge16(lo, hi, load8pad(a, 0, na), load8pad(b, 0, nb));
+  int ia = 8, ib = 8, m = 0;
+  _mm512_storeu_si512(out, lo);
+  m = 8;
+  while (m < want) {
+    const uint64_t xa = ia < na ? a[ia] : ~0ull, xb = ib < nb ? b[ib] : ~0ull;
+    __m512i nx;
+    if (xa == ~0ull && xb == ~0ull) {
+      _mm512_storeu_si512(out + m, hi);
+      m += 8;
+      break;
+    }
+    if (xa < xb) {
+      nx = load8pad(a, ia, na);
+      ia += 8;
+    } else {
+      nx = load8pad(b, ib, nb);
+      ib += 8;
+    }
+    merge16(lo, hi, hi, nx);
+    _mm512_storeu_si512(out + m, lo);
+    m += 8;
+  }
+  return std::min(m, want);
+}
+static const bool kHaveAvx512 = __builtin_cpu_supports("avx512f");
+
 struct PeError {
   int code;
   std::string msg;
@@ -2285,12 +2407,13 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     struct DumpClose { FILE*& f; ~DumpClose() { if (f) std::fclose(f); } } dump_close{dump};
     // PE_GREEDY_TRACE=1: per-window wait / resolve / post times, summarised on stderr (diagnostics)
     const bool trace = std::getenv("PE_GREEDY_TRACE") != nullptr;
-    std::vector<double> tr_wait, tr_res, tr_post;
+    std::vector<double> tr_wait, tr_res, tr_post, tr_xspin, tr_xmerge, tr_xblock;
     int helper_cpu = -1;
     struct TraceOut {
       int& helper_cpu;
       const bool& on;
       std::vector<double>& a; std::vector<double>& b; std::vector<double>& c;
+      std::vector<double>& d; std::vector<double>& e; std::vector<double>& f;
       ~TraceOut() {
         if (!on || a.empty()) return;
         auto pr = [](const char* n, std::vector<double>& v) {
@@ -2304,6 +2427,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         pr("wait   ", a);
         pr("resolve", b);
         pr("post   ", c);
+        pr("xspin  ", d);   // exchange thread: waiting for the ranks' signals, per window
+        pr("xmerge ", e);   // exchange thread: merging, per window
+        pr("xblock ", f);   // main thread: waiting for the exchange thread before posting
         auto sib = [](int cpu) {
           char path[128], buf[64] = {0};
           std::snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", cpu);
@@ -2319,7 +2445,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         std::fprintf(stderr, "cpus: main %d (siblings %s) helper %d (siblings %s)\n", mc, sib(mc).c_str(), helper_cpu,
                      helper_cpu >= 0 ? sib(helper_cpu).c_str() : "-");
       }
-    } trace_out{helper_cpu, trace, tr_wait, tr_res, tr_post};
+    } trace_out{helper_cpu, trace, tr_wait, tr_res, tr_post, tr_xspin, tr_xmerge, tr_xblock};
     int64_t dump_left = std::getenv("PE_DUMP_MAX_WINDOWS") ? std::atoll(std::getenv("PE_DUMP_MAX_WINDOWS")) : INT64_MAX;
     const int K = ctx->topk;
     const size_t gb = pe::cand_group_bytes(K);
@@ -2443,7 +2569,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     pe::WindowFeed feed;
     struct StreamIdle {
       hipStream_t s;
-      const SpinWorker* x = nullptr;   // the exchange thread (split exchange): a merge it has not launched yet
+      const SpinQueue* x = nullptr;   // the exchange thread (split exchange): a merge it has not launched yet
       // a faulted walk / merge kernel surfaces as its own HIP error (PE_EHIP with the HIP string),
       // and a failed exchange as its own error, not as the feed's "never signalled"
       static bool stream_busy(hipStream_t s) {
@@ -2454,7 +2580,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       static bool busy(void* u) {
         auto* t = static_cast<StreamIdle*>(u);
-        if (t->x && t->x->failed()) const_cast<SpinWorker*>(t->x)->wait();   // rethrows the exchange's error
+        if (t->x && t->x->failed()) const_cast<SpinQueue*>(t->x)->wait();   // rethrows the exchange's error
         return (t->x && t->x->busy()) || stream_busy(t->s);
       }
     } stream_idle{s};
@@ -2490,15 +2616,22 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       const double t = e ? std::atof(e) : 60.0;
       return (int64_t)((t > 0 ? t : 60.0) * 1e8);   // wall_clock64: 100 MHz
     }();
-    const bool split_x = use_exchange && pipelined && signalled && walk && !zc && !std::getenv("PE_NO_SPLIT_EXCHANGE");
-    std::unique_ptr<SpinWorker> xworker;
+    // Merging a zero-copy window: by default on the host, by the exchange thread, group by group as
+    // every rank's walk signals it into the segment (zc_host: no kernel, no PCIe read-back, the
+    // resolver streams the merged groups as in an unsharded window); PE_ZC_DEV_MERGE=1 (A/B): a
+    // one-block device wait and the merge kernel behind the walk (zc_dev).
+    const bool zc_dev = zc && std::getenv("PE_ZC_DEV_MERGE");
+    const bool zc_host = zc && !zc_dev;
+    const bool split_x =
+        use_exchange && pipelined && signalled && walk && !zc_dev && !std::getenv("PE_NO_SPLIT_EXCHANGE");
+    std::unique_ptr<SpinQueue> xworker;
     if (split_x) {
-      xworker.reset(new SpinWorker(ctx->device));
+      xworker.reset(new SpinQueue(ctx->device));
       if (pin.on) xworker->pin(pin.l3);
       stream_idle.x = xworker.get();
     }
     struct XWait {   // every exit: the exchange thread's task is over before the buffers it uses go
-      std::unique_ptr<SpinWorker>& w;
+      std::unique_ptr<SpinQueue>& w;
       ~XWait() {
         if (w) try {
             w->wait();
@@ -2512,6 +2645,89 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // The rule is merge_shards_kernel's: the keys below the smallest shard limit, the K + 1 smallest
     // of them; limit = the (K+1)-th, else that minimum.
     const bool xhost_merge = use_exchange && dev_merge && std::getenv("PE_XCHG_HOST_MERGE");
+    // merge_shards_kernel's rule on the host: the keys below the smallest shard limit, the K + 1
+    // smallest of them (two shards: a branch-free two-way merge); group w of shard r at
+    // gath + r * stride + w * gb
+    auto host_merge_zc = [&](const uint8_t* gath, size_t stride, int w, uint8_t* out, uint32_t gen) {
+      const int W = ctx->world;
+      uint8_t* og = out + (size_t)w * gb;
+      uint64_t* dst = reinterpret_cast<uint64_t*>(og + sizeof(pe::CandHdr));
+      uint64_t L = pe::NO_KEY;
+      const uint64_t* lists[pe::RM_MAX_WORLD];
+      int ns[pe::RM_MAX_WORLD];
+      for (int r = 0; r < W; ++r) {
+        const uint8_t* g = gath + (size_t)r * stride + (size_t)w * gb;
+        pe::CandHdr h;
+        std::memcpy(&h, g, sizeof(h));
+        L = std::min(L, h.limit);
+        lists[r] = reinterpret_cast<const uint64_t*>(g + sizeof(h));
+        ns[r] = std::max(0, std::min(h.n, K));
+      }
+      for (int r = 0; r < W; ++r)   // keys below L only (ascending lists: cut each at L)
+        ns[r] = (int)(std::lower_bound(lists[r], lists[r] + ns[r], L) - lists[r]);
+      int m = 0;
+      uint64_t lim = L;
+      if (W >= 2 && kHaveAvx512) {   // pairwise: the K + 1 smallest of shards 0..r, merged with shard r + 1
+        alignas(64) uint64_t tmp[2][pe::MG_CAP + 16];
+        const uint64_t* acc = lists[0];
+        int na = std::min(ns[0], K + 1);
+        for (int r = 1; r < W; ++r) {
+          const int want = std::min(K + 1, na + ns[r]);
+          uint64_t* o = tmp[r & 1];
+          na = want > 0 ? merge2_avx512(acc, na, lists[r], ns[r], want, o) : 0;
+          acc = o;
+        }
+        m = na;
+        std::memcpy(dst, acc, (size_t)std::min(m, K) * 8);
+        if (m > K) lim = acc[K];
+      } else if (W == 2) {
+        const uint64_t *a = lists[0], *b = lists[1];
+        const int na = ns[0], nb = ns[1];
+        int i = 0, j = 0;
+        const int want = std::min(K + 1, na + nb);
+        while (m < want && i < na && j < nb) {
+          const uint64_t x = a[i], y = b[j];
+          const bool t = x < y;
+          const uint64_t v = t ? x : y;
+          if (m < K) dst[m] = v;
+          else lim = v;   // (the (K+1)-th key is the merged list's limit)
+          ++m;
+          i += t;
+          j += !t;
+        }
+        for (; m < want && i < na; ++m, ++i) {
+          if (m < K) dst[m] = a[i];
+          else lim = a[i];
+        }
+        for (; m < want && j < nb; ++m, ++j) {
+          if (m < K) dst[m] = b[j];
+          else lim = b[j];
+        }
+      } else {
+        int hd[pe::RM_MAX_WORLD] = {0};
+        for (;;) {
+          int br = -1;
+          uint64_t bk = pe::NO_KEY;
+          for (int r = 0; r < W; ++r)
+            if (hd[r] < ns[r] && lists[r][hd[r]] < bk) {
+              bk = lists[r][hd[r]];
+              br = r;
+            }
+          if (br < 0) break;
+          ++hd[br];
+          if (m == K) {
+            lim = bk;
+            ++m;
+            break;
+          }
+          dst[m++] = bk;
+        }
+      }
+      pe::CandHdr* hp = reinterpret_cast<pe::CandHdr*>(og);
+      hp->n = std::min(m, K);
+      hp->limit = m > K ? lim : L;
+      __atomic_store_n(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE);   // the group's signal, last
+    };
     auto host_merge_group = [&](const uint8_t* gath, int Wg, int w, uint8_t* out, uint32_t gen) {
       const int W = ctx->world;
       std::vector<const uint64_t*>& lists = ctx->x_lists;
@@ -2554,8 +2770,53 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       hp->limit = lim;
       __atomic_store_n(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE);   // the group's signal, last
     };
-    auto exchange_window = [&](int b, int Wg, uint32_t gen, bool own_direct, const SpinWorker* launcher) {
+    auto exchange_window = [&](int b, int Wg, uint32_t gen, bool own_direct, const SpinWorker* launcher,
+                               const pe::HxWindow* hw = nullptr) {
       const size_t bytes = (size_t)Wg * gb;
+      if (zc_host) {   // every rank's lists are in the segment: merge each group as all ranks signalled it
+        const double tmo = pe::hx_timeout_s();
+        const auto t0 = std::chrono::steady_clock::now();
+        double spun = 0, merged = 0;
+        for (int w = 0; w < Wg; ++w) {
+          const auto ts = trace ? std::chrono::steady_clock::now() : t0;
+          for (int r = 0; r < ctx->world; ++r) {
+            const pe::CandHdr* h = reinterpret_cast<const pe::CandHdr*>(hw->host + (size_t)r * hw->slot + (size_t)w * gb);
+            for (unsigned spin = 1; __atomic_load_n(&h->flags, __ATOMIC_ACQUIRE) != (int32_t)hw->gen; ++spin) {
+              _mm_pause();
+              if ((spin & 4095) == 0) {
+                const hipError_t e = hipStreamQuery(s);   // a faulted walk of this rank: its own error
+                if (e != hipErrorNotReady) hipchk(e, "walk window stream");
+                if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > tmo)
+                  throw pe::ExchangeError("host exchange: rank " + std::to_string(r) +
+                                          "'s candidate lists never arrived (peer stalled or failed; PE_HX_TIMEOUT_S)");
+              }
+            }
+          }
+          const auto tm = trace ? std::chrono::steady_clock::now() : t0;
+          // the next groups' lists on their way from DRAM (the device wrote them past the CPU caches;
+          // a line fetched before the device's write is snooped out again, harmless) and the output
+          // lines owned for writing: the merge is otherwise a chain of cache misses
+          for (int a = 1; a <= 2 && w + a < Wg; ++a) {
+            for (int r = 0; r < ctx->world; ++r) {
+              const uint8_t* gl = hw->host + (size_t)r * hw->slot + (size_t)(w + a) * gb;
+              for (size_t o = 0; o < gb; o += 64) __builtin_prefetch(gl + o, 0, 3);
+            }
+            uint8_t* ol = outbuf(b) + (size_t)(w + a) * gb;
+            for (size_t o = 0; o < gb; o += 64) __builtin_prefetch(ol + o, 1, 3);
+          }
+          host_merge_zc(hw->host, hw->slot, w, outbuf(b), gen);
+          if (trace) {
+            spun += std::chrono::duration<double, std::micro>(tm - ts).count();
+            merged += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tm).count();
+          }
+        }
+        if (trace) {
+          tr_xspin.push_back(spun);
+          tr_xmerge.push_back(merged);
+        }
+        pe::hx_zc_consumed(hx, *hw);
+        return;
+      }
       if (own_direct && ctx->Ns > 0) {   // every own group signalled: the lists are in h_own
         struct Idle {   // busy while the launcher has not launched the walk yet, or the stream runs
           const SpinWorker* l;
@@ -2586,7 +2847,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     };
     // gen_in: the window's generation assigned by the caller (split exchange: the exchange thread
     // must know it before the launch); defer_x: leave the exchange to the exchange thread
-    auto enqueue_window = [&](const std::vector<int32_t>& groups, int b, uint32_t gen_in = 0, bool defer_x = false) {
+    auto enqueue_window = [&](const std::vector<int32_t>& groups, int b, uint32_t gen_in = 0, bool defer_x = false,
+                              const pe::HxWindow* hw_in = nullptr) {
       const int Wg = (int)groups.size();
       const int Wgp = (int)round_up(Wg, pe::SC_GT);
       auto& hg = hgroups(b);
@@ -2598,7 +2860,11 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       // a pipelined host exchange's walk (its own lists, signalled per group: no D2H, no stream sync)
       const bool own_direct = walk && use_exchange && pipelined && !zc;
       pe::HxWindow hw;   // zero-copy: this window's slots and their generation (every rank, every window)
-      if (zc) hw = pe::hx_zc_next(hx);
+      if (zc) {
+        hw = hw_in ? *hw_in : pe::hx_zc_next(hx);
+        if (zc_host && !pe::hx_zc_wait_reuse(hx, hw))   // (every rank read the window that used the slots)
+          throw pe::ExchangeError("host exchange: a rank never finished reading a window (peer stalled or failed)");
+      }
       uint8_t* const dst = zc           ? hw.dev + (size_t)ctx->rank * hw.slot
                            : direct_out ? outbufdev(b)
                            : own_direct ? ctx->h_own.dev
@@ -2660,6 +2926,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       const size_t bytes = (size_t)Wg * gb;
       if (direct_out) {
         // written in place
+      } else if (zc_host) {   // the exchange thread (or, not deferred, this thread) merges on the host
+        ctx->stats.xchg_zc_windows += 1;
+        if (!defer_x) exchange_window(b, Wg, gen, false, nullptr, &hw);
       } else if (zc) {   // merged once every rank's walk signalled every group (pe_hostx.h)
         ctx->stats.xchg_zc_windows += 1;
         hipchk(pe::launch_xwait(s, hw.dev, ctx->world, Wg, K, (int64_t)hw.slot, hw.gen, zc_ticks, ctx->g_xstatus.p),
@@ -2845,27 +3114,34 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (split_x) {
         // generations assigned here, in launch order: the exchange thread waits for these windows' own
         // lists (signalled with them) while the launch helper launches the walks
+        // (zero-copy: the windows' slots too, taken in the same order on every rank)
         struct XWin {
           int buf, wg;
           uint32_t gen;
+          pe::HxWindow hw;
         };
         std::vector<XWin> xs;
-        std::vector<std::pair<Flight*, uint32_t>> ws;
+        std::vector<std::pair<Flight*, XWin>> ws;
         for (Flight* f : to_scan) {
           if (++ctx->walk_gen == 0) ++ctx->walk_gen;
-          xs.push_back(XWin{f->buf, (int)f->groups.size(), ctx->walk_gen});
-          ws.emplace_back(f, ctx->walk_gen);
+          xs.push_back(XWin{f->buf, (int)f->groups.size(), ctx->walk_gen, zc_host ? pe::hx_zc_next(hx) : pe::HxWindow{}});
+          ws.emplace_back(f, xs.back());
         }
-        xworker->wait();   // (the previous window's exchange: over once its merged groups were seen)
+        const auto txb = std::chrono::steady_clock::now();
+        // (the copying exchange: the previous window's exchange is over before the next one, its
+        // buffers are shared; host-merged zero-copy windows queue up -- slot reuse is counted)
+        if (!zc_host) xworker->wait();
+        if (trace) tr_xblock.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - txb).count());
         worker->post([&, to_apply, ws] {
           const auto tp = std::chrono::steady_clock::now();
           if (trace) helper_cpu = sched_getcpu();
           for (const auto& a : to_apply) enqueue_apply(*a.first, a.second);
-          for (const auto& w : ws) enqueue_window(w.first->groups, w.first->buf, w.second, true);
+          for (const auto& w : ws)
+            enqueue_window(w.first->groups, w.first->buf, w.second.gen, true, zc_host ? &w.second.hw : nullptr);
           if (trace) tr_post.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
         });
         xworker->post([&, xs] {
-          for (const XWin& x : xs) exchange_window(x.buf, x.wg, x.gen, true, worker.get());
+          for (const XWin& x : xs) exchange_window(x.buf, x.wg, x.gen, true, worker.get(), zc_host ? &x.hw : nullptr);
         });
       } else {
         worker->post([&, to_apply, to_scan] {

@@ -33,6 +33,7 @@ namespace {
 
 constexpr uint64_t kMagic = 0x70655f6878303031ull;   // "pe_hx001"
 constexpr size_t kHdr = 4096;
+constexpr int kZcMaxWorld = 32;
 
 struct Hdr {
   std::atomic<uint64_t> magic;
@@ -41,6 +42,8 @@ struct Hdr {
   uint64_t slot_bytes;
   std::atomic<int32_t> attached;
   alignas(64) std::atomic<uint64_t> ctr[2][8];   // ctr[p][0]; the rest pads to separate cache lines
+  // zero-copy windows: consumed[r][0] = windows rank r has read every slot of (pe_hostx.h)
+  alignas(64) std::atomic<uint64_t> consumed[kZcMaxWorld][8];
 };
 static_assert(sizeof(Hdr) <= kHdr, "header");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics must be lock-free");
@@ -108,6 +111,7 @@ int pe_host_exchange_open(const char* name, int32_t rank, int32_t world, size_t 
     h->slot_bytes = slot;
     new (&h->attached) std::atomic<int32_t>(0);
     for (auto& c : h->ctr) new (&c[0]) std::atomic<uint64_t>(0);
+    for (auto& c : h->consumed) new (&c[0]) std::atomic<uint64_t>(0);
     h->magic.store(kMagic, std::memory_order_release);
   } else {
     while (h->magic.load(std::memory_order_acquire) != kMagic) {
@@ -182,7 +186,7 @@ namespace pe {
 bool hx_is(pe_allgather_fn fn) { return fn == &pe_host_exchange_allgather; }
 
 bool hx_zc_register(pe_host_exchange* x) {
-  if (!x) return false;
+  if (!x || x->world > kZcMaxWorld) return false;
   if (x->zc_reg == 0) {
     void* dev = nullptr;
     x->zc_reg = -1;
@@ -206,9 +210,35 @@ HxWindow hx_zc_next(pe_host_exchange* x) {
   const size_t slot = x->h->slot_bytes;
   const uint64_t k = x->zc_windows++;
   w.dev = x->zc_dev + (2 + (size_t)(k & 1)) * x->world * slot;
+  w.host = x->data + (2 + (size_t)(k & 1)) * x->world * slot;
+  w.index = k;
   w.slot = slot;
   w.gen = (uint32_t)(k % 0xFFFFFFFFull) + 1;   // (slot headers start zeroed: generation 0 is never current)
   return w;
 }
+
+}  // namespace pe
+
+namespace pe {
+
+bool hx_zc_wait_reuse(pe_host_exchange* x, const HxWindow& w) {
+  if (w.index < 2) return true;
+  const uint64_t need = w.index - 1;   // windows 0 .. index - 2 read by every rank
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int r = 0; r < x->world; ++r)
+    for (unsigned spin = 0; x->h->consumed[r][0].load(std::memory_order_acquire) < need; ++spin) {
+      _mm_pause();
+      if ((spin & 4095) == 4095 &&
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s())
+        return false;
+    }
+  return true;
+}
+
+void hx_zc_consumed(pe_host_exchange* x, const HxWindow& w) {
+  x->h->consumed[x->rank][0].store(w.index + 1, std::memory_order_release);
+}
+
+double hx_timeout_s() { return timeout_s(); }
 
 }  // namespace pe
