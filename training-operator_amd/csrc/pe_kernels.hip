@@ -1358,7 +1358,34 @@ __device__ void hist_cut(TopkShared& s, int need) {
 // writes it to s.keys[rank] if rank <= K.  The count loop reads 16 keys per step (every lane the same
 // address: LDS broadcast) before comparing, so 16 reads are in flight instead of one read latency per
 // key (the one-at-a-time loop was ~11 us of the walk's ~30 us per group at C ~ 300).
+// P threads per key when C x P fits the block (P = 2..16, lanes of one wave): each counts a 1/P slice
+// of the keys, the slices' counts are summed by lane shuffles -- the count loop is P times shorter
+// (C ~ 240 -> 4 threads per key).  PE_RANK_ONE=1 at build time: one thread per key (A/B).
 __device__ __forceinline__ void rank_place(TopkShared& s, int C, int K) {
+#ifndef PE_RANK_ONE
+  int P = 1;   // (block-uniform)
+  while (P < 16 && C * (P * 2) <= MG_THREADS) P *= 2;
+  if (P > 1) {
+    const int t = threadIdx.x / P, part = threadIdx.x & (P - 1);
+    const bool live = t < C;
+    const uint64_t k = live ? s.sel[t] : 0;
+    const int j0 = (int)((int64_t)C * part / P), j1 = (int)((int64_t)C * (part + 1) / P);
+    int rank = 0, j = j0;
+    if (live) {
+      for (; j + 8 <= j1; j += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = s.sel[j + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) rank += v[u] < k;
+      }
+      for (; j < j1; ++j) rank += s.sel[j] < k;
+    }
+    for (int off = P >> 1; off >= 1; off >>= 1) rank += __shfl_xor(rank, off, 64);
+    if (live && part == 0 && rank <= K) s.keys[rank] = k;
+    return;
+  }
+#endif
   for (int t = threadIdx.x; t < C; t += MG_THREADS) {
     const uint64_t k = s.sel[t];
     int rank = 0, j = 0;
@@ -2110,7 +2137,9 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
     for (int u = 0; u < WK_MULTI; ++u)
       if (u < nstep) topk_append(s, k[u], k[u] != NO_KEY);
     __syncthreads();
-    if (s.total > MG_CAP - WK_MULTI * WK_ROUND) {   // room for the next step's appends
+    // (room for the next step's appends.  Cutting long walks' keys to K + 1 early, at 1024 or 2048,
+    // with later appends filtered below the (K+1)-th, was measured slower: 62-64 vs 52 us per launch)
+    if (s.total > MG_CAP - WK_MULTI * WK_ROUND) {
       const int T2 = s.total;
       const uint64_t* sk = topk_sort(s, T2, K);
       const int m = T2 < K + 1 ? T2 : K + 1;
