@@ -2088,10 +2088,17 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   if (!done) r = next_round(r);
   uint64_t xstop = NO_KEY;
   int tests = 0;
+  // the next step's first round and its smallest key are found during the current step (the load
+  // in flight with the step's node loads): the stop test does not wait for its own load
+  uint64_t rm_r = !done && r < nr ? w.rmin[r] : 0;
   while (!done && r < nr) {
     const int T = s.total;
     if (T >= K + 1) {                      // stop once K + 1 keys lie below every unvisited key
+#ifdef PE_WALK_NO_RM_PREFETCH   // (A/B)
       const uint64_t rm = w.rmin[r];
+#else
+      const uint64_t rm = rm_r;
+#endif
       const uint64_t X = rm > KQ2 ? rm - KQ2 : 0;
       int c = 0;
       for (int i = tid; i < T; i += WK_ROUND) c += s.keys[i] < X;
@@ -2121,16 +2128,27 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
         if (nx >= nr) break;
         rr[nstep] = nx;
       }
+    const int64_t r_next = next_round(rr[nstep - 1] + 1);
+    const uint64_t rm_next = r_next < nr ? w.rmin[r_next] : 0;
     uint64_t k[WK_MULTI];
 #pragma unroll
     for (int u = 0; u < WK_MULTI; ++u) {
       k[u] = NO_KEY;
       const int64_t i = rr[u < nstep ? u : 0] * WK_ROUND + tid;
       if (u < nstep && i < Ns) {
+#ifdef PE_WALK_COND_LOAD   // (A/B: the state loads behind the sorted key's validity test)
         const uint64_t Kn = w.sk[i];
         if (Kn != WK_INVALID)
           k[u] = node_key(w.sr[i], w.sr[w.sstride + i], w.sr[2 * w.sstride + i], w.sr[3 * w.sstride + i], w.sl[i], q0,
                           q1, q2, q3, need, Kn & 0xFFFFFFull);
+#else   // all six loads in flight at once (one memory latency per step, not two); an invalid
+        // entry's state is read and dropped
+        const uint64_t Kn = w.sk[i];
+        const int64_t s0 = w.sr[i], s1 = w.sr[w.sstride + i], s2 = w.sr[2 * w.sstride + i], s3 = w.sr[3 * w.sstride + i];
+        const uint32_t sl = w.sl[i];
+        const uint64_t kk = node_key(s0, s1, s2, s3, sl, q0, q1, q2, q3, need, Kn & 0xFFFFFFull);
+        k[u] = Kn != WK_INVALID ? kk : NO_KEY;
+#endif
       }
     }
 #pragma unroll
@@ -2149,7 +2167,8 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
       if (tid == 0) s.total = m;
       __syncthreads();
     }
-    r = next_round(rr[nstep - 1] + 1);
+    r = r_next;
+    rm_r = rm_next;
     rounds += nstep;
   }
   WPT(3);
