@@ -114,7 +114,9 @@ type HostExchange struct {
 }
 
 // OpenHostExchange opens (rank 0: creates) the segment; maxBytes bounds one rank's block per call
-// (WindowGroups x (16 + 8 x TopK) for the greedy windows).
+// (WindowGroups x (16 + 8 x TopK) for the greedy windows).  Passed as Config.HostExchange, the
+// library recognises its own exchange and runs the greedy windows zero-copy: each rank's walk writes
+// into the segment and an exchange thread merges every group on the host (Stats.xchg_zc_windows).
 func OpenHostExchange(name string, rank, world int32, maxBytes int) (*HostExchange, error) {
 	cn := C.CString(name)
 	defer C.free(unsafe.Pointer(cn))
