@@ -2030,11 +2030,25 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   __syncthreads();
   if (walk) {
     int cnt = 0;
-    for (int64_t r = tid; r < nr; r += WK_ROUND) {
-      cnt += w.rmin[r] < KQ;
-      const bool can = q0 <= w.rmax[r] && q1 <= w.rmax[nr + r] && q2 <= w.rmax[2 * nr + r] &&
-                       q3 <= w.rmax[3 * nr + r] && (w.ror[r] & need) == need;
+    for (int64_t r0 = 0; r0 < nr; r0 += WK_ROUND) {   // (block-uniform bound: the ballot is wave-wide)
+      const int64_t r = r0 + tid;
+      bool can = false;
+      if (r < nr) {
+        cnt += w.rmin[r] < KQ;
+        can = q0 <= w.rmax[r] && q1 <= w.rmax[nr + r] && q2 <= w.rmax[2 * nr + r] && q3 <= w.rmax[3 * nr + r] &&
+              (w.ror[r] & need) == need;
+      }
+#ifdef PE_PREPASS_ATOMIC   // (A/B: one LDS atomic per round, 32 lanes of a wave on one word)
       if (can) atomicOr(&cbits[r >> 5], 1u << (r & 31));
+#else
+      // the wave's 64 rounds are two whole bitmap words, owned by this wave: one ballot, two stores
+      const uint64_t bal = __ballot(can);
+      const int64_t wr = r0 + (tid & ~63);
+      if (lane == 0 && wr < nr) {
+        cbits[wr >> 5] = (uint32_t)bal;
+        if (wr + 32 < nr) cbits[(wr >> 5) + 1] = (uint32_t)(bal >> 32);
+      }
+#endif
     }
     for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
     if (lane == 0 && cnt) atomicAdd(&start_cnt, cnt);
