@@ -364,7 +364,7 @@ def main(argv=None):
     sys.path[:0] = [p for p in (ROOT, os.path.join(ROOT, "training-operator_amd"), PROFILES) if p not in sys.path]
     import numpy as np
 
-    from placement import Engine, HostExchange, comm_id, synth
+    from placement import Engine, HostExchange, PlacementError, comm_id, synth
     from provenance import source_hash
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -497,12 +497,48 @@ def main(argv=None):
         fallbacks.append(err)
         return Engine(device, rank=rank, world_size=world, comm=None, exchange=shm_exchange(), **kw)
 
+    PE_ERCCL = -5
+
+    def exchange_cost(st):
+        """The host exchange's cost per greedy window (engine counters, this rank): waiting for the
+        ranks' lists and merging them on the host -- null on one GPU and on the RCCL transport."""
+        if world == 1 or st["windows"] == 0 or st["xchg_wait_ms"] + st["xchg_merge_ms"] == 0:
+            return None
+        return {"wait": st["xchg_wait_ms"] / st["windows"] * 1e3, "merge": st["xchg_merge_ms"] / st["windows"] * 1e3}
+
+    def place_timed(holder, batch, kw, node_inv):
+        """One timed greedy batch (barrier + wall clock, max over ranks) on holder[0].  A window whose
+        RCCL all-gather does not complete within PE_RCCL_TIMEOUT_S makes pe_place_greedy abort the
+        communicator and return PE_ERCCL (its peers' windows time out the same way); the ranks then
+        agree through gloo, rebuild the engine on the node's shared-memory exchange, reload the
+        inventory and place the batch again -- flagged "degraded" like a failed set-up."""
+        for attempt in range(2):
+            barrier()
+            g0 = time.perf_counter()
+            err, r = None, None
+            try:
+                r = holder[0].place_batch(batch)
+            except PlacementError as ex:
+                if world == 1 or ex.code != PE_ERCCL or attempt:
+                    raise
+                err = f"rank {rank}: PlacementError: {ex}"
+            t = time.perf_counter() - g0
+            err = first_error(err) if world > 1 else err
+            if err is None:
+                barrier()
+                return r, allmax(t)
+            holder[0].close()
+            fallbacks.append(f"mid-batch: {err}")
+            holder[0] = Engine(device, rank=rank, world_size=world, comm=None, exchange=shm_exchange(), **kw)
+            holder[0].load_nodes(node_inv.cap, node_inv.used, node_inv.labels, node_inv.island)
+        raise AssertionError("unreachable")
+
     N = args.nodes
     J = args.fit_jobs * (world if args.scaling == "weak" else 1)
     inv = synth.make_inventory(N, synth.SEED["cfg5"], gpu_frac=0.2)
-    eng = make_engine(max_nodes=N, topk=args.topk, window_groups=args.window_groups, window_pods=args.window_pods,
-                      fit_path_mask=args.fit_path_mask, greedy_flags=args.greedy_flags,
-                      resort_nodes=args.resort_nodes)
+    eng_kw = dict(max_nodes=N, topk=args.topk, window_groups=args.window_groups, window_pods=args.window_pods,
+                  fit_path_mask=args.fit_path_mask, greedy_flags=args.greedy_flags, resort_nodes=args.resort_nodes)
+    eng = make_engine(**eng_kw)
     eng.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     b, e = eng.shard_range()
     Ns = e - b
@@ -715,19 +751,21 @@ def main(argv=None):
     if not args.no_greedy:
         progress("greedy")
         batch = synth.make_jobs(args.greedy_jobs, synth.SEED["cfg3"], "mixed")
+        holder = [eng]
         eng.reset_residuals()
-        eng.place_batch(batch)                      # warm-up pass (allocations, code paths)
+        place_timed(holder, batch, eng_kw, inv)     # warm-up pass (allocations, code paths)
+        eng = holder[0]
         eng.reset_stats()
         times = []
         placed = 0
         for _ in range(args.greedy_steps):
             eng.reset_residuals()
             eng.synchronize()
-            barrier()
-            g0 = time.perf_counter()
-            pods, st = eng.place_batch(batch)
-            barrier()
-            times.append(allmax(time.perf_counter() - g0))
+            (pods, st), t = place_timed(holder, batch, eng_kw, inv)
+            if holder[0] is not eng:                # rebuilt mid-run: its stats start here
+                eng = holder[0]
+                times = []
+            times.append(t)
             placed = int((st == 0).sum())
         s = eng.stats()
         gt = float(np.median(times))
@@ -739,6 +777,7 @@ def main(argv=None):
                          "device_wait_ms_per_batch": s["greedy_wait_ms"] / gs,
                          "host_resolve_ms_per_batch": s["greedy_host_ms"] / gs,
                          "zero_copy_exchange_windows_per_batch": s["xchg_zc_windows"] / gs,
+                         "exchange_us_per_window": exchange_cost(s),
                          "naive_pod_x_node_evals_per_s": batch.n_pods * float(N) / gt}
         if s["walk_groups"] > 0:
             # greedy roofline of the walk kernel.  Bytes it reads per batch (engine counters of the timed
@@ -813,21 +852,22 @@ def main(argv=None):
             progress(cfg)
             cinv = synth.make_inventory(n_nodes, synth.SEED[cfg[:4]], gpu_frac)
             cb = synth.make_jobs(n_jobs, synth.SEED[cfg[:4]], mix)
-            ce = make_engine(max_nodes=n_nodes, topk=args.topk, window_groups=args.window_groups,
-                             window_pods=args.window_pods, greedy_flags=args.greedy_flags,
-                             resort_nodes=args.resort_nodes)
-            ce.load_nodes(cinv.cap, cinv.used, cinv.labels, cinv.island)
-            ce.place_batch(cb)                       # warm-up
+            ckw = dict(max_nodes=n_nodes, topk=args.topk, window_groups=args.window_groups,
+                       window_pods=args.window_pods, greedy_flags=args.greedy_flags, resort_nodes=args.resort_nodes)
+            ch = [make_engine(**ckw)]
+            ch[0].load_nodes(cinv.cap, cinv.used, cinv.labels, cinv.island)
+            place_timed(ch, cb, ckw, cinv)           # warm-up
+            ce = ch[0]
             ce.reset_stats()
             ts = []
             for _ in range(3):
                 ce.reset_residuals()
                 ce.synchronize()
-                barrier()
-                g0 = time.perf_counter()
-                _, cst = ce.place_batch(cb)
-                barrier()
-                ts.append(allmax(time.perf_counter() - g0))
+                (_, cst), t = place_timed(ch, cb, ckw, cinv)
+                if ch[0] is not ce:                  # rebuilt mid-run: its stats start here
+                    ce = ch[0]
+                    ts = []
+                ts.append(t)
             ct = float(np.median(ts))
             cs = ce.stats()
             out["configs"][cfg] = {"workload": what, "nodes": n_nodes, "jobs": n_jobs, "pods": cb.n_pods,
@@ -836,7 +876,8 @@ def main(argv=None):
                                    "rescans_per_batch": cs["rescans"] / 3.0,
                                    "host_resolve_ms_per_batch": cs["greedy_host_ms"] / 3.0,
                                    "device_wait_ms_per_batch": cs["greedy_wait_ms"] / 3.0,
-                                   "zero_copy_exchange_windows_per_batch": cs["xchg_zc_windows"] / 3.0}
+                                   "zero_copy_exchange_windows_per_batch": cs["xchg_zc_windows"] / 3.0,
+                                   "exchange_us_per_window": exchange_cost(cs)}
             ce.close()
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

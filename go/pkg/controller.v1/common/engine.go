@@ -13,13 +13,19 @@ type name, one of the orders the reference can produce), Replicas nil -> -1 (the
 util.go:129), and per container the effective list AddResourceList adds (util.go:79-104): Requests,
 or Limits only when the Requests map is nil (an empty non-nil map does not fall back).  Init
 containers and pod overhead are not counted (util.go:138).  The engine counts pods up to minMember
-exactly as the per-pod loop.  Inputs the tensor path does not hold exactly go to the reference's
-CalcPGMinResources unchanged, so the answer is the reference's for every input.
+exactly as the per-pod loop.  Inputs the tensor path does not hold exactly (domain refusals: an
+inexact quantity, an unknown key, int64 overflow) go to the reference's CalcPGMinResources unchanged,
+so the answer is the reference's for every input; an ENGINE error is never answered that way -- it is
+returned (CalcPGMinResourcesEngineE, PGMinResourcesBatch) or counted and logged (EngineErrors).
 */
 package common
 
 import (
+	"fmt"
 	"sort"
+	"sync/atomic"
+
+	log "github.com/sirupsen/logrus"
 
 	apiv1 "github.com/kubeflow/training-operator/pkg/apis/kubeflow.org/v1"
 	"github.com/kubeflow/training-operator/pkg/placement/hip"
@@ -91,21 +97,53 @@ func effectiveList(c v1.Container) v1.ResourceList {
 	return c.Resources.Requests
 }
 
-// CalcPGMinResourcesEngine returns a CalcPGMinResources with the pod counting and the resource sums
-// on the GPU.  Like the reference it never returns nil.
-func CalcPGMinResourcesEngine(eng *hip.Engine, gpuName string) func(int32, map[apiv1.ReplicaType]*apiv1.ReplicaSpec,
-	PriorityClassGetFunc) *v1.ResourceList {
-	return func(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpec, pcGetFunc PriorityClassGetFunc) *v1.ResourceList {
-		csr, formats, err := flattenV1(minMember, replicas, pcGetFunc, gpuName)
-		if err != nil {
-			return CalcPGMinResources(minMember, replicas, pcGetFunc) // exact reference path
+// EngineErrors counts the engine failures (PE_EHIP, PE_ENODEV, a lost device ...) the v1-signature
+// adapter below could not return to its caller.  Monitor it: every count is a PodGroup written with an
+// empty MinResources and a log line, never an answer computed some other way.
+var EngineErrors uint64
+
+// CalcPGMinResourcesEngineE is CalcPGMinResources with the pod counting and the resource sums on the
+// GPU, and the engine's failures returned.  Only DOMAIN refusals go to the reference's
+// CalcPGMinResources (util.go:108): a quantity the int64 tensor path does not hold exactly, an
+// unknown resource key (flattenV1's error) or an int64 overflow (the reference switches to inf.Dec).
+// An engine error is returned as it is -- like the v2 plugin's Build -- so the reconcile fails and is
+// retried (job.go:313's SyncPodGroup error path); it is never answered by the reference's CPU loop.
+func CalcPGMinResourcesEngineE(eng *hip.Engine, gpuName string) func(int32, map[apiv1.ReplicaType]*apiv1.ReplicaSpec,
+	PriorityClassGetFunc) (*v1.ResourceList, error) {
+	return func(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpec, pcGetFunc PriorityClassGetFunc) (*v1.ResourceList, error) {
+		csr, formats, ferr := flattenV1(minMember, replicas, pcGetFunc, gpuName)
+		if ferr != nil {
+			return CalcPGMinResources(minMember, replicas, pcGetFunc), nil // domain refusal: exact reference path
 		}
 		agg, err := eng.PGMinResources(hip.ModeV1, csr)
-		if err != nil || agg.Overflow[0] != 0 {
-			return CalcPGMinResources(minMember, replicas, pcGetFunc)
+		if err != nil {
+			return nil, fmt.Errorf("placement engine: CalcPGMinResources: %w", err)
+		}
+		if agg.Overflow[0] != 0 {
+			return CalcPGMinResources(minMember, replicas, pcGetFunc), nil // domain refusal: inf.Dec sums
 		}
 		rl := agg.Unflatten(0, gpuName, formats.Formats()) // printed as the reference's sums print
-		return &rl
+		return &rl, nil
+	}
+}
+
+// CalcPGMinResourcesEngine keeps util.go:108's signature (no error result) for a one-line swap of
+// jc.calcPGMinResourcesFn.  Like the reference it never returns nil.  An engine error cannot be
+// returned through that signature, so it is counted in EngineErrors, logged, and answered with an
+// EMPTY list (the gang scheduler then checks no minimum) -- not with the reference's CPU result.
+// Wire CalcPGMinResourcesEngineE instead where job.go can return the error (INTEGRATION.md section 2).
+func CalcPGMinResourcesEngine(eng *hip.Engine, gpuName string) func(int32, map[apiv1.ReplicaType]*apiv1.ReplicaSpec,
+	PriorityClassGetFunc) *v1.ResourceList {
+	calc := CalcPGMinResourcesEngineE(eng, gpuName)
+	return func(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpec, pcGetFunc PriorityClassGetFunc) *v1.ResourceList {
+		rl, err := calc(minMember, replicas, pcGetFunc)
+		if err != nil {
+			atomic.AddUint64(&EngineErrors, 1)
+			log.Errorf("CalcPGMinResources: %v (PodGroup MinResources left empty; EngineErrors=%d)", err,
+				atomic.LoadUint64(&EngineErrors))
+			return &v1.ResourceList{}
+		}
+		return rl
 	}
 }
 
@@ -118,18 +156,19 @@ type PGRequest struct {
 
 // PGMinResourcesBatch is CalcPGMinResources for many jobs at once -- a resync of every job's
 // PodGroup (job.go:455-457 called in a loop) -- with ONE engine call for all the jobs the tensor path
-// holds; the others (and any overflowed job) take the reference's CalcPGMinResources.  out[i] is the
-// answer for reqs[i], exactly the reference's.  The engine pays off above hip.BatchCrossoverJobs jobs.
-func PGMinResourcesBatch(eng *hip.Engine, gpuName string, reqs []PGRequest) []*v1.ResourceList {
+// holds.  Jobs the tensor path refuses (flatten error) or that overflow take the reference's
+// CalcPGMinResources (domain refusals, as CalcPGMinResourcesEngineE); an engine error fails the whole
+// call (out is nil) and is returned.  out[i] is the answer for reqs[i], exactly the reference's.  The
+// engine pays off above hip.BatchCrossoverJobs jobs.
+func PGMinResourcesBatch(eng *hip.Engine, gpuName string, reqs []PGRequest) ([]*v1.ResourceList, error) {
 	out := make([]*v1.ResourceList, len(reqs))
 	batch := &hip.CSR{}
 	idx := make([]int, 0, len(reqs))          // batch job -> request
 	formats := make([]*hip.FormatAcc, 0, len(reqs))
 	for i, r := range reqs {
-		csr, f, err := flattenV1(r.MinMember, r.Replicas, r.PcGetFunc, gpuName)
-		if err != nil {
-			rl := CalcPGMinResources(r.MinMember, r.Replicas, r.PcGetFunc) // exact reference path
-			out[i] = rl
+		csr, f, ferr := flattenV1(r.MinMember, r.Replicas, r.PcGetFunc, gpuName)
+		if ferr != nil {
+			out[i] = CalcPGMinResources(r.MinMember, r.Replicas, r.PcGetFunc) // domain refusal: exact reference path
 			continue
 		}
 		batch.AppendJobs(csr)
@@ -137,17 +176,20 @@ func PGMinResourcesBatch(eng *hip.Engine, gpuName string, reqs []PGRequest) []*v
 		formats = append(formats, f)
 	}
 	if len(idx) == 0 {
-		return out
+		return out, nil
 	}
 	agg, err := eng.PGMinResources(hip.ModeV1, batch)
+	if err != nil {
+		return nil, fmt.Errorf("placement engine: PGMinResourcesBatch (%d jobs): %w", len(idx), err)
+	}
 	for j, i := range idx {
 		r := reqs[i]
-		if err != nil || agg.Overflow[j] != 0 {
-			out[i] = CalcPGMinResources(r.MinMember, r.Replicas, r.PcGetFunc)
+		if agg.Overflow[j] != 0 {
+			out[i] = CalcPGMinResources(r.MinMember, r.Replicas, r.PcGetFunc) // domain refusal: inf.Dec sums
 			continue
 		}
 		rl := agg.Unflatten(j, gpuName, formats[j].Formats())
 		out[i] = &rl
 	}
-	return out
+	return out, nil
 }

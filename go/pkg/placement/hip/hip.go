@@ -140,6 +140,7 @@ func (x *HostExchange) Allgather(send, recv []byte) error {
 	if rc := C.pe_host_exchange_allgather(unsafe.Pointer(x.h), sp, rp, C.size_t(len(send))); rc != C.PE_OK {
 		return fmt.Errorf("placement: pe_host_exchange_allgather: %d", int(rc))
 	}
+	runtime.KeepAlive(x) // the finalizer must not unmap the segment during the call
 	return nil
 }
 
@@ -156,6 +157,9 @@ func (x *HostExchange) Close() {
 type Engine struct {
 	ctx  *C.pe_ctx
 	name *C.char
+	// hx keeps the HostExchange the context was created with reachable for the context's lifetime:
+	// its walks and exchange thread use the mapped segment, which HostExchange's finalizer unmaps.
+	hx *HostExchange
 }
 
 // Stats mirrors pe_stats.
@@ -239,6 +243,7 @@ func New(cfg Config) (*Engine, error) {
 	if cfg.HostExchange != nil {
 		c.exchange = C.hx_allgather_fn()
 		c.exchange_user = unsafe.Pointer(cfg.HostExchange.h)
+		e.hx = cfg.HostExchange
 	}
 	rc := C.pe_create(&c, &e.ctx)
 	if rc != C.PE_OK {
@@ -258,6 +263,7 @@ func (e *Engine) Close() {
 		C.pe_destroy(e.ctx)
 		e.ctx = nil
 		C.free(unsafe.Pointer(e.name))
+		e.hx = nil // the segment may be unmapped now (the caller's Close, or its finalizer)
 	}
 }
 

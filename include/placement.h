@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 5
+#define PE_ABI_VERSION 6
 #define PE_DIMS 4
 #define PE_COMM_ID_BYTES 128
 #define PE_MAX_NODES (1LL << 24) /* node ids live in the low 24 bits of the best-fit key */
@@ -157,6 +157,11 @@ typedef struct {
                                 was pending (written into both index sets' overlays) */
   int64_t xchg_zc_windows;   /* multi-rank greedy windows exchanged zero-copy through the shared-memory
                                 exchange's registered segment (no host copy, no host barrier) */
+  /* (ABI 6) the host exchange's cost, summed over windows: time its thread waited for the ranks'
+     lists (zero-copy: spinning on peers' group signals; copying: inside the all-gather callback) and
+     time it spent merging them on the host (zero-copy windows) */
+  double xchg_wait_ms;
+  double xchg_merge_ms;
 } pe_stats;
 
 int pe_abi_version(void);

@@ -85,6 +85,9 @@ def test_cgo_preamble_and_package():
     assert '#include "placement.h"' in text and 'import "C"' in text
     # the Go side pins slices only for the call: no C pointer into Go memory is stored
     assert "runtime.SetFinalizer" in text
+    # the engine holds its HostExchange (the segment its walks write into) until Close; the
+    # all-gather keeps the exchange alive across the cgo call
+    assert "e.hx = cfg.HostExchange" in text and "runtime.KeepAlive(x)" in text
 
 
 @pytest.mark.parametrize("path,needles", [
@@ -102,7 +105,10 @@ def test_cgo_preamble_and_package():
              "c.Resources.Limits", "CalcPGMinResources(minMember, replicas, pcGetFunc)", "pc.Value",
              # print formats of AddResourceList's sums, replayed over the counted pods (util.go:79-104,126-141)
              "acc.AddList(effectiveList(c), gpuName, 1)", "agg.Unflatten(0, gpuName, formats.Formats())",
-             "func PGMinResourcesBatch(", "batch.AppendJobs(csr)", "agg.Unflatten(j, gpuName, formats[j].Formats())"]),
+             "func PGMinResourcesBatch(", "batch.AppendJobs(csr)", "agg.Unflatten(j, gpuName, formats[j].Formats())",
+             # engine errors are returned (E form, batch) or counted + logged, never answered by the reference
+             "func CalcPGMinResourcesEngineE(", "var EngineErrors uint64", "atomic.AddUint64(&EngineErrors, 1)",
+             "return nil, fmt.Errorf(\"placement engine: CalcPGMinResources: %w\", err)"]),
     (FLATTEN_GO, ["type FormatAcc struct", "func (a *FormatAcc) Add(", "func (a *FormatAcc) Formats()",
                   "if !a.nonzero[d] {", "func (b *CSR) AppendJobs(o *CSR)", "BatchCrossoverJobs"]),
 ])
@@ -110,6 +116,33 @@ def test_adapters(path, needles):
     text = open(path).read()
     for n in needles:
         assert n in text, (os.path.basename(path), n)
+
+
+def _go_code(path):
+    text = re.sub(r"//[^\n]*", "", open(path).read())
+    return re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+
+
+@pytest.mark.parametrize("path", [V1_GO, COSCHED_GO])
+def test_engine_errors_never_reach_the_reference(path):
+    """Only domain refusals (a flatten error, int64 overflow) may take the reference's CPU function;
+    an engine error is returned (or, in the v1 signature form, counted and logged): no branch tests
+    the engine's error together with a fallback condition, and every reference call sits under a
+    flatten error or an Overflow test."""
+    code = _go_code(path)
+    assert "err != nil ||" not in code and "|| err != nil" not in code
+    ref = "CalcPGMinResources(" if path == V1_GO else "c.CoScheduling.Build("
+    lines = code.splitlines()
+    for i, line in enumerate(lines):
+        if ref in line and "func " not in line and "Engine" not in line:
+            guard = "\n".join(lines[max(0, i - 2):i])
+            assert "ferr != nil" in guard or "Overflow" in guard or ("err != nil" in guard and "flatten" in guard), \
+                (os.path.basename(path), i + 1, guard)
+        if "eng.PGMinResources(" in line:
+            after = "\n".join(lines[i + 1:i + 5])
+            # the first test after the engine call is its error, answered by returning / recording it
+            assert ("if err != nil" in after and "return" in after) or \
+                   ("case err != nil:" in after and "errs[i] = err" in after), after
 
 
 def test_podgroup_emission_not_duplicated():

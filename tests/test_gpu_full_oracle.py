@@ -8,13 +8,14 @@ invariants:
 - the cfg5 fit mask: all 100k x 1M mask rows (in chunks of 4096 jobs) and all 100k counts vs
   `oracle.fit_mask`.
 The oracle is the checker only; the engine results come from libplacement.so on the GPU."""
+import os
 import threading
 
 import numpy as np
 import pytest
 
 import oracle
-from placement import Engine, synth
+from placement import Engine, HostExchange, synth
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
@@ -105,6 +106,65 @@ def test_bench_greedy_batch_two_shards_vs_oracle(bench_inv, greedy_batch, greedy
         np.testing.assert_array_equal(engines[r].read_residuals(), w_res[:, lo:hi])
     for en in engines:
         en.close()
+
+
+def _run_ranks(engines, batch, timeout=600):
+    out = [None] * len(engines)
+    errs = []
+
+    def run(r):
+        try:
+            out[r] = engines[r].place_batch(batch)
+        except Exception as ex:   # noqa: BLE001 -- reported below
+            errs.append((r, ex))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(len(engines))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=timeout)
+    assert not any(t.is_alive() for t in th), "a rank never returned"
+    assert not errs, errs
+    return out
+
+
+def test_bench_greedy_batch_eight_shards_vs_oracle(bench_inv, greedy_batch, greedy_oracle):
+    """The bench's greedy batch split EIGHT ways, as BASELINE cfg3 shards it over the 8 GPUs of a
+    node (verdict r4, item 2a): 8 shard contexts of 125k nodes in one process on the one GPU, over the
+    production transport of one node's ranks -- the native shared-memory exchange with zero-copy
+    windows (every walk writes its rank's lists into the registered segment, each rank's exchange
+    thread merges every group on the host as all 8 ranks signalled it).  Every rank's pods and job
+    statuses against the ORACLE, each device shard against its slice of the oracle's residuals, and
+    a second batch after pe_reset_residuals (the bench's repeated batches)."""
+    inv, b = bench_inv, greedy_batch
+    W = 8
+    name = f"/pe_fo8_{os.getpid()}"
+    hxs = [HostExchange(name, r, W, 128 * (16 + 8 * 256)) for r in range(W)]
+    engines = [Engine(0, rank=r, world_size=W, exchange=hxs[r], max_nodes=N_NODES) for r in range(W)]
+    for en in engines:
+        en.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    w_pods, w_st, w_res = greedy_oracle
+    covered = 0
+    for rep in range(2):
+        if rep:
+            for en in engines:
+                en.reset_residuals()
+        out = _run_ranks(engines, b)
+        for r in range(W):
+            np.testing.assert_array_equal(out[r][1], w_st)
+            np.testing.assert_array_equal(out[r][0], w_pods)
+            lo, hi = engines[r].shard_range()
+            np.testing.assert_array_equal(engines[r].read_residuals(), w_res[:, lo:hi])
+            if not rep:
+                covered += hi - lo
+    assert covered == N_NODES
+    for en in engines:
+        s = en.stats()
+        assert s["xchg_zc_windows"] > 0 and s["xchg_zc_windows"] == s["windows"], s   # every window zero-copy
+    for en in engines:
+        en.close()
+    for x in hxs:
+        x.close()
 
 
 def test_cfg5_fit_mask_every_row_vs_oracle(bench_inv):

@@ -54,7 +54,12 @@ def _env(**kv):
                                                                            (2, "mixed", 20000, 600, False, "shm-devmerge"),
                                                                            (3, "gang8", 9000, 300, False, "shm-devmerge"),
                                                                            (3, "island8", 9000, 300, False, "gloo-ranked"),
-                                                                           (2, "gang8", 6000, 300, True, "shm")])
+                                                                           (2, "gang8", 6000, 300, True, "shm"),
+                                                                           # eight ranks: BASELINE cfg3's split
+                                                                           (8, "mixed", 40000, 600, False, "shm"),
+                                                                           (8, "island8", 16000, 300, False,
+                                                                            "shm-devmerge"),
+                                                                           (8, "mixed", 40000, 600, False, "shm-copy")])
 def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, host_merge, transport):
     """host_merge False: the gathered shard lists are merged on the device (merge_shards, the
     default); True: PE_HOST_MERGE=1, the host's lazy k-way merge.  transport: the Python gloo
@@ -74,7 +79,7 @@ def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, 
     outs = []
     try:
         for p in procs:
-            out, _ = p.communicate(timeout=100)
+            out, _ = p.communicate(timeout=100 if world <= 3 else 200)
             outs.append(out)
     finally:
         for p in procs:

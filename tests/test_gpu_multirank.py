@@ -81,10 +81,16 @@ def test_bench_two_ranks_matches_one():
     for k in ("fit_many_values", "fit_worst_case", "fit_adversarial"):
         assert two[k]["feasible_pairs"] == one[k]["feasible_pairs"], k
     assert two["value"] > 0 and two["fit_weak_scaling"]["value"] > 0
-    # no throughput cliff on the fallback transport (both ranks share this box's one GPU)
-    for k in ("cfg3", "cfg4"):
+    # no throughput cliff on the fallback transport (both ranks share this box's one GPU): every greedy
+    # line within 2x of one rank, and the exchange's per-window cost reported for the 8-GPU runs
+    for k in one["configs"]:
         assert two["configs"][k]["ms_per_batch"] <= 2.0 * one["configs"][k]["ms_per_batch"], \
             (k, two["configs"][k], one["configs"][k])
+        assert one["configs"][k]["exchange_us_per_window"] is None
+        x = two["configs"][k]["exchange_us_per_window"]
+        assert x is not None and x["merge"] > 0 and x["wait"] >= 0, (k, x)
+    assert two["greedy"]["ms_per_batch"] <= 2.0 * one["greedy"]["ms_per_batch"], (two["greedy"], one["greedy"])
+    assert two["greedy"]["exchange_us_per_window"]["merge"] > 0
 
 
 _INIT = r"""

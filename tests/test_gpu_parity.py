@@ -461,6 +461,91 @@ def test_greedy_rccl_single_rank(host_merge, flags):
         os.environ.pop("PE_HOST_MERGE", None)
 
 
+def test_greedy_rccl_window_timeout_aborts():
+    """A window whose all-gather never completes (verdict r4, item 3): a test kernel holds the stream
+    for 8 s right before window 3's ncclAllGather (PE_TEST_STALL_*), so the window's merged lists
+    cannot arrive while the stream stays busy -- the case the idle test cannot tell from a slow walk.
+    With PE_RCCL_TIMEOUT_S = 2 the call returns PE_ERCCL within the bound, the communicator is aborted,
+    and every later call fails fast with PE_ERCCL (the caller rebuilds the context)."""
+    import time
+
+    from placement import PlacementError, comm_id
+    env = {"PE_TEST_STALL_WINDOW": "3", "PE_TEST_STALL_MS": "8000", "PE_RCCL_TIMEOUT_S": "2"}
+    os.environ.update(env)
+    try:
+        e = Engine(0, world_size=1, comm=comm_id(), topk=8, window_groups=16)
+        assert e.comm_ranks() == 1
+        inv = synth.make_inventory(3000, 83, 0.25)
+        batch = synth.make_jobs(250, 89, "mixed")
+        e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+        t0 = time.monotonic()
+        with pytest.raises(PlacementError) as ei:
+            e.place_batch(batch)
+        dt = time.monotonic() - t0
+        assert ei.value.code == -5, ei.value                     # PE_ERCCL
+        assert "PE_RCCL_TIMEOUT_S" in str(ei.value), str(ei.value)
+        assert 1.5 < dt < 6.0, dt                                # the bound, not the 8 s stall
+        assert e.comm_ranks() == 0                               # the communicator is gone
+        t1 = time.monotonic()
+        with pytest.raises(PlacementError) as ei2:
+            e.place_batch(batch)
+        assert ei2.value.code == -5 and "aborted" in str(ei2.value), ei2.value
+        assert time.monotonic() - t1 < 1.0
+        e.close()                                                # (joins the abort; the stall has drained)
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+    # the device is fine afterwards: a fresh context places the batch bit-exact
+    e2 = Engine(0, world_size=1, comm=comm_id(), topk=8, window_groups=16)
+    check_greedy(e2, inv, batch)
+    e2.close()
+
+
+@pytest.mark.parametrize("W", [17, 20])
+def test_greedy_wide_host_exchange(W):
+    """More ranks than the device merge and the zero-copy windows take (world > 16: several ranks per
+    GPU): W shard contexts in one process over the native shared-memory exchange fall back to the
+    copying all-gather and the host merge -- still the unsharded oracle's answer on every rank."""
+    from placement import HostExchange
+    inv = synth.make_inventory(4000, 97, 0.25)
+    batch = synth.make_jobs(160, 101, "mixed")
+    name = f"/pe_wide_{os.getpid()}_{W}"
+    hxs = [HostExchange(name, r, W, 32 * (16 + 8 * 16)) for r in range(W)]
+    engines = [Engine(0, rank=r, world_size=W, exchange=hxs[r], topk=16, window_groups=32) for r in range(W)]
+    for e in engines:
+        e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
+    results, errs = [None] * W, []
+
+    def run(r):
+        try:
+            results[r] = engines[r].place_batch(batch)
+        except Exception as ex:   # noqa: BLE001 -- reported below
+            errs.append((r, ex))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th) and not errs, errs
+    w_pods, w_st, w_res = oracle.place_greedy(inv.residual(), inv.labels, batch.job_group_off, batch.priority,
+                                              batch.group_count, batch.group_req, batch.group_need)
+    covered = 0
+    for r in range(W):
+        pods, st = results[r]
+        np.testing.assert_array_equal(st, w_st)
+        np.testing.assert_array_equal(pods, w_pods)
+        b, en = engines[r].shard_range()
+        covered += en - b
+        np.testing.assert_array_equal(engines[r].read_residuals(), w_res[:, b:en])
+        assert engines[r].stats()["xchg_zc_windows"] == 0
+    assert covered == 4000
+    for e in engines:
+        e.close()
+    for x in hxs:
+        x.close()
+
+
 def test_greedy_reset_residuals(eng):
     inv = synth.make_inventory(800, 59)
     batch = synth.make_jobs(60, 61)

@@ -338,6 +338,15 @@ ncclComm_t comm_init_bounded(int device, int world, const ncclUniqueId& id, int 
   return st->comm;
 }
 
+// Bound of one RCCL window of the greedy: PE_RCCL_TIMEOUT_S seconds (default 60) blocked on a window
+// whose all-gather has not completed (a peer lost mid-batch) -- then the communicator is aborted and
+// the call returns PE_ERCCL.
+double rccl_timeout_s() {
+  const char* e = std::getenv("PE_RCCL_TIMEOUT_S");
+  const double s = e ? std::atof(e) : 60.0;
+  return s > 0 ? s : 60.0;
+}
+
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // pe_config.fit_path_mask bits
@@ -359,6 +368,11 @@ struct pe_ctx {
   int device = 0;
   int rank = 0, world = 1;
   ncclComm_t comm = nullptr;
+  // a greedy window's collective timed out: the communicator was handed to comm_abort (ncclCommAbort
+  // on its own thread -- it returns once the device work it aborts has drained) and every later
+  // sharded call fails with PE_ERCCL; the caller rebuilds the context (e.g. on the host exchange)
+  bool comm_aborted = false;
+  std::thread comm_abort;
   pe_allgather_fn exchange = nullptr;
   void* exchange_user = nullptr;
   void* zc_hx = nullptr;   // the shared-memory exchange whose zero-copy use the ranks agreed on (zc_ok)
@@ -492,6 +506,7 @@ struct pe_ctx {
 
   ~pe_ctx() {
     (void)hipSetDevice(device);
+    if (comm_abort.joinable()) comm_abort.join();
     if (stream) (void)hipStreamSynchronize(stream);
     res0.release(); res.release(); labels.release(); island.release(); n_upd.release();
     fit_jobs.release(); fit_jobs32.release(); res32.release(); mask.release();
@@ -523,6 +538,22 @@ struct pe_ctx {
 
 namespace {
 
+// A collective timed out (pe::CollectiveTimeout): abort the communicator without blocking the caller.
+// ncclCommAbort raises the communicator's abort flag, which the stuck collective kernel polls, and then
+// frees its resources (the frees wait for the device work in flight); on its own thread, so the call
+// that timed out returns PE_ERCCL within the bound; pe_destroy joins it.
+void rccl_abort(pe_ctx* ctx) {
+  if (!ctx->comm) return;
+  ncclComm_t c = ctx->comm;
+  ctx->comm = nullptr;
+  ctx->comm_aborted = true;
+  const int dev = ctx->device;
+  ctx->comm_abort = std::thread([c, dev] {
+    (void)hipSetDevice(dev);
+    (void)ncclCommAbort(c);
+  });
+}
+
 // Every ABI entry runs its body through here: lock, select device, map exceptions to codes.
 template <class F>
 int guarded(pe_ctx* ctx, F&& body) {
@@ -538,6 +569,10 @@ int guarded(pe_ctx* ctx, F&& body) {
   } catch (const std::bad_alloc&) {
     ctx->err = "host allocation failed";
     return PE_ENOMEM;
+  } catch (const pe::CollectiveTimeout& e) {   // an RCCL window's all-gather never completed
+    ctx->err = e.what();
+    rccl_abort(ctx);
+    return PE_ERCCL;
   } catch (const pe::ExchangeError& e) {   // a zero-copy window's peer lists never arrived
     ctx->err = e.what();
     return PE_ERCCL;
@@ -2344,6 +2379,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
   return guarded(ctx, [&]() -> int {
     const auto t0 = std::chrono::steady_clock::now();
     if (!ctx->loaded) raise(PE_ESTATE, "no inventory loaded");
+    if (ctx->comm_aborted)
+      raise(PE_ERCCL, "the RCCL communicator was aborted after a window's all-gather timed out; recreate the context");
     if (n_jobs < 0) raise(PE_EINVAL, "n_jobs < 0");
     if (n_jobs == 0) return PE_OK;
     need_ptr(job_group_off, "job_group_off");
@@ -2536,17 +2573,38 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // PE_HOST_MERGE=1: the gathered blob is copied and merged lazily on the host instead.
     // (PE_HOST_MERGE=1 with a host exchange, measured: the lazy host merge doubled the resolve --
     // the seed helper cannot pre-skip merged lists -- 20.4 vs 8.9 ms per 2-rank cfg3 batch)
-    const bool dev_merge = !direct_out && (int64_t)ctx->world * K <= pe::MG_CAP && !std::getenv("PE_HOST_MERGE");
+    // (merge_shards_kernel stages one header per rank in a wave's lanes: world <= MG_THREADS / 64;
+    // wider sharded runs take the host merge)
+    const bool dev_merge = !direct_out && (int64_t)ctx->world * K <= pe::MG_CAP &&
+                           ctx->world <= pe::MG_THREADS / 64 && !std::getenv("PE_HOST_MERGE");
     // the shard merge kernel: PE_MERGE_RANKED=1 the rank merge (256-thread blocks, no sort; A/B)
     const bool ranked = std::getenv("PE_MERGE_RANKED") && ctx->world <= pe::RM_MAX_WORLD &&
                         (int64_t)ctx->world * K * 8 <= 64 * 1024;
     auto* const merge_fn = ranked ? &pe::launch_merge_ranked : &pe::launch_merge_shards;
     const bool signalled = pipelined && !std::getenv("PE_NO_GROUP_SIGNAL") && (direct_out ? walk : dev_merge);
+    // Zero-copy shared-memory exchange (pe_hostx.h): decided first, the pipeline depth depends on it.
+    bool zc = false;
+    pe_host_exchange* const hx = pe::hx_is(ctx->exchange) ? static_cast<pe_host_exchange*>(ctx->exchange_user) : nullptr;
+    if (hx && use_exchange && pipelined && signalled && ctx->walk && !std::getenv("PE_NO_ZC_EXCHANGE")) {
+      if (ctx->zc_hx != hx) {
+        const uint8_t ok = ctx->world <= pe::HX_ZC_MAX_WORLD && pe::hx_zc_register(hx) &&
+                                   (size_t)Wmax * gb <= pe::hx_slot_bytes(hx) ? 1 : 0;
+        std::vector<uint8_t> all((size_t)ctx->world, 0);
+        if (ctx->exchange(ctx->exchange_user, &ok, all.data(), 1) != 0) raise(PE_ERCCL, "exchange callback failed");
+        ctx->zc_ok = std::all_of(all.begin(), all.end(), [](uint8_t v) { return v == 1; });
+        ctx->zc_hx = hx;
+      }
+      zc = ctx->zc_ok;
+      if (zc) hipchk(ctx->g_xstatus.ensure(1), "alloc exchange status");
+    }
     // Pipeline depth D (signalled windows; PE_PIPE_DEPTH, 1..3, default 1): windows i+1 .. i+D are
     // scanned while window i is resolved (D + 1 blob / request buffers, D update staging slots).  (2
     // measured on a 2-rank host-exchange run: 36 vs 22 ms per cfg3 batch -- every dropped speculation
     // throws away two scans.)
-    const int depth = !pipelined ? 0 : !signalled ? 1 : [&] {
+    // A copying split exchange (below) reads this rank's lists from the one h_own buffer while the
+    // walk of the next window would overwrite it: depth 1 there (only zero-copy windows go deeper).
+    const bool copy_split = use_exchange && walk && !zc;
+    const int depth = !pipelined ? 0 : !signalled || copy_split ? 1 : [&] {
       const char* e = std::getenv("PE_PIPE_DEPTH");
       return e ? std::min(3, std::max(1, std::atoi(e))) : 1;
     }();
@@ -2586,6 +2644,33 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     } stream_idle{s};
     feed.idle = &StreamIdle::busy;
     feed.idle_user = &stream_idle;
+    // RCCL transport: every wait for the stream is bounded (PE_RCCL_TIMEOUT_S) -- a collective that
+    // never completes keeps the stream busy, which the idle test above cannot tell from a slow walk
+    const double coll_tmo = !use_exchange && ctx->comm ? rccl_timeout_s() : 0.0;
+    feed.timeout_s = coll_tmo;
+    auto sync_stream = [&](const char* what) {
+      if (coll_tmo <= 0) return hipchk(hipStreamSynchronize(s), what);
+      const auto ts = std::chrono::steady_clock::now();
+      for (unsigned spin = 1;; ++spin) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipErrorNotReady) return hipchk(e, what);
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if ((spin & 63) == 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count() > coll_tmo)
+          throw pe::CollectiveTimeout(std::string(what) + ": the stream did not drain within " +
+                                      std::to_string(coll_tmo) +
+                                      " s -- a window's all-gather is stuck (a peer stalled or was lost; PE_RCCL_TIMEOUT_S)");
+      }
+    };
+    // PE_TEST_STALL_WINDOW=n, PE_TEST_STALL_MS=m (test knob, RCCL transport): a one-thread kernel that
+    // holds the stream for m ms (wall clock, bounded) is queued right before window n's all-gather --
+    // a stand-in for a collective whose peer is gone
+    const int64_t stall_window = std::getenv("PE_TEST_STALL_WINDOW") ? std::atoll(std::getenv("PE_TEST_STALL_WINDOW")) : -1;
+    const int64_t stall_ticks = [] {
+      const char* e = std::getenv("PE_TEST_STALL_MS");
+      const double ms = e ? std::atof(e) : 0.0;
+      return (int64_t)(std::min(std::max(ms, 0.0), 30000.0) * 1e5);   // wall_clock64: 100 MHz; at most 30 s
+    }();
     double feed_spin_seen = 0;   // feed.spin_ms() already counted as device wait
     // A pipelined host exchange with device merge runs on its own thread (split_x): the launch helper
     // only launches window w+1's walk (its lists signalled into pinned memory), the exchange thread
@@ -2595,20 +2680,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // its slot of the registered segment and the shard merge, queued behind it, waits on the device
     // for every rank's signal of its group -- no exchange thread, no host barrier, no copies.  The
     // ranks agree on it once per context and segment (each says whether it could register the
-    // segment); PE_NO_ZC_EXCHANGE=1 (every rank): the copying exchange below.
-    bool zc = false;
-    pe_host_exchange* const hx = pe::hx_is(ctx->exchange) ? static_cast<pe_host_exchange*>(ctx->exchange_user) : nullptr;
-    if (hx && use_exchange && pipelined && signalled && ctx->walk && !std::getenv("PE_NO_ZC_EXCHANGE")) {
-      if (ctx->zc_hx != hx) {
-        const uint8_t ok = pe::hx_zc_register(hx) && (size_t)Wmax * gb <= pe::hx_slot_bytes(hx) ? 1 : 0;
-        std::vector<uint8_t> all((size_t)ctx->world, 0);
-        if (ctx->exchange(ctx->exchange_user, &ok, all.data(), 1) != 0) raise(PE_ERCCL, "exchange callback failed");
-        ctx->zc_ok = std::all_of(all.begin(), all.end(), [](uint8_t v) { return v == 1; });
-        ctx->zc_hx = hx;
-      }
-      zc = ctx->zc_ok;
-      if (zc) hipchk(ctx->g_xstatus.ensure(1), "alloc exchange status");
-    }
+    // segment); PE_NO_ZC_EXCHANGE=1 (every rank): the copying exchange below.  (zc is set above.)
     // a rank whose peer stalls: its wait gives up after PE_HX_GPU_TIMEOUT_S (default 60) and the
     // resolver raises (the merged lists come back with n = -1), the GPU is not held
     const int64_t zc_ticks = [] {
@@ -2653,8 +2725,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       uint8_t* og = out + (size_t)w * gb;
       uint64_t* dst = reinterpret_cast<uint64_t*>(og + sizeof(pe::CandHdr));
       uint64_t L = pe::NO_KEY;
-      const uint64_t* lists[pe::RM_MAX_WORLD];
-      int ns[pe::RM_MAX_WORLD];
+      static_assert(pe::HX_ZC_MAX_WORLD >= pe::RM_MAX_WORLD, "zero-copy merge arrays");
+      const uint64_t* lists[pe::HX_ZC_MAX_WORLD];   // (zero-copy windows: world <= HX_ZC_MAX_WORLD)
+      int ns[pe::HX_ZC_MAX_WORLD];
       for (int r = 0; r < W; ++r) {
         const uint8_t* g = gath + (size_t)r * stride + (size_t)w * gb;
         pe::CandHdr h;
@@ -2704,7 +2777,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           else lim = b[j];
         }
       } else {
-        int hd[pe::RM_MAX_WORLD] = {0};
+        int hd[pe::HX_ZC_MAX_WORLD] = {0};
         for (;;) {
           int br = -1;
           uint64_t bk = pe::NO_KEY;
@@ -2777,10 +2850,13 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         const double tmo = pe::hx_timeout_s();
         const auto t0 = std::chrono::steady_clock::now();
         double spun = 0, merged = 0;
+        double waited = 0;   // (stats: the clock is read only around a wait that happens)
         for (int w = 0; w < Wg; ++w) {
           const auto ts = trace ? std::chrono::steady_clock::now() : t0;
           for (int r = 0; r < ctx->world; ++r) {
             const pe::CandHdr* h = reinterpret_cast<const pe::CandHdr*>(hw->host + (size_t)r * hw->slot + (size_t)w * gb);
+            if (__atomic_load_n(&h->flags, __ATOMIC_ACQUIRE) == (int32_t)hw->gen) continue;
+            const auto tw = std::chrono::steady_clock::now();
             for (unsigned spin = 1; __atomic_load_n(&h->flags, __ATOMIC_ACQUIRE) != (int32_t)hw->gen; ++spin) {
               _mm_pause();
               if ((spin & 4095) == 0) {
@@ -2791,6 +2867,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
                                           "'s candidate lists never arrived (peer stalled or failed; PE_HX_TIMEOUT_S)");
               }
             }
+            waited += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
           }
           const auto tm = trace ? std::chrono::steady_clock::now() : t0;
           // the next groups' lists on their way from DRAM (the device wrote them past the CPU caches;
@@ -2814,6 +2891,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           tr_xspin.push_back(spun);
           tr_xmerge.push_back(merged);
         }
+        const double all_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        ctx->stats.xchg_wait_ms += waited;
+        ctx->stats.xchg_merge_ms += all_ms - waited;
         pe::hx_zc_consumed(hx, *hw);
         return;
       }
@@ -2836,10 +2916,14 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         hipchk(hipMemcpyAsync(ctx->h_own.p, ctx->g_out.p, bytes, hipMemcpyDeviceToHost, s), "D2H cands");
         hipchk(hipStreamSynchronize(s), "sync own cands");
       }
+      const auto tx = std::chrono::steady_clock::now();
       if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, dev_merge ? ctx->h_xg[b].p : outbuf(b), bytes) != 0)
         raise(PE_ERCCL, "exchange callback failed");
+      ctx->stats.xchg_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tx).count();
       if (xhost_merge) {
+        const auto tm = std::chrono::steady_clock::now();
         for (int w = 0; w < Wg; ++w) host_merge_group(ctx->h_xg[b].p, Wg, w, outbuf(b), gen);
+        ctx->stats.xchg_merge_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tm).count();
       } else if (dev_merge) {   // the gathered lists (pinned) merged on the device, signalled per group
         hipchk(merge_fn(s, ctx->h_xg[b].dev, ctx->world, Wg, K, outbufdev(b), gen, 0, nullptr),
                "launch merge_shards");
@@ -2942,6 +3026,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         else if (!defer_x)   // (the launch helper, or the main thread at a restart) exchange now
           exchange_window(b, Wg, gen, own_direct, nullptr);
       } else {
+        if (stall_window >= 0 && ctx->stats.windows == stall_window && stall_ticks > 0)
+          hipchk(pe::launch_stall(s, stall_ticks), "launch stall (test knob)");
         ncclchk(ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
         if (dev_merge)
           hipchk(merge_fn(s, ctx->g_gath.p, ctx->world, Wg, K, outbufdev(b), gen, 0, nullptr), "launch merge_shards");
@@ -2968,15 +3054,17 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         if (trace) tr_wait.push_back(std::chrono::duration<double, std::micro>(th - tw).count());
         return;
       }
-      hipchk(hipStreamSynchronize(s), "sync window");
+      sync_stream("sync window");
       last_blob = outbuf(b);
       if (use_exchange && !pipelined) {
+        const auto tx = std::chrono::steady_clock::now();
         if (ctx->exchange(ctx->exchange_user, ctx->h_own.p, outbuf(b), bytes) != 0)
           raise(PE_ERCCL, "exchange callback failed");
+        ctx->stats.xchg_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tx).count();
         if (dev_merge) {   // the gathered blob (pinned) merged by the device into h_merged
           hipchk(merge_fn(s, outbufdev(b), ctx->world, Wg, K, ctx->h_merged.dev, 0u, 0, nullptr),
                  "launch merge_shards");
-          hipchk(hipStreamSynchronize(s), "sync merge");
+          sync_stream("sync merge");
           last_blob = ctx->h_merged.p;
         }
       }
@@ -3179,17 +3267,17 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       // done, or speculation dropped: finish the device work, apply what is left, in order (one
       // launch per window: a node may be in several windows' updates)
       if (xworker) xworker->wait();   // (its merge launch first: it is stream work too)
-      hipchk(hipStreamSynchronize(s), "sync speculative");
+      sync_stream("sync speculative");
       for (; n_app < hist.size(); ++n_app) {   // (depth > 1 only; slot 0 is rewritten after each)
         enqueue_apply(hist[n_app], 0);
-        hipchk(hipStreamSynchronize(s), "sync apply");
+        sync_stream("sync apply");
       }
       enqueue_apply(upd, 0);
       if (R.done()) break;
       restart();
     }
     if (xworker) xworker->wait();
-    hipchk(hipStreamSynchronize(s), "sync greedy");
+    sync_stream("sync greedy");
     walk_drop_pending(ctx);   // (the next call rebuilds in line anyway)
     if (walk) {
       unsigned long long wc[2] = {0, 0};

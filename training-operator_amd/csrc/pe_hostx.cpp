@@ -33,7 +33,7 @@ namespace {
 
 constexpr uint64_t kMagic = 0x70655f6878303031ull;   // "pe_hx001"
 constexpr size_t kHdr = 4096;
-constexpr int kZcMaxWorld = 32;
+constexpr int kZcMaxWorld = pe::HX_ZC_MAX_WORLD;
 
 struct Hdr {
   std::atomic<uint64_t> magic;

@@ -23,6 +23,9 @@
 
 namespace pe {
 
+// the most ranks a segment runs zero-copy windows for (its consumed[] counters; pe_hostx.cpp)
+constexpr int HX_ZC_MAX_WORLD = 32;
+
 struct HxWindow {
   uint8_t* dev = nullptr;    // device address of the phase's slot 0 (slot r at dev + r * slot)
   uint8_t* host = nullptr;   // the same bytes, host address

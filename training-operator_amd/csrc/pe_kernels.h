@@ -363,6 +363,9 @@ hipError_t launch_merge_ranked(hipStream_t s, const uint8_t* gath, int world, in
                                int64_t rank_stride = 0, const uint64_t* xstatus = nullptr);
 // Wg empty lists (n = 0, limit = NO_KEY), signalled with gen
 hipError_t launch_empty_groups(hipStream_t s, int Wg, int K, uint8_t* out, uint32_t gen);
+// Test knob (PE_TEST_STALL_*): one thread that holds the stream for `ticks` of wall_clock64 (100 MHz),
+// sleeping between polls -- bounded, so the stream always drains
+hipError_t launch_stall(hipStream_t s, int64_t ticks);
 // One block per group: overlay + walk, exact top-K keys and limit, same blob as merge.  gen != 0:
 // each group's header.flags is set to gen after its keys, n and limit are visible to the host
 // (system-scope release; out is pinned host memory the host polls per group).

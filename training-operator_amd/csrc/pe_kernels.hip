@@ -1842,6 +1842,17 @@ __global__ __launch_bounds__(64) void empty_groups_kernel(int Wg, int K, uint8_t
   write_group(nullptr, 0, 0, NO_KEY, K, blockIdx.x, out, gen);
 }
 
+__global__ __launch_bounds__(64) void stall_kernel(int64_t ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+hipError_t launch_stall(hipStream_t s, int64_t ticks) {
+  if (ticks <= 0 || ticks > (int64_t)30 * 100000000) return hipErrorInvalidValue;   // at most 30 s
+  hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, s, ticks);
+  return hipGetLastError();
+}
+
 hipError_t launch_empty_groups(hipStream_t s, int Wg, int K, uint8_t* out, uint32_t gen) {
   if (Wg <= 0) return hipSuccess;
   hipLaunchKernelGGL(empty_groups_kernel, dim3(Wg), dim3(64), 0, s, Wg, K, out, gen);

@@ -390,10 +390,17 @@ void WindowFeed::wait(size_t w) {
       advance();
       if (w < parsed_.load(std::memory_order_relaxed)) break;
     }
-    if ((spin & 4095) == 0 && idle && !idle(idle_user)) {
-      advance();   // the device is idle: every group it will ever signal is visible now
-      if (w < parsed_.load(std::memory_order_relaxed)) break;
-      throw std::runtime_error("walk window: group " + std::to_string(w) + " was never signalled");
+    if ((spin & 4095) == 0) {
+      if (idle && !idle(idle_user)) {
+        advance();   // the device is idle: every group it will ever signal is visible now
+        if (w < parsed_.load(std::memory_order_relaxed)) break;
+        throw std::runtime_error("walk window: group " + std::to_string(w) + " was never signalled");
+      }
+      if (timeout_s > 0 &&
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+        throw CollectiveTimeout("RCCL window: group " + std::to_string(w) + " not merged within " +
+                                std::to_string(timeout_s) +
+                                " s -- its all-gather is stuck (a peer stalled or was lost; PE_RCCL_TIMEOUT_S)");
     }
   }
   spin_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -708,6 +715,13 @@ void Resolver::finish_job(bool ok) {
     }
     job_status_[j] = 1;
     ++jobs_failed_;
+  }
+  // the states recorded for rollbacks so far belong to this job's windows: a later job rolls back
+  // only nodes it placed on, whose states are recorded after it started (bounded memory)
+  if (!changed_.empty()) {
+    changed_slot_.clear(changed_gid_.begin(), changed_gid_.end());
+    changed_.clear();
+    changed_gid_.clear();
   }
   ++oi_;
   p_ = 0;
@@ -1042,8 +1056,12 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     updates.push_back(u);
     if (!mirror_.nodes) {   // (record-form lists: the resolver keeps the states it gave for rollbacks)
       const int32_t c = changed_slot_.insert(u.gid, (int32_t)changed_.size());
-      if (c == (int32_t)changed_.size()) changed_.push_back(st);
-      else changed_[(size_t)c] = st;
+      if (c == (int32_t)changed_.size()) {
+        changed_.push_back(st);
+        changed_gid_.push_back(u.gid);
+      } else {
+        changed_[(size_t)c] = st;
+      }
     }
   }
   for (size_t i = 0; i < dirty_.size(); ++i) any_[(size_t)dirty_.gid[i] >> 6] = 0;   // (whole words: every bit set is listed)

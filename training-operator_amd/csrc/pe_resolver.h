@@ -131,6 +131,12 @@ void parse_window_keys(const uint8_t* blob, int n_shards, int n_groups, int K, s
 struct ExchangeError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
+// A window of the RCCL transport did not arrive within PE_RCCL_TIMEOUT_S -- its collective is stuck
+// (a peer lost mid-batch keeps the stream busy, so the feed's idle test never fires): the engine
+// aborts the communicator and reports PE_ERCCL
+struct CollectiveTimeout : ExchangeError {
+  using ExchangeError::ExchangeError;
+};
 
 class WindowFeed {
  public:
@@ -144,6 +150,9 @@ class WindowFeed {
   void wait(size_t w);
   bool (*idle)(void*) = nullptr;
   void* idle_user = nullptr;
+  // > 0: wait() gives up after this many seconds blocked on one group, busy device or not, and
+  // throws CollectiveTimeout (the RCCL transport; the other transports have bounds of their own)
+  double timeout_s = 0;
   double spin_ms() const { return spin_ms_; }   // time spent blocked in wait() since reset
  private:
   bool signalled(size_t w) const;
@@ -431,8 +440,10 @@ class Resolver {
   // resolved window), else -- record-form lists without a mirror (pe_resolver_* ABI) -- the last state
   // this resolver gave the node in an earlier window (changed_).
   NodeState current_state(int64_t gid) const;
+  // (cleared when a job finishes: only the in-flight job can roll back what they record)
   IdMap changed_slot_;
   std::vector<NodeState> changed_;
+  std::vector<int64_t> changed_gid_;
   int64_t jobs_placed_ = 0, jobs_failed_ = 0, pods_placed_ = 0, rescans_ = 0;
 };
 

@@ -47,7 +47,8 @@ class PeStats(ctypes.Structure):
                 ("fit_runs_lds", ctypes.c_int64), ("fit_runs_sets", ctypes.c_int64), ("walk_rounds", ctypes.c_int64),
                 ("walk_overlay", ctypes.c_int64), ("walk_groups", ctypes.c_int64), ("walk_prepass", ctypes.c_int64),
                 ("walk_ms", ctypes.c_double), ("walk_pend_updates", ctypes.c_int64),
-                ("xchg_zc_windows", ctypes.c_int64)]
+                ("xchg_zc_windows", ctypes.c_int64), ("xchg_wait_ms", ctypes.c_double),
+                ("xchg_merge_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
