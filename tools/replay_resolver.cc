@@ -62,7 +62,7 @@ int main(int argc, char** argv) {
   for (int r = 0; r < reps; ++r) {
     const auto t0 = std::chrono::steady_clock::now();
     pe::Resolver R(J, jgo.data(), pri.data(), cnt.data(), req.data(), need.data());
-    std::vector<pe::NodeState> mirror = mirror0;
+    std::vector<pe::NodeState, pe::HugeAlloc<pe::NodeState>> mirror(mirror0.begin(), mirror0.end());   // (as the engine's)
     R.set_mirror(pe::Mirror{mirror.data(), N});
     std::vector<pe::GroupCands> cands;
     std::vector<pe::Update> upd;

@@ -388,7 +388,7 @@ struct pe_ctx {
   bool loaded = false;
   // host mirror of the GLOBAL inventory (node states by id, and the reset copy): the greedy
   // windows ship candidate keys only and the resolver reads node states here
-  std::vector<pe::NodeState> m_nodes, m_nodes0;
+  std::vector<pe::NodeState, pe::HugeAlloc<pe::NodeState>> m_nodes, m_nodes0;   // (2 MiB pages: random reads)
   DevBuf<int64_t> res0, res;
   DevBuf<uint32_t> labels;
   DevBuf<int32_t> island;

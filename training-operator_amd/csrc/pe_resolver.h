@@ -13,6 +13,8 @@
 #include <sched.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <sys/mman.h>
 
 #include <atomic>
 #include <condition_variable>
@@ -37,6 +39,37 @@ constexpr int RD = 4;
 struct alignas(PE_NODESTATE_ALIGN) NodeState {
   int64_t res[RD];
   uint32_t labels;
+};
+
+// Allocator of the host mirror (one 64-B record per node of the global inventory, 64 MB at 1M nodes,
+// read at random ids by the resolver): 2 MiB-aligned and marked MADV_HUGEPAGE, so its reads do not
+// also miss the TLB (4 KiB pages: 16k pages for 1M nodes, several times the L2 TLB).  Small arrays
+// and PE_NO_HUGE=1 (A/B) take ordinary pages.
+template <class T>
+struct HugeAlloc {
+  using value_type = T;
+  HugeAlloc() = default;
+  template <class U>
+  HugeAlloc(const HugeAlloc<U>&) {}
+  T* allocate(size_t n) {
+    constexpr size_t kHuge = (size_t)2 << 20;
+    size_t bytes = n * sizeof(T);
+    const bool huge = bytes >= 2 * kHuge && !getenv("PE_NO_HUGE");
+    size_t align = alignof(T) < 64 ? 64 : alignof(T);
+    if (huge) {
+      bytes = (bytes + kHuge - 1) / kHuge * kHuge;
+      align = kHuge;
+    }
+    void* p = nullptr;
+    if (posix_memalign(&p, align, bytes ? bytes : align) != 0) throw std::bad_alloc();
+    if (huge) (void)madvise(p, bytes, MADV_HUGEPAGE);
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t) { free(p); }
+  template <class U>
+  bool operator==(const HugeAlloc<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const HugeAlloc<U>&) const { return false; }
 };
 
 // One candidate record of the pe_resolver_* ABI blob (placement.h): key + the node's residual
