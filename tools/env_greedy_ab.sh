@@ -12,6 +12,6 @@ for i in $(seq $reps); do for spec in "$@"; do
 import json, sys
 g = json.loads(open("gpurun_out/eab.json").read().strip().splitlines()[-1])["greedy"]
 print(f'{sys.argv[1]:<8} {g["ms_per_batch"]:6.2f} ms  {g["gang_placements_per_s"]:8.0f}/s  wait {g["device_wait_ms_per_batch"]:.2f}'
-      f'  host {g["host_resolve_ms_per_batch"]:.2f}  walk {g["roofline"]["walk_ms_per_batch"]:.2f}', flush=True)
+      f'  host {g["host_resolve_ms_per_batch"]:.2f}  walk {g["roofline"].get("warm", {}).get("walk_ms_per_batch", float("nan")):.2f}', flush=True)
 PY
 done; done

@@ -1992,6 +1992,24 @@ hipError_t launch_walk_build(hipStream_t s, const int64_t* res, int64_t stride, 
   return hipGetLastError();
 }
 
+// Appends of one walk step: positions from the block-uniform total T0 of the keys before the step
+// plus a per-step counter (one LDS atomic per wave).  The walk rotates three counters so that no
+// barrier is needed between reading a step's count and the next step's appends: step t appends to
+// wcnt[t % 3], every thread reads it after step t's barrier (before reaching the next one), and
+// thread 0 zeroes wcnt[(t + 1) % 3] -- last read before step t - 1's barrier -- during step t.  (With
+// one shared total, a thread that skipped the stop test could append the next step's keys before a
+// slower wave had read the step's total: the threads' views of T diverged.)  Keys past MG_CAP are
+// counted but dropped, as in topk_append.
+__device__ __forceinline__ void step_append(TopkShared& s, int T0, int* cnt, uint64_t k, bool take) {
+  const uint64_t bal = __ballot(take);
+  if (bal == 0) return;
+  const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+  int base = 0;
+  if (take && rank == 0) base = atomicAdd(cnt, __popcll(bal));
+  base = T0 + __shfl(base, __ffsll((unsigned long long)bal) - 1, 64);
+  if (take && base + rank < MG_CAP) s.keys[base + rank] = k;
+}
+
 #ifdef PE_WALK_PROF   // phase timings of walk_kernel (wall clock ticks, summed over blocks), diagnostics build only
 __device__ unsigned long long walk_prof[16];
 #define WPT(i) unsigned long long wpt##i = wall_clock64()
@@ -2016,7 +2034,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   static_assert(WK_ROUND == MG_THREADS, "the walk uses the merge's block-wide selection");
   __shared__ TopkShared s;
   __shared__ uint32_t cbits[WK_MAXR / 32];
-  __shared__ int start_cnt, below[2];
+  __shared__ int start_cnt, below[2], wcnt[3];
   const int g = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   WPT(0);
@@ -2037,6 +2055,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
     s.total = 0;
     start_cnt = 0;
     below[0] = below[1] = 0;
+    wcnt[0] = wcnt[1] = wcnt[2] = 0;
   }
   __syncthreads();
   if (walk) {
@@ -2064,39 +2083,21 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
     for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
     if (lane == 0 && cnt) atomicAdd(&start_cnt, cnt);
   }
+  __syncthreads();   // (start_cnt and the candidate-round bitmap, read block-uniformly below)
   WPT(1);
-  // overlay: every node changed since the sort (and the saturating ones), current values
-  // OV entries per thread between barriers (the overlay holds up to resort_nodes entries, and up to
-  // ~1.5 x resort_nodes while a side-stream rebuild is pending: one barrier, append and compaction
-  // check per 4096 instead of per 1024)
-  constexpr int OV = 4;
-  const int no = *w.ovl_n;
-  for (int i0 = 0; i0 < no; i0 += OV * WK_ROUND) {
-    uint64_t k[OV];
-#pragma unroll
-    for (int u = 0; u < OV; ++u) {
-      const int i = i0 + u * WK_ROUND + tid;
-      k[u] = NO_KEY;
-      if (i < no)   // the overlay keeps its own state copy: independent, coalesced loads
-        k[u] = node_key(w.ovl_res[i], w.ovl_res[w.sstride + i], w.ovl_res[2 * w.sstride + i],
-                        w.ovl_res[3 * w.sstride + i], w.ovl_lab[i], q0, q1, q2, q3, need, id_base + (uint64_t)w.ovl[i]);
-    }
-#pragma unroll
-    for (int u = 0; u < OV; ++u) topk_append(s, k[u], k[u] != NO_KEY);
-    __syncthreads();
-    if (s.total > MG_CAP - OV * WK_ROUND) {   // keep the K + 1 smallest (the rest can never matter)
-      const int T = s.total;
-      const uint64_t* sk = topk_sort(s, T, K);
-      const int m = T < K + 1 ? T : K + 1;
-      uint64_t v = tid < m ? sk[tid] : 0;
-      __syncthreads();
-      if (tid < m) s.keys[tid] = v;
-      if (tid == 0) s.total = m;
-      __syncthreads();
-    }
-  }
-  __syncthreads();
-  WPT(2);
+  // The sorted rounds first, the overlay after them.  The walk stops once >= K + 1 of ITS keys lie
+  // below X (every unvisited round's keys are >= X); the overlay then appends only keys below that
+  // xstop -- a key >= xstop can never be among the K + 1 smallest -- instead of every fitting overlay
+  // node ahead of the walk (round 4: 7.3k overlay entries per group, about half of the keys the
+  // selection sorted).  Exact either way: the K + 1 smallest keys of (walked rounds + overlay) are
+  // all below xstop, and every key below it is collected.
+  //
+  // Stop test without rescanning every collected key (it was O(T) per step, quadratic in the long
+  // walks that set a launch's length): a round r's keys are <= rmin(next candidate round) - KQ
+  // (K(n) <= every later sorted key, key <= K(n) - (s(q) << 24)), so once a step's bound lies below
+  // the test's X, every key that step appended is below every later X too (X only grows): it is
+  // counted once (cnt_certain) and not read again.  Only the keys of the last few steps, whose bound
+  // is not below X yet, are compared -- they sit at [lo_idx, T), appended after the certain ones.
   bool done = !walk;
   int rounds = 0;
   int64_t r = walk ? (start_cnt > 0 ? start_cnt - 1 : 0) : nr;
@@ -2113,11 +2114,54 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   if (!done) r = next_round(r);
   uint64_t xstop = NO_KEY;
   int tests = 0;
+  int lo_idx = 0, cnt_certain = 0;   // keys [0, lo_idx): below every X from now on (block-uniform)
+  constexpr int PEND = 4;            // pending steps, oldest first: end index and key bound
+  int pend_n = 0;
+  int pend_end[PEND];
+  uint64_t pend_b[PEND];
+  auto pend_push = [&](int end, uint64_t b) {
+    if (pend_n == PEND) {            // merge the two oldest (contiguous ranges, bounds ascending)
+#pragma unroll
+      for (int i = 0; i + 1 < PEND; ++i) {
+        pend_end[i] = pend_end[i + 1];
+        pend_b[i] = pend_b[i + 1];
+      }
+      --pend_n;
+    }
+#pragma unroll
+    for (int i = 0; i < PEND; ++i)
+      if (i == pend_n) {
+        pend_end[i] = end;
+        pend_b[i] = b;
+      }
+    ++pend_n;
+  };
+  int Tcur = 0;      // keys collected so far (block-uniform)
+  int step = 0;      // append steps so far (walk and overlay): counter wcnt[step % 3]
+  auto compact = [&]() {   // keep the K + 1 smallest of the Tcur keys; ends with a barrier
+    const int T2 = Tcur < MG_CAP ? Tcur : MG_CAP;
+    const uint64_t* sk = topk_sort(s, T2, K);
+    const int m = T2 < K + 1 ? T2 : K + 1;
+    uint64_t v = tid < m ? sk[tid] : 0;
+    __syncthreads();
+    if (tid < m) s.keys[tid] = v;
+    __syncthreads();
+    Tcur = m;
+    return m;
+  };
+  auto step_begin = [&]() -> int* {   // this step's counter; the one after the next zeroed
+    if (tid == 0) wcnt[(step + 1) % 3] = 0;
+    return &wcnt[step % 3];
+  };
+  auto step_end = [&]() {             // after the step's barrier
+    Tcur += wcnt[step % 3];
+    ++step;
+  };
   // the next step's first round and its smallest key are found during the current step (the load
   // in flight with the step's node loads): the stop test does not wait for its own load
   uint64_t rm_r = !done && r < nr ? w.rmin[r] : 0;
   while (!done && r < nr) {
-    const int T = s.total;
+    const int T = Tcur < MG_CAP ? Tcur : MG_CAP;
     if (T >= K + 1) {                      // stop once K + 1 keys lie below every unvisited key
 #ifdef PE_WALK_NO_RM_PREFETCH   // (A/B)
       const uint64_t rm = w.rmin[r];
@@ -2125,8 +2169,38 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
       const uint64_t rm = rm_r;
 #endif
       const uint64_t X = rm > KQ2 ? rm - KQ2 : 0;
+      while (pend_n > 0 && pend_b[0] < X) {   // a whole step below X: certain from now on
+        cnt_certain += pend_end[0] - lo_idx;
+        lo_idx = pend_end[0];
+#pragma unroll
+        for (int i = 0; i + 1 < PEND; ++i) {
+          pend_end[i] = pend_end[i + 1];
+          pend_b[i] = pend_b[i + 1];
+        }
+        --pend_n;
+      }
+#ifdef PE_WALK_CHECK
+      if (cnt_certain >= K + 1) {
+        __shared__ int full2;
+        if (tid == 0) full2 = 0;
+        __syncthreads();
+        int cf = 0;
+        for (int i = tid; i < T; i += WK_ROUND) cf += s.keys[i] < X;
+        for (int off = 32; off >= 1; off >>= 1) cf += __shfl_xor(cf, off, 64);
+        if (lane == 0 && cf) atomicAdd(&full2, cf);
+        __syncthreads();
+        if (tid == 0 && full2 < cnt_certain)
+          printf("walk check: g %d early full %d < certain %d (lo_idx %d T %d X %llx)\n", g, full2, cnt_certain, lo_idx, T,
+                 (unsigned long long)X);
+        __syncthreads();
+      }
+#endif
+      if (cnt_certain >= K + 1) {
+        xstop = X;
+        break;
+      }
       int c = 0;
-      for (int i = tid; i < T; i += WK_ROUND) c += s.keys[i] < X;
+      for (int i = lo_idx + tid; i < T; i += WK_ROUND) c += s.keys[i] < X;
       for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
       // two counters used in turn: the one for the next test is zeroed after this test's barrier (every
       // thread read it at the previous test, and an append barrier lies between) -- one barrier per test
@@ -2135,7 +2209,23 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
       const int nb = below[tests & 1];
       if (tid == 0) below[(tests + 1) & 1] = 0;
       ++tests;
-      if (nb >= K + 1) {
+#ifdef PE_WALK_CHECK   // (diagnostics: the incremental count equals a full count)
+      {
+        __shared__ int full;
+        if (tid == 0) full = 0;
+        __syncthreads();
+        int cf = 0;
+        for (int i = tid; i < T; i += WK_ROUND) cf += s.keys[i] < X;
+        for (int off = 32; off >= 1; off >>= 1) cf += __shfl_xor(cf, off, 64);
+        if (lane == 0 && cf) atomicAdd(&full, cf);
+        __syncthreads();
+        if (tid == 0 && full != cnt_certain + nb)
+          printf("walk check: g %d full %d != certain %d + %d (lo_idx %d T %d pend %d X %llx)\n", g, full, cnt_certain,
+                 nb, lo_idx, T, pend_n, (unsigned long long)X);
+        __syncthreads();
+      }
+#endif
+      if (cnt_certain + nb >= K + 1) {
         xstop = X;                         // >= K + 1 collected keys lie below it: the rest never matter
         break;
       }
@@ -2176,28 +2266,53 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
 #endif
       }
     }
+    int* const cnt = step_begin();
 #pragma unroll
     for (int u = 0; u < WK_MULTI; ++u)
-      if (u < nstep) topk_append(s, k[u], k[u] != NO_KEY);
+      if (u < nstep) step_append(s, Tcur, cnt, k[u], k[u] != NO_KEY);
     __syncthreads();
+    step_end();
+    // this step's keys: [previous total, Tcur), each <= rmin(r_next) - KQ (the last round has no
+    // bound: its keys stay pending)
+    pend_push(Tcur, r_next < nr ? (rm_next > KQ ? rm_next - KQ : 0) : NO_KEY);
     // (room for the next step's appends.  Cutting long walks' keys to K + 1 early, at 1024 or 2048,
     // with later appends filtered below the (K+1)-th, was measured slower: 62-64 vs 52 us per launch)
-    if (s.total > MG_CAP - WK_MULTI * WK_ROUND) {
-      const int T2 = s.total;
-      const uint64_t* sk = topk_sort(s, T2, K);
-      const int m = T2 < K + 1 ? T2 : K + 1;
-      uint64_t v = tid < m ? sk[tid] : 0;
-      __syncthreads();
-      if (tid < m) s.keys[tid] = v;
-      if (tid == 0) s.total = m;
-      __syncthreads();
+    if (Tcur > MG_CAP - WK_MULTI * WK_ROUND) {
+      const int m = compact();
+      lo_idx = cnt_certain = pend_n = 0;   // the kept keys, ascending: pending up to the largest
+      pend_push(m, m > 0 ? s.keys[m - 1] : 0);
     }
     r = r_next;
     rm_r = rm_next;
     rounds += nstep;
   }
+  WPT(2);
+  // overlay: every node changed since the sort (and the saturating ones), current values; only keys
+  // below xstop.  OV entries per thread between barriers (the overlay holds up to resort_nodes
+  // entries, and up to ~1.5 x resort_nodes while a side-stream rebuild is pending: one barrier,
+  // append and compaction check per 4096 instead of per 1024)
+  constexpr int OV = 4;
+  const int no = *w.ovl_n;
+  for (int i0 = 0; i0 < no; i0 += OV * WK_ROUND) {
+    uint64_t k[OV];
+#pragma unroll
+    for (int u = 0; u < OV; ++u) {
+      const int i = i0 + u * WK_ROUND + tid;
+      k[u] = NO_KEY;
+      if (i < no)   // the overlay keeps its own state copy: independent, coalesced loads
+        k[u] = node_key(w.ovl_res[i], w.ovl_res[w.sstride + i], w.ovl_res[2 * w.sstride + i],
+                        w.ovl_res[3 * w.sstride + i], w.ovl_lab[i], q0, q1, q2, q3, need, id_base + (uint64_t)w.ovl[i]);
+    }
+    int* const cnt = step_begin();
+#pragma unroll
+    for (int u = 0; u < OV; ++u) step_append(s, Tcur, cnt, k[u], k[u] < xstop);   // (NO_KEY never is)
+    __syncthreads();
+    step_end();
+    if (Tcur > MG_CAP - OV * WK_ROUND) compact();
+  }
+  __syncthreads();
   WPT(3);
-  const int T = s.total;
+  const int T = Tcur < MG_CAP ? Tcur : MG_CAP;
   const uint64_t* sk = topk_sort(s, T, K, xstop);
   WPT(4);
   write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : NO_KEY, K, g, out, gen);
@@ -2243,10 +2358,10 @@ hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(p, HIP_SYMBOL(walk_prof), sizeof(p));
     const double n = (double)p[5], us = 100.0;   // wall_clock64 runs at 100 MHz: ticks / 100 = us
-    fprintf(stderr, "walk prof over %.0f blocks (us/block): setup+prepass %.2f overlay %.2f walk %.2f sort %.2f write %.2f"
+    fprintf(stderr, "walk prof over %.0f blocks (us/block): setup+prepass %.2f walk %.2f overlay %.2f sort %.2f write %.2f"
                     " | overlay %.0f rounds %.2f T %.0f\n", n, p[0] / n / us, p[1] / n / us, p[2] / n / us,
             p[3] / n / us, p[4] / n / us, p[6] / n, p[7] / n, p[8] / n);
-    fprintf(stderr, "walk prof max: block %.2f us setup %.2f overlay %.2f walk %.2f sort %.2f | rounds %llu T %llu\n",
+    fprintf(stderr, "walk prof max: block %.2f us setup %.2f walk %.2f overlay %.2f sort %.2f | rounds %llu T %llu\n",
             p[9] / us, p[15] / us, p[10] / us, p[11] / us, p[12] / us, p[13], p[14]);
     unsigned long long t[8];
     (void)hipMemcpyFromSymbol(t, HIP_SYMBOL(topk_prof), sizeof(t));
