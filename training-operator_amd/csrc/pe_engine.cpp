@@ -484,10 +484,11 @@ struct pe_ctx {
     DevBuf<int64_t> sr, rmax;
     DevBuf<uint32_t> sl, pos, ror, inovl, ovidx, ovlab;
     DevBuf<int64_t> ovres;
+    DevBuf<uint64_t> ovkn;
     DevBuf<int32_t> ovl, ovln;
     void release() {
       sk.release(); rmin.release(); sr.release(); rmax.release(); sl.release(); pos.release(); ror.release();
-      inovl.release(); ovidx.release(); ovlab.release(); ovres.release(); ovl.release(); ovln.release();
+      inovl.release(); ovidx.release(); ovlab.release(); ovres.release(); ovkn.release(); ovl.release(); ovln.release();
     }
   } ws[2];
   int w_cur = 0;
@@ -2265,6 +2266,7 @@ static pe::WalkIndex walk_index(pe_ctx* ctx, int set) {
   w.ovl_idx = x.ovidx.p;
   w.ovl_res = x.ovres.p;
   w.ovl_lab = x.ovlab.p;
+  w.ovl_kn = x.ovkn.p;
   w.stat = ctx->w_stat.p;
   w.sstride = ctx->stride;
   w.nr = (ctx->Ns + pe::WK_ROUND - 1) / pe::WK_ROUND;
@@ -2292,6 +2294,7 @@ static size_t walk_set_prepare(pe_ctx* ctx, int set, hipStream_t s) {
   hipchk(x.ovidx.ensure(st), "alloc overlay");
   hipchk(x.ovlab.ensure(st), "alloc overlay");
   hipchk(x.ovres.ensure((size_t)pe::D * st), "alloc overlay");
+  hipchk(x.ovkn.ensure(st), "alloc overlay");
   size_t tb = 0;
   hipchk(pe::sort_keys_u64(nullptr, &tb, ctx->w_kin.p, x.sk.p, Ns, s), "sort size");
   hipchk(ctx->w_temp.ensure(tb), "alloc sort scratch");

@@ -321,6 +321,7 @@ struct WalkIndex {
   uint32_t* ovl_idx;   // [stride] a node's overlay slot (valid while in_ovl)
   int64_t* ovl_res;    // [4][sstride] residuals by overlay slot (kept current by apply)
   uint32_t* ovl_lab;   // [stride] labels by overlay slot
+  uint64_t* ovl_kn;    // [stride] K(n) of each overlay slot's state (node_prep; KEY_SLOW: always evaluated)
   unsigned long long* stat;   // nullable: [0] += rounds walked, [1] += overlay entries, per group
   int64_t sstride, nr;
 };

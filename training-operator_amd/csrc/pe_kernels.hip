@@ -1868,14 +1868,17 @@ hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt,
 
 // ------------------------------------------------------------------ sorted walk (greedy default)
 
-// Appends local node n with state (r, lab) to the overlay (slot, state copy, membership).
-__device__ __forceinline__ void overlay_add(const WalkIndex& w, int64_t n, const int64_t (&r)[D], uint32_t lab) {
+// Appends local node n with state (r, lab) and node-only key Kn to the overlay (slot, state copy,
+// membership).
+__device__ __forceinline__ void overlay_add(const WalkIndex& w, int64_t n, const int64_t (&r)[D], uint32_t lab,
+                                            uint64_t Kn) {
   const int32_t i = atomicAdd(w.ovl_n, 1);
   w.ovl[i] = (int32_t)n;
   w.ovl_idx[n] = (uint32_t)i;
 #pragma unroll
   for (int d = 0; d < D; ++d) w.ovl_res[d * w.sstride + i] = r[d];
   w.ovl_lab[i] = lab;
+  w.ovl_kn[i] = Kn;
 }
 
 __global__ __launch_bounds__(256) void walk_prep_kernel(const int64_t* __restrict__ res, int64_t stride, int64_t Ns,
@@ -1896,7 +1899,7 @@ __global__ __launch_bounds__(256) void walk_prep_kernel(const int64_t* __restric
       slow[n] = 1u;                  // (side-stream rebuild: walk_switch adds it)
     } else {
       w.in_ovl[n] = 1u;
-      overlay_add(w, n, r, labels[n]);
+      overlay_add(w, n, r, labels[n], KEY_SLOW);
     }
   }
   kin[n] = k;
@@ -1924,7 +1927,7 @@ __global__ __launch_bounds__(256) void walk_switch_kernel(const int64_t* __restr
   } else if (slow[n]) {
     const int64_t r[D] = {res[n], res[stride + n], res[2 * stride + n], res[3 * stride + n]};
     nx.in_ovl[n] = 1u;
-    overlay_add(nx, n, r, labels[n]);
+    overlay_add(nx, n, r, labels[n], KEY_SLOW);
   }
 }
 
@@ -2291,15 +2294,25 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   // below xstop.  OV entries per thread between barriers (the overlay holds up to resort_nodes
   // entries, and up to ~1.5 x resort_nodes while a side-stream rebuild is pending: one barrier,
   // append and compaction check per 4096 instead of per 1024)
+  // An entry is read in full only when its node-only key allows a key below xstop: a fit needs
+  // K(n) >= KQ, and its key is >= K(n) - KQ2 (KEY_SLOW entries always) -- 8 B per entry instead of
+  // 44 (the overlay phase streamed ~300 KB per group: CU-bandwidth-bound, not latency-bound).
   constexpr int OV = 4;
   const int no = *w.ovl_n;
+  const uint64_t klim = xstop > NO_KEY - KQ2 ? NO_KEY : xstop + KQ2;   // (NO_KEY: no bound)
   for (int i0 = 0; i0 < no; i0 += OV * WK_ROUND) {
+    uint64_t kn[OV];
+#pragma unroll
+    for (int u = 0; u < OV; ++u) {
+      const int i = i0 + u * WK_ROUND + tid;
+      kn[u] = i < no ? w.ovl_kn[i] : 0;
+    }
     uint64_t k[OV];
 #pragma unroll
     for (int u = 0; u < OV; ++u) {
       const int i = i0 + u * WK_ROUND + tid;
       k[u] = NO_KEY;
-      if (i < no)   // the overlay keeps its own state copy: independent, coalesced loads
+      if (i < no && (kn[u] == KEY_SLOW || (kn[u] >= KQ && kn[u] < klim)))   // the overlay keeps its own state copy
         k[u] = node_key(w.ovl_res[i], w.ovl_res[w.sstride + i], w.ovl_res[2 * w.sstride + i],
                         w.ovl_res[3 * w.sstride + i], w.ovl_lab[i], q0, q1, q2, q3, need, id_base + (uint64_t)w.ovl[i]);
     }
@@ -2386,10 +2399,10 @@ __global__ __launch_bounds__(256) void apply_kernel(int64_t* __restrict__ res, i
   const int64_t node = u[0];
 #pragma unroll
   for (int d = 0; d < D; ++d) res[d * stride + node] = u[1 + d];
+  uint64_t K;                                 // the node-only key of the new state
+  uint32_t l1, l3;
+  node_prep(u[1], u[2], u[3], u[4], id_base + (uint64_t)node, K, l1, l3);
   if (kn) {                                   // keep the scan's node-only score terms current
-    uint64_t K;
-    uint32_t l1, l3;
-    node_prep(u[1], u[2], u[3], u[4], id_base + (uint64_t)node, K, l1, l3);
     kn[node] = K;
     lo[node] = l1;
     lo[stride + node] = l3;
@@ -2402,19 +2415,21 @@ __global__ __launch_bounds__(256) void apply_kernel(int64_t* __restrict__ res, i
     }
     const int64_t r[D] = {u[1], u[2], u[3], u[4]};
     if (atomicExch(&w.in_ovl[node], 1u) == 0u) {
-      overlay_add(w, node, r, labels[node]);
+      overlay_add(w, node, r, labels[node], K);
     } else {                                  // already there: refresh its state copy
       const uint32_t i = w.ovl_idx[node];
 #pragma unroll
       for (int d = 0; d < D; ++d) w.ovl_res[d * w.sstride + i] = r[d];
+      w.ovl_kn[i] = K;
     }
     if (pend) {                               // the index being rebuilt: overlay only (walk_switch
       if (atomicExch(&nx.in_ovl[node], 1u) == 0u) {   // drops its sorted entry)
-        overlay_add(nx, node, r, labels[node]);
+        overlay_add(nx, node, r, labels[node], K);
       } else {
         const uint32_t i = nx.ovl_idx[node];
 #pragma unroll
         for (int d = 0; d < D; ++d) nx.ovl_res[d * nx.sstride + i] = r[d];
+        nx.ovl_kn[i] = K;
       }
     }
   }
