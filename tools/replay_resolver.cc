@@ -21,6 +21,7 @@ int main(int argc, char** argv) {
   FILE* f = std::fopen(argv[1], "rb");
   if (!f) return 2;
   const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
+  const int warm = std::getenv("REPLAY_WARM") ? std::atoi(std::getenv("REPLAY_WARM")) : 0;
   int64_t hdr[3];
   if (std::fread(hdr, 8, 3, f) != 3) return 2;
   const int64_t J = hdr[0], G = hdr[1];
@@ -76,6 +77,12 @@ int main(int argc, char** argv) {
     for (; wi < wins.size(); ++wi) {       // the resolve calls of the run, in order
       const Win& w = wins[wi];
       pe::parse_window_keys(w.blob.data(), 1, (int)w.groups.size(), K, cands);
+      if (warm) {   // REPLAY_WARM=n (experiment): the first n list entries' mirror lines cached before the resolve
+        volatile int64_t sink = 0;
+        for (const pe::GroupCands& gc : cands)
+          for (size_t i = 0; i < std::min<size_t>((size_t)warm, gc.size()); ++i) sink += mirror[gc.key(i) & 0xFFFFFF].res[0];
+        for (size_t i = 0; i < w.blob.size(); i += 64) sink += w.blob[i];
+      }
       upd.clear();
       const auto a = std::chrono::steady_clock::now();
       const double c0 = cpu_ms();
