@@ -2014,7 +2014,7 @@ __device__ __forceinline__ void step_append(TopkShared& s, int T0, int* cnt, uin
 }
 
 #ifdef PE_WALK_PROF   // phase timings of walk_kernel (wall clock ticks, summed over blocks), diagnostics build only
-__device__ unsigned long long walk_prof[16];
+__device__ unsigned long long walk_prof[32];
 #define WPT(i) unsigned long long wpt##i = wall_clock64()
 #else
 #define WPT(i)
@@ -2353,6 +2353,18 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
     atomicMax(&walk_prof[13], (unsigned long long)rounds);
     atomicMax(&walk_prof[14], (unsigned long long)T);
     atomicMax(&walk_prof[15], wpt1 - wpt0);
+    if (wpt5 - wpt0 > 3500) {   // slow blocks (> 35 us): where their time goes
+      atomicAdd(&walk_prof[16], 1ull);
+      atomicAdd(&walk_prof[17], wpt1 - wpt0);
+      atomicAdd(&walk_prof[18], wpt2 - wpt1);
+      atomicAdd(&walk_prof[19], wpt3 - wpt2);
+      atomicAdd(&walk_prof[20], wpt4 - wpt3);
+      atomicAdd(&walk_prof[21], wpt5 - wpt4);
+      atomicAdd(&walk_prof[22], (unsigned long long)rounds);
+      atomicAdd(&walk_prof[23], (unsigned long long)T);
+      atomicAdd(&walk_prof[24], (unsigned long long)no);
+      atomicAdd(&walk_prof[25], (unsigned long long)tests);
+    }
   }
 #endif
 }
@@ -2367,7 +2379,7 @@ hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const
 #ifdef PE_WALK_PROF
   static int launches = 0;
   if (++launches % 500 == 0) {
-    unsigned long long p[16];
+    unsigned long long p[32];
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(p, HIP_SYMBOL(walk_prof), sizeof(p));
     const double n = (double)p[5], us = 100.0;   // wall_clock64 runs at 100 MHz: ticks / 100 = us
@@ -2376,6 +2388,10 @@ hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const
             p[3] / n / us, p[4] / n / us, p[6] / n, p[7] / n, p[8] / n);
     fprintf(stderr, "walk prof max: block %.2f us setup %.2f walk %.2f overlay %.2f sort %.2f | rounds %llu T %llu\n",
             p[9] / us, p[15] / us, p[10] / us, p[11] / us, p[12] / us, p[13], p[14]);
+    const double ns = (double)(p[16] ? p[16] : 1);
+    fprintf(stderr, "walk prof slow blocks (> 35 us): %.0f (%.2f%%): setup %.2f walk %.2f overlay %.2f sort %.2f write %.2f"
+                    " us | rounds %.2f T %.0f overlay %.0f tests %.2f\n", (double)p[16], 100.0 * p[16] / n, p[17] / ns / us,
+            p[18] / ns / us, p[19] / ns / us, p[20] / ns / us, p[21] / ns / us, p[22] / ns, p[23] / ns, p[24] / ns, p[25] / ns);
     unsigned long long t[8];
     (void)hipMemcpyFromSymbol(t, HIP_SYMBOL(topk_prof), sizeof(t));
     const double c = (double)t[0];
