@@ -259,7 +259,12 @@ int pe_fit_mask_row_pitch(const pe_ctx* ctx, int64_t* words);
  * out_job_status[J]: PE_JOB_PLACED / PE_JOB_UNSCHEDULABLE.  Residuals are updated in place
  * (successful placements stay; failed jobs are rolled back).  Every rank of a sharded context
  * must make the same call; all ranks return the same placements.  group_need bit 31
- * (PE_NEED_ISLAND) makes the group an island group (see PE_LABEL_ISLAND). */
+ * (PE_NEED_ISLAND) makes the group an island group (see PE_LABEL_ISLAND).
+ * RCCL transport: a window whose all-gather does not complete within PE_RCCL_TIMEOUT_S seconds
+ * (environment, default 60; a peer lost mid-batch) makes the call return PE_ERCCL; the context's
+ * communicator is then aborted (ncclCommAbort, on a thread of its own: the call returns at once)
+ * and every later sharded call on the context returns PE_ERCCL -- destroy it and rebuild (e.g. on a
+ * pe_host_exchange), as bench.py does.  The host exchange's bound is PE_HX_TIMEOUT_S. */
 int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority,
                     const int32_t* group_count, const int64_t* group_req, const uint32_t* group_need,
                     int32_t* out_pod_node, int32_t* out_job_status);

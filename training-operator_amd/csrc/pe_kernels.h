@@ -299,13 +299,16 @@ hipError_t launch_merge(hipStream_t s, const uint64_t* cand, const int32_t* cnt,
 constexpr int WK_ROUND = 1024;          // sorted entries per round = walk threads per group
 constexpr int WK_MAXR = 16384;          // rounds per shard (PE_MAX_NODES / WK_ROUND)
 constexpr uint64_t WK_INVALID = ~0ull;
-// Walk steps: one round at a time for the first WK_MULTI_AFTER rounds (90 % of the groups stop within
-// them), then up to WK_MULTI candidate rounds per step (the long walks that set a launch's length).
+// Walk steps: one round at a time for the first WK_MULTI_AFTER rounds, then up to WK_MULTI candidate
+// rounds per step (their loads in flight together, one barrier and one stop test per step).  Round 5
+// (tools/walk_ab.py, interleaved, one box): 4 rounds per step after 4 single ones 43.8-45.7 us per
+// launch, 2 after 1 39.1-40.2, 2 after 0 / 2 / 4 39.8-41.1, 3 after 2 41.1-42.1 -- with the stop test
+// no longer rescanning every key, finer steps collect fewer surplus keys for the selection.
 #ifndef WK_MULTI
-#define WK_MULTI 4
+#define WK_MULTI 2
 #endif
 #ifndef WK_MULTI_AFTER
-#define WK_MULTI_AFTER 4
+#define WK_MULTI_AFTER 1
 #endif
 struct WalkIndex {
   uint64_t* sk;        // [Ns] sorted keys (WK_INVALID = not walked)

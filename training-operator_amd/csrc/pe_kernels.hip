@@ -2297,7 +2297,10 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   // An entry is read in full only when its node-only key allows a key below xstop: a fit needs
   // K(n) >= KQ, and its key is >= K(n) - KQ2 (KEY_SLOW entries always) -- 8 B per entry instead of
   // 44 (the overlay phase streamed ~300 KB per group: CU-bandwidth-bound, not latency-bound).
-  constexpr int OV = 4;
+#ifndef WK_OV
+#define WK_OV 8   // (4: the same within noise; 8 halves the barriers of a long overlay)
+#endif
+  constexpr int OV = WK_OV;
   const int no = *w.ovl_n;
   const uint64_t klim = xstop > NO_KEY - KQ2 ? NO_KEY : xstop + KQ2;   // (NO_KEY: no bound)
   for (int i0 = 0; i0 < no; i0 += OV * WK_ROUND) {
