@@ -420,7 +420,7 @@ def main(argv=None):
             if not hx:
                 names = [f"/pe_bench_{os.getpid()}_{time.time_ns() & 0xFFFFFFFF:x}" if rank == 0 else None]
                 dist.broadcast_object_list(names, src=0, group=gloo)
-                wg = args.window_groups or 128
+                wg = args.window_groups or 112
                 k = args.topk or 256
                 hx.append(HostExchange(names[0], rank, world, wg * (16 + 8 * k)))
                 dist.barrier(group=gloo)

@@ -109,7 +109,7 @@ typedef struct {
   const char* gpu_resource_name; /* resource key of dim 2, e.g. "amd.com/gpu" (informational) */
   int32_t topk;                  /* best-fit candidates kept per group and window (0 = 256; above
                                     1023 the windows take the full scan instead of the sorted walk) */
-  int32_t window_groups;         /* groups per scan window (0 = 128) */
+  int32_t window_groups;         /* groups per scan window (0 = 112) */
   int64_t window_pods;           /* pods per scan window (0 = 1024) */
   int32_t fit_path_mask;         /* allowed fit-mask kernels: bit0 int64 compare, bit1 int32 compare,
                                     bit2 dictionary-coded, bit4 bit planes (batches with more than 32

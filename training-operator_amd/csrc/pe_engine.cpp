@@ -377,7 +377,7 @@ struct pe_ctx {
   void* exchange_user = nullptr;
   void* zc_hx = nullptr;   // the shared-memory exchange whose zero-copy use the ranks agreed on (zc_ok)
   bool zc_ok = false;
-  int topk = 256, window_groups = 128;
+  int topk = 256, window_groups = 112;
   bool pipeline = true;   // greedy: scan window w+1 while the host resolves window w (greedy_flags bit0 = off)
   int64_t window_pods = 1024;
   int64_t max_nodes = 0;
@@ -785,7 +785,10 @@ int pe_create(const pe_config* cfg, pe_ctx** out) {
   ctx->exchange_user = cfg->exchange_user;
   ctx->max_nodes = cfg->max_nodes > 0 ? cfg->max_nodes : PE_MAX_NODES;
   ctx->topk = cfg->topk > 0 ? std::min(cfg->topk, pe::MG_CAP) : 256;
-  ctx->window_groups = cfg->window_groups > 0 ? cfg->window_groups : 128;
+  // 112 groups per window (round 5, 4 interleaved reps on the bench batch: 128 / 112 / 104 / 96 groups
+  // 9.53 / 9.25 / 9.53 / 9.50 ms per batch, host 7.98 / 7.65 / 7.70 / 7.38 ms -- smaller windows shrink
+  // the resolver's dirty sets, below ~112 the walk + apply chain per window outlasts the resolve)
+  ctx->window_groups = cfg->window_groups > 0 ? cfg->window_groups : 112;
   ctx->window_pods = cfg->window_pods > 0 ? cfg->window_pods : 1024;
   ctx->gpu_name = cfg->gpu_resource_name ? cfg->gpu_resource_name : "amd.com/gpu";
   ctx->fit_path_mask = cfg->fit_path_mask & (PATHS_ALL | PATH_NO_THERM | PATH_PLANES_BLOCKS);
