@@ -525,8 +525,9 @@ SeedScorer::~SeedScorer() {
 
 void SeedScorer::start(const DirtySet* seeds, const std::vector<int32_t>* groups,
                        const std::vector<GroupCands>* cands, const int64_t* scan_req, const uint32_t* need,
-                       const WindowFeed* feed) {
+                       const WindowFeed* feed, const NodeState* mirror) {
   seeds_ = seeds;
+  mirror_ = mirror;
   groups_ = groups;
   cands_ = cands;
   feed_ = feed;
@@ -631,6 +632,15 @@ void SeedScorer::loop() {
         break;
       }
       slots_[wi].gen.store(gen, std::memory_order_release);
+      if (mirror_) {   // the first non-seed entries' states, read here (see mirror_)
+        const GroupCands& gc = (*cands_)[wi];
+        if (gc.keys) {
+          int64_t sink = 0;
+          for (size_t i = slots_[wi].top.head, e = std::min(gc.size(), i + (size_t)kWarmStates); i < e; ++i)
+            sink += mirror_[gc.keys[i] & 0xFFFFFFull].res[0];
+          warm_sink_ += sink;
+        }
+      }
     }
     // done with the window: wait for stop() (state 2, acknowledged at the top of the loop)
     for (int spin = 0; state_.load(std::memory_order_acquire) == 1; ++spin)
@@ -811,7 +821,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         seeds_.upsert(u.gid, st);
       }
     }
-    scorer_.start(&seeds_, &groups, &cands, qeff_.data(), need_, feed);
+    scorer_.start(&seeds_, &groups, &cands, qeff_.data(), need_, feed, mirror_.nodes);
     for (size_t i = 0; i < seeds_.size(); ++i) any_set(seeds_.gid[i]);
   }
   if (feed) feed->advance();
@@ -856,21 +866,17 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
     t_ = RP_T();
     // Look ahead: the list lines of the group kLookLines ahead on their way; the first clean entries
     // of the group kLookStates ahead found (the dirty entries before them skipped for good -- the
-    // dirty set only grows during a resolve) and their mirror states prefetched.
+    // dirty set only grows during a resolve; the seed helper reads their mirror states).
     if (wi + kLookLines < groups.size() && have(wi + kLookLines) && cands[wi + kLookLines].keys)
       for (int l = 0; l < 2; ++l) __builtin_prefetch(cands[wi + kLookLines].keys + 8 * l);
     if (wi + kLookStates < groups.size() && have(wi + kLookStates) && cands[wi + kLookStates].keyed) {
       const size_t wn = wi + kLookStates;
       const GroupCands& gn = cands[wn];
       size_t p = useS && scorer_.ready(wn) ? scorer_.top(wn).head : 0;   // (the helper skipped the seeds)
-      int c = 0;
       while (p < gn.size() && is_dirty((int64_t)(gn.key(p) & 0xFFFFFFull))) ++p;
       head_[wn] = p;
-      for (; p < gn.size() && c < 3; ++p)
-        if (!is_dirty((int64_t)(gn.key(p) & 0xFFFFFFull))) {
-          __builtin_prefetch(&mirror_.nodes[gn.key(p) & 0xFFFFFFull]);
-          ++c;
-        }
+      // (its first clean entries' mirror states are read by the seed helper: SeedScorer::mirror_.
+      // Prefetching them here as well was ~1.5 % slower in the box replay, profiles/r17_resolver_ab.txt)
     }
     RP_ADD(la, t_);
     unsigned long long t2_ = RP_T();
@@ -977,11 +983,16 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         if (gc.keyed) {   // clean: the mirror holds the snapshot state
           st = mirror_.nodes[gid];
           // keep the next two clean entries' states on their way
-          for (int c = 0; pf < gc.size() && c < 2; ++pf)
+#ifndef PE_PLACE_PREFETCH
+#define PE_PLACE_PREFETCH 2
+#endif
+#ifndef PE_NO_PLACE_PREFETCH   // (A/B: without it the box replay took 10.6-11.1 instead of 8.2-8.5 ms)
+          for (int c = 0; pf < gc.size() && c < PE_PLACE_PREFETCH; ++pf)
             if (pf > ptr && !is_dirty((int64_t)(gc.key(pf) & 0xFFFFFFull))) {
               __builtin_prefetch(&mirror_.nodes[gc.key(pf) & 0xFFFFFFull]);
               ++c;
             }
+#endif
         } else {
           const Cand& c = gc.data[ptr];
           for (int d = 0; d < RD; ++d) st.res[d] = c.res[d];

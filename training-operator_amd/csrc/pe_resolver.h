@@ -346,7 +346,8 @@ class SeedScorer {
   // Main thread: start scoring a window (seeds, cands and the request arrays must stay unchanged
   // until stop()).
   void start(const DirtySet* seeds, const std::vector<int32_t>* groups, const std::vector<GroupCands>* cands,
-             const int64_t* scan_req, const uint32_t* need, const WindowFeed* feed = nullptr);
+             const int64_t* scan_req, const uint32_t* need, const WindowFeed* feed = nullptr,
+             const NodeState* mirror = nullptr);
   bool ready(size_t wi) const { return slots_[wi].gen.load(std::memory_order_acquire) == gen_; }
   const SeedTop& top(size_t wi) const { return slots_[wi].top; }
   // the resolver is at group wi: the helper skips what it would finish too late
@@ -380,6 +381,14 @@ class SeedScorer {
   const std::vector<int32_t>* groups_ = nullptr;
   const std::vector<GroupCands>* cands_ = nullptr;
   const WindowFeed* feed_ = nullptr;   // groups at or above feed_->parsed() are not there yet
+  // host mirror: the helper reads the states of each group's first non-seed list entries, so the
+  // resolver finds those lines in a cache of its CCD (a cross-core hit) instead of in DRAM
+  const NodeState* mirror_ = nullptr;
+#ifndef PE_WARM_STATES
+#define PE_WARM_STATES 4
+#endif
+  static constexpr int kWarmStates = PE_WARM_STATES;
+  volatile int64_t warm_sink_ = 0;   // (keeps the reads)
   const int64_t* req_ = nullptr;
   const uint32_t* need_ = nullptr;
   std::vector<uint64_t> out_;
