@@ -373,6 +373,7 @@ struct pe_ctx {
   // sharded call fails with PE_ERCCL; the caller rebuilds the context (e.g. on the host exchange)
   bool comm_aborted = false;
   std::thread comm_abort;
+  std::unique_ptr<pe::Resolver> resolver;   // the greedy's host resolver, reset per batch
   pe_allgather_fn exchange = nullptr;
   void* exchange_user = nullptr;
   void* zc_hx = nullptr;   // the shared-memory exchange whose zero-copy use the ranks agreed on (zc_ok)
@@ -2428,8 +2429,13 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     hipchk(ctx->w_stat.ensure(2), "alloc walk counters");
     hipchk(hipMemsetAsync(ctx->w_stat.p, 0, 2 * sizeof(unsigned long long), ctx->stream), "memset walk counters");
     if (walk) walk_resort(ctx);
-    pe::Resolver R(n_jobs, job_group_off, priority, group_count, group_req, group_need);
+    const auto t_prep = std::chrono::steady_clock::now();
+    // one resolver per context, reset per batch (its arrays and seed helper thread are reused)
+    if (ctx->resolver) ctx->resolver->reset(n_jobs, job_group_off, priority, group_count, group_req, group_need);
+    else ctx->resolver.reset(new pe::Resolver(n_jobs, job_group_off, priority, group_count, group_req, group_need));
+    pe::Resolver& R = *ctx->resolver;
     R.set_mirror(pe::Mirror{ctx->m_nodes.data(), ctx->n_total});
+    const auto t_res = std::chrono::steady_clock::now();
     // PE_DUMP_WINDOWS=<file>: record the batch and every window's groups + blob (host resolver
     // replay, tools/replay_resolver.cc); diagnostics only
     FILE* dump = nullptr;
@@ -2562,6 +2568,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       worker.reset(new SpinWorker(ctx->device));
       if (pin.on) worker->pin(pin.l3);
     }
+    if (pin.on) R.pin_helper(pin.l3);
     // blob buffer b (0: h_out, 1: h_out2, 2-3: h_outx): the windows scanned ahead land in their own
     // buffers while the host still resolves from the current one's
     auto outbuf = [&](int b) { return b == 0 ? ctx->h_out.p : b == 1 ? ctx->h_out2.p : ctx->h_outx[b - 2].p; };
@@ -3180,6 +3187,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       next_buf = 0;
       if (Flight* f = add_flight(R.cursor())) enqueue_window(f->groups, f->buf);
     };
+    const auto t_setup = std::chrono::steady_clock::now();
     restart();
     std::vector<pe::Update> seed, upd;
     while (!fl.empty()) {
@@ -3282,6 +3290,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (R.done()) break;
       restart();
     }
+    const auto t_loop = std::chrono::steady_clock::now();
     if (xworker) xworker->wait();
     sync_stream("sync greedy");
     walk_drop_pending(ctx);   // (the next call rebuilds in line anyway)
@@ -3306,6 +3315,14 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     ctx->stats.jobs_failed += R.jobs_failed();
     ctx->stats.last_greedy_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (trace) {
+      auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::micro>(b - a).count();
+      };
+      std::fprintf(stderr, "greedy phases (us): checks+prep %.0f resolver %.0f setup %.0f loop %.0f tail %.0f\n",
+                   us(t0, t_prep), us(t_prep, t_res), us(t_res, t_setup), us(t_setup, t_loop),
+                   us(t_loop, std::chrono::steady_clock::now()));
+    }
     return PE_OK;
   });
 }

@@ -353,6 +353,9 @@ class SeedScorer {
   // the resolver is at group wi: the helper skips what it would finish too late
   void at(size_t wi) { main_wi_.store(wi, std::memory_order_relaxed); }
   void stop();   // cancel the window and wait until the helper is idle
+  // CPUs of the helper thread (applied now, or when the thread starts); without a call the helper
+  // takes the L3 of the CPU that starts it
+  void pin(const cpu_set_t& set);
   // one group's top (any thread; out / idx are the caller's scratch)
   static void compute(const DirtySet& seeds, const GroupCands& gc, const int64_t q[RD], uint32_t need, SeedTop& top,
                       std::vector<uint64_t>& out, std::vector<int32_t>& idx);
@@ -360,6 +363,8 @@ class SeedScorer {
  private:
   void loop();
   std::unique_ptr<std::thread> th_;
+  bool have_pin_ = false;
+  cpu_set_t pin_set_;
   std::atomic<int> state_{0};            // 0 idle, 1 window posted, 2 cancel, 3 exit
   // One slot per window group, its own cache lines: the ready generation sits on the same line as
   // the top's head and first keys, so the resolver's check-and-read of a group is one line handed
@@ -399,6 +404,11 @@ class Resolver {
  public:
   Resolver(int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority, const int32_t* group_count,
            const int64_t* group_req, const uint32_t* group_need);
+  // A new batch on the same object: every per-batch state cleared, allocations (and the seed helper
+  // thread) kept -- a fresh resolver per batch page-faulted its ~1 MB of arrays and started a thread.
+  void reset(int64_t n_jobs, const int32_t* job_group_off, const int32_t* priority, const int32_t* group_count,
+             const int64_t* group_req, const uint32_t* group_need);
+  void pin_helper(const cpu_set_t& set) { scorer_.pin(set); }
 
   bool done() const { return oi_ >= (int64_t)order_.size(); }
   // Groups (global ids, count > 0) of the next window, starting at the cursor (or at `from`);
