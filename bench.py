@@ -32,7 +32,6 @@ PROFILES = os.path.join(ROOT, "profiles")
 
 METRIC = "job×node fit evals/sec + gang placements/sec, 1M-node inventory, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-L3_PEAK_GBS = 8600.0    # MI355X_MICROARCH.md: Infinity Cache, uniformly random rows of a 38 MB table, measured
 # chip-wide integer VALU issue ceiling, wave-instructions/s: profiles/r1_ubench_valu.txt
 # (v_add_u32 / v_addc_co at 8 waves per SIMD: 4.24 cycles per wave-instruction per SIMD, 256 CUs x 4 SIMDs)
 VALU_ISSUE_CEILING = 5.79e11
@@ -808,7 +807,13 @@ def main(argv=None):
                     "rounds_per_group": s["walk_rounds"] / max(1, s["walk_groups"]),
                     "overlay_per_group": s["walk_overlay"] / max(1, s["walk_groups"]), "unit": "GB/s",
                     "profile": gprof.get("profile")}
-            for mode, bound, peak in (("warm", "l3", L3_PEAK_GBS), ("cold", "hbm", HBM_PEAK_GBS)):
+            # The walk is LATENCY-bound (one block per group walks a few dependent rounds; the launch lasts
+            # as long as its slowest block), not bandwidth-bound: "bound" says so, "achieved" is the
+            # algorithmic read rate it reaches anyway, hbm_frac that rate against the HBM spec (no Infinity
+            # Cache peak is claimed).  Per launch and per walked round: launch time / mean rounds per group
+            # (the slow blocks that set a launch walk ~2x the mean; profiles/r17_walk_prof.txt has the
+            # per-phase block times).
+            for mode in ("warm", "cold"):
                 avg_ns = gprof.get(mode)
                 if avg_ns:
                     ms, src = avg_ns * launches / 1e6, f"rocprof average walk_kernel duration ({gprof['profile']}) x launches"
@@ -816,10 +821,14 @@ def main(argv=None):
                     ms, src = ev_ms[mode], "hipEvents around every walk launch (live pass; events inflate it)"
                 else:
                     continue
-                roof[mode] = {"bound": bound, "walk_ms_per_batch": ms, "time_source": src,
-                              "achieved": walked / (ms * 1e-3) / 1e9, "peak": peak,
-                              "frac": walked / (ms * 1e-3) / 1e9 / peak,
-                              "hbm_frac": walked / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                us_launch = ms * 1e3 / max(1.0, launches)
+                roof[mode] = {"bound": "latency", "walk_ms_per_batch": ms, "time_source": src,
+                              "us_per_launch": us_launch,
+                              "us_per_launch_per_mean_round": us_launch / max(1e-9, roof["rounds_per_group"]),
+                              "achieved": walked / (ms * 1e-3) / 1e9, "peak": None,
+                              "hbm_frac": walked / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                              "cache": "L2 + Infinity Cache resident index" if mode == "warm"
+                                       else "index evicted before every launch (PE_WALK_FLUSH): reads from HBM"}
                 if mode in ev_ms:
                     roof[mode]["events_walk_ms_per_batch"] = ev_ms[mode]
             if "traffic_per_launch" in gprof:
@@ -829,12 +838,15 @@ def main(argv=None):
                 roof["traffic_read"] = gprof["read_per_launch"] * launches
                 roof["traffic_write"] = gprof["write_per_launch"] * launches
                 roof["traffic_ratio"] = roof["traffic"] / walked if walked else None
+                # share of the walk's algorithmic reads served by the caches (L2 / Infinity Cache): 1 - the
+                # HBM-side reads (FETCH_SIZE, gfx950-corrected) over the algorithmic read bytes
+                roof["cache_hit_share"] = 1.0 - roof["traffic_read"] / walked if walked else None
                 roof["traffic_source"] = f"{gprof['profile']} greedy PMC passes (FETCH_SIZE x2 + WRITE_SIZE per walk launch)"
             else:
                 roof["traffic"] = None
-            roof["note"] = ("latency-bound, not bandwidth-bound: one 1024-thread block per group walks 1-7 rounds of 1024 "
-                            "sorted nodes; warm peak = the Infinity Cache's measured random-row read rate "
-                            "(MI355X_MICROARCH.md: 38 MB table, 8.6 TB/s), cold peak = HBM 8 TB/s")
+            roof["note"] = ("latency-bound, not bandwidth-bound: one 1024-thread block per group walks a few rounds of "
+                            "1024 sorted nodes (dependent steps: loads, key, append, barrier, stop test) and the launch "
+                            "lasts as long as its slowest group; cache_hit_share = the reads the caches served")
             out["greedy"]["roofline"] = roof
 
     if not args.no_configs:
