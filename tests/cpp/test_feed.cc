@@ -95,7 +95,22 @@ static void test_order_and_wait() {
     threw = true;
   }
   CHECK(threw && calls == 3 && g.parsed() == 1);
-  std::printf("ok   order/wait/idle\n");
+  // a producer that stays busy and never signals (a stuck collective): with a deadline set, wait()
+  // throws CollectiveTimeout once it has passed, and not before
+  pe::WindowFeed h;
+  h.idle = [](void*) { return true; };
+  h.timeout_s = 0.05;
+  h.reset(b2.b.data(), 2, 4, 9, &cands);
+  const auto t0 = std::chrono::steady_clock::now();
+  bool timed_out = false;
+  try {
+    h.wait(1);
+  } catch (const pe::CollectiveTimeout&) {
+    timed_out = true;
+  }
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  CHECK(timed_out && dt >= 0.05 && dt < 5.0 && h.parsed() == 1);
+  std::printf("ok   order/wait/idle/deadline\n");
 }
 
 // exact candidate lists of a window: per group every fitting node's key, ascending, cut at K

@@ -25,6 +25,7 @@ def build_and_run(out, flags):
 def test_window_feed(tmp_path):
     out = build_and_run(str(tmp_path / "feed_tests"), ["-O2"])
     assert out.count("ok   fed resolve") == 6
+    assert "ok   order/wait/idle/deadline" in out
     assert "ok   seed scorer start/stop handshake" in out
 
 
