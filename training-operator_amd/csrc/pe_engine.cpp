@@ -1557,6 +1557,9 @@ static bool build_planes(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd, bool 
       sp.kind[sp.n++] = kind;
     }
     ctx->plane = sp;
+    hipchk(ctx->pl_specs_d.ensure(1), "alloc plane spec");
+    hipchk(hipMemcpyAsync(ctx->pl_specs_d.p, &ctx->plane, sizeof(pe::PlaneSpec), hipMemcpyHostToDevice, ctx->stream),
+           "H2D plane spec");
     int64_t R, Jr;
     phases(n_jobs, R, Jr);
     // each job's code straight into its phase-major slot (row-major kernel) or job order
@@ -2049,7 +2052,10 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
 static void fit_run(pe_ctx* ctx) {
   if (!ctx->fit_uploaded) raise(PE_ESTATE, "pe_jobs_upload first");
   const int64_t J = ctx->fit_J;
-  hipchk(hipMemsetAsync(ctx->counts.p, 0, ctx->counts.n * sizeof(unsigned long long), ctx->stream), "memset counts");
+  // the single-plane-set encode zeroes the count slots itself (one launch fewer per step)
+  const bool encode_zeroes = ctx->fit_path == 3 && ctx->pl_sets.empty() && J > 0 && ctx->Ns > 0 && ctx->pl_nblk > 0;
+  if (!encode_zeroes)
+    hipchk(hipMemsetAsync(ctx->counts.p, 0, ctx->counts.n * sizeof(unsigned long long), ctx->stream), "memset counts");
   if (J == 0 || ctx->Ns == 0) return;
   // enough waves to fill 256 CUs several times over; at most 16 tiles (4096 nodes) per wave
   const int64_t waves_y = (J + pe::FM_JT - 1) / pe::FM_JT;
@@ -2089,7 +2095,7 @@ static void fit_run(pe_ctx* ctx) {
       return;
     }
     hipchk(pe::launch_encode_planes(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->pl_nblk,
-                                    ctx->plane, ctx->planes.p),
+                                    ctx->plane, ctx->pl_specs_d.p, ctx->planes.p, ctx->counts.p, ctx->counts.n),
            "launch encode_planes");
     if (ctx->pl_rows) {
       hipchk(pe::launch_fit_mask_planes_rows(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p, J, ctx->pl_R,

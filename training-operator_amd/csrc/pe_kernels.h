@@ -178,7 +178,9 @@ struct PlaneSpec {
 };
 // planes: [nblk][PL_MAX][64 * PL_R] u32; word w of block b covers nodes b*PL_BLK + 32w .. +31
 hipError_t launch_encode_planes(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
-                                int64_t Ns, int64_t nblk, const PlaneSpec& spec, uint32_t* planes);
+                                int64_t Ns, int64_t nblk, const PlaneSpec& spec, const PlaneSpec* spec_d,
+                                uint32_t* planes, unsigned long long* zero = nullptr,
+                                int64_t n_zero = 0);   // spec_d: the same spec on the device; + zero[0..n_zero)
 // jcode[j] = 5 fields of 7 bits (dims 0..3 at bits 0/7/14/21, need at bit 32), each 4 x the plane index.  Mask block-major:
 // u32 word w of row j (nodes 32w..32w+31) at (w / 256 * J + j) * 256 + w % 256, i.e. per 8192-node
 // block a [J][1 KiB] slab.

@@ -570,41 +570,6 @@ hipError_t launch_fit_mask_coded(hipStream_t s, int therm, const uint32_t* X, in
 
 // ------------------------------------------------------------------ bit-plane fit mask
 
-// One wave = 64 nodes; per plane one predicate per lane, ballot -> two transposed u32 words.
-__global__ __launch_bounds__(256) void encode_planes_kernel(const int64_t* __restrict__ res, int64_t stride,
-                                                            const uint32_t* __restrict__ labels, int64_t Ns,
-                                                            int64_t nblk, PlaneSpec spec,
-                                                            uint32_t* __restrict__ planes) {
-  const int lane = threadIdx.x & 63;
-  const int64_t g = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t n0 = g * 64;
-  if (n0 >= nblk * PL_BLK) return;
-  const int64_t n = n0 + lane;
-  const bool valid = n < Ns;
-  int64_t r[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) r[d] = valid ? res[d * stride + n] : 0;
-  const uint32_t lab = valid ? labels[n] : 0u;
-  const int64_t blk = n0 / PL_BLK;
-  const int64_t w0 = (n0 % PL_BLK) / 32;           // even: this wave's two words
-  uint32_t* out = planes + blk * PL_MAX * (64 * PL_R) + w0;
-#pragma unroll
-  for (int p = 0; p < PL_MAX; ++p) {
-    bool pr = false;
-    if (p < spec.n) {
-      const int k = spec.kind[p];
-      const int64_t v = spec.val[p];
-      int64_t rv = r[0];
-      rv = k == 1 ? r[1] : rv;
-      rv = k == 2 ? r[2] : rv;
-      rv = k == 3 ? r[3] : rv;
-      pr = valid && (k == 4 ? (lab & (uint32_t)v) == (uint32_t)v : rv >= v);
-    }
-    const uint64_t b = __builtin_amdgcn_ballot_w64(pr);
-    if (lane < 2) out[p * (64 * PL_R) + lane] = (uint32_t)(lane ? b >> 32 : b);
-  }
-}
-
 // Every plane set of a batch: the same planes as the encode above, set t = blockIdx.y (spec from
 // device memory, uniform), planes of set t at planes + t * nblk * PL_MAX * 256.  One wave owns a
 // segment of ES_G x 64 nodes = 2 ES_G plane words: it ballots the segment's node groups one after
@@ -613,16 +578,13 @@ __global__ __launch_bounds__(256) void encode_planes_kernel(const int64_t* __res
 // 8-byte store per plane and 64 nodes (the per-set cost of that pattern was ~68 us at 1M nodes).
 constexpr int ES_G = 8;                                   // node groups per wave: 16 words, 64 B
 static_assert(PL_BLK % (64 * ES_G) == 0, "segments tile a block");
-__global__ __launch_bounds__(256) void encode_planes_sets_kernel(const int64_t* __restrict__ res, int64_t stride,
-                                                                 const uint32_t* __restrict__ labels, int64_t Ns,
-                                                                 int64_t nblk, const PlaneSpec* __restrict__ specs,
-                                                                 uint32_t* __restrict__ planes) {
+constexpr int64_t ES_SEGS_PER_BLK = PL_BLK / (64 * ES_G);
+__device__ __forceinline__ void encode_segment(const int64_t* __restrict__ res, int64_t stride,
+                                               const uint32_t* __restrict__ labels, int64_t Ns, int64_t nblk,
+                                               const PlaneSpec& spec, int64_t t, int64_t seg,
+                                               uint32_t* __restrict__ planes) {
   const int lane = threadIdx.x & 63;
-  const int64_t seg = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  constexpr int64_t SEGS_PER_BLK = PL_BLK / (64 * ES_G);
-  if (seg >= nblk * SEGS_PER_BLK) return;
-  const int64_t t = blockIdx.y;
-  const PlaneSpec& spec = specs[t];
+  constexpr int64_t SEGS_PER_BLK = ES_SEGS_PER_BLK;
   const int np = spec.n;
   const int64_t blk = seg / SEGS_PER_BLK;
   const int64_t wbase = (seg % SEGS_PER_BLK) * (2 * ES_G);   // first plane word of the segment
@@ -669,22 +631,91 @@ __global__ __launch_bounds__(256) void encode_planes_sets_kernel(const int64_t* 
   }
 }
 
+__global__ __launch_bounds__(256) void encode_planes_sets_kernel(const int64_t* __restrict__ res, int64_t stride,
+                                                                 const uint32_t* __restrict__ labels, int64_t Ns,
+                                                                 int64_t nblk, const PlaneSpec* __restrict__ specs,
+                                                                 uint32_t* __restrict__ planes) {
+  const int64_t seg = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (seg >= nblk * ES_SEGS_PER_BLK) return;
+  encode_segment(res, stride, labels, Ns, nblk, specs[blockIdx.y], blockIdx.y, seg, planes);
+}
+
+// Single spec: one workgroup = 1024 nodes (16 waves of 64), whose 32 words per plane are parked
+// in LDS by the ballots and stored as one full 128-B line per plane.  The spec's planes come
+// grouped by field (dimension 0..3, then label needs), so each field is a plain loop whose plane
+// value is read out of a VGPR (lane p holds plane p's value) and whose predicate is one compare:
+// ~8 instructions per plane.  (The per-plane generic form -- kind selects behind branches, a scalar
+// load and wait per plane, a 2-lane 8-byte store per plane and 64 nodes -- took 22 us alone and
+// 31 us after the fit kernel at 1M nodes.)  Also zeroes the step's count slots (one launch fewer).
+constexpr int EP_NODES = 1024;
+static_assert(PL_BLK % EP_NODES == 0 && EP_NODES / 32 == 32, "a workgroup covers 32 words of every plane");
+struct PlaneBounds {
+  int32_t end[D + 1];   // end[f]: one past field f's last plane (end[D] = planes in use)
+};
+__global__ __launch_bounds__(EP_NODES) void encode_planes_kernel(const int64_t* __restrict__ res, int64_t stride,
+                                                                  const uint32_t* __restrict__ labels, int64_t Ns,
+                                                                  const PlaneSpec* __restrict__ spec, PlaneBounds pb,
+                                                                  uint32_t* __restrict__ planes,
+                                                                  unsigned long long* __restrict__ zero,
+                                                                  int64_t n_zero) {
+  __shared__ uint32_t words[PL_MAX][EP_NODES / 32 + 1];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  for (int64_t i = (int64_t)blockIdx.x * EP_NODES + threadIdx.x; i < n_zero; i += (int64_t)gridDim.x * EP_NODES)
+    zero[i] = 0;
+  const int64_t n = (int64_t)blockIdx.x * EP_NODES + threadIdx.x;
+  const bool valid = n < Ns;
+  int64_t r[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) r[d] = valid ? res[d * stride + n] : 0;
+  const uint32_t lab = valid ? labels[n] : 0u;
+  const int64_t vl = lane < PL_MAX ? spec->val[lane] : 0;
+  const int vlo = (int)(uint32_t)vl, vhi = (int)(uint32_t)((uint64_t)vl >> 32);
+  int p = 0;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    for (; p < pb.end[d]; ++p) {
+      const int64_t v = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, p) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane(vlo, p));
+      const uint64_t b = __builtin_amdgcn_ballot_w64(valid && r[d] >= v);
+      if (lane < 2) words[p][2 * wv + lane] = (uint32_t)(lane ? b >> 32 : b);
+    }
+  }
+  for (; p < pb.end[D]; ++p) {
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane(vlo, p);
+    const uint64_t b = __builtin_amdgcn_ballot_w64(valid && (lab & v) == v);
+    if (lane < 2) words[p][2 * wv + lane] = (uint32_t)(lane ? b >> 32 : b);
+  }
+  __syncthreads();
+  const int64_t n0 = (int64_t)blockIdx.x * EP_NODES;
+  const int q = threadIdx.x >> 5, w = threadIdx.x & 31;
+  planes[(n0 / PL_BLK) * PL_MAX * (64 * PL_R) + q * (64 * PL_R) + (n0 % PL_BLK) / 32 + w] =
+      q < pb.end[D] ? words[q][w] : 0u;
+}
+
 hipError_t launch_encode_planes_sets(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
                                      int64_t Ns, int64_t nblk, const PlaneSpec* specs, int nsets, uint32_t* planes) {
   if (nblk <= 0 || nsets <= 0) return hipSuccess;
   if (nsets > 65535) return hipErrorInvalidValue;
-  const int64_t segs = nblk * (PL_BLK / (64 * ES_G));
+  const int64_t segs = nblk * ES_SEGS_PER_BLK;
   hipLaunchKernelGGL(encode_planes_sets_kernel, dim3((unsigned)((segs + 3) / 4), (unsigned)nsets), dim3(256), 0, s,
                      res, stride, labels, Ns, nblk, specs, planes);
   return hipGetLastError();
 }
 
 hipError_t launch_encode_planes(hipStream_t s, const int64_t* res, int64_t stride, const uint32_t* labels,
-                                int64_t Ns, int64_t nblk, const PlaneSpec& spec, uint32_t* planes) {
+                                int64_t Ns, int64_t nblk, const PlaneSpec& spec, const PlaneSpec* spec_d,
+                                uint32_t* planes, unsigned long long* zero, int64_t n_zero) {
   if (nblk <= 0) return hipSuccess;
-  const int64_t waves = nblk * PL_BLK / 64;
-  hipLaunchKernelGGL(encode_planes_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, res, stride, labels, Ns,
-                     nblk, spec, planes);
+  if (spec.n < 0 || spec.n > PL_MAX) return hipErrorInvalidValue;
+  PlaneBounds pb{};
+  for (int p = 0, f = 0; p <= spec.n; ++p) {   // fields in order 0..D, each a contiguous run
+    const int k = p < spec.n ? spec.kind[p] : D + 1;
+    if (k < f || k > D + 1) return hipErrorInvalidValue;
+    for (; f < k && f <= D; ++f) pb.end[f] = p;
+  }
+  hipLaunchKernelGGL(encode_planes_kernel, dim3((unsigned)(nblk * (PL_BLK / EP_NODES))), dim3(EP_NODES), 0, s, res,
+                     stride, labels, Ns, spec_d, pb, planes, zero, zero ? n_zero : 0);
   return hipGetLastError();
 }
 
