@@ -2425,6 +2425,18 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
                                  ctx->g_lo.p),
            "launch prep_nodes");
     const bool walk = ctx->walk && ctx->Ns > 0;
+    // Candidate lists that grow after a rescan (one GPU, sorted walk): windows start with lists of
+    // topk keys; once a window's lists ran out (a rescan: its groups consumed more list entries than
+    // it had -- whole-node gangs, all of a window's groups after the same few nodes), the rest of the
+    // batch walks lists of 2 x topk.  Longer lists cost walk time (cfg3: 0.58 -> 1.25 ms of device
+    // wait at 512), rescans cost a drained pipeline each (cfg4: 41 rescans at 256, none at 384).
+    // The blob stride is the grown length from the start.  Multi-rank runs keep topk (the exchange
+    // moves whole strides).  PE_NO_LIST_GROWTH=1 keeps topk throughout (A/B).
+    static const bool no_growth = std::getenv("PE_NO_LIST_GROWTH") != nullptr;
+    const int K0 = ctx->topk;
+    const bool kgrow = walk && ctx->world == 1 && !ctx->comm && !no_growth;
+    const int K = kgrow ? std::max(K0, std::min(2 * K0, pe::WK_ROUND - 1)) : K0;   // blob stride (list capacity)
+    int k_win = K0;                                                                  // list length walked
     // PE_ASYNC_RESORT=0: rebuild the walk index in line, on the main stream (A/B; read per call).
     // Otherwise the rebuild starts kResortEarly updates before the threshold on the side stream and
     // is taken over once done -- or waited for past kResortLate updates over the threshold.
@@ -2448,7 +2460,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     if (const char* dp = std::getenv("PE_DUMP_WINDOWS")) {
       dump = std::fopen(dp, "wb");
       if (dump) {
-        const int64_t hdr[3] = {n_jobs, G, (int64_t)ctx->topk};
+        const int64_t hdr[3] = {n_jobs, G, (int64_t)K};   // (the blob stride)
         std::fwrite(hdr, 8, 3, dump);
         std::fwrite(job_group_off, 4, (size_t)n_jobs + 1, dump);
         std::fwrite(priority, 4, (size_t)n_jobs, dump);
@@ -2502,7 +2514,6 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
     } trace_out{helper_cpu, trace, tr_wait, tr_res, tr_post, tr_xspin, tr_xmerge, tr_xblock};
     int64_t dump_left = std::getenv("PE_DUMP_MAX_WINDOWS") ? std::atoll(std::getenv("PE_DUMP_MAX_WINDOWS")) : INT64_MAX;
-    const int K = ctx->topk;
     const size_t gb = pe::cand_group_bytes(K);
     const int Wmax = ctx->window_groups;
     const int Wpad = (int)round_up(Wmax, pe::SC_GT);
@@ -2998,8 +3009,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           walk_events.push_back(evp);
           hipchk(hipEventRecord(evp.first, s), "event record");
         }
-        hipchk(pe::launch_walk(s, hg.dev, Wg, K, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns,
-                               (uint64_t)ctx->begin, dst, zc ? hw.gen : direct_out || own_direct ? gen : 0u),
+        hipchk(pe::launch_walk(s, hg.dev, Wg, k_win, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns,
+                               (uint64_t)ctx->begin, dst, zc ? hw.gen : direct_out || own_direct ? gen : 0u, K),
                "launch walk");
         if (wev) hipchk(hipEventRecord(evp.second, s), "event record");
         walk_launch_groups += Wg;
@@ -3201,7 +3212,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       cb = cur.buf;
       collect_window(cur.groups, cur.buf);       // cur's lists: snapshot = device state at its launch
       if (!pipelined) {
-        timed_resolve(cur.groups, upd, nullptr);
+        if (!timed_resolve(cur.groups, upd, nullptr)) k_win = K;
         enqueue_apply(upd, 0);
         if (R.done()) break;
         fl.clear();
@@ -3294,6 +3305,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       enqueue_apply(upd, 0);
       if (R.done()) break;
+      if (!consumed) k_win = K;   // lists ran out: longer ones from here (the helper is idle now)
       restart();
     }
     const auto t_loop = std::chrono::steady_clock::now();

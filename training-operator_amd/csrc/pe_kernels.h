@@ -374,10 +374,11 @@ hipError_t launch_empty_groups(hipStream_t s, int Wg, int K, uint8_t* out, uint3
 hipError_t launch_stall(hipStream_t s, int64_t ticks);
 // One block per group: overlay + walk, exact top-K keys and limit, same blob as merge.  gen != 0:
 // each group's header.flags is set to gen after its keys, n and limit are visible to the host
-// (system-scope release; out is pinned host memory the host polls per group).
+// (system-scope release; out is pinned host memory the host polls per group).  K_stride: the blob's
+// list capacity per group (cand_group_bytes(K_stride) apart; 0 = K), K <= K_stride.
 hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const WalkIndex& w, const int64_t* res,
                        int64_t stride, const uint32_t* labels, int64_t Ns, uint64_t id_base, uint8_t* out,
-                       uint32_t gen = 0);
+                       uint32_t gen = 0, int K_stride = 0);
 
 // upd: [n] records {local node (i64), res[4]} -> res[d][node] = value (absolute)
 // (kn, lo nullable: refreshed for the updated nodes when given; w nullable: the updated nodes

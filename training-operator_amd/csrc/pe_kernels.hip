@@ -2061,7 +2061,7 @@ __device__ unsigned long long walk_prof[32];
 //     rounds can produce (their K(n) >= rmin, key = K(n) - ((s(q) + borrows) << 24)).
 // Then the same exact selection and blob as merge: top-K records, limit = the (K+1)-th key (or
 // NO_KEY once every candidate round was walked and at most K fit).
-__global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict__ groups, int K, WalkIndex w,
+__global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict__ groups, int K, int Kst, WalkIndex w,
                                                         const int64_t* __restrict__ res, int64_t stride,
                                                         const uint32_t* __restrict__ labels, int64_t Ns,
                                                         uint64_t id_base, uint8_t* __restrict__ out, uint32_t gen) {
@@ -2362,7 +2362,7 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
   const int T = Tcur < MG_CAP ? Tcur : MG_CAP;
   const uint64_t* sk = topk_sort(s, T, K, xstop);
   WPT(4);
-  write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : NO_KEY, K, g, out, gen);
+  write_group(sk, T < K ? T : K, 0, T > K ? sk[K] : NO_KEY, Kst, g, out, gen);   // (stride: Kst keys)
   if (tid == 0 && w.stat) {
     atomicAdd(&w.stat[0], (unsigned long long)rounds);
     atomicAdd(&w.stat[1], (unsigned long long)no);
@@ -2405,10 +2405,11 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
 
 hipError_t launch_walk(hipStream_t s, const ReqRec* groups, int Wg, int K, const WalkIndex& w, const int64_t* res,
                        int64_t stride, const uint32_t* labels, int64_t Ns, uint64_t id_base, uint8_t* out,
-                       uint32_t gen) {
+                       uint32_t gen, int K_stride) {
   if (Wg <= 0) return hipSuccess;
-  if (w.nr > WK_MAXR || K + 1 > WK_ROUND) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(walk_kernel, dim3((unsigned)Wg), dim3(WK_ROUND), 0, s, groups, K, w, res, stride, labels, Ns,
+  const int Kst = K_stride > 0 ? K_stride : K;
+  if (w.nr > WK_MAXR || K + 1 > WK_ROUND || K > Kst) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(walk_kernel, dim3((unsigned)Wg), dim3(WK_ROUND), 0, s, groups, K, Kst, w, res, stride, labels, Ns,
                      id_base, out, gen);
 #ifdef PE_WALK_PROF
   static int launches = 0;
