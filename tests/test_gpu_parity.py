@@ -381,6 +381,29 @@ def test_greedy_vs_oracle(eng, mix, N, J, gpu_frac):
     assert (st == 0).any()
 
 
+@pytest.mark.parametrize("mix,topk", [("gang8", 8), ("island8", 16), ("gang8", 600)])
+def test_greedy_list_growth(monkeypatch, mix, topk):
+    """Whole-node gangs exhaust short candidate lists (rescans); after the first rescan the engine walks
+    lists of 2 x topk (capped at 1023) for the rest of the batch (pe_engine.cpp, one GPU).  Both ways
+    bit-exact vs the oracle; growth never rescans more than the fixed length."""
+    inv = synth.make_inventory(3000, 71, 1.0)
+    batch = synth.make_jobs(400, 73, mix)
+    rescans = {}
+    for growth in (False, True):
+        if growth:
+            monkeypatch.delenv("PE_NO_LIST_GROWTH", raising=False)
+        else:
+            monkeypatch.setenv("PE_NO_LIST_GROWTH", "1")
+        e = Engine(0, topk=topk, window_groups=32)
+        check_greedy(e, inv, batch)
+        rescans[growth] = e.stats()["rescans"]
+        e.close()
+    assert rescans[True] <= rescans[False]
+    if topk < 100:
+        assert rescans[False] > 0          # the case does exhaust its lists
+        assert rescans[True] < rescans[False]
+
+
 @pytest.mark.parametrize("topk,wg,wp", [(1, 1, 1), (2, 8, 32), (8, 64, 1024), (256, 16, 4096), (1023, 64, 1024)])
 def test_greedy_window_configs(topk, wg, wp):
     e = Engine(0, topk=topk, window_groups=wg, window_pods=wp)

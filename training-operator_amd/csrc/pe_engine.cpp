@@ -2431,8 +2431,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // batch walks lists of 2 x topk.  Longer lists cost walk time (cfg3: 0.58 -> 1.25 ms of device
     // wait at 512), rescans cost a drained pipeline each (cfg4: 41 rescans at 256, none at 384).
     // The blob stride is the grown length from the start.  Multi-rank runs keep topk (the exchange
-    // moves whole strides).  PE_NO_LIST_GROWTH=1 keeps topk throughout (A/B).
-    static const bool no_growth = std::getenv("PE_NO_LIST_GROWTH") != nullptr;
+    // moves whole strides).  PE_NO_LIST_GROWTH=1 keeps topk throughout (A/B; read per call).
+    const bool no_growth = std::getenv("PE_NO_LIST_GROWTH") != nullptr;
     const int K0 = ctx->topk;
     const bool kgrow = walk && ctx->world == 1 && !ctx->comm && !no_growth;
     const int K = kgrow ? std::max(K0, std::min(2 * K0, pe::WK_ROUND - 1)) : K0;   // blob stride (list capacity)
