@@ -223,13 +223,29 @@ def time_calls(call, reps: int, warm: int = 20):
     return ts[len(ts) // 2] / 1e3, ts[int(len(ts) * 0.9)] / 1e3
 
 
-def profile_summary():
-    """The committed profile profiles/LATEST names (summary.json), or None."""
+def profile_summaries():
+    """The committed profiles profiles/LATEST names, one tag per line -- [(tag, summary.json)].  Several
+    tags are profiles of the same sources taken on different boxes (their HBM rates differ by up to
+    ~10 %): the fit check below takes the one whose step time is closest to this run's."""
+    out = []
     try:
-        tag = open(os.path.join(PROFILES, "LATEST")).read().strip()
-        return tag, json.load(open(os.path.join(PROFILES, tag, "summary.json")))
-    except (OSError, ValueError):
-        return None, None
+        tags = [t.strip() for t in open(os.path.join(PROFILES, "LATEST")).read().split() if t.strip()]
+    except OSError:
+        return out
+    for tag in tags:
+        try:
+            out.append((tag, json.load(open(os.path.join(PROFILES, tag, "summary.json")))))
+        except (OSError, ValueError):
+            pass
+    return out
+
+
+def profile_summary(src_hash: str | None = None):
+    """The first committed profile (of these sources, when src_hash is given), or (None, None)."""
+    for tag, summ in profile_summaries():
+        if src_hash is None or summ.get("source_hash") == src_hash:
+            return tag, summ
+    return None, None
 
 
 def profile_check(path: str, n_nodes: int, n_jobs: int, kern_ms: float, src_hash: str):
@@ -237,15 +253,24 @@ def profile_check(path: str, n_nodes: int, n_jobs: int, kern_ms: float, src_hash
     step (sum of the step kernels' average durations) within PROFILE_TOL of this run's hipEvent time
     (the same kernel measures 2.16-2.36 ms across boxes and mask allocations, profiles/r8_fit_waves.txt;
     the traffic is a property of the code and the workload, which the hash and workload checks pin).
-    Returns the roofline fields taken from it (traffic and counters are null unless all hold)."""
-    tag, summ = profile_summary()
+    Returns the roofline fields taken from it (traffic and counters are null unless all hold).  Among
+    several committed profiles of these sources (LATEST), the one whose step is closest to this run's."""
+    names = STEP_KERNELS[path]
+
+    def step_ms(summ):
+        k = summ.get("kernels", {})
+        return sum(k[n]["avg_ns"] for n in names if n in k) / 1e6 if names[0] in k else None
+
+    cands = profile_summaries()
+    same_src = [(t, sm) for t, sm in cands if sm.get("source_hash") == src_hash and step_ms(sm) is not None]
+    pool = same_src or cands[:1]
+    tag, summ = min(pool, key=lambda c: abs((step_ms(c[1]) or 0.0) - kern_ms)) if pool else (None, None)
     out = {"profile": None, "profile_kernel_ms": None, "profile_step_ms": None, "profile_matches": False,
            "traffic": None, "traffic_source": None, "pmc": {}}
     if summ is None:
         return out
     out["profile"] = f"profiles/{tag}/summary.json"
     kernels = summ.get("kernels", {})
-    names = STEP_KERNELS[path]
     if names[0] not in kernels:
         return out
     out["profile_kernel_ms"] = kernels[names[0]]["avg_ns"] / 1e6
@@ -272,8 +297,8 @@ def agg_profile_ms(src_hash: str):
     """Kernel time of one 1M-job pe_pg_min_resources call (the sum of its chunk launches of
     pg_agg_seg_kernel) in the committed profile's aggregation pass (tools/agg_calls.py), when taken
     on the same engine sources; else None."""
-    _, summ = profile_summary()
-    if summ is None or summ.get("source_hash") != src_hash:
+    _, summ = profile_summary(src_hash)
+    if summ is None:
         return None
     k = summ.get("aggregation", {}).get("pe::pg_agg_seg_kernel")
     return k["total_ns"] / AGG_PROFILE_CALLS / 1e6 if k else None
@@ -301,8 +326,8 @@ def agg_roofline(in_bytes: int, out_bytes: int, events_ms: float, profile_ms, pc
 def greedy_profile(src_hash: str):
     """Average walk_kernel durations (ns) of the committed profile's greedy passes (warm; cold =
     PE_WALK_FLUSH), only when taken on the same engine sources; {} otherwise."""
-    tag, summ = profile_summary()
-    if summ is None or summ.get("source_hash") != src_hash or "greedy" not in summ:
+    tag, summ = profile_summary(src_hash)
+    if summ is None or "greedy" not in summ:
         return {}
     g = summ["greedy"]
     out = {"profile": f"profiles/{tag}/summary.json"}

@@ -2,8 +2,9 @@
 """Copy the judged part of a run_profile.sh output (gpurun_out/prof_<tag>) into profiles/<name>:
 the rocprofv3 --stats kernel summary, the bench line printed under the trace, the PMC rows of the
 step kernels (fit mask, encode, walk, apply; the full counter CSVs hold every launch of the run)
-and summary.json.
-    python3 profiles/collect.py gpurun_out/prof_r8a r8a_head [--latest]"""
+and summary.json.  --latest: LATEST names this profile alone; --latest-add: appended to LATEST (another
+box's profile of the same sources -- bench.py takes the one whose fit step is closest to its run's).
+    python3 profiles/collect.py gpurun_out/prof_r8a r8a_head [--latest | --latest-add]"""
 import csv
 import os
 import shutil
@@ -41,11 +42,18 @@ def main(src, name, latest):
                 if any(s in k[0] for s in KEEP) and seen.get(k, 0) < 4:
                     seen[k] = seen.get(k, 0) + 1
                     w.writerow(r)
-    if latest:
+    if latest == "add":
+        path = os.path.join(root, "LATEST")
+        tags = open(path).read().split() if os.path.exists(path) else []
+        if name not in tags:
+            tags.append(name)
+        with open(path, "w") as f:
+            f.write("".join(t + "\n" for t in tags))
+    elif latest:
         with open(os.path.join(root, "LATEST"), "w") as f:
             f.write(name + "\n")
     print("profiles/" + name)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], "--latest" in sys.argv[3:])
+    main(sys.argv[1], sys.argv[2], "add" if "--latest-add" in sys.argv[3:] else "--latest" in sys.argv[3:])

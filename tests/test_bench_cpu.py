@@ -84,6 +84,19 @@ def test_profile_check_requires_same_build(tmp_path, monkeypatch):
     assert bench.profile_check("planes", 100, 10, 1.08, "abc")["traffic"] is None          # > 5 % apart
     assert bench.profile_check("planes", 100, 10, 1.20, "abc")["traffic"] is None
     assert bench.profile_check("planes", 100, 11, 1.03, "abc")["traffic"] is None          # other workload
+    # a second profile of the same sources from a slower box: the closest step is taken
+    slow = tmp_path / "q"
+    slow.mkdir()
+    summ2 = json.loads(json.dumps(summ))
+    summ2["kernels"]["pe::fit_mask_planes_rows_kernel"]["avg_ns"] = 1.10e6
+    summ2["pmc"]["pe::fit_mask_planes_rows_kernel"]["hbm_traffic_bytes"] = 124.0
+    (slow / "summary.json").write_text(json.dumps(summ2))
+    (tmp_path / "LATEST").write_text("p\nq\n")
+    r = bench.profile_check("planes", 100, 10, 1.14, "abc")
+    assert r["profile_matches"] and r["traffic"] == 124.0 and r["profile"].endswith("q/summary.json")
+    r = bench.profile_check("planes", 100, 10, 1.03, "abc")
+    assert r["profile_matches"] and r["traffic"] == 123.0
+    assert not bench.profile_check("planes", 100, 10, 1.30, "abc")["profile_matches"]     # neither within 5 %
 
 
 def test_aggregation_slices_partition_the_batch():
