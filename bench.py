@@ -446,9 +446,23 @@ def main(argv=None):
                 dist.broadcast_object_list(names, src=0, group=gloo)
                 wg = args.window_groups or 112
                 k = args.topk or 256
+                k = max(k, min(2 * k, 1023))   # slots for the lists grown after a rescan (pe_engine.cpp)
                 hx.append(HostExchange(names[0], rank, world, wg * (16 + 8 * k)))
                 dist.barrier(group=gloo)
             return hx[0]
+
+        hb = []
+
+        def tight_barrier():
+            """A barrier whose ranks leave within microseconds: a one-byte all-gather over a shared-memory
+            segment of its own (pe_host_exchange spins; gloo's barrier lets ranks leave up to ~0.5 ms
+            apart, which a 1-2 ms greedy batch would time as exchange waits)."""
+            if not hb:
+                names = [f"/pe_bench_b{os.getpid()}_{time.time_ns() & 0xFFFFFFFF:x}" if rank == 0 else None]
+                dist.broadcast_object_list(names, src=0, group=gloo)
+                hb.append(HostExchange(names[0], rank, world, 8))
+                dist.barrier(group=gloo)
+            hb[0].allgather(b"\0")
 
         def first_error(err):
             """Every rank's set-up error (None = fine) -> the first one, on every rank."""
@@ -485,6 +499,9 @@ def main(argv=None):
 
         def first_error(err):
             return err
+
+        def tight_barrier():
+            pass
 
         def allmax(x):
             return x
@@ -538,6 +555,7 @@ def main(argv=None):
         inventory and place the batch again -- flagged "degraded" like a failed set-up."""
         for attempt in range(2):
             barrier()
+            tight_barrier()
             g0 = time.perf_counter()
             err, r = None, None
             try:

@@ -6,7 +6,8 @@ the engine on device 0, exchanging the per-window candidate blobs with the other
 
 Transport "shm": the native shared-memory exchange (pe_host_exchange) instead of the Python gloo
 callback -- its zero-copy windows unless PE_NO_ZC_EXCHANGE=1; gloo then only broadcasts the segment
-name.  Transport "shm-stall": both ranks place a small batch, then rank 0 places the test batch while
+name.  Transport "shm-grow": the zero-copy exchange with lists of 8 keys (rescans) and segment slots
+that hold the grown stride, so the ranks' lists grow to 16 after the first rescan.  Transport "shm-stall": both ranks place a small batch, then rank 0 places the test batch while
 the other ranks sleep and exit -- rank 0 must fail with PE_ERCCL within the device timeout (no hang).
 """
 import os
@@ -37,12 +38,13 @@ def main():
     if transport.startswith("shm"):
         names = [f"/pe_mp_{port}_{os.getpid()}" if rank == 0 else None]
         dist.broadcast_object_list(names, src=0)
-        exchange = HostExchange(names[0], rank, world, 128 * (16 + 8 * 256))
+        exchange = HostExchange(names[0], rank, world, 128 * (16 + 8 * (16 if transport == "shm-grow" else 256)))
         dist.barrier()
+    topk = 8 if transport == "shm-grow" else 0
 
     inv = synth.make_inventory(n_nodes, 3, 0.2 if mix != "gang8" else 1.0)
     batch = synth.make_jobs(n_jobs, 3, mix)
-    e = Engine(0, rank=rank, world_size=world, exchange=exchange, max_nodes=n_nodes)
+    e = Engine(0, rank=rank, world_size=world, exchange=exchange, max_nodes=n_nodes, topk=topk)
     e.load_nodes(inv.cap, inv.used, inv.labels, inv.island)
     b, en = e.shard_range()
     if transport == "shm-stall":
@@ -72,7 +74,7 @@ def main():
     res2 = e.read_residuals()
     s = e.stats()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), pods=pods, st=st, res=res, pods2=pods2, st2=st2, res2=res2,
-             b=b, e=en, windows=s["windows"], zc=s["xchg_zc_windows"])
+             b=b, e=en, windows=s["windows"], zc=s["xchg_zc_windows"], rescans=s["rescans"])
     e.close()
     dist.destroy_process_group()
 

@@ -55,6 +55,8 @@ def _env(**kv):
                                                                            (3, "gang8", 9000, 300, False, "shm-devmerge"),
                                                                            (3, "island8", 9000, 300, False, "gloo-ranked"),
                                                                            (2, "gang8", 6000, 300, True, "shm"),
+                                                                           (2, "gang8", 6000, 300, False, "shm-grow"),
+                                                                           (3, "island8", 9000, 300, False, "shm-grow"),
                                                                            # eight ranks: BASELINE cfg3's split
                                                                            (8, "mixed", 40000, 600, False, "shm"),
                                                                            (8, "island8", 16000, 300, False,
@@ -67,14 +69,16 @@ def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, 
     windows (walk into the registered segment, the exchange thread merges each group on the host as
     every rank signalled it), "shm-devmerge": zero-copy with the device wait + merge kernel
     (PE_ZC_DEV_MERGE=1), "shm-copy": the copying all-gather (PE_NO_ZC_EXCHANGE=1); "-ranked": the
-    rank merge kernel (PE_MERGE_RANKED=1).  Either way the windows are pipelined.  (3 ranks over
+    rank merge kernel (PE_MERGE_RANKED=1); "shm-grow": zero-copy with lists of 8 keys that rescan and
+    segment slots for the grown stride (the ranks' lists grow after the first rescan).  Either way the
+    windows are pipelined.  (3 ranks over
     2 nodes: one rank's shard is empty -- its windows are empty lists, signalled.)"""
     base, _, variant = transport.partition("-")
     extra = {"copy": {"PE_NO_ZC_EXCHANGE": "1"}, "ranked": {"PE_MERGE_RANKED": "1"},
-             "devmerge": {"PE_ZC_DEV_MERGE": "1"}, "": {}}[variant]
+             "devmerge": {"PE_ZC_DEV_MERGE": "1"}, "grow": {}, "": {}}[variant]
     env = _env(**({"PE_HOST_MERGE": "1"} if host_merge else {}), **extra)
     zc_expected = base == "shm" and variant != "copy" and not host_merge
-    transport = base
+    transport = "shm-grow" if variant == "grow" else base
     procs = _spawn(tmp_path, world, mix, n_nodes, n_jobs, transport, env)
     outs = []
     try:
@@ -108,6 +112,8 @@ def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, 
         covered += e - b
         assert int(d["windows"]) > 1
         assert (int(d["zc"]) > 0) == zc_expected, (r, int(d["zc"]))
+        if variant == "grow":
+            assert int(d["rescans"]) > 0   # the short lists did run out
     assert covered == n_nodes
     np.testing.assert_array_equal(full, w_res)
     np.testing.assert_array_equal(full2, w_res2)

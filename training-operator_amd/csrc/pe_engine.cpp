@@ -2430,13 +2430,21 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // it had -- whole-node gangs, all of a window's groups after the same few nodes), the rest of the
     // batch walks lists of 2 x topk.  Longer lists cost walk time (cfg3: 0.58 -> 1.25 ms of device
     // wait at 512), rescans cost a drained pipeline each (cfg4: 41 rescans at 256, none at 384).
-    // The blob stride is the grown length from the start.  Multi-rank runs keep topk (the exchange
-    // moves whole strides).  PE_NO_LIST_GROWTH=1 keeps topk throughout (A/B; read per call).
+    // The blob stride is the grown length from the start.  Sharded runs grow too when they exchange
+    // through a node's shared-memory segment whose slots hold the grown stride (every rank resolves
+    // alike, so all switch at the same window; the host merge cuts at the window's length); the RCCL
+    // transport keeps topk (its all-gather moves whole strides).  PE_NO_LIST_GROWTH=1 keeps topk
+    // throughout (A/B; read per call).
     const bool no_growth = std::getenv("PE_NO_LIST_GROWTH") != nullptr;
     const int K0 = ctx->topk;
-    const bool kgrow = walk && ctx->world == 1 && !ctx->comm && !no_growth;
-    const int K = kgrow ? std::max(K0, std::min(2 * K0, pe::WK_ROUND - 1)) : K0;   // blob stride (list capacity)
-    int k_win = K0;                                                                  // list length walked
+    const int Kg = std::max(K0, std::min(2 * K0, pe::WK_ROUND - 1));
+    pe_host_exchange* const hx_grow = ctx->world > 1 && pe::hx_is(ctx->exchange)
+                                          ? static_cast<pe_host_exchange*>(ctx->exchange_user) : nullptr;
+    const bool kgrow = walk && !no_growth &&
+                       ((ctx->world == 1 && !ctx->comm) ||
+                        (hx_grow && (size_t)ctx->window_groups * pe::cand_group_bytes(Kg) <= pe::hx_slot_bytes(hx_grow)));
+    const int K = kgrow ? Kg : K0;   // blob stride (list capacity)
+    int k_win = K0;                  // list length walked (changed only while the helper threads are idle)
     // PE_ASYNC_RESORT=0: rebuild the walk index in line, on the main stream (A/B; read per call).
     // Otherwise the rebuild starts kResortEarly updates before the threshold on the side stream and
     // is taken over once done -- or waited for past kResortLate updates over the threshold.
@@ -2752,6 +2760,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // gath + r * stride + w * gb
     auto host_merge_zc = [&](const uint8_t* gath, size_t stride, int w, uint8_t* out, uint32_t gen) {
       const int W = ctx->world;
+      const int Kc = k_win;   // the merged list's length: the window's (the stride may be longer)
       uint8_t* og = out + (size_t)w * gb;
       uint64_t* dst = reinterpret_cast<uint64_t*>(og + sizeof(pe::CandHdr));
       uint64_t L = pe::NO_KEY;
@@ -2773,37 +2782,37 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (W >= 2 && kHaveAvx512) {   // pairwise: the K + 1 smallest of shards 0..r, merged with shard r + 1
         alignas(64) uint64_t tmp[2][pe::MG_CAP + 16];
         const uint64_t* acc = lists[0];
-        int na = std::min(ns[0], K + 1);
+        int na = std::min(ns[0], Kc + 1);
         for (int r = 1; r < W; ++r) {
-          const int want = std::min(K + 1, na + ns[r]);
+          const int want = std::min(Kc + 1, na + ns[r]);
           uint64_t* o = tmp[r & 1];
           na = want > 0 ? merge2_avx512(acc, na, lists[r], ns[r], want, o) : 0;
           acc = o;
         }
         m = na;
-        std::memcpy(dst, acc, (size_t)std::min(m, K) * 8);
-        if (m > K) lim = acc[K];
+        std::memcpy(dst, acc, (size_t)std::min(m, Kc) * 8);
+        if (m > Kc) lim = acc[Kc];
       } else if (W == 2) {
         const uint64_t *a = lists[0], *b = lists[1];
         const int na = ns[0], nb = ns[1];
         int i = 0, j = 0;
-        const int want = std::min(K + 1, na + nb);
+        const int want = std::min(Kc + 1, na + nb);
         while (m < want && i < na && j < nb) {
           const uint64_t x = a[i], y = b[j];
           const bool t = x < y;
           const uint64_t v = t ? x : y;
-          if (m < K) dst[m] = v;
+          if (m < Kc) dst[m] = v;
           else lim = v;   // (the (K+1)-th key is the merged list's limit)
           ++m;
           i += t;
           j += !t;
         }
         for (; m < want && i < na; ++m, ++i) {
-          if (m < K) dst[m] = a[i];
+          if (m < Kc) dst[m] = a[i];
           else lim = a[i];
         }
         for (; m < want && j < nb; ++m, ++j) {
-          if (m < K) dst[m] = b[j];
+          if (m < Kc) dst[m] = b[j];
           else lim = b[j];
         }
       } else {
@@ -2818,7 +2827,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
             }
           if (br < 0) break;
           ++hd[br];
-          if (m == K) {
+          if (m == Kc) {
             lim = bk;
             ++m;
             break;
@@ -2827,8 +2836,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         }
       }
       pe::CandHdr* hp = reinterpret_cast<pe::CandHdr*>(og);
-      hp->n = std::min(m, K);
-      hp->limit = m > K ? lim : L;
+      hp->n = std::min(m, Kc);
+      hp->limit = m > Kc ? lim : L;
       __atomic_store_n(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE);   // the group's signal, last
     };
     auto host_merge_group = [&](const uint8_t* gath, int Wg, int w, uint8_t* out, uint32_t gen) {
