@@ -3211,7 +3211,21 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       hist.clear();
       n_app = 0;
       next_buf = 0;
-      if (Flight* f = add_flight(R.cursor())) enqueue_window(f->groups, f->buf);
+      Flight* f = add_flight(R.cursor());
+      if (!f) return;
+      if (split_x && zc_host) {
+        // a zero-copy window: merged group by group on the exchange thread as in the loop below, so
+        // the resolver starts on the first merged group (merging the whole window here first put the
+        // walk's tail and the full merge in front of every batch start and every rescan)
+        if (++ctx->walk_gen == 0) ++ctx->walk_gen;
+        const uint32_t gen = ctx->walk_gen;
+        const pe::HxWindow hw = pe::hx_zc_next(hx);
+        enqueue_window(f->groups, f->buf, gen, true, &hw);
+        const int b = f->buf, wg = (int)f->groups.size();
+        xworker->post([&, b, wg, gen, hw] { exchange_window(b, wg, gen, true, worker.get(), &hw); });
+      } else {
+        enqueue_window(f->groups, f->buf);
+      }
     };
     const auto t_setup = std::chrono::steady_clock::now();
     restart();
