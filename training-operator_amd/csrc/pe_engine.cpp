@@ -2043,7 +2043,8 @@ static void fit_upload(pe_ctx* ctx, int64_t n_jobs, const int64_t* req, const ui
   static const unsigned mask_flags = std::getenv("PE_MASK_CONTIG") ? hipDeviceMallocContiguous : 0u;
   hipchk(ctx->mask.ensure(mask_words, mask_flags), "alloc fit mask");
   const int64_t n_counts = std::max<int64_t>(Jp, ctx->fit_path == 3 ? ctx->pl_counts_n : 0);
-  hipchk(ctx->counts.ensure(n_counts), "alloc fit counts");
+  // (+ the row sweep's per-block work-unit counters, zeroed with the counts every step)
+  hipchk(ctx->counts.ensure(n_counts + (ctx->fit_path == 3 ? ctx->pl_nblk : 0)), "alloc fit counts");
   hipchk(ctx->h_counts.ensure(n_counts), "alloc pinned counts");
   hipchk(hipStreamSynchronize(ctx->stream), "sync fit upload");
   ctx->fit_uploaded = true;
@@ -2098,8 +2099,11 @@ static void fit_run(pe_ctx* ctx) {
                                     ctx->plane, ctx->pl_specs_d.p, ctx->planes.p, ctx->counts.p, ctx->counts.n),
            "launch encode_planes");
     if (ctx->pl_rows) {
+      // PE_FIT_STATIC=1: every wave keeps its own phase (no work units; A/B, read per call)
+      unsigned long long* const units = std::getenv("PE_FIT_STATIC") ? nullptr : ctx->counts.p + ctx->pl_counts_n;
       hipchk(pe::launch_fit_mask_planes_rows(ctx->stream, ctx->planes.p, ctx->pl_nblk, ctx->plane_jobs.p, J, ctx->pl_R,
-                                             reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p, ctx->pl_pitch),
+                                             reinterpret_cast<uint32_t*>(ctx->mask.p), ctx->counts.p, ctx->pl_pitch,
+                                             units),
              "launch fit_mask_planes_rows");
     } else {
       const int64_t ranges = std::max<int64_t>(1, (16384 + ctx->pl_nblk - 1) / ctx->pl_nblk);

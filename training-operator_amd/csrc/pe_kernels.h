@@ -191,9 +191,11 @@ hipError_t launch_fit_mask_planes(hipStream_t s, const uint32_t* planes, int64_t
 // phase-major: entry r * Jr + i belongs to job r + R * i (Jr = ceil(J / R) rounded up to 4), so
 // every wave reads and counts a contiguous run.
 // pitch_blk >= nblk: mask row pitch in 8192-node blocks (1 KiB each; words past nblk are not written)
+// unit_ctr (nblk zeroed counters, or nullptr): the waves of a block share its (phase, 64-job batch)
+// units through the block's counter instead of each taking its own phase -- same rows, same counts.
 hipError_t launch_fit_mask_planes_rows(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
                                        int64_t J, int64_t R, uint32_t* mask, unsigned long long* counts,
-                                       int64_t pitch_blk);
+                                       int64_t pitch_blk, unsigned long long* unit_ctr = nullptr);
 // Plane-set form (batches with more than PL_MAX distinct request values), all sets in one launch
 // each: encode writes set t's planes at planes + t * nblk * PL_MAX * 256; the sweep has the rows
 // kernel's grid (R phases common to all sets); set t's codes and counts start at meta[3t] (phase-

@@ -888,26 +888,30 @@ __device__ __forceinline__ void rows_batch(uint32_t (&p)[64], uint32_t lo, uint3
 // batch ahead (read out with v_readlane), and the per-job counts are one 64 x 64 column-sum
 // (reduce64x64) instead of 64 dependent wave sums.  Mask layout row-major: u32 word w of row j at
 // j * row_words + w, row_words = nblk * 256.
+// Work units (ctr != nullptr): the waves of a block take (phase, 64-job batch) units from the
+// block's counter, batch-major, instead of each working through its own phase.  The even and odd
+// XCDs of a part do not write the mask at the same rate (per-wave finish times, one launch: XCDs
+// 0/2/4/6 done at 1.82-1.97 ms, 1/3/5/7 at 2.20-2.31 ms), and a block's R waves sit on different
+// XCDs -- so the fast ones take over the slow ones' batches and the launch ends near the mean.  The
+// units in flight stay one contiguous window of rows (batch k of every phase = rows 64kR .. 64(k+1)R).
+// A unit's index is fetched two batches ahead and its codes one batch ahead.
 __global__ __launch_bounds__(256) void fit_mask_planes_rows_kernel(const uint32_t* __restrict__ planes, int64_t nblk,
                                                                    const uint64_t* __restrict__ jcode, int64_t J,
                                                                    int64_t R, int64_t Jr, uint32_t* __restrict__ mask,
                                                                    unsigned long long* __restrict__ counts,
-                                                                   int64_t row_vec) {
+                                                                   int64_t row_vec, unsigned long long* __restrict__ ctr) {
   static_assert(PL_MAX == 32 && PL_R == 4, "register map assumes 32 planes x 4 words");
   const int lane = threadIdx.x & 63;
   const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = wave_id % nblk;
-  const int64_t r = wave_id / nblk;
-  if (r >= R || r >= J) return;
+  const int64_t r_own = wave_id / nblk;
+  if (r_own >= R || r_own >= J) return;
   const u32x4* pb = reinterpret_cast<const u32x4*>(planes + blk * PL_MAX * (64 * PL_R)) + lane;
   const u32x32 A = load_planes8(pb), B = load_planes8(pb + 8 * 64), C = load_planes8(pb + 16 * 64),
                Dq = load_planes8(pb + 24 * 64);
   // row_vec: u32x4 per row (the pitch, >= nblk * 64)
   u32x4* const rows0 = reinterpret_cast<u32x4*>(mask) + blk * 64;   // this block's column, row 0
   u32x4* out = rows0 + lane;
-  const uint64_t* jc = jcode + r * Jr;         // this phase's codes, contiguous
-  unsigned long long* cnt = counts + r * Jr;   // and its counts (the host un-permutes)
-  const int64_t ni = (J - r + R - 1) / R;      // jobs of this phase
   uint32_t sigma;                              // lane l of a batch sum counts batch job sigma
   {
     uint32_t probe[64];
@@ -915,45 +919,78 @@ __global__ __launch_bounds__(256) void fit_mask_planes_rows_kernel(const uint32_
     for (int k = 0; k < 64; ++k) probe[k] = lane == 0 ? (uint32_t)k : 0u;
     sigma = reduce64x64(probe, lane);
   }
-  int64_t i0 = 0;
-  uint64_t cv = ni >= 64 ? jc[lane] : 0;       // lane l: code of batch job l
-  for (; i0 + 64 <= ni; i0 += 64) {
-    const uint32_t lo = (uint32_t)cv, hi = (uint32_t)(cv >> 32);
-    if (i0 + 128 <= ni) cv = jc[i0 + 64 + lane];   // next batch, in flight during this one
-    uint32_t p[64];
-    // buffer stores: batch base in the resource, per-job advance in soffset (SALU), lane offset
-    // in voffset -- no per-job VALU address arithmetic
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(rows0 + (r + i0 * R) * row_vec), 0, -1, 0x00020000);
-    rows_batch<0>(p, lo, hi, A, B, C, Dq, rs, 0u, (uint32_t)(R * row_vec * 16), (uint32_t)lane * 16u);
-    const uint32_t F = reduce64x64(p, lane);
-    if (F) atomicAdd(&cnt[i0 + sigma], (unsigned long long)F);
+  const int64_t Rj = R < J ? R : J;            // phases that have jobs
+  const int64_t nb = ((J + R - 1) / R + 63) / 64;   // batches of the longest phase
+  const int64_t U = ctr ? Rj * nb : 0;         // units of the block (work-unit mode)
+  // unit u: phase u % Rj, batch u / Rj; static mode: this wave's phase, batch by batch
+  auto phase_of = [&](int64_t u) { return ctr ? u % Rj : r_own; };
+  auto batch_of = [&](int64_t u) { return ctr ? u / Rj : u; };
+  auto jobs_of = [&](int64_t r) { return (J - r + R - 1) / R; };
+  const int64_t Ulast = ctr ? U : (jobs_of(r_own) + 63) / 64;
+  auto grab = [&](int64_t& st) -> int64_t {    // static mode: the next batch; units: the counter
+    if (!ctr) return st++;
+    unsigned long long v = 0;
+    if (lane == 0) v = atomicAdd(ctr + blk, 1ull);
+    return (int64_t)v;                         // (lane 0's; read out where used)
+  };
+  auto first = [&](int64_t v) { return (int64_t)__builtin_amdgcn_readfirstlane((int)v); };
+  auto codes = [&](int64_t u) -> uint64_t {    // lane l: code of the unit's job l (0 past the end)
+    if (u >= Ulast) return 0;
+    const int64_t r = phase_of(u), i0 = batch_of(u) * 64;
+    return i0 + lane < jobs_of(r) ? jcode[r * Jr + i0 + lane] : 0;
+  };
+  int64_t st = 0;
+  int64_t u0 = first(grab(st));
+  int64_t u1v = grab(st);                      // (the next unit: lane 0's value in flight)
+  uint64_t c0 = codes(u0);
+  while (u0 < Ulast) {
+    const int64_t u1 = first(u1v);
+    const int64_t u2v = grab(st);              // two ahead, in flight during this batch
+    const uint64_t c1 = codes(u1);             // one ahead
+    const int64_t r = phase_of(u0), i0 = batch_of(u0) * 64, ni = jobs_of(r);
+    unsigned long long* cnt = counts + r * Jr;   // this phase's counts (the host un-permutes)
+    if (i0 + 64 <= ni) {
+      const uint32_t lo = (uint32_t)c0, hi = (uint32_t)(c0 >> 32);
+      uint32_t p[64];
+      // buffer stores: batch base in the resource, per-job advance in soffset (SALU), lane offset
+      // in voffset -- no per-job VALU address arithmetic
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(rows0 + (r + i0 * R) * row_vec), 0, -1, 0x00020000);
+      rows_batch<0>(p, lo, hi, A, B, C, Dq, rs, 0u, (uint32_t)(R * row_vec * 16), (uint32_t)lane * 16u);
+      const uint32_t F = reduce64x64(p, lane);
+      if (F) atomicAdd(&cnt[i0 + sigma], (unsigned long long)F);
+    } else if (i0 < ni) {                      // a phase's last, short batch: per-job wave sums
+      const uint64_t* jc = jcode + r * Jr;
+      uint32_t acc = 0;
+      for (int64_t i = i0; i < ni; ++i) {
+        const uint64_t c = jc[i];
+        u32x4 f;
+        plane_sel(f, (uint32_t)c & 127, A, B, C, Dq);
+        plane_and(f, (uint32_t)(c >> 7) & 127, A, B, C, Dq);
+        plane_and(f, (uint32_t)(c >> 14) & 127, A, B, C, Dq);
+        plane_and(f, (uint32_t)(c >> 21) & 127, A, B, C, Dq);
+        plane_and(f, (uint32_t)(c >> 32) & 127, A, B, C, Dq);
+        *(gu32x4*)(out + (r + i * R) * row_vec) = f;
+        const uint32_t n = wave_sum(__popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w));
+        acc = writelane_s(acc, n, (uint32_t)(i - i0));
+      }
+      if (lane < ni - i0 && acc) atomicAdd(&cnt[i0 + lane], (unsigned long long)acc);
+    }
+    u0 = u1;
+    c0 = c1;
+    u1v = u2v;
   }
-  uint32_t acc = 0;                            // tail (< 64 jobs): per-job wave sums
-  for (int64_t i = i0; i < ni; ++i) {
-    const uint64_t c = jc[i];
-    u32x4 f;
-    plane_sel(f, (uint32_t)c & 127, A, B, C, Dq);
-    plane_and(f, (uint32_t)(c >> 7) & 127, A, B, C, Dq);
-    plane_and(f, (uint32_t)(c >> 14) & 127, A, B, C, Dq);
-    plane_and(f, (uint32_t)(c >> 21) & 127, A, B, C, Dq);
-    plane_and(f, (uint32_t)(c >> 32) & 127, A, B, C, Dq);
-    *(gu32x4*)(out + (r + i * R) * row_vec) = f;
-    const uint32_t n = wave_sum(__popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w));
-    acc = writelane_s(acc, n, (uint32_t)(i - i0));
-  }
-  if (lane < ni - i0 && acc) atomicAdd(&cnt[i0 + lane], (unsigned long long)acc);
 }
 
 hipError_t launch_fit_mask_planes_rows(hipStream_t s, const uint32_t* planes, int64_t nblk, const uint64_t* jcode,
                                        int64_t J, int64_t R, uint32_t* mask, unsigned long long* counts,
-                                       int64_t pitch_blk) {
+                                       int64_t pitch_blk, unsigned long long* unit_ctr) {
   if (J <= 0 || nblk <= 0 || R <= 0) return hipSuccess;
   if (pitch_blk < nblk) return hipErrorInvalidValue;
   const int64_t Jr = ((J + R - 1) / R + 3) / 4 * 4;   // phase stride (the engine pads codes alike)
   const int64_t waves = nblk * R;
   hipLaunchKernelGGL(fit_mask_planes_rows_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, planes, nblk,
-                     jcode, J, R, Jr, mask, counts, pitch_blk * 64);
+                     jcode, J, R, Jr, mask, counts, pitch_blk * 64, unit_ctr);
   return hipGetLastError();
 }
 
