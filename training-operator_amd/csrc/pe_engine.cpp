@@ -1944,7 +1944,8 @@ static bool build_lds(pe_ctx* ctx, int64_t n_jobs, const BatchDict& bd) {
   ctx->lds_nblk = nblk;
   ctx->lds_R = R;
   ctx->lds_Tpad = Tpad;
-  hipchk(ctx->lds_slots.ensure((size_t)R * 16 * Tpad), "alloc count slots");
+  // (+ the kernel's per-block work-unit counters, zeroed with the slots every step)
+  hipchk(ctx->lds_slots.ensure((size_t)R * 16 * Tpad + (size_t)ctx->lds_nblk), "alloc count slots");
   hipchk(ctx->lds_rows.ensure((size_t)R * 16 * Tpad), "alloc count rows");
   hipchk(hipMemcpyAsync(ctx->lds_rows.p, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, ctx->stream),
          "H2D lds rows");
@@ -2064,7 +2065,7 @@ static void fit_run(pe_ctx* ctx) {
   int64_t tpw = (ctx->Ns + 256 * want_x - 1) / (256 * want_x);
   tpw = std::min<int64_t>(16, std::max<int64_t>(1, tpw));
   if (ctx->fit_path == 4) {
-    hipchk(hipMemsetAsync(ctx->lds_slots.p, 0, (size_t)ctx->lds_R * 16 * ctx->lds_Tpad * 4, ctx->stream),
+    hipchk(hipMemsetAsync(ctx->lds_slots.p, 0, ((size_t)ctx->lds_R * 16 * ctx->lds_Tpad + ctx->lds_nblk) * 4, ctx->stream),
            "memset count slots");
     hipchk(pe::launch_node_ranks(ctx->stream, ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns, ctx->lds_npad,
                                  ctx->lds_spec_d.p, ctx->lds_vals.p, ctx->lds_ranks.p, ctx->lds_aux.p),
@@ -2073,7 +2074,9 @@ static void fit_run(pe_ctx* ctx) {
                                    ctx->lds_ranks.p,
                                    ctx->lds_npad, ctx->lds_aux.p, ctx->lds_nblk, ctx->lds_codes.p, J,
                                    ctx->lds_R, ctx->lds_Tpad, ctx->lds_pitch * 8,
-                                   reinterpret_cast<uint8_t*>(ctx->mask.p), ctx->lds_slots.p),
+                                   reinterpret_cast<uint8_t*>(ctx->mask.p), ctx->lds_slots.p,
+                                   std::getenv("PE_FIT_STATIC") ? nullptr
+                                                                : ctx->lds_slots.p + (size_t)ctx->lds_R * 16 * ctx->lds_Tpad),
            "launch fit_mask_lds");
     hipchk(pe::launch_lds_counts(ctx->stream, ctx->lds_slots.p, ctx->lds_rows.p, ctx->lds_R * 16 * ctx->lds_Tpad,
                                  ctx->counts.p),

@@ -277,7 +277,7 @@ hipError_t launch_node_ranks(hipStream_t s, const int64_t* res, int64_t stride, 
 hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[4], const LdsSpec* spec, int nplanes,
                                const uint32_t* ranks, int64_t npad, const uint32_t* aux, int64_t nblk,
                                const uint16_t* codes, int64_t J, int64_t R, int64_t Tpad, int64_t pitch_bytes,
-                               uint8_t* mask, uint32_t* slots);
+                               uint8_t* mask, uint32_t* slots, uint32_t* units = nullptr);   // units: nblk zeroed counters
 hipError_t launch_lds_counts(hipStream_t s, const uint32_t* slots, const uint32_t* rows, int64_t nslots,
                              unsigned long long* counts);
 

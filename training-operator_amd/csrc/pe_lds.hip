@@ -56,7 +56,7 @@ hipError_t launch_node_ranks(hipStream_t s, const int64_t* res, int64_t stride, 
 hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[4], const LdsSpec* spec, int nplanes,
                                const uint32_t* ranks, int64_t npad, const uint32_t* aux, int64_t nblk,
                                const uint16_t* codes, int64_t J, int64_t R, int64_t Tpad, int64_t pitch_bytes,
-                               uint8_t* mask, uint32_t* slots) {
+                               uint8_t* mask, uint32_t* slots, uint32_t* units) {
   if (J <= 0 || nblk <= 0 || R <= 0) return hipSuccess;
   const size_t lds = (size_t)nplanes * 2048 * W / 8;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
@@ -69,7 +69,8 @@ hipError_t launch_fit_mask_lds(hipStream_t s, int W, const int shape[4], const L
   if (e != hipSuccess) return e;
   const uint2* c = reinterpret_cast<const uint2*>(codes);
   void* args[] = {(void*)&spec, (void*)&ranks, (void*)&npad, (void*)&aux,         (void*)&nblk,   (void*)&c,
-                  (void*)&J,    (void*)&R,     (void*)&Tpad, (void*)&pitch_bytes, (void*)&mask,   (void*)&slots};
+                  (void*)&J,    (void*)&R,     (void*)&Tpad, (void*)&pitch_bytes, (void*)&mask,   (void*)&slots,
+                  (void*)&units};
   e = hipLaunchKernel(fn, dim3((unsigned)(nblk * R)), dim3(LD_THREADS), args, lds, s);
   if (e != hipSuccess) return e;
   return hipGetLastError();

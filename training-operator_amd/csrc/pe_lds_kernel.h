@@ -71,7 +71,8 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
                                                                   const uint2* __restrict__ codes, int64_t J,
                                                                   int64_t R, int64_t Tpad, int64_t pitch_bytes,
                                                                   uint8_t* __restrict__ mask,
-                                                                  uint32_t* __restrict__ slots) {
+                                                                  uint32_t* __restrict__ slots,
+                                                                  uint32_t* __restrict__ units) {
   typedef typename LdVec<W>::T V;
   constexpr int S = 2048 * W;                 // nodes per block
   constexpr int WPP = S / 32;                 // u32 words per plane
@@ -144,20 +145,28 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
   }
   __syncthreads();
 
-  // 3. the jobs of this wave: j = r + R (wave + 16 t), t < T.  Their codes are contiguous (the t-major
-  //    run of wave (r, wave), padded to 16 jobs): a 16-job batch is 512 B, one 8-B load per lane
-  //    issued a batch ahead; lane 4K + i holds dwords 2i, 2i + 1 of batch job K (v_readlane).
+  // 3. the jobs: run (r', w') = jobs r' + R (w' + 16 t), t < T(r', w'), in 16-job batches.  A run's codes
+  //    are contiguous (t-major, padded to 16 jobs): a batch is 512 B, one 8-B load per lane issued a
+  //    batch ahead; lane 4K + i holds dwords 2i, 2i + 1 of batch job K (v_readlane).  units != nullptr:
+  //    the block's R x 16 waves take (run, batch) units batch-major from the block's counter (the odd
+  //    XCDs write slower -- pe_kernels.hip fit_mask_planes_rows_kernel), so a fast wave takes over a slow
+  //    one's batches; else wave (r, wave) streams its own run.  Either way a batch lands in its run's rows
+  //    and count slots.
   //    (Round-3 A/B, profiles/r10_lds_ab.txt: scalar loads of the codes instead of the readlanes were
   //    35 % slower -- they share lgkmcnt with the LDS reads -- and sorting the batch by digits so that
   //    consecutive jobs reuse plane pairs kept in VGPRs saved 3.6 % on the adversarial batch but cost
   //    7-8 % elsewhere: the sorted jobs' rows scatter the mask stores, which this job interleave keeps
   //    in one sweeping window.)
-  const int64_t j0 = r + R * wave, step = 16 * R;
-  const int64_t T = j0 < J ? (J - j0 + step - 1) / step : 0;
+  const int64_t step = 16 * R;
+  auto runT = [&](int64_t q) -> int64_t {     // jobs of run q = r' * 16 + w'
+    const int64_t j0q = q / 16 + R * (q % 16);
+    return j0q < J ? (J - j0q + step - 1) / step : 0;
+  };
+  const int64_t nq = R * 16;                  // runs
+  const int64_t nbt = (runT(0) + 15) / 16;    // batches of the longest run
+  const int64_t Ulast = units ? nq * nbt : (runT(r * 16 + wave) + 15) / 16;
   uint8_t* const col0 = mask + blk * (S / 8);       // this block's column of row 0 (wave-uniform)
   const uint32_t lane_off = (uint32_t)lane * (4 * W);
-  const uint2* const cb = codes + (r * 16 + wave) * Tpad * (LD_CODE / 4);
-  uint32_t* const sl = slots + (r * 16 + wave) * Tpad;
   uint32_t sigma;
   {
     uint32_t probe[16];
@@ -165,22 +174,41 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
     for (int k = 0; k < 16; ++k) probe[k] = lane == 0 ? (uint32_t)k : 0u;
     sigma = reduce16x64(probe, lane);
   }
-  // No branch inside a batch: the next batch's codes are loaded unconditionally (index clamped into the
-  // padded run) and the stores are buffer stores whose resource holds the job's row slice, with 0 bytes
-  // for a job past the wave's last (the hardware drops an out-of-range store: no traffic, no scratch
-  // row).  A batch is then one basic block -- job K + 1's plane reads overlap job K's combines -- and
-  // the compiler's wait for the code load counts exactly the batch's 16 stores behind it (with
-  // conditional stores it drained every store of the batch, vmcnt(0), once per batch).
-  uint2 cv = cb[lane];
+  auto run_of = [&](int64_t u) -> int64_t { return units ? u % nq : r * 16 + wave; };
+  auto batch_of = [&](int64_t u) -> int64_t { return units ? u / nq : u; };
+  int64_t st = 0;
+  auto grab = [&]() -> int64_t {
+    if (!units) return st++;
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(units + blk, 1u);
+    return (int64_t)v;                        // (lane 0's; read out where used)
+  };
+  auto codes_of = [&](int64_t u) -> uint2 {   // the unit's batch codes (index clamped into the padded run)
+    const int64_t q = u < Ulast ? run_of(u) : 0, t0 = u < Ulast ? 16 * batch_of(u) : 0;
+    return codes[q * Tpad * (LD_CODE / 4) + min<int64_t>(t0, Tpad - 16) * (LD_CODE / 4) + lane];
+  };
+  int64_t u0 = __builtin_amdgcn_readfirstlane((int)grab());
+  int64_t u1v = grab();
+  uint2 cv = codes_of(u0);
   // (wait for the first batch's codes here, once: left pending into the loop, the header would merge
   // that pending load with the latch's state and wait vmcnt(0) -- every store drained -- per batch)
   asm volatile("" : : "v"(cv.x), "v"(cv.y));
-  for (int64_t t0 = 0; t0 < T; t0 += 16) {
+  while (u0 < Ulast) {
+    const int64_t u1 = __builtin_amdgcn_readfirstlane((int)u1v);
+    const int64_t u2v = grab();               // two ahead, in flight during this batch
+    const int64_t q = run_of(u0), t0 = 16 * batch_of(u0), T = runT(q);
+    const int64_t j0 = q / 16 + R * (q % 16);
+    uint32_t* const sl = slots + q * Tpad;
     // (a 32-bit wave-uniform count: the per-job `K < n` tests of the store sizes stay scalar compares;
     // as a 64-bit value they were 15 v_cmp_gt_u64 per batch)
-    const int n = __builtin_amdgcn_readfirstlane((int)min<int64_t>(16, T - t0));
+    const int n = __builtin_amdgcn_readfirstlane((int)max<int64_t>(0, min<int64_t>(16, T - t0)));
     const uint2 cur = cv;
-    cv = cb[min<int64_t>(t0 + 16, Tpad - 16) * (LD_CODE / 4) + lane];   // next batch, in flight meanwhile
+    cv = codes_of(u1);                        // next batch, in flight meanwhile
+    // No branch inside a batch: the stores are buffer stores whose resource holds the job's row slice,
+    // with 0 bytes for a job past the run's last (the hardware drops an out-of-range store: no traffic,
+    // no scratch row).  A batch is then one basic block -- job K + 1's plane reads overlap job K's
+    // combines -- and the compiler's wait for the code load counts exactly the batch's 16 stores behind
+    // it (with conditional stores it drained every store of the batch, vmcnt(0), once per batch).
     uint32_t p[16];
 #pragma unroll
     for (int K = 0; K < 16; ++K) {
@@ -235,6 +263,8 @@ __global__ __launch_bounds__(LD_THREADS) void fit_mask_lds_kernel(const LdsSpec*
     }
     const uint32_t F = reduce16x64(p, lane);
     if ((lane & 3) == 0 && sigma < (uint32_t)n && F) atomicAdd(&sl[t0 + sigma], F);
+    u0 = u1;
+    u1v = u2v;
   }
 }
 
