@@ -13,10 +13,12 @@ type name, one of the orders the reference can produce), Replicas nil -> -1 (the
 util.go:129), and per container the effective list AddResourceList adds (util.go:79-104): Requests,
 or Limits only when the Requests map is nil (an empty non-nil map does not fall back).  Init
 containers and pod overhead are not counted (util.go:138).  The engine counts pods up to minMember
-exactly as the per-pod loop.  Inputs the tensor path does not hold exactly (domain refusals: an
-inexact quantity, an unknown key, int64 overflow) go to the reference's CalcPGMinResources unchanged,
-so the answer is the reference's for every input; an ENGINE error is never answered that way -- it is
-returned (CalcPGMinResourcesEngineE, PGMinResourcesBatch) or counted and logged (EngineErrors).
+exactly as the per-pod loop.  Every resource key is summed on the GPU (a per-call key table,
+pe_pg_min_resources_keys: hugepages-*, rdma/*, any accelerator name, cpu finer than 1m), each at the
+decimal scale its quantities need.  The ONE input handed to the reference's CalcPGMinResources is a
+job whose sum has no int64 at its scale (Overflow: Go holds it in inf.Dec), so the answer is the
+reference's for every input; an ENGINE error is never answered that way -- it is returned
+(CalcPGMinResourcesEngineE, PGMinResourcesBatch) or counted and logged (EngineErrors).
 */
 package common
 
@@ -33,11 +35,11 @@ import (
 )
 
 // flattenV1 builds the one-job v1 CSR of CalcPGMinResources(minMember, replicas, pcGetFunc), and the
-// print formats the reference's AddResourceList sums end with (hip.FormatAcc, util.go:79-104): the
+// print formats the reference's AddResourceList sums end with (hip.KeyFormatAcc, util.go:79-104): the
 // same walk over the pods util.go:126-141 counts (a type's second pod only re-adds the formats of
 // its first, so at most two per type are replayed).
-func flattenV1(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpec, pcGetFunc PriorityClassGetFunc,
-	gpuName string) (*hip.CSR, *hip.FormatAcc, error) {
+func flattenV1(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpec,
+	pcGetFunc PriorityClassGetFunc) (*hip.KeyCSR, *hip.KeyFormatAcc, error) {
 	type typed struct {
 		name     string
 		priority int32
@@ -57,12 +59,12 @@ func flattenV1(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpe
 		}
 		return order[i].name < order[j].name
 	})
-	b := &hip.CSR{}
-	acc := &hip.FormatAcc{}
+	b := &hip.KeyCSR{}
+	acc := &hip.KeyFormatAcc{}
 	podCnt := int64(0)
 	for _, t := range order {
 		for _, c := range t.spec.Template.Spec.Containers {
-			if err := b.AddContainer(effectiveList(c), hip.KindContainer, gpuName); err != nil {
+			if err := b.AddContainer(effectiveList(c), hip.KindContainer); err != nil {
 				return nil, nil, err
 			}
 		}
@@ -75,7 +77,7 @@ func flattenV1(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpe
 			}
 			for pod := int64(0); pod < k && pod < 2; pod++ {
 				for _, c := range t.spec.Template.Spec.Containers {
-					acc.AddList(effectiveList(c), gpuName, 1)
+					acc.AddList(effectiveList(c), 1)
 				}
 			}
 			if k > 0 {
@@ -103,26 +105,28 @@ func effectiveList(c v1.Container) v1.ResourceList {
 var EngineErrors uint64
 
 // CalcPGMinResourcesEngineE is CalcPGMinResources with the pod counting and the resource sums on the
-// GPU, and the engine's failures returned.  Only DOMAIN refusals go to the reference's
-// CalcPGMinResources (util.go:108): a quantity the int64 tensor path does not hold exactly, an
-// unknown resource key (flattenV1's error) or an int64 overflow (the reference switches to inf.Dec).
-// An engine error is returned as it is -- like the v2 plugin's Build -- so the reconcile fails and is
-// retried (job.go:313's SyncPodGroup error path); it is never answered by the reference's CPU loop.
+// GPU, and the engine's failures returned.  Only an int64 OVERFLOW goes to the reference's
+// CalcPGMinResources (util.go:108; the reference switches to inf.Dec there).  Every other outcome is
+// the engine's: an engine error is returned as it is -- like the v2 plugin's Build -- so the reconcile
+// fails and is retried (job.go:313's SyncPodGroup error path), and so is a flatten error (a negative
+// quantity, which API validation never admits).  gpuName is kept for the signature of earlier wirings:
+// every key is summed now, whatever its name.
 func CalcPGMinResourcesEngineE(eng *hip.Engine, gpuName string) func(int32, map[apiv1.ReplicaType]*apiv1.ReplicaSpec,
 	PriorityClassGetFunc) (*v1.ResourceList, error) {
+	_ = gpuName
 	return func(minMember int32, replicas map[apiv1.ReplicaType]*apiv1.ReplicaSpec, pcGetFunc PriorityClassGetFunc) (*v1.ResourceList, error) {
-		csr, formats, ferr := flattenV1(minMember, replicas, pcGetFunc, gpuName)
+		csr, formats, ferr := flattenV1(minMember, replicas, pcGetFunc)
 		if ferr != nil {
-			return CalcPGMinResources(minMember, replicas, pcGetFunc), nil // domain refusal: exact reference path
+			return nil, fmt.Errorf("placement engine: CalcPGMinResources: %w", ferr)
 		}
-		agg, err := eng.PGMinResources(hip.ModeV1, csr)
+		agg, err := eng.PGMinResourcesKeys(hip.ModeV1, csr)
 		if err != nil {
 			return nil, fmt.Errorf("placement engine: CalcPGMinResources: %w", err)
 		}
 		if agg.Overflow[0] != 0 {
-			return CalcPGMinResources(minMember, replicas, pcGetFunc), nil // domain refusal: inf.Dec sums
+			return CalcPGMinResources(minMember, replicas, pcGetFunc), nil // the inf.Dec case: exact reference path
 		}
-		rl := agg.Unflatten(0, gpuName, formats.Formats()) // printed as the reference's sums print
+		rl := agg.Unflatten(0, formats.Formats()) // printed as the reference's sums print
 		return &rl, nil
 	}
 }
@@ -155,40 +159,37 @@ type PGRequest struct {
 }
 
 // PGMinResourcesBatch is CalcPGMinResources for many jobs at once -- a resync of every job's
-// PodGroup (job.go:455-457 called in a loop) -- with ONE engine call for all the jobs the tensor path
-// holds.  Jobs the tensor path refuses (flatten error) or that overflow take the reference's
-// CalcPGMinResources (domain refusals, as CalcPGMinResourcesEngineE); an engine error fails the whole
-// call (out is nil) and is returned.  out[i] is the answer for reqs[i], exactly the reference's.  The
-// engine pays off above hip.BatchCrossoverJobs jobs.
+// PodGroup (job.go:455-457 called in a loop) -- with ONE engine call (per slice of hip.MaxKeys keys) for
+// all the jobs.  Jobs whose sums overflow take the reference's CalcPGMinResources (the inf.Dec case,
+// as CalcPGMinResourcesEngineE); a flatten error or an engine error fails the whole call (out is nil)
+// and is returned.  out[i] is the answer for reqs[i], exactly the reference's.  The engine pays off
+// above hip.BatchCrossoverJobs jobs.
 func PGMinResourcesBatch(eng *hip.Engine, gpuName string, reqs []PGRequest) ([]*v1.ResourceList, error) {
+	_ = gpuName
 	out := make([]*v1.ResourceList, len(reqs))
-	batch := &hip.CSR{}
-	idx := make([]int, 0, len(reqs))          // batch job -> request
-	formats := make([]*hip.FormatAcc, 0, len(reqs))
+	batch := &hip.KeyCSR{}
+	formats := make([]*hip.KeyFormatAcc, 0, len(reqs))
 	for i, r := range reqs {
-		csr, f, ferr := flattenV1(r.MinMember, r.Replicas, r.PcGetFunc, gpuName)
+		csr, f, ferr := flattenV1(r.MinMember, r.Replicas, r.PcGetFunc)
 		if ferr != nil {
-			out[i] = CalcPGMinResources(r.MinMember, r.Replicas, r.PcGetFunc) // domain refusal: exact reference path
-			continue
+			return nil, fmt.Errorf("placement engine: PGMinResourcesBatch: request %d: %w", i, ferr)
 		}
 		batch.AppendJobs(csr)
-		idx = append(idx, i)
 		formats = append(formats, f)
 	}
-	if len(idx) == 0 {
+	if len(reqs) == 0 {
 		return out, nil
 	}
-	agg, err := eng.PGMinResources(hip.ModeV1, batch)
+	agg, err := eng.PGMinResourcesKeys(hip.ModeV1, batch)
 	if err != nil {
-		return nil, fmt.Errorf("placement engine: PGMinResourcesBatch (%d jobs): %w", len(idx), err)
+		return nil, fmt.Errorf("placement engine: PGMinResourcesBatch (%d jobs): %w", len(reqs), err)
 	}
-	for j, i := range idx {
-		r := reqs[i]
-		if agg.Overflow[j] != 0 {
-			out[i] = CalcPGMinResources(r.MinMember, r.Replicas, r.PcGetFunc) // domain refusal: inf.Dec sums
+	for i, r := range reqs {
+		if agg.Overflow[i] != 0 {
+			out[i] = CalcPGMinResources(r.MinMember, r.Replicas, r.PcGetFunc) // the inf.Dec case: exact reference path
 			continue
 		}
-		rl := agg.Unflatten(j, gpuName, formats[j].Formats())
+		rl := agg.Unflatten(i, formats[i].Formats())
 		out[i] = &rl
 	}
 	return out, nil

@@ -1,17 +1,261 @@
 package hip
 
 // Object graph <-> engine CSR conversion shared by the v1 and v2 adapters (pure Go, no cgo).
-// Canonical units (SURVEY.md Appendix A): cpu in milli-cores (exact iff the Quantity has no finer
-// scale), memory / ephemeral-storage in bytes and the accelerator in units (exact iff integral).
-// Anything else -- another resource key, an inexact or negative value -- is refused, and the
-// adapters answer those objects with the reference's own arbitrary-precision code.
+//
+// KeyCSR (the adapters' form, pe_pg_min_resources_keys): any resource key -- the reference sums every
+// ResourceName (util.go:80-103, coscheduling.go:112-116) -- numbered per call, each key at the finest
+// decimal scale its quantities need, so every value is an exact int64 count of 10^scale units.  Only a
+// value or a sum with no int64 at that scale (Go's inf.Dec case) is flagged for the reference.
+//
+// CSR (pe_pg_min_resources, the four fixed dimensions): canonical units (SURVEY.md Appendix A), cpu
+// in milli-cores, memory / ephemeral-storage in bytes, one accelerator in units.
 
 import (
 	"fmt"
+	"math/big"
 
 	corev1 "k8s.io/api/core/v1"
 	"k8s.io/apimachinery/pkg/api/resource"
 )
+
+// KeyCSR is the flattened batch of pe_pg_min_resources_keys: the job / group / container structure
+// of CSR, and per container its (key, quantity) entries over the batch's key table.
+type KeyCSR struct {
+	JobGroupOff   []int32 // [J+1]
+	MinMember     []int32 // [J] (v1)
+	GroupReplicas []int32 // [G], -1 = nil (v1)
+	GroupContOff  []int32 // [G+1]
+	ContKind      []uint8 // [C] KindContainer / KindInit / KindSidecar / KindOverhead
+	EntOff        []int32 // [C+1]: container c's entries are [EntOff[c], EntOff[c+1])
+	EntKey        []int32 // key id of each entry
+	EntQ          []resource.Quantity
+	Keys          []corev1.ResourceName // key id -> name, first-seen order
+	keyID         map[corev1.ResourceName]int32
+}
+
+func (b *KeyCSR) init() {
+	if len(b.JobGroupOff) == 0 {
+		b.JobGroupOff = append(b.JobGroupOff, 0)
+	}
+	if len(b.GroupContOff) == 0 {
+		b.GroupContOff = append(b.GroupContOff, 0)
+	}
+	if len(b.EntOff) == 0 {
+		b.EntOff = append(b.EntOff, 0)
+	}
+	if b.keyID == nil {
+		b.keyID = map[corev1.ResourceName]int32{}
+		for i, k := range b.Keys {
+			b.keyID[k] = int32(i)
+		}
+	}
+}
+
+func (b *KeyCSR) key(name corev1.ResourceName) int32 {
+	id, ok := b.keyID[name]
+	if !ok {
+		id = int32(len(b.Keys))
+		b.keyID[name] = id
+		b.Keys = append(b.Keys, name)
+	}
+	return id
+}
+
+// AddContainer appends one container record: every key of rl (present even when zero).  A negative
+// quantity -- which API validation never admits into a PodSpec -- is an error, not a fallback.
+func (b *KeyCSR) AddContainer(rl corev1.ResourceList, kind uint8) error {
+	b.init()
+	for name, q := range rl {
+		if q.Sign() < 0 {
+			return &ErrNotTensor{fmt.Sprintf("negative quantity %s=%s", name, q.String())}
+		}
+	}
+	for name, q := range rl {
+		b.EntKey = append(b.EntKey, b.key(name))
+		b.EntQ = append(b.EntQ, q)
+	}
+	b.ContKind = append(b.ContKind, kind)
+	b.EntOff = append(b.EntOff, int32(len(b.EntKey)))
+	return nil
+}
+
+// EndGroup closes the current group (replicas: -1 = nil, v1) and EndJob the current job.
+func (b *KeyCSR) EndGroup(replicas int32) {
+	b.init()
+	b.GroupReplicas = append(b.GroupReplicas, replicas)
+	b.GroupContOff = append(b.GroupContOff, int32(len(b.ContKind)))
+}
+
+func (b *KeyCSR) EndJob(minMember int32) {
+	b.init()
+	b.MinMember = append(b.MinMember, minMember)
+	b.JobGroupOff = append(b.JobGroupOff, int32(len(b.GroupReplicas)))
+}
+
+// AppendJobs appends every job of o (one flattenV1 / flattenInfo result per object) to b, rebasing the
+// offsets and mapping o's key ids into b's key table: a resync of many PodGroups is ONE batch.
+func (b *KeyCSR) AppendJobs(o *KeyCSR) {
+	if len(o.JobGroupOff) < 2 {
+		return
+	}
+	b.init()
+	g0, c0, e0 := int32(len(b.GroupReplicas)), int32(len(b.ContKind)), int32(len(b.EntKey))
+	for _, v := range o.JobGroupOff[1:] {
+		b.JobGroupOff = append(b.JobGroupOff, g0+v)
+	}
+	for _, v := range o.GroupContOff[1:] {
+		b.GroupContOff = append(b.GroupContOff, c0+v)
+	}
+	for _, v := range o.EntOff[1:] {
+		b.EntOff = append(b.EntOff, e0+v)
+	}
+	for _, k := range o.EntKey {
+		b.EntKey = append(b.EntKey, b.key(o.Keys[k]))
+	}
+	b.MinMember = append(b.MinMember, o.MinMember...)
+	b.GroupReplicas = append(b.GroupReplicas, o.GroupReplicas...)
+	b.ContKind = append(b.ContKind, o.ContKind...)
+	b.EntQ = append(b.EntQ, o.EntQ...)
+}
+
+// exp10 is the exponent e of q = m * 10^e with m an integer not divisible by 10 (0 for zero): the
+// finest decimal scale q needs.
+func exp10(q resource.Quantity) int32 {
+	d := q.AsDec()
+	u := new(big.Int).Set(d.UnscaledBig())
+	e := -int32(d.Scale())
+	if u.Sign() == 0 {
+		return 0
+	}
+	ten, r := big.NewInt(10), new(big.Int)
+	for {
+		qq := new(big.Int)
+		qq.QuoRem(u, ten, r)
+		if r.Sign() != 0 {
+			return e
+		}
+		u = qq
+		e++
+	}
+}
+
+// scaled is q / 10^s when that is an exact int64 >= 0.
+func scaled(q resource.Quantity, s int32) (int64, bool) {
+	d := q.AsDec()
+	u := new(big.Int).Set(d.UnscaledBig())
+	if u.Sign() < 0 {
+		return 0, false
+	}
+	k := -int32(d.Scale()) - s // q / 10^s = u * 10^k
+	if k >= 0 {
+		u.Mul(u, new(big.Int).Exp(big.NewInt(10), big.NewInt(int64(k)), nil))
+	} else {
+		r := new(big.Int)
+		u.QuoRem(u, new(big.Int).Exp(big.NewInt(10), big.NewInt(int64(-k)), nil), r)
+		if r.Sign() != 0 {
+			return 0, false
+		}
+	}
+	if !u.IsInt64() {
+		return 0, false
+	}
+	return u.Int64(), true
+}
+
+// Scales is each key's decimal scale: the finest exponent of its nonzero quantities in the batch (0
+// when it has none), so every quantity is an integer count of 10^scale.
+func (b *KeyCSR) Scales() []int32 {
+	sc := make([]int32, len(b.Keys))
+	seen := make([]bool, len(b.Keys))
+	for i, q := range b.EntQ {
+		if q.IsZero() {
+			continue
+		}
+		k, x := b.EntKey[i], exp10(q)
+		if !seen[k] || x < sc[k] {
+			sc[k] = x
+		}
+		seen[k] = true
+	}
+	return sc
+}
+
+// scaledValues converts every entry to its key's scale; a value with no int64 there flags its job
+// (jobOvf), as an overflowed sum is flagged.
+func (b *KeyCSR) scaledValues(scale []int32) (val []int64, jobOvf []uint8) {
+	J := len(b.JobGroupOff) - 1
+	val = make([]int64, len(b.EntQ))
+	jobOvf = make([]uint8, J)
+	for j := 0; j < J; j++ {
+		for g := b.JobGroupOff[j]; g < b.JobGroupOff[j+1]; g++ {
+			for c := b.GroupContOff[g]; c < b.GroupContOff[g+1]; c++ {
+				for x := b.EntOff[c]; x < b.EntOff[c+1]; x++ {
+					v, ok := scaled(b.EntQ[x], scale[b.EntKey[x]])
+					if !ok {
+						jobOvf[j] = 1
+						continue
+					}
+					val[x] = v
+				}
+			}
+		}
+	}
+	return val, jobOvf
+}
+
+// Unflatten turns job j's result back into a ResourceList: one entry per present key (zero values
+// included), each NewScaledQuantity(value, scale) printed in the format the reference's sum ends with
+// (KeyFormatAcc; DecimalSI when the key has none).
+func (a *KeyAgg) Unflatten(j int, formats map[corev1.ResourceName]resource.Format) corev1.ResourceList {
+	nk := len(a.Keys)
+	out := corev1.ResourceList{}
+	for k := 0; k < nk; k++ {
+		if !a.Present[j*nk+k] {
+			continue
+		}
+		q := *resource.NewScaledQuantity(a.MinRes[j*nk+k], resource.Scale(a.Scale[k]))
+		if f, ok := formats[a.Keys[k]]; ok {
+			q.Format = f
+		}
+		out[a.Keys[k]] = q
+	}
+	return out
+}
+
+// KeyFormatAcc is FormatAcc (below) for any resource key: the Quantity.Add format rule, per name.
+type KeyFormatAcc struct {
+	fmt     map[corev1.ResourceName]resource.Format
+	nonzero map[corev1.ResourceName]bool
+}
+
+// Add one contribution of key name (zero = a zero-valued addend, e.g. a product with 0 replicas).
+func (a *KeyFormatAcc) Add(name corev1.ResourceName, q resource.Quantity, zero bool) {
+	if a.fmt == nil {
+		a.fmt = map[corev1.ResourceName]resource.Format{}
+		a.nonzero = map[corev1.ResourceName]bool{}
+	}
+	if _, seen := a.fmt[name]; !seen {
+		a.fmt[name] = q.Format
+		a.nonzero[name] = !zero
+		return
+	}
+	if !a.nonzero[name] {
+		a.fmt[name] = q.Format
+	}
+	if !zero {
+		a.nonzero[name] = true
+	}
+}
+
+// AddList adds every key of rl, scaled by `scale` for the zero test.
+func (a *KeyFormatAcc) AddList(rl corev1.ResourceList, scale int64) {
+	for name, q := range rl {
+		a.Add(name, q, q.IsZero() || scale == 0)
+	}
+}
+
+// Formats is Unflatten's formats argument.
+func (a *KeyFormatAcc) Formats() map[corev1.ResourceName]resource.Format { return a.fmt }
 
 // DimNames are the resource keys of the four engine dimensions.
 func DimNames(gpuName string) [4]corev1.ResourceName {

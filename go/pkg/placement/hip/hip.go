@@ -31,6 +31,8 @@ import (
 	"fmt"
 	"runtime"
 	"unsafe"
+
+	corev1 "k8s.io/api/core/v1"
 )
 
 // Aggregation modes (PE_MODE_*).
@@ -367,6 +369,89 @@ func (e *Engine) PGMinResources(mode int, b *CSR) (*Agg, error) {
 	return out, e.err(rc, "pe_pg_min_resources")
 }
 
+// MaxKeys is PE_MAX_KEYS: the keys of one pe_pg_min_resources_keys call (a batch with more takes one
+// call per slice of keys; keys never interact).
+const MaxKeys = int(C.PE_MAX_KEYS)
+
+// KeysKindShift is PE_KEYS_KIND_SHIFT: the kind bits of a key-table container flag word.
+const KeysKindShift = uint(C.PE_KEYS_KIND_SHIFT)
+
+// KeyAgg holds the per-job results of PGMinResourcesKeys over the batch's key table.
+type KeyAgg struct {
+	Keys     []corev1.ResourceName
+	Scale    []int32 // per key: MinRes values are counts of 10^Scale
+	MinRes   []int64 // [J][len(Keys)]
+	Present  []bool  // [J][len(Keys)] (keys with value 0 included)
+	Members  []int32
+	Overflow []uint8 // 1 = a sum (or a value) with no int64 at its key's scale: the reference's inf.Dec case
+}
+
+// PGMinResourcesKeys aggregates a batch over its per-call key table (pe_pg_min_resources_keys): any
+// resource key, each at the finest decimal scale its quantities need (KeyCSR.Scales), one engine call
+// per slice of MaxKeys keys.  A value with no int64 at its key's scale flags its job like an
+// overflowed sum; flagged jobs are the caller's to hand to the reference.  Every other outcome is
+// exact; an engine error is returned.
+func (e *Engine) PGMinResourcesKeys(mode int, b *KeyCSR) (*KeyAgg, error) {
+	J := len(b.JobGroupOff) - 1
+	if J < 0 {
+		return nil, errors.New("placement: JobGroupOff needs J+1 entries")
+	}
+	nk := len(b.Keys)
+	out := &KeyAgg{Keys: b.Keys, Scale: b.Scales(), MinRes: make([]int64, J*nk), Present: make([]bool, J*nk),
+		Members: make([]int32, J), Overflow: make([]uint8, J)}
+	if J == 0 {
+		return out, nil
+	}
+	val, jobOvf := b.scaledValues(out.Scale)
+	for j := 0; j < J; j++ {
+		out.Overflow[j] = jobOvf[j]
+	}
+	nc := len(b.ContKind)
+	flags := make([]uint32, nc)
+	pres := make([]uint16, J)
+	ovf := make([]uint8, J)
+	for lo := 0; lo < nk || (lo == 0 && nk == 0); lo += MaxKeys {
+		n := nk - lo
+		if n > MaxKeys {
+			n = MaxKeys
+		}
+		if n < 1 {
+			n = 1 // no key at all: one empty key, for Members
+		}
+		req := make([]int64, nc*n)
+		res := make([]int64, J*n)
+		for c := 0; c < nc; c++ {
+			f := uint32(b.ContKind[c]) << KeysKindShift
+			for x := b.EntOff[c]; x < b.EntOff[c+1]; x++ {
+				k := int(b.EntKey[x]) - lo
+				if k < 0 || k >= n || lo+k >= nk {
+					continue
+				}
+				req[c*n+k] = val[x]
+				f |= 1 << uint(k)
+			}
+			flags[c] = f
+		}
+		rc := C.pe_pg_min_resources_keys(e.ctx, C.int32_t(mode), C.int64_t(J), C.int32_t(n), ptr32(b.JobGroupOff),
+			ptr32(b.MinMember), ptr32(b.GroupReplicas), ptr32(b.GroupContOff), ptr64(req), ptru32(flags), ptr64(res),
+			(*C.uint16_t)(unsafe.Pointer(&pres[0])), ptr32(out.Members), ptr8(ovf))
+		if rc != C.PE_OK && rc != C.PE_EOVERFLOW {
+			return nil, e.err(rc, "pe_pg_min_resources_keys")
+		}
+		for j := 0; j < J; j++ {
+			out.Overflow[j] |= ovf[j]
+			for k := 0; k < n && lo+k < nk; k++ {
+				out.MinRes[j*nk+lo+k] = res[j*n+k]
+				out.Present[j*nk+lo+k] = pres[j]>>uint(k)&1 != 0
+			}
+		}
+		if nk == 0 {
+			break
+		}
+	}
+	return out, nil
+}
+
 // FitMask evaluates every job against every node of the shard (device-resident mask); returns the
 // per-job feasible counts of this shard and the mask's words per row.
 func (e *Engine) FitMask(req []int64, need []uint32) (counts []int64, wordsPerRow int64, err error) {
@@ -475,6 +560,16 @@ func (r *Resolver) Close() {
 		C.pe_resolver_destroy(r.r)
 		r.r = nil
 	}
+}
+
+// SetNodes bounds the node ids the blobs and seeds may list (pe_resolver_set_nodes): a blob from any
+// transport with a header count outside [0, topK], an id >= nNodes or unsorted keys is then refused
+// (PE_EINVAL) before the resolver moves.
+func (r *Resolver) SetNodes(nNodes int64) error {
+	if rc := C.pe_resolver_set_nodes(r.r, C.int64_t(nNodes)); rc != C.PE_OK {
+		return fmt.Errorf("placement: pe_resolver_set_nodes: %d", int(rc))
+	}
+	return nil
 }
 
 func (r *Resolver) Done() bool { return C.pe_resolver_done(r.r) != 0 }

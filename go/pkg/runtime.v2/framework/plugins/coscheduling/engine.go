@@ -5,9 +5,10 @@ The reference plugin is pkg/runtime.v2/framework/plugins/coscheduling/coscheduli
 added next to it (same package) and keeps everything but the aggregation: EnforcePodGroupPolicy,
 the watch extension (ReconcilerBuilders, coscheduling.go:298-320), the indexers set up by New
 (:71-85) and needsCreateOrUpdate (:150-153) are the reference's own.  Build (:103-148) computes
-MinMember / MinResources (:108-118) with one pe_pg_min_resources(PE_MODE_V2) call on the GPU
-instead of the Quantity loop; objects the int64 tensor path does not hold exactly (another resource
-key, an inexact value, an int64 overflow) go through the reference's Build unchanged.
+MinMember / MinResources (:108-118) with one pe_pg_min_resources_keys(PE_MODE_V2) call on the GPU
+instead of the Quantity loop, over every resource key the TotalRequests name (a per-call key table,
+each key at the decimal scale its quantities need).  The one object handed to the reference's Build
+is one whose sum has no int64 at its scale (Overflow: the reference's inf.Dec case).
 
 Registration (registry.go:32-42) -- the same name, so the framework's type assertions
 (framework.go:53-77) see the same capabilities:
@@ -67,20 +68,20 @@ func NewWithEngine(eng *hip.Engine, gpuName string) func(ctx context.Context, c 
 // TotalRequests, runtime.go:130-136).  Entries in name order: the sums do not depend on it, and the
 // print formats (hip.FormatAcc: the first nonzero quantity x replicas Build adds per key) follow
 // one of the orders the reference's map range can take.
-func flattenInfo(info *runtime.Info, gpuName string) (*hip.CSR, *hip.FormatAcc, error) {
+func flattenInfo(info *runtime.Info) (*hip.KeyCSR, *hip.KeyFormatAcc, error) {
 	names := make([]string, 0, len(info.TotalRequests))
 	for name := range info.TotalRequests {
 		names = append(names, name)
 	}
 	sort.Strings(names)
-	b := &hip.CSR{}
-	acc := &hip.FormatAcc{}
+	b := &hip.KeyCSR{}
+	acc := &hip.KeyFormatAcc{}
 	for _, name := range names {
 		trr := info.TotalRequests[name]
-		if err := b.AddContainer(trr.PodRequests, hip.KindContainer, gpuName); err != nil {
+		if err := b.AddContainer(trr.PodRequests, hip.KindContainer); err != nil {
 			return nil, nil, err
 		}
-		acc.AddList(trr.PodRequests, gpuName, int64(trr.Replicas))
+		acc.AddList(trr.PodRequests, int64(trr.Replicas))
 		b.EndGroup(trr.Replicas)
 	}
 	b.EndJob(0)
@@ -88,8 +89,8 @@ func flattenInfo(info *runtime.Info, gpuName string) (*hip.CSR, *hip.FormatAcc, 
 }
 
 // unflatten is job 0's ResourceList, printed in the formats the reference's Build would print.
-func unflatten(agg *hip.Agg, gpuName string, formats *hip.FormatAcc) corev1.ResourceList {
-	return agg.Unflatten(0, gpuName, formats.Formats())
+func unflatten(agg *hip.KeyAgg, formats *hip.KeyFormatAcc) corev1.ResourceList {
+	return agg.Unflatten(0, formats.Formats())
 }
 
 // Build is coscheduling.go:103-148 with the aggregation (:108-118) on the engine; the PodGroup is
@@ -99,40 +100,40 @@ func (c *EngineCoScheduling) Build(ctx context.Context, obj client.Object, info 
 	if info == nil || info.RuntimePolicy.PodGroupPolicy == nil || info.RuntimePolicy.PodGroupPolicy.Coscheduling == nil || trainJob == nil {
 		return nil, nil
 	}
-	csr, formats, err := flattenInfo(info, c.gpuName)
-	if err != nil {
-		return c.CoScheduling.Build(ctx, obj, info, trainJob) // exact reference path (inf.Dec, other keys)
+	csr, formats, ferr := flattenInfo(info)
+	if ferr != nil {
+		return nil, ferr // a negative quantity: API validation never admits one
 	}
-	agg, err := c.eng.PGMinResources(hip.ModeV2, csr)
+	agg, err := c.eng.PGMinResourcesKeys(hip.ModeV2, csr)
 	if err != nil {
 		return nil, err
 	}
 	if agg.Overflow[0] != 0 {
-		return c.CoScheduling.Build(ctx, obj, info, trainJob)
+		return c.CoScheduling.Build(ctx, obj, info, trainJob) // the inf.Dec case: exact reference path
 	}
-	return c.CoScheduling.buildPodGroup(ctx, info, trainJob, agg.Members[0], unflatten(agg, c.gpuName, formats))
+	return c.CoScheduling.buildPodGroup(ctx, info, trainJob, agg.Members[0], unflatten(agg, formats))
 }
 
 // BuildBatch is Build for many TrainJobs at once (a resync of every TrainJob's PodGroup): ONE engine
-// call aggregates every (info, trainJob) pair the tensor path holds, the PodGroups are then emitted
-// one by one exactly as Build emits them; pairs the tensor path refuses or that overflow take the
-// reference's Build.  objs[i] / errs[i] answer (infos[i], trainJobs[i]).  The engine pays off above
-// hip.BatchCrossoverJobs pairs; the C++ mirror's kf::CoScheduling::BuildBatch is the same loop.
+// call (per slice of hip.MaxKeys keys) aggregates every (info, trainJob) pair, the PodGroups are then
+// emitted one by one exactly as Build emits them; pairs whose sums overflow take the reference's
+// Build (the inf.Dec case).  objs[i] / errs[i] answer (infos[i], trainJobs[i]).  The engine pays off
+// above hip.BatchCrossoverJobs pairs; the C++ mirror's kf::CoScheduling::BuildBatch is the same loop.
 func (c *EngineCoScheduling) BuildBatch(ctx context.Context, infos []*runtime.Info,
 	trainJobs []*kubeflowv2.TrainJob) ([]client.Object, []error) {
 	objs := make([]client.Object, len(infos))
 	errs := make([]error, len(infos))
-	batch := &hip.CSR{}
+	batch := &hip.KeyCSR{}
 	idx := make([]int, 0, len(infos))
-	formats := make([]*hip.FormatAcc, 0, len(infos))
+	formats := make([]*hip.KeyFormatAcc, 0, len(infos))
 	for i, info := range infos {
 		if info == nil || info.RuntimePolicy.PodGroupPolicy == nil || info.RuntimePolicy.PodGroupPolicy.Coscheduling == nil ||
 			trainJobs[i] == nil {
 			continue // (nil, nil), as Build
 		}
-		csr, f, err := flattenInfo(info, c.gpuName)
-		if err != nil {
-			objs[i], errs[i] = c.CoScheduling.Build(ctx, nil, info, trainJobs[i])
+		csr, f, ferr := flattenInfo(info)
+		if ferr != nil {
+			errs[i] = ferr // a negative quantity, as Build
 			continue
 		}
 		batch.AppendJobs(csr)
@@ -142,16 +143,16 @@ func (c *EngineCoScheduling) BuildBatch(ctx context.Context, infos []*runtime.In
 	if len(idx) == 0 {
 		return objs, errs
 	}
-	agg, err := c.eng.PGMinResources(hip.ModeV2, batch)
+	agg, err := c.eng.PGMinResourcesKeys(hip.ModeV2, batch)
 	for j, i := range idx {
 		switch {
 		case err != nil:
 			errs[i] = err
 		case agg.Overflow[j] != 0:
-			objs[i], errs[i] = c.CoScheduling.Build(ctx, nil, infos[i], trainJobs[i])
+			objs[i], errs[i] = c.CoScheduling.Build(ctx, nil, infos[i], trainJobs[i]) // the inf.Dec case
 		default:
 			objs[i], errs[i] = c.CoScheduling.buildPodGroup(ctx, infos[i], trainJobs[i], agg.Members[j],
-				agg.Unflatten(j, c.gpuName, formats[j].Formats()))
+				agg.Unflatten(j, formats[j].Formats()))
 		}
 	}
 	return objs, errs

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define PE_ABI_VERSION 6
+#define PE_ABI_VERSION 7
 #define PE_DIMS 4
 #define PE_COMM_ID_BYTES 128
 #define PE_MAX_NODES (1LL << 24) /* node ids live in the low 24 bits of the best-fit key */
@@ -223,6 +223,26 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
                         const int64_t* cont_req, const uint8_t* cont_flags, int64_t* out_min_res,
                         uint8_t* out_present, int32_t* out_members, uint8_t* out_overflow);
 
+/* (ABI 7) The same aggregation over a per-call KEY TABLE: any ResourceName the reference sums
+ * (util.go:80-103 AddResourceList; coscheduling.go:112-116), not only the four engine dimensions --
+ * hugepages-2Mi, rdma/hca, several accelerator names, cpu finer than 1m.  The caller numbers the
+ * call's distinct keys 0..n_keys-1 (n_keys <= PE_MAX_KEYS; a batch with more keys takes one call
+ * per key slice: keys never interact) and gives each key a decimal scale s_k of its choosing:
+ * cont_req[c][k] is container c's quantity of key k as an exact int64 count of 10^s_k units (e.g.
+ * s = -9 for "1500u" cpu = 1500000 x 1e-9; bytes at s = 0).  The engine sums the integers per key,
+ * exactly as pe_pg_min_resources does per dimension, and the caller reads result k back at s_k.
+ * A value with no exact int64 at s_k, or a sum that overflows int64 (out_overflow), is what Go
+ * would hold in inf.Dec: the caller's fallback to the reference is for those jobs only.
+ *   cont_flags[c] = presence bits 0..n_keys-1 (keys with value 0 are present) | kind << PE_KEYS_KIND_SHIFT
+ *   out_min_res[J][n_keys], out_present[J] (bit k = key k present), out_members / out_overflow as above.
+ * Other bits in cont_flags are PE_EINVAL. */
+#define PE_MAX_KEYS 16
+#define PE_KEYS_KIND_SHIFT 16
+int pe_pg_min_resources_keys(pe_ctx* ctx, int32_t mode, int64_t n_jobs, int32_t n_keys, const int32_t* job_group_off,
+                             const int32_t* min_member, const int32_t* group_replicas, const int32_t* group_cont_off,
+                             const int64_t* cont_req, const uint32_t* cont_flags, int64_t* out_min_res,
+                             uint16_t* out_present, int32_t* out_members, uint8_t* out_overflow);
+
 /* What-if feasibility (config 5): bit (j, n) = fit(job j, node n) against the CURRENT residuals
  * of this shard, device-resident.  The kernel picks the fastest exact path for the batch and the
  * device layout follows it (pe_fit_mask_layout):
@@ -282,6 +302,12 @@ int pe_resolver_create(int64_t n_jobs, const int32_t* job_group_off, const int32
                        const int32_t* group_count, const int64_t* group_req, const uint32_t* group_need,
                        pe_resolver** out);
 void pe_resolver_destroy(pe_resolver* r);
+/* (ABI 7) Inventory size for the id checks below (default PE_MAX_NODES).  Blobs may arrive over any
+ * transport, so pe_resolver_resolve* validate every header and record before the resolver moves: a
+ * header count outside [0, topk], a listed node id >= n_nodes or keys not strictly ascending within a
+ * shard list (and a seed id >= n_nodes) return PE_EINVAL with no update written and the resolver's
+ * position unchanged -- never a read past the blob. */
+int pe_resolver_set_nodes(pe_resolver* r, int64_t n_nodes);
 int pe_resolver_done(const pe_resolver* r); /* 1 when every job is decided */
 int pe_resolver_next_window(pe_resolver* r, int32_t max_groups, int64_t max_pods, int32_t* out_groups,
                             int32_t* out_n);

@@ -40,6 +40,8 @@ def lib():
         i64, i32 = ctypes.c_int64, ctypes.c_int32
         L.orc_pg_min_resources.argtypes = [i32, i64, P, P, P, P, P, P, P, P, P, P]
         L.orc_pg_min_resources.restype = ctypes.c_int
+        L.orc_pg_min_resources_keys.argtypes = [i32, i64, i32, P, P, P, P, P, P, P, P, P, P]
+        L.orc_pg_min_resources_keys.restype = ctypes.c_int
         L.orc_fit_mask.argtypes = [i64, P, P, i64, P, P, P, P, ctypes.c_int]
         L.orc_fit_mask.restype = ctypes.c_int
         L.orc_place_greedy.argtypes = [i64, P, P, i64, P, P, P, P, P, P, P, ctypes.c_int]
@@ -75,6 +77,26 @@ def pg_min_resources(mode, job_group_off, min_member, group_replicas, group_cont
     ovf = np.zeros(J, dtype=np.uint8)
     rc = lib().orc_pg_min_resources(mode, J, _p(jgo), _p(mm), _p(gr), _p(gco), _p(cr), _p(cf),
                                     _p(out), _p(pres), _p(mem), _p(ovf))
+    assert rc == 0
+    return out, pres, mem, ovf
+
+
+def pg_min_resources_keys(mode, job_group_off, min_member, group_replicas, group_cont_off, cont_req, cont_flags):
+    """Key-table form: cont_req [C][n_keys], cont_flags u32 (presence bits 0..n_keys-1 | kind << 16)."""
+    J = len(job_group_off) - 1
+    jgo = _c(job_group_off, np.int32)
+    mm = _c(min_member if min_member is not None else np.zeros(J), np.int32)
+    gr = _c(group_replicas, np.int32)
+    gco = _c(group_cont_off, np.int32)
+    cr = np.ascontiguousarray(cont_req, dtype=np.int64)
+    nk = cr.shape[1]
+    cf = _c(cont_flags, np.uint32)
+    out = np.zeros((J, nk), dtype=np.int64)
+    pres = np.zeros(J, dtype=np.uint16)
+    mem = np.zeros(J, dtype=np.int32)
+    ovf = np.zeros(J, dtype=np.uint8)
+    rc = lib().orc_pg_min_resources_keys(mode, J, nk, _p(jgo), _p(mm), _p(gr), _p(gco), _p(cr), _p(cf),
+                                         _p(out), _p(pres), _p(mem), _p(ovf))
     assert rc == 0
     return out, pres, mem, ovf
 

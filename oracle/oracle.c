@@ -56,41 +56,50 @@
 static int add_ovf(int64_t a, int64_t b, int64_t* r) { return __builtin_add_overflow(a, b, r); }
 static int mul_ovf(int64_t a, int64_t b, int64_t* r) { return __builtin_mul_overflow(a, b, r); }
 
-/* container flags: bits 0-3 presence of dims, bits 4-5 kind */
+/* container flags: bits 0-3 presence of dims, bits 4-5 kind (the four engine dimensions), or, for a
+ * per-call key table (pe_pg_min_resources_keys), bits 0-15 presence of keys, bits 16-17 kind */
 #define K_CONTAINER 0
 #define K_INIT 1
 #define K_SIDECAR 2
 #define K_OVERHEAD 3
+#define ORC_MAX_KEYS 16
+
+/* flag word of container c: u8 (fixed dims) or u32 (key table) */
+static uint32_t flag_at(const void* fl, int fb, int32_t c) {
+  return fb == 1 ? ((const uint8_t*)fl)[c] : ((const uint32_t*)fl)[c];
+}
 
 /* v1 pod vector: sum of regular containers (util.go:133-140; init containers ignored). */
-static int v1_pod(int32_t c0, int32_t c1, const int64_t* req, const uint8_t* fl, int64_t out[ORC_D],
-                  uint8_t* present) {
+static int v1_pod(int32_t c0, int32_t c1, int nd, int ks, const int64_t* req, const void* fl, int fb,
+                  int64_t out[ORC_MAX_KEYS], uint32_t* present) {
   int ovf = 0;
-  memset(out, 0, sizeof(int64_t) * ORC_D);
+  memset(out, 0, sizeof(int64_t) * ORC_MAX_KEYS);
   *present = 0;
   for (int32_t c = c0; c < c1; ++c) {
-    if (((fl[c] >> 4) & 3) != K_CONTAINER) continue;
-    for (int d = 0; d < ORC_D; ++d)
-      if (fl[c] & (1u << d)) {
-        ovf |= add_ovf(out[d], req[(int64_t)c * ORC_D + d], &out[d]);
-        *present |= (uint8_t)(1u << d);
+    const uint32_t f = flag_at(fl, fb, c);
+    if (((f >> ks) & 3) != K_CONTAINER) continue;
+    for (int d = 0; d < nd; ++d)
+      if (f & (1u << d)) {
+        ovf |= add_ovf(out[d], req[(int64_t)c * nd + d], &out[d]);
+        *present |= 1u << d;
       }
   }
   return ovf;
 }
 
 /* v2 pod vector: kueue v0.6.3 limitrange.TotalRequests restated (runtime.go:134). */
-static int v2_pod(int32_t c0, int32_t c1, const int64_t* req, const uint8_t* fl, int64_t out[ORC_D],
-                  uint8_t* present) {
+static int v2_pod(int32_t c0, int32_t c1, int nd, int ks, const int64_t* req, const void* fl, int fb,
+                  int64_t out[ORC_MAX_KEYS], uint32_t* present) {
   int ovf = 0;
-  int64_t side[ORC_D] = {0}, initmax[ORC_D] = {0}, main_[ORC_D] = {0}, over[ORC_D] = {0};
+  int64_t side[ORC_MAX_KEYS] = {0}, initmax[ORC_MAX_KEYS] = {0}, main_[ORC_MAX_KEYS] = {0}, over[ORC_MAX_KEYS] = {0};
   *present = 0;
   for (int32_t c = c0; c < c1; ++c) {
-    const int kind = (fl[c] >> 4) & 3;
-    for (int d = 0; d < ORC_D; ++d) {
-      if (!(fl[c] & (1u << d))) continue;
-      const int64_t v = req[(int64_t)c * ORC_D + d];
-      *present |= (uint8_t)(1u << d);
+    const uint32_t f = flag_at(fl, fb, c);
+    const int kind = (f >> ks) & 3;
+    for (int d = 0; d < nd; ++d) {
+      if (!(f & (1u << d))) continue;
+      const int64_t v = req[(int64_t)c * nd + d];
+      *present |= 1u << d;
       if (kind == K_SIDECAR) ovf |= add_ovf(side[d], v, &side[d]);
       else if (kind == K_CONTAINER) ovf |= add_ovf(main_[d], v, &main_[d]);
       else if (kind == K_OVERHEAD) ovf |= add_ovf(over[d], v, &over[d]);
@@ -101,7 +110,7 @@ static int v2_pod(int32_t c0, int32_t c1, const int64_t* req, const uint8_t* fl,
       }
     }
   }
-  for (int d = 0; d < ORC_D; ++d) {
+  for (int d = 0; d < nd; ++d) {
     int64_t t;
     ovf |= add_ovf(side[d], main_[d], &t);
     if (initmax[d] > t) t = initmax[d];
@@ -110,20 +119,22 @@ static int v2_pod(int32_t c0, int32_t c1, const int64_t* req, const uint8_t* fl,
   return ovf;
 }
 
-int orc_pg_min_resources(int32_t mode, int64_t n_jobs, const int32_t* job_group_off,
-                         const int32_t* min_member, const int32_t* group_replicas,
-                         const int32_t* group_cont_off, const int64_t* cont_req,
-                         const uint8_t* cont_flags, int64_t* out_res, uint8_t* out_present,
-                         int32_t* out_members, uint8_t* out_overflow) {
+/* nd values per container / job, flags of fb bytes with the kind at bit ks; presence out as u8 or u16 */
+static int pg_min_resources_nd(int32_t mode, int64_t n_jobs, int nd, int fb, const int32_t* job_group_off,
+                               const int32_t* min_member, const int32_t* group_replicas,
+                               const int32_t* group_cont_off, const int64_t* cont_req, const void* cont_flags,
+                               int64_t* out_res, void* out_present, int32_t* out_members, uint8_t* out_overflow) {
   if (mode != ORC_V1 && mode != ORC_V2) return -1;
+  const int ks = fb == 1 ? 4 : 16;
   for (int64_t j = 0; j < n_jobs; ++j) {
-    int64_t acc[ORC_D] = {0};
-    uint8_t pres = 0, ovf = 0;
+    int64_t acc[ORC_MAX_KEYS] = {0};
+    uint32_t pres = 0;
+    uint8_t ovf = 0;
     int32_t pod_cnt = 0;
     uint32_t members = 0; /* Go int32 arithmetic wraps */
     for (int32_t g = job_group_off[j]; g < job_group_off[j + 1]; ++g) {
-      int64_t pod[ORC_D];
-      uint8_t pp;
+      int64_t pod[ORC_MAX_KEYS];
+      uint32_t pp;
       int64_t k;
       const int32_t r = group_replicas[g];
       if (mode == ORC_V1) {
@@ -132,13 +143,13 @@ int orc_pg_min_resources(int32_t mode, int64_t n_jobs, const int32_t* job_group_
         if (room <= 0) continue;
         k = r < room ? r : room;
         pod_cnt += (int32_t)k;
-        ovf |= v1_pod(group_cont_off[g], group_cont_off[g + 1], cont_req, cont_flags, pod, &pp);
+        ovf |= v1_pod(group_cont_off[g], group_cont_off[g + 1], nd, ks, cont_req, cont_flags, fb, pod, &pp);
       } else {
         members += (uint32_t)r;
         k = r;
-        ovf |= v2_pod(group_cont_off[g], group_cont_off[g + 1], cont_req, cont_flags, pod, &pp);
+        ovf |= v2_pod(group_cont_off[g], group_cont_off[g + 1], nd, ks, cont_req, cont_flags, fb, pod, &pp);
       }
-      for (int d = 0; d < ORC_D; ++d)
+      for (int d = 0; d < nd; ++d)
         if (pp & (1u << d)) {
           int64_t t;
           ovf |= mul_ovf(pod[d], k, &t);
@@ -147,12 +158,35 @@ int orc_pg_min_resources(int32_t mode, int64_t n_jobs, const int32_t* job_group_
       pres |= pp;
     }
     /* an overflowed job has no int64 answer (Go holds it in inf.Dec): values are defined as 0 */
-    for (int d = 0; d < ORC_D; ++d) out_res[j * ORC_D + d] = ovf ? 0 : acc[d];
-    out_present[j] = pres;
+    for (int d = 0; d < nd; ++d) out_res[j * nd + d] = ovf ? 0 : acc[d];
+    if (fb == 1) ((uint8_t*)out_present)[j] = (uint8_t)pres;
+    else ((uint16_t*)out_present)[j] = (uint16_t)pres;
     out_members[j] = mode == ORC_V1 ? pod_cnt : (int32_t)members;
     out_overflow[j] = ovf ? 1 : 0;
   }
   return 0;
+}
+
+int orc_pg_min_resources(int32_t mode, int64_t n_jobs, const int32_t* job_group_off,
+                         const int32_t* min_member, const int32_t* group_replicas,
+                         const int32_t* group_cont_off, const int64_t* cont_req,
+                         const uint8_t* cont_flags, int64_t* out_res, uint8_t* out_present,
+                         int32_t* out_members, uint8_t* out_overflow) {
+  return pg_min_resources_nd(mode, n_jobs, ORC_D, 1, job_group_off, min_member, group_replicas, group_cont_off,
+                             cont_req, cont_flags, out_res, out_present, out_members, out_overflow);
+}
+
+/* Key-table form (placement.h pe_pg_min_resources_keys): n_keys <= 16 keys of the caller's choosing,
+ * each an exact int64 at the caller's per-key decimal scale; the same rule per key (util.go:80-103 and
+ * coscheduling.go:112-116 sum any ResourceName). */
+int orc_pg_min_resources_keys(int32_t mode, int64_t n_jobs, int32_t n_keys, const int32_t* job_group_off,
+                              const int32_t* min_member, const int32_t* group_replicas,
+                              const int32_t* group_cont_off, const int64_t* cont_req,
+                              const uint32_t* cont_flags, int64_t* out_res, uint16_t* out_present,
+                              int32_t* out_members, uint8_t* out_overflow) {
+  if (n_keys < 1 || n_keys > ORC_MAX_KEYS) return -1;
+  return pg_min_resources_nd(mode, n_jobs, n_keys, 4, job_group_off, min_member, group_replicas, group_cont_off,
+                             cont_req, cont_flags, out_res, out_present, out_members, out_overflow);
 }
 
 /* ------------------------------------------------------------------ fit / score */

@@ -176,14 +176,14 @@ static std::map<ReplicaType, ReplicaSpec> mnist(int workers) {
 }
 
 TEST_CPU(TestFlattenV1Mnist) {
-  Dims dims{"nvidia.com/gpu"};
   Flat f;
-  FlattenV1Job(dims, 2, mnist(1), kNoPC, &f);
+  FlattenV1Job(2, mnist(1), kNoPC, &f);
   CHECK((f.job_group_off == std::vector<int32_t>{0, 2}));
   CHECK((f.group_replicas == std::vector<int32_t>{1, 1}));
   CHECK((f.group_cont_off == std::vector<int32_t>{0, 1, 2}));
-  CHECK((f.cont_flags == std::vector<uint8_t>{1u << 2, 1u << 2}));   // limits -> gpu dim present
-  CHECK(f.cont_req[2] == 1 && f.cont_req[6] == 1);
+  CHECK((f.keys == std::vector<std::string>{"nvidia.com/gpu"}));   // limits -> the gpu key present
+  CHECK((f.ent_off == std::vector<int32_t>{0, 1, 2}));
+  CHECK(f.ent_q[0].Equal(Quantity::Parse("1")) && f.ent_q[1].Equal(Quantity::Parse("1")));
 }
 
 TEST_CPU(TestFlattenV1EmptyRequestsDoNotFallBack) {
@@ -192,8 +192,8 @@ TEST_CPU(TestFlattenV1EmptyRequestsDoNotFallBack) {
   w.replicas = 2;
   w.template_spec.containers = {Ctr(ResourceList{}, RL({{"cpu", "4"}}))};
   Flat f;
-  FlattenV1Job(Dims{}, 2, {{"Worker", w}}, kNoPC, &f);
-  CHECK(f.cont_flags[0] == 0);
+  FlattenV1Job(2, {{"Worker", w}}, kNoPC, &f);
+  CHECK(f.ent_off.size() == 2 && f.ent_off[1] == 0 && f.keys.empty());
 }
 
 TEST_CPU(TestFlattenV1PriorityOrder) {
@@ -207,24 +207,41 @@ TEST_CPU(TestFlattenV1PriorityOrder) {
     return n == "high" ? std::optional<PriorityClass>(PriorityClass{1000}) : std::nullopt;
   };
   Flat f;
-  FlattenV1Job(Dims{}, 2, {{"Worker", w}, {"Master", m}}, pc, &f);
-  CHECK(f.cont_req[0] == 16000);                 // the high-priority Master is counted first
+  FlattenV1Job(2, {{"Worker", w}, {"Master", m}}, pc, &f);
+  CHECK(f.ent_q[0].Equal(Quantity::Parse("16")));   // the high-priority Master is counted first
   CHECK((f.group_replicas == std::vector<int32_t>{1, 3}));
 }
 
-TEST_CPU(TestFlattenRejectsUnknownResource) {
+// Key tables (verdict r5 item 2): any ResourceName flattens -- hugepages, rdma, a second accelerator,
+// cpu finer than 1m -- each key at the finest decimal scale its quantities need; only a negative
+// quantity is refused (all-or-nothing append).
+TEST_CPU(TestFlattenAnyResourceKeyAndScales) {
   ReplicaSpec w;
   w.replicas = 1;
-  w.template_spec.containers = {Ctr(RL({{"hugepages-2Mi", "1Gi"}}))};
+  w.template_spec.containers = {Ctr(RL({{"hugepages-2Mi", "1Gi"}, {"rdma/hca", "1"}, {"cpu", "1500u"}})),
+                                Ctr(RL({{"cpu", "2"}, {"amd.com/gpu", "8"}, {"nvidia.com/gpu", "1"}}))};
   Flat f;
+  FlattenV1Job(1, {{"Worker", w}}, kNoPC, &f);
+  CHECK(f.keys.size() == 5 && f.key_id.count("hugepages-2Mi") && f.key_id.count("amd.com/gpu"));
+  const std::vector<int> sc = f.Scales();
+  CHECK(sc[f.key_id.at("cpu")] == -4 && sc[f.key_id.at("hugepages-2Mi")] == 0 && sc[f.key_id.at("rdma/hca")] == 0);
+  CHECK(Quantity::Parse("1500u").Scaled(-4) == 15 && Quantity::Parse("2").Scaled(-4) == 20000);
+  CHECK(Quantity::Parse("1Gi").Scaled(0) == (1LL << 30) && !Quantity::Parse("1500u").Scaled(-3));
+  CHECK(Quantity::Parse("5e18").Scaled(0) == 5000000000000000000LL && !Quantity::Parse("1e19").Scaled(0));
+  CHECK(Quantity::Parse("1e19").Scaled(19) == 1 && Quantity::Parse("3k").Exp10() == 3 && Quantity::Parse("1.5Ki").Exp10() == 0);
+  CHECK(Quantity::FromScaled(1003, -3, Format::kDecimalSI).String() == "1003m");
+  CHECK(Quantity::FromScaled(2560LL << 20, 0, Format::kBinarySI).String() == "2560Mi");
+  ReplicaSpec bad;
+  bad.replicas = 1;
+  bad.template_spec.containers = {Ctr(RL({{"cpu", "-1"}}))};
   bool threw = false;
   try {
-    FlattenV1Job(Dims{}, 1, {{"Worker", w}}, kNoPC, &f);
+    FlattenV1Job(1, {{"Worker", bad}}, kNoPC, &f);
   } catch (const Error& e) {
     threw = e.code == PE_EINVAL;
   }
   CHECK(threw);
-  CHECK(f.job_group_off.size() == 1 && f.cont_flags.empty());   // all-or-nothing append
+  CHECK(f.job_group_off.size() == 2 && f.cont_kind.size() == 2);   // all-or-nothing append
 }
 
 // a started PriorityClass informer and the deterministic tie policy
@@ -256,7 +273,7 @@ TEST_CPU(TestPriorityClassInformerAndTiePolicy) {
          std::vector<ReplicaType>{"Launcher", "Worker", "Master"}));
   // the flattened CSR follows the order
   Flat f;
-  FlattenV1Job(Dims{"nvidia.com/gpu"}, 2, reps, inf.Lister(), &f, V1OrderPolicy{{"Worker"}});
+  FlattenV1Job(2, reps, inf.Lister(), &f, V1OrderPolicy{{"Worker"}});
   CHECK((f.group_replicas == std::vector<int32_t>{1, 4, 1}));   // Launcher(7), Worker(tie first), Master
 }
 
@@ -587,6 +604,73 @@ TEST_GPU(TestCalcPGMinResourcesBatchAndOverflow) {
   bool threw = false;
   try {
     CalcPGMinResources(eng(), 4, {{"Worker", w}}, kNoPC);
+  } catch (const Error& e) {
+    threw = e.code == PE_EOVERFLOW;
+  }
+  CHECK(threw);
+}
+
+// Verdict r5 item 2: keys beyond the four engine dimensions reach the GPU (tests/golden/wide_keys.json
+// cases 1-2 and the v2 sidecar case, hand-derived); only an int64 overflow is the reference's.
+TEST_GPU(TestCalcPGMinResourcesWideKeys) {
+  ReplicaSpec m, w;
+  m.replicas = 1;
+  m.template_spec.containers = {Ctr(RL({{"cpu", "2"}, {"memory", "8Gi"}, {"hugepages-2Mi", "1Gi"}, {"rdma/hca", "1"},
+                                        {"nvidia.com/gpu", "1"}}))};
+  w.replicas = 3;
+  w.template_spec.containers = {Ctr(RL({{"cpu", "2"}, {"memory", "8Gi"}, {"hugepages-2Mi", "512Mi"}, {"rdma/hca", "1"},
+                                        {"nvidia.com/gpu", "1"}}))};
+  auto pg = CalcPodGroupSpecV1(eng(), {{"Master", m}, {"Worker", w}}, nullptr, kNoPC);
+  CHECK(pg.min_member == 4);
+  CHECK(EqualResourceList(pg.min_resources, RL({{"cpu", "8"}, {"memory", "32Gi"}, {"hugepages-2Mi", "2560Mi"},
+                                                {"rdma/hca", "4"}, {"nvidia.com/gpu", "4"}})));
+  CHECK(pg.min_resources.at("hugepages-2Mi").String() == "2560Mi");
+  ReplicaSpec a, b;
+  a.replicas = 1;
+  a.template_spec.containers = {Ctr(RL({{"nvidia.com/gpu", "1"}, {"cpu", "1"}}))};
+  b.replicas = 2;
+  b.template_spec.containers = {Ctr(RL({{"amd.com/gpu", "8"}, {"cpu", "1500u"}}))};
+  auto pg2 = CalcPodGroupSpecV1(eng(), {{"Master", a}, {"Worker", b}}, nullptr, kNoPC);
+  CHECK(EqualResourceList(pg2.min_resources, RL({{"nvidia.com/gpu", "1"}, {"amd.com/gpu", "16"}, {"cpu", "1003m"}})));
+  CHECK(pg2.min_resources.at("cpu").String() == "1003m");
+  // v2: a sidecar in micro-cores, an extended key, pod overhead; 2 trainer nodes
+  InfoOptions o;
+  PodSpec pod;
+  pod.init_containers = {Ctr(RL({{"cpu", "1500u"}, {"example.com/fpga", "1"}}), std::nullopt, std::string("Always"))};
+  pod.containers = {Ctr(RL({{"cpu", "2"}, {"memory", "1Gi"}}))};
+  pod.overhead = RL({{"cpu", "100m"}});
+  o.pod_spec_replicas = {{"trainer-node", 1, pod}};
+  o.ml_policy = MLPolicy{2, MLPolicy::kPlainML};
+  o.pod_group_policy = PodGroupPolicy{CoschedulingPodGroupPolicySource{}};
+  Info info = NewInfo(eng(), o);
+  TrainJob tj;
+  tj.name = "wide";
+  PlainML().EnforceMLPolicy(&info, &tj);
+  CoScheduling cs(eng());
+  auto r = cs.Build(&info, &tj, nullptr);
+  CHECK(r.object && !r.error);
+  if (r.object) {
+    CHECK(r.object->min_member == 2);
+    CHECK(EqualResourceList(r.object->min_resources,
+                            RL({{"cpu", "4203m"}, {"example.com/fpga", "2"}, {"memory", "2Gi"}})));
+  }
+  // 21 keys: two key slices of one call
+  ResourceList many;
+  for (int i = 0; i < 20; ++i) many["example.com/r" + std::to_string(100 + i)] = Quantity::Parse("1");
+  many["cpu"] = Quantity::Parse("1");
+  ReplicaSpec z;
+  z.replicas = 5;
+  z.template_spec.containers = {Ctr(many)};
+  ResourceList want;
+  for (auto& kv : many) want[kv.first] = Quantity::Parse("5");
+  CHECK(EqualResourceList(CalcPGMinResources(eng(), 5, {{"Worker", z}}, kNoPC), want));
+  // an int64 sum overflow stays the one refused case
+  ReplicaSpec h;
+  h.replicas = 2;
+  h.template_spec.containers = {Ctr(RL({{"example.com/huge", "5e18"}})), Ctr(RL({{"example.com/huge", "1"}}))};
+  bool threw = false;
+  try {
+    CalcPGMinResources(eng(), 2, {{"Worker", h}}, kNoPC);
   } catch (const Error& e) {
     threw = e.code == PE_EOVERFLOW;
   }

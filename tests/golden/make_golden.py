@@ -204,10 +204,76 @@ V1_PODGROUP = {
 }
 
 
+# Keys outside the four engine dimensions (verdict r5 item 2): the reference sums ANY ResourceName
+# (util.go:80-103 AddResourceList, coscheduling.go:112-116), so the engine's key-table path
+# (placement.h pe_pg_min_resources_keys) must too.  No reference test uses such keys: the answers are
+# derived by hand from the cited code ("pinned": false), and tests/test_oracle_golden.py checks them
+# against the object-level restatement (oracle/semantics.py) as well.  "overflow": true marks a case
+# whose int64 sum overflows -- the one case the adapters hand to the reference (inf.Dec).
+FAT_POD = {"cpu": "2", "memory": "8Gi", "hugepages-2Mi": "1Gi", "rdma/hca": "1", "nvidia.com/gpu": "1"}
+MANY_KEYS = dict({f"example.com/r{i:02d}": "1" for i in range(20)}, cpu="1")
+WIDE_KEYS = {
+    "source": "hand-derived: keys beyond cpu/memory/one accelerator/ephemeral-storage (parity unpinned)",
+    "v1": [
+        {"name": "hugepages + rdma + gpu, Master 1 + Worker 3", "ref": "util.go:79-104,126-141", "pinned": False,
+         "replicas": {"Master": {"replicas": 1, "template": {"containers": [{"requests": FAT_POD}]}},
+                      "Worker": {"replicas": 3, "template": {"containers": [
+                          {"requests": dict(FAT_POD, **{"hugepages-2Mi": "512Mi"})}]}}},
+         "scheduling_policy": None, "want_min_member": 4,
+         "want": {"cpu": "8", "memory": "32Gi", "hugepages-2Mi": "2560Mi", "rdma/hca": "4", "nvidia.com/gpu": "4"}},
+        {"name": "two accelerator names and cpu in micro-cores", "ref": "util.go:79-104", "pinned": False,
+         "replicas": {"Master": {"replicas": 1, "template": {"containers": [
+                          {"requests": {"nvidia.com/gpu": "1", "cpu": "1"}}]}},
+                      "Worker": {"replicas": 2, "template": {"containers": [
+                          {"requests": {"amd.com/gpu": "8", "cpu": "1500u"}}]}}},
+         "scheduling_policy": None, "want_min_member": 3,
+         "want": {"nvidia.com/gpu": "1", "amd.com/gpu": "16", "cpu": "1003m"}},
+        {"name": "cpu finer than 1m under minAvailable", "ref": "job.go:258-260; util.go:126-141", "pinned": False,
+         "replicas": {"Worker": {"replicas": 4, "template": {"containers": [
+                          {"requests": {"cpu": "250u", "memory": "100Mi"}}]}}},
+         "scheduling_policy": {"minAvailable": 2}, "want_min_member": 2,
+         "want": {"cpu": "500u", "memory": "200Mi"}},
+        {"name": "limits of extended resources when Requests is nil", "ref": "util.go:90-101", "pinned": False,
+         "replicas": {"Worker": {"replicas": 2, "template": {"containers": [
+                          {"limits": {"rdma/hca": "2", "hugepages-1Gi": "3Gi"}}]}}},
+         "scheduling_policy": None, "want_min_member": 2, "want": {"rdma/hca": "4", "hugepages-1Gi": "6Gi"}},
+    ],
+    "v2": [
+        {"name": "hugepages / rdma in init and main containers, 3 trainer nodes",
+         "ref": "runtime.go:134 (kueue TotalRequests); coscheduling.go:108-118", "pinned": False,
+         "replicated_jobs": [
+             ["initializer", {"initContainers": [{"requests": {"cpu": "1", "hugepages-1Gi": "2Gi"}}],
+                              "containers": [{"requests": {"cpu": "500m", "rdma/hca": "1"}}]}],
+             ["trainer-node", trainer_pod({"cpu": "4", "amd.com/gpu": "8", "rdma/hca": "2", "hugepages-1Gi": "4Gi"})]],
+         "ml_policy": {"numNodes": 3, "source": "plainml"}, "trainjob_num_nodes": None,
+         "want": {"minMember": 4, "minResources": {"cpu": "13", "hugepages-1Gi": "14Gi", "rdma/hca": "7",
+                                                   "amd.com/gpu": "24"}}},
+        {"name": "sidecar in micro-cores, an extended key, pod overhead",
+         "ref": "runtime.go:134 (kueue TotalRequests); coscheduling.go:108-118", "pinned": False,
+         "replicated_jobs": [
+             ["trainer-node", {"initContainers": [{"requests": {"cpu": "1500u", "example.com/fpga": "1"},
+                                                   "restartPolicy": "Always"}],
+                               "containers": [{"requests": {"cpu": "2", "memory": "1Gi"}}],
+                               "overhead": {"cpu": "100m"}}]],
+         "ml_policy": {"numNodes": 2, "source": "plainml"}, "trainjob_num_nodes": None,
+         "want": {"minMember": 2, "minResources": {"cpu": "4203m", "example.com/fpga": "2", "memory": "2Gi"}}},
+        {"name": "21 keys: more than one 16-key slice", "ref": "coscheduling.go:112-116", "pinned": False,
+         "replicated_jobs": [["trainer-node", trainer_pod(MANY_KEYS)]],
+         "ml_policy": {"numNodes": 5, "source": "plainml"}, "trainjob_num_nodes": None,
+         "want": {"minMember": 5, "minResources": {k: "5" for k in MANY_KEYS}}},
+        {"name": "an int64 overflow is the reference's (inf.Dec) case", "ref": "coscheduling.go:112-116", "pinned": False,
+         "replicated_jobs": [["trainer-node", {"containers": [{"requests": {"example.com/huge": "5e18"}},
+                                                              {"requests": {"example.com/huge": "1"}}]}]],
+         "ml_policy": {"numNodes": 2, "source": "plainml"}, "trainjob_num_nodes": None, "overflow": True,
+         "want": {"minMember": 2, "minResources": {"example.com/huge": "10000000000000000002"}}},
+    ],
+}
+
+
 def main():
     for name, obj in [("v2_total_requests", V2_TOTAL_REQUESTS), ("v2_enforce_ml_policy", V2_ENFORCE_ML_POLICY),
                       ("v2_podgroup", V2_PODGROUP), ("v2_build_from_info", V2_BUILD_FROM_INFO),
-                      ("v1_podgroup", V1_PODGROUP)]:
+                      ("v1_podgroup", V1_PODGROUP), ("wide_keys", WIDE_KEYS)]:
         with open(os.path.join(HERE, name + ".json"), "w") as f:
             json.dump(obj, f, indent=1, sort_keys=False)
             f.write("\n")

@@ -31,7 +31,7 @@ def test_every_declared_symbol_is_exported():
 
 def test_abi_version_and_structs(tmp_path):
     lib = _abi.load()
-    assert lib.pe_abi_version() == 6
+    assert lib.pe_abi_version() == 7
     # pe_config / pe_stats layouts mirrored in _abi must match the C compiler's (size and offsets)
     src = tmp_path / "sz.c"
     fields = [f for f, _ in _abi.PeConfig._fields_]

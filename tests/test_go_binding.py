@@ -92,25 +92,31 @@ def test_cgo_preamble_and_package():
 
 @pytest.mark.parametrize("path,needles", [
     (COSCHED_GO, ["package coscheduling", "func NewWithEngine(", "func flattenInfo(", "func unflatten(",
-                  "PGMinResources(hip.ModeV2", "needsCreateOrUpdate(oldPG, newPG", "SetControllerReference",
+                  "PGMinResourcesKeys(hip.ModeV2", "needsCreateOrUpdate(oldPG, newPG", "SetControllerReference",
                   "c.CoScheduling.Build(ctx, obj, info, trainJob)", "framework.ComponentBuilderPlugin",
                   # the PodGroup emission (coscheduling.go:119-147) exists once, as a helper both Builds call
                   "func (c *CoScheduling) buildPodGroup(", "return c.CoScheduling.buildPodGroup(ctx, info, trainJob",
                   # print formats of the reference's Build sums (first nonzero quantity x replicas per key)
-                  "acc.AddList(trr.PodRequests, gpuName, int64(trr.Replicas))", "formats.Formats()",
+                  "acc.AddList(trr.PodRequests, int64(trr.Replicas))", "formats.Formats()",
                   # batch entry point (a resync of many TrainJobs): one engine call, emission per object
                   "func (c *EngineCoScheduling) BuildBatch(", "batch.AppendJobs(csr)",
                   "c.CoScheduling.buildPodGroup(ctx, infos[i], trainJobs[i], agg.Members[j]"]),
-    (V1_GO, ["package common", "func flattenV1(", "func CalcPGMinResourcesEngine(", "PGMinResources(hip.ModeV1",
+    (V1_GO, ["package common", "func flattenV1(", "func CalcPGMinResourcesEngine(", "PGMinResourcesKeys(hip.ModeV1",
              "c.Resources.Limits", "CalcPGMinResources(minMember, replicas, pcGetFunc)", "pc.Value",
              # print formats of AddResourceList's sums, replayed over the counted pods (util.go:79-104,126-141)
-             "acc.AddList(effectiveList(c), gpuName, 1)", "agg.Unflatten(0, gpuName, formats.Formats())",
-             "func PGMinResourcesBatch(", "batch.AppendJobs(csr)", "agg.Unflatten(j, gpuName, formats[j].Formats())",
+             "acc.AddList(effectiveList(c), 1)", "agg.Unflatten(0, formats.Formats())",
+             "func PGMinResourcesBatch(", "batch.AppendJobs(csr)", "agg.Unflatten(i, formats[i].Formats())",
              # engine errors are returned (E form, batch) or counted + logged, never answered by the reference
              "func CalcPGMinResourcesEngineE(", "var EngineErrors uint64", "atomic.AddUint64(&EngineErrors, 1)",
              "return nil, fmt.Errorf(\"placement engine: CalcPGMinResources: %w\", err)"]),
     (FLATTEN_GO, ["type FormatAcc struct", "func (a *FormatAcc) Add(", "func (a *FormatAcc) Formats()",
-                  "if !a.nonzero[d] {", "func (b *CSR) AppendJobs(o *CSR)", "BatchCrossoverJobs"]),
+                  "if !a.nonzero[d] {", "func (b *CSR) AppendJobs(o *CSR)", "BatchCrossoverJobs",
+                  # key tables (ABI 7): any key, per-key decimal scale, key ids remapped on append
+                  "type KeyCSR struct", "func (b *KeyCSR) Scales() []int32", "func exp10(", "func scaled(",
+                  "b.EntKey = append(b.EntKey, b.key(o.Keys[k]))", "func (a *KeyAgg) Unflatten(",
+                  "type KeyFormatAcc struct", "if !a.nonzero[name] {"]),
+    (HIP_GO, ["func (e *Engine) PGMinResourcesKeys(", "lo += MaxKeys", "out.Overflow[j] |= ovf[j]",
+              "rc != C.PE_OK && rc != C.PE_EOVERFLOW", "func (r *Resolver) SetNodes("]),
 ])
 def test_adapters(path, needles):
     text = open(path).read()
@@ -125,24 +131,30 @@ def _go_code(path):
 
 @pytest.mark.parametrize("path", [V1_GO, COSCHED_GO])
 def test_engine_errors_never_reach_the_reference(path):
-    """Only domain refusals (a flatten error, int64 overflow) may take the reference's CPU function;
-    an engine error is returned (or, in the v1 signature form, counted and logged): no branch tests
-    the engine's error together with a fallback condition, and every reference call sits under a
-    flatten error or an Overflow test."""
+    """The reference's CPU function is called for int64 OVERFLOW only (verdict r5 item 2: the key table
+    takes every resource key, so no other domain refusal is left): every reference call sits under an
+    Overflow test, a flatten error is returned like an engine error, and no branch tests the engine's
+    error together with a fallback condition."""
     code = _go_code(path)
     assert "err != nil ||" not in code and "|| err != nil" not in code
     ref = "CalcPGMinResources(" if path == V1_GO else "c.CoScheduling.Build("
     lines = code.splitlines()
+    n_ref = 0
     for i, line in enumerate(lines):
         if ref in line and "func " not in line and "Engine" not in line:
+            n_ref += 1
             guard = "\n".join(lines[max(0, i - 2):i])
-            assert "ferr != nil" in guard or "Overflow" in guard or ("err != nil" in guard and "flatten" in guard), \
-                (os.path.basename(path), i + 1, guard)
-        if "eng.PGMinResources(" in line:
+            assert "Overflow[" in guard, (os.path.basename(path), i + 1, guard)
+        if "ferr != nil" in line:
+            after = "\n".join(lines[i + 1:i + 3])
+            assert ref not in after and ("return" in after or "errs[i] = ferr" in after), after
+        if "eng.PGMinResourcesKeys(" in line:
             after = "\n".join(lines[i + 1:i + 5])
             # the first test after the engine call is its error, answered by returning / recording it
             assert ("if err != nil" in after and "return" in after) or \
                    ("case err != nil:" in after and "errs[i] = err" in after), after
+        assert "eng.PGMinResources(" not in line, "the adapters use the key-table entry point"
+    assert n_ref >= 2
 
 
 def test_podgroup_emission_not_duplicated():

@@ -131,3 +131,82 @@ def test_agg_resync_batch_equals_per_object_calls(eng, mode):
         one = eng.pg_min_resources(mode, *parts[i])
         for a, b in zip(one, got):
             np.testing.assert_array_equal(a[0], b[i])
+
+
+# ------------------------------------------------------------------ key tables (ABI 7)
+
+def random_keys_csr(J, n_keys, seed, big=False):
+    """random_csr's structure with n_keys values per container and u32 flags (presence bits of the
+    n_keys keys | kind << 16)."""
+    jgo, mm, rep, gco, _, fl8 = random_csr(J, seed, big)
+    rng = np.random.default_rng(seed + 1)
+    C = int(gco[-1])
+    hi = 2**62 if big else 2**40
+    req = rng.integers(0, hi, (C, n_keys), dtype=np.int64)
+    req[rng.random((C, n_keys)) < 0.3] = 0
+    pres = rng.integers(0, 1 << n_keys, C, dtype=np.int64).astype(np.uint32)
+    fl = pres | ((fl8.astype(np.uint32) >> 4) << 16)
+    return jgo, mm, rep, gco, req, fl
+
+
+def _check_keys(eng, mode, arrs):
+    got = eng.pg_min_resources_keys(mode, *arrs)
+    want = oracle.pg_min_resources_keys(mode, *arrs)
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+    return got
+
+
+@pytest.mark.parametrize("n_keys", [1, 3, 4, 5, 8, 9, 13, 16])
+@pytest.mark.parametrize("J", [1, 20, 300, 9000, 40000])
+def test_agg_keys_random_vs_oracle(eng, n_keys, J):
+    """pe_pg_min_resources_keys for every kernel width (4 / 8 / 16 keys, narrower tables padded) on
+    every call path (kernel arguments, one latency launch, chunked batches, the multi-range planner),
+    random values incl. int64 overflow, bit-exact vs orc_pg_min_resources_keys."""
+    for mode in (V1, V2):
+        _check_keys(eng, mode, random_keys_csr(J, n_keys, 40 + J + n_keys + mode, big=(J % 2 == 0)))
+
+
+def test_agg_keys_equal_fixed_dims(eng):
+    """A 4-key table with the fixed dimensions' values gives exactly pe_pg_min_resources' answers."""
+    for mode in (V1, V2):
+        jgo, mm, rep, gco, req, fl8 = random_csr(5000, 77 + mode, big=True)
+        fl = (fl8.astype(np.uint32) & 15) | ((fl8.astype(np.uint32) >> 4) << 16)
+        a = eng.pg_min_resources(mode, jgo, mm, rep, gco, req, fl8)
+        b = eng.pg_min_resources_keys(mode, jgo, mm, rep, gco, req, fl)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+
+
+def test_agg_keys_rejects_bad_flags(eng):
+    from placement import PlacementError
+    jgo, mm, rep, gco, req, fl = random_keys_csr(50, 5, 3)
+    fl = fl.copy()
+    fl[7] |= 1 << 5                 # a presence bit past n_keys
+    with pytest.raises(PlacementError) as ei:
+        eng.pg_min_resources_keys(V1, jgo, mm, rep, gco, req, fl)
+    assert ei.value.code == -1 and "cont_flags[7]" in str(ei.value)
+    with pytest.raises(PlacementError):
+        eng.pg_min_resources_keys(V1, jgo, mm, rep, gco, np.zeros((len(fl), 17), np.int64), fl & 0xFFFF0000)
+
+
+def test_agg_keys_wide_golden(eng, golden_dir):
+    """wide_keys.json on the GPU (verdict r5 item 2): hugepages-2Mi / -1Gi, rdma/hca, nvidia.com/gpu +
+    amd.com/gpu, cpu in micro-cores, 21 keys over two 16-key slices, and the overflow case -- every
+    answer exact (per-key scales), only the overflow case flagged, bit-exact vs the C oracle."""
+    import json
+    import os
+
+    import wide_keys as W
+    with open(os.path.join(golden_dir, "wide_keys.json")) as f:
+        g = json.load(f)
+    for mode, cases, flat in ((W.V1, g["v1"], W.v1_flat(g["v1"])), (W.V2, g["v2"], W.v2_flat(g["v2"]))):
+        res, members, ovf, raw = W.run(eng.pg_min_resources_keys, mode, flat)
+        for arrs, out in raw:
+            for a, b in zip(out, oracle.pg_min_resources_keys(mode, *arrs)):
+                np.testing.assert_array_equal(a, b)
+        for j, case in enumerate(cases):
+            want = case["want"] if mode == W.V1 else case["want"]["minResources"]
+            assert ovf[j] == int(case.get("overflow", False)), case["name"]
+            if not ovf[j]:
+                assert W.same(res[j], W.want_list(want)), (case["name"], res[j])

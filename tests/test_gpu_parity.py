@@ -722,6 +722,33 @@ def test_greedy_walk_overlay_compaction():
     e.close()
 
 
+def test_greedy_walk_long_walk_then_large_overlay():
+    """A walk that collects > 8192 keys followed by an overlay with > 2048 fitting entries (advice r5):
+    a homogeneous inventory makes every walk visit all of its rounds (equal node-only keys never fall
+    below the stop bound), and 7000 nodes changed by phase 1 (one 1-GPU pod each, cpu 1 + i so the
+    LATER-changed nodes are the tighter ones) are all in the overlay and all fit phase 2's cpu-only
+    pods.  The overlay step's compaction must run before its appends, or the walk's 14000 keys + up
+    to 8192 overlay keys overrun the 16384-key LDS buffer and drop some of the best keys."""
+    from placement.synth import Inventory, JobBatch
+    N, J1, J2 = 21_000, 7000, 300
+    cap = np.zeros((4, N), np.int64)
+    cap[0], cap[1], cap[2] = 100_000, 64 << 30, 1
+    inv = Inventory(cap, np.zeros_like(cap), np.zeros(N, np.uint32), np.full(N, -1, np.int32))
+    J = J1 + J2
+    req = np.zeros((J, 4), np.int64)
+    req[:J1, 0] = 1 + np.arange(J1)
+    req[:J1, 2] = 1
+    req[J1:, 0] = 1 + np.arange(J2) % 3
+    batch = JobBatch(np.arange(J + 1, dtype=np.int32), np.r_[np.full(J1, 2), np.ones(J2)].astype(np.int32),
+                     np.ones(J, np.int32), req, np.zeros(J, np.uint32), np.zeros(J, np.int8))
+    e = Engine(0, resort_nodes=1 << 30)
+    st = check_greedy(e, inv, batch)
+    assert (st == 0).all()
+    s = e.stats()
+    assert s["resorts"] == 1                    # one index for the whole batch: the changed nodes stay overlaid
+    e.close()
+
+
 def test_greedy_unfittable_and_empty_lists():
     """Requests no node can hold (16 GPUs, more memory than any node, an unknown label) next to
     normal ones: their walks visit every candidate round and return empty lists with limit

@@ -208,3 +208,50 @@ def test_total_requests_edge_cases(name, pod, want):
     flat.end_job(0)
     out, pres, mem, ovf = oracle.pg_min_resources(2, *flat.arrays())
     assert F.unflatten(out[0], pres[0], GPU) == want and mem[0] == 1 and ovf[0] == 0
+
+
+# ----------------------------------------------------------------- keys beyond the four dimensions
+
+def test_wide_keys_semantics(golden_dir):
+    """The object-level restatement gives the hand-derived answers of wide_keys.json (hugepages, rdma,
+    two accelerator names, cpu in micro-cores, 21 keys, an int64 overflow)."""
+    g = load(golden_dir, "wide_keys")
+    for case in g["v1"]:
+        mm, res = S.v1_pg_spec(case["replicas"], case["scheduling_policy"], _pc_get(case))
+        assert mm == case["want_min_member"], case["name"]
+        assert S.same_resource_list(res, rlist(case["want"])), case["name"]
+    for case in g["v2"]:
+        _, pg = _v2_pipeline(dict(case, coscheduling={}))
+        assert pg["minMember"] == case["want"]["minMember"], case["name"]
+        assert S.same_resource_list(pg["minResources"], rlist(case["want"]["minResources"])), case["name"]
+
+
+def test_wide_keys_c_oracle(golden_dir):
+    """The C restatement over the key table (orc_pg_min_resources_keys), 16-key slices, per-key
+    scales: every answer exact, and only the overflow case flagged (the adapters' reference case)."""
+    import wide_keys as W
+    g = load(golden_dir, "wide_keys")
+    for mode, cases, flat in ((W.V1, g["v1"], W.v1_flat(g["v1"])), (W.V2, g["v2"], W.v2_flat(g["v2"]))):
+        res, members, ovf, _ = W.run(oracle.pg_min_resources_keys, mode, flat)
+        for j, case in enumerate(cases):
+            want = case["want"] if mode == W.V1 else case["want"]["minResources"]
+            assert ovf[j] == int(case.get("overflow", False)), case["name"]
+            if not ovf[j]:
+                assert W.same(res[j], W.want_list(want)), (case["name"], res[j])
+            if mode == W.V2:
+                assert members[j] == case["want"]["minMember"]
+    assert len(W.v2_flat(g["v2"]).keys) > 16                 # the slicing is exercised
+
+
+def test_key_scales():
+    flat = F.KeyFlat()
+    flat.add_container({"cpu": S.parse_quantity("1500u"), "memory": S.parse_quantity("1Gi"),
+                        "x/y": S.parse_quantity("3k")}, F.K_CONTAINER)
+    flat.add_container({"cpu": S.parse_quantity("2"), "x/y": S.parse_quantity("5000")}, F.K_CONTAINER)
+    flat.end_group(1)
+    flat.end_job(1)
+    assert flat.keys == ["cpu", "memory", "x/y"]
+    assert flat.scales() == [-4, 0, 3]
+    arrs, host_ovf = flat.arrays()
+    assert arrs[4].tolist() == [[15, 1 << 30, 3], [20000, 0, 5]] and host_ovf.tolist() == [0]
+    assert arrs[5].tolist() == [7, 5]

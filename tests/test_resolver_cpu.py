@@ -184,3 +184,70 @@ def test_resolver_seeded_rejects_bad_seeds():
     blob = shard_blob(inv.residual(), inv.labels, 0, batch.group_req[groups], batch.group_need[groups], 4)
     with pytest.raises(PlacementError):
         R.resolve(groups, blob, 1, 4, seeds=np.array([[-1, 0, 0, 0, 0, 0]], np.int64))
+
+
+def _corrupt(blob: bytes, G: int, K: int, g: int, *, count=None, node=None, entry=0, swap=False) -> bytes:
+    """A copy of a one-shard record blob (16-B header + K x 48-B records per group) with group g's
+    header count, one listed node id, or the order of its first two keys corrupted."""
+    b = bytearray(blob)
+    base = g * (16 + 48 * K)
+    if count is not None:
+        b[base:base + 4] = np.int32(count).tobytes()
+    if node is not None:
+        o = base + 16 + 48 * entry
+        k = int(np.frombuffer(bytes(b[o:o + 8]), np.uint64)[0])
+        b[o:o + 8] = np.uint64((k & ~0xFFFFFF) | node).tobytes()
+    if swap:
+        o = base + 16
+        b[o:o + 48], b[o + 48:o + 96] = b[o + 48:o + 96], b[o:o + 48]
+    return bytes(b)
+
+
+@pytest.mark.parametrize("case", ["count_2e9", "count_topk_plus_1", "count_negative", "node_out_of_range",
+                                  "keys_unsorted"])
+def test_resolver_rejects_corrupt_candidate_lists(case):
+    """Verdict r5 item 1: the blobs reach pe_resolver_resolve over any transport, so every header and
+    record is validated before the resolver moves.  A header count past topk (the r5 repro: 2e9 with
+    topk 4 returned rc 0 with node id 8592128), a negative count, a node id outside the inventory or
+    out-of-order keys give PE_EINVAL, no update, and the resolver is where it was: the same window with
+    the intact blob then resolves exactly as the oracle does."""
+    from placement import PlacementError
+    N, K = 300, 4
+    inv, batch = small_world(N, 30, 17, "mixed", 0.3)
+    want = oracle_run(inv, batch)
+    R = Resolver(batch.job_group_off, batch.priority, batch.group_count, batch.group_req, batch.group_need)
+    R.set_nodes(N)
+    groups = R.next_window(8, 256)
+    req = synth.scan_requests(batch)
+    blob = shard_blob(inv.residual(), inv.labels, 0, req[groups], batch.group_need[groups], K)
+    G = len(groups)
+    bad = {"count_2e9": dict(count=2_000_000_000), "count_topk_plus_1": dict(count=K + 1),
+           "count_negative": dict(count=-3), "node_out_of_range": dict(node=N + 5, entry=1),
+           "keys_unsorted": dict(swap=True)}[case]
+    with pytest.raises(PlacementError) as ei:
+        R.resolve(groups, _corrupt(blob, G, K, G - 1, **bad), 1, K)
+    assert ei.value.code == -1                              # PE_EINVAL
+    np.testing.assert_array_equal(R.next_window(8, 256), groups)   # not moved
+    # the intact window, then the rest of the batch, as the oracle places it
+    res = inv.residual().copy()
+    while not R.done():
+        g = R.next_window(8, 256)
+        upd, _ = R.resolve(g, shard_blob(res, inv.labels, 0, req[g], batch.group_need[g], K), 1, K)
+        for row in upd:
+            res[:, int(row[0])] = row[1:]
+    pods, st = R.results()
+    np.testing.assert_array_equal(st, want[1])
+    np.testing.assert_array_equal(pods, want[0])
+
+
+def test_resolver_set_nodes_bounds_seeds():
+    from placement import PlacementError
+    inv, batch = small_world(100, 5, 3)
+    R = Resolver(batch.job_group_off, batch.priority, batch.group_count, batch.group_req, batch.group_need)
+    R.set_nodes(100)
+    groups = R.next_window(4, 64)
+    blob = shard_blob(inv.residual(), inv.labels, 0, batch.group_req[groups], batch.group_need[groups], 4)
+    with pytest.raises(PlacementError):
+        R.resolve(groups, blob, 1, 4, seeds=np.array([[100, 0, 0, 0, 0, 0]], np.int64))
+    with pytest.raises(PlacementError):
+        R.set_nodes(-1)

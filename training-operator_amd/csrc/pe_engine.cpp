@@ -1083,20 +1083,23 @@ void ensure_pinned(HostBuf<T>& b, size_t count, const char* what) {
   hipchk(b.ensure(std::max(count, b.n + b.n / 2), kZeroCopy), what);
 }
 
-}  // namespace
-
-extern "C" {
-
 // Call path (pe_kernels.h AggSegHdr): validate + pack the batch into segments of <= 256 jobs in a
 // pinned, device-mapped staging buffer (on the planning pool for large batches), one launch (one
 // block per segment: the segment comes into LDS over PCIe in one round of coalesced 16-B loads),
 // outputs written by the kernel straight into a pinned buffer in the caller's layout, then copied
 // out.  One segment (the operator's per-reconcile call: one job) waits on a flag the kernel stores
 // in pinned memory instead of a stream synchronisation.  No input ever goes through a DMA copy.
-int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t* job_group_off,
-                        const int32_t* min_member, const int32_t* group_replicas, const int32_t* group_cont_off,
-                        const int64_t* cont_req, const uint8_t* cont_flags, int64_t* out_min_res,
-                        uint8_t* out_present, int32_t* out_members, uint8_t* out_overflow) {
+// ak / n_keys: the fixed four dimensions ({4, 1}, n_keys 4) or a per-call key table of n_keys <= 16
+// keys padded to ak.nd (pe_pg_min_resources_keys); cont_flags / out_present are u8 or u32 / u16.
+int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_keys, const int32_t* job_group_off,
+                    const int32_t* min_member, const int32_t* group_replicas, const int32_t* group_cont_off,
+                    const int64_t* cont_req, const void* cont_flags_v, int64_t* out_min_res, void* out_present_v,
+                    int32_t* out_members, uint8_t* out_overflow) {
+  const uint8_t* cont_flags = static_cast<const uint8_t*>(cont_flags_v);
+  uint8_t* out_present = static_cast<uint8_t*>(out_present_v);
+  const bool wide = ak.fb != 1;
+  const int ND = ak.nd;
+  const int pb = wide ? 2 : 1;   // presence bytes per job out
   return guarded(ctx, [&]() -> int {
     if (mode != PE_MODE_V1 && mode != PE_MODE_V2) raise(PE_EINVAL, "mode must be PE_MODE_V1 or PE_MODE_V2");
     if (n_jobs < 0) raise(PE_EINVAL, "n_jobs < 0");
@@ -1119,7 +1122,14 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       need_ptr(cont_req, "cont_req");
       need_ptr(cont_flags, "cont_flags");
     }
-    if (std::getenv("PE_AGG_DEVICE")) {
+    if (wide && C > 0) {   // a key table's flags: presence bits of the call's keys and the kind only
+      const uint32_t allowed = ((n_keys >= 32 ? 0u : (1u << n_keys)) - 1u) | (3u << PE_KEYS_KIND_SHIFT);
+      const uint32_t* f32 = static_cast<const uint32_t*>(cont_flags_v);
+      for (int64_t c = 0; c < C; ++c)
+        if (f32[c] & ~allowed)
+          raise(PE_EINVAL, "cont_flags[" + std::to_string(c) + "]: presence bit past n_keys or unknown bits");
+    }
+    if (!wide && std::getenv("PE_AGG_DEVICE")) {
       agg_device_path(ctx, mode, n_jobs, G, C, job_group_off, min_member, group_replicas, group_cont_off, cont_req,
                       cont_flags, out_min_res, out_present, out_members, out_overflow);
     } else {
@@ -1157,7 +1167,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
           while (j < jb && sg.nj < seg_jobs) {
             const int64_t g0 = job_group_off[j], g1 = job_group_off[j + 1];
             const int64_t nc = gco ? (int64_t)gco[g1] - gco[g0] : 0;
-            pe::agg_seg_layout(sg.nj + 1, sg.ng + (g1 - g0), sg.nc + nc, v1, off);
+            pe::agg_seg_layout(sg.nj + 1, sg.ng + (g1 - g0), sg.nc + nc, v1, off, ak);
             if (sg.nj > 0 && off[6] > pe::AGG_SEG_BYTES) break;
             ++sg.nj;
             sg.ng += (int32_t)(g1 - g0);
@@ -1180,7 +1190,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
         for (const AggSeg& sg : segs[t]) so[k + 1] = so[k] + sg.bytes, ++k;
       const int64_t total = so[nseg];
       int64_t oo[4];
-      pe::agg_out_layout(n_jobs, oo);
+      pe::agg_out_layout(n_jobs, oo, ak);
       const int64_t out_bytes = oo[3] + pe::agg_r16(n_jobs);
       ensure_pinned(ctx->a_stage, (size_t)total, "alloc pinned aggregation batch");
       ensure_pinned(ctx->a_outh, (size_t)out_bytes, "alloc pinned aggregation outputs");
@@ -1216,7 +1226,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
           h.c0 = sg.ng > 0 ? gco[g0] : 0;
           std::memcpy(b, &h, sizeof(h));
           int64_t off[7];
-          pe::agg_seg_layout(sg.nj, sg.ng, sg.nc, v1, off);
+          pe::agg_seg_layout(sg.nj, sg.ng, sg.nc, v1, off, ak);
           // offsets copied as they are (the kernel rebases by h.g0 / h.c0): every section is a memcpy
           std::memcpy(b + off[0], job_group_off + sg.j0, (size_t)(sg.nj + 1) * 4);
           if (v1) std::memcpy(b + off[1], min_member + sg.j0, (size_t)sg.nj * 4);
@@ -1225,14 +1235,25 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
             const int32_t c0 = h.c0;
             std::memcpy(b + off[3], gco + g0, (size_t)(sg.ng + 1) * 4);
             if (sg.nc > 0) {
-              const int64_t* q = cont_req + (int64_t)c0 * pe::D;
-              const int64_t nq = (int64_t)sg.nc * pe::D;
-              const int64_t any = copy_or_i64(reinterpret_cast<int64_t*>(b + off[4]), q, nq);   // one pass
-              std::memcpy(b + off[5], cont_flags + c0, (size_t)sg.nc);
+              const int64_t* q = cont_req + (int64_t)c0 * n_keys;
+              const int64_t nq = (int64_t)sg.nc * n_keys;
+              int64_t any;
+              if (n_keys == ND) {
+                any = copy_or_i64(reinterpret_cast<int64_t*>(b + off[4]), q, nq);   // one pass
+              } else {   // a key table narrower than its kernel: rows padded with zeros (never present)
+                int64_t* d = reinterpret_cast<int64_t*>(b + off[4]);
+                int64_t acc = 0;
+                for (int32_t c = 0; c < sg.nc; ++c) {
+                  for (int k = 0; k < n_keys; ++k) acc |= d[(int64_t)c * ND + k] = q[(int64_t)c * n_keys + k];
+                  for (int k = n_keys; k < ND; ++k) d[(int64_t)c * ND + k] = 0;
+                }
+                any = acc;
+              }
+              std::memcpy(b + off[5], cont_flags + (int64_t)c0 * ak.fb, (size_t)sg.nc * ak.fb);
               if (any < 0 && badv == INT64_MAX)
                 for (int64_t i = 0; i < nq; ++i)
                   if (q[i] < 0) {
-                    badv = (int64_t)c0 * pe::D + i;
+                    badv = (int64_t)c0 * n_keys + i;
                     break;
                   }
             }
@@ -1244,9 +1265,14 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
       uint8_t* const od = ctx->a_outh.dev;
       const uint8_t* oh = ctx->a_outh.p;
       auto unpack = [&](int64_t a, int64_t e) {   // outputs of jobs [a, e) into the caller's arrays
-        std::memcpy(out_min_res + a * pe::D, oh + oo[0] + a * 32, (size_t)(e - a) * 32);
+        if (n_keys == ND) {
+          std::memcpy(out_min_res + a * n_keys, oh + oo[0] + a * 8 * ND, (size_t)(e - a) * 8 * ND);
+        } else {
+          const int64_t* src = reinterpret_cast<const int64_t*>(oh + oo[0]);
+          for (int64_t j = a; j < e; ++j) std::memcpy(out_min_res + j * n_keys, src + j * ND, (size_t)n_keys * 8);
+        }
         std::memcpy(out_members + a, oh + oo[1] + a * 4, (size_t)(e - a) * 4);
-        std::memcpy(out_present + a, oh + oo[2] + a, (size_t)(e - a));
+        std::memcpy(out_present + a * pb, oh + oo[2] + a * pb, (size_t)(e - a) * pb);
         std::memcpy(out_overflow + a, oh + oo[3] + a, (size_t)(e - a));
       };
       int64_t unpacked = 0;   // jobs [0, unpacked) already copied out
@@ -1264,12 +1290,12 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
             // the segment in the kernel arguments (no zero-copy read; PE_AGG_NO_KARG=1: A/B)
             static thread_local pe::AggKarg karg;   // (512 B)
             std::memcpy(karg.b, ctx->a_stage.p, (size_t)total);
-            hipchk(pe::launch_pg_agg_karg(ctx->stream, mode, karg, total, od, n_jobs, ctx->a_flag.dev, ctx->agg_gen),
+            hipchk(pe::launch_pg_agg_karg(ctx->stream, mode, karg, total, od, n_jobs, ctx->a_flag.dev, ctx->agg_gen, ak),
                    "launch pg_agg_karg");
           } else {
             hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev,
                                               nseg == 1 ? nullptr : ctx->a_segoff.dev, nseg, total, od, n_jobs,
-                                              ctx->a_flag.dev, ctx->agg_gen, ctx->a_ctr.p),
+                                              ctx->a_flag.dev, ctx->agg_gen, ctx->a_ctr.p, ak),
                    "launch pg_agg_segments");
           }
           const auto tw = now();
@@ -1303,7 +1329,7 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
           first_neg = *std::min_element(bad, bad + T);
           if (first_neg != INT64_MAX) break;
           hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, ctx->a_segoff.dev + s0, s1 - s0, 0, od,
-                                            n_jobs, nullptr, 0, nullptr),
+                                            n_jobs, nullptr, 0, nullptr, ak),
                  "launch pg_agg_segments");
           hipchk(hipEventRecord(ctx->a_ev[(size_t)c], ctx->stream), "event record");
           if (prev_s1 > prev_s0) {   // the previous chunk's outputs, while this chunk runs
@@ -1340,6 +1366,31 @@ int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t
     }
     return PE_OK;
   });
+}
+
+}  // namespace
+
+extern "C" {
+
+int pe_pg_min_resources(pe_ctx* ctx, int32_t mode, int64_t n_jobs, const int32_t* job_group_off,
+                        const int32_t* min_member, const int32_t* group_replicas, const int32_t* group_cont_off,
+                        const int64_t* cont_req, const uint8_t* cont_flags, int64_t* out_min_res,
+                        uint8_t* out_present, int32_t* out_members, uint8_t* out_overflow) {
+  return agg_call(ctx, mode, n_jobs, pe::AggKeys{4, 1}, 4, job_group_off, min_member, group_replicas, group_cont_off,
+                  cont_req, cont_flags, out_min_res, out_present, out_members, out_overflow);
+}
+
+int pe_pg_min_resources_keys(pe_ctx* ctx, int32_t mode, int64_t n_jobs, int32_t n_keys, const int32_t* job_group_off,
+                             const int32_t* min_member, const int32_t* group_replicas, const int32_t* group_cont_off,
+                             const int64_t* cont_req, const uint32_t* cont_flags, int64_t* out_min_res,
+                             uint16_t* out_present, int32_t* out_members, uint8_t* out_overflow) {
+  if (n_keys < 1 || n_keys > PE_MAX_KEYS) {
+    if (ctx) ctx->err = "n_keys must be in [1, " + std::to_string(PE_MAX_KEYS) + "]";
+    return PE_EINVAL;
+  }
+  const pe::AggKeys ak{n_keys <= 4 ? 4 : n_keys <= 8 ? 8 : 16, 4};
+  return agg_call(ctx, mode, n_jobs, ak, n_keys, job_group_off, min_member, group_replicas, group_cont_off, cont_req,
+                  cont_flags, out_min_res, out_present, out_members, out_overflow);
 }
 
 // ------------------------------------------------------------------ fit mask

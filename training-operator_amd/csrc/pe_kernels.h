@@ -39,6 +39,11 @@ struct CandHdr {
   uint64_t limit;  // every clean node with key < limit is in the list
 };
 static_assert(sizeof(CandHdr) == 16, "CandHdr must be 16 B");
+// CandHdr.n values that are not a count: a zero-copy exchange wait timed out (limit = the xwait status),
+// and a merged group one of whose shard lists was corrupt (a shard header with n outside [0, K]).  The
+// host resolver raises on either (pe_resolver.cpp parse_group_keys); it never reads past a list.
+constexpr int32_t CAND_TIMEOUT = -1;
+constexpr int32_t CAND_CORRUPT = -2;
 
 __host__ __device__ inline size_t cand_group_bytes(int K) { return sizeof(CandHdr) + (size_t)K * sizeof(uint64_t); }
 
@@ -71,25 +76,35 @@ struct AggSegHdr {
 };
 static_assert(sizeof(AggSegHdr) == 32, "AggSegHdr must be 32 B");
 __host__ __device__ inline int64_t agg_r16(int64_t x) { return (x + 15) & ~int64_t(15); }
+// Key layout of a call: nd int64 values per container record and per job result, fb bytes of flags
+// per container.  {4, 1}: the fixed engine dimensions (pe_pg_min_resources: presence bits 0-3 | kind
+// << 4, u8 presence out); {4 | 8 | 16, 4}: a per-call key table (pe_pg_min_resources_keys: presence
+// bits 0-15 | kind << 16, u16 presence out), n_keys rounded up to nd.
+struct AggKeys {
+  int nd = 4;
+  int fb = 1;
+};
+constexpr int AGG_MAX_KEYS = 16;
 // byte offsets of the sections in a segment: [0] jgo (nj+1 i32, absolute group ids), [1] min_member
 // (nj i32, V1 only), [2] replicas (ng i32), [3] gco (ng+1 i32, absolute container ids), [4] req
-// (nc x 4 i64), [5] flags (nc u8), [6] = size
-__host__ __device__ inline void agg_seg_layout(int64_t nj, int64_t ng, int64_t nc, bool v1, int64_t off[7]) {
+// (nc x nd i64), [5] flags (nc x fb), [6] = size
+__host__ __device__ inline void agg_seg_layout(int64_t nj, int64_t ng, int64_t nc, bool v1, int64_t off[7],
+                                               AggKeys ak = AggKeys{}) {
   off[0] = (int64_t)sizeof(AggSegHdr);
   off[1] = off[0] + agg_r16((nj + 1) * 4);
   off[2] = off[1] + (v1 ? agg_r16(nj * 4) : 0);
   off[3] = off[2] + agg_r16(ng * 4);
   off[4] = off[3] + agg_r16((ng + 1) * 4);
-  off[5] = off[4] + nc * 32;
-  off[6] = off[5] + agg_r16(nc);
+  off[5] = off[4] + nc * 8 * ak.nd;
+  off[6] = off[5] + agg_r16(nc * ak.fb);
 }
-// Output buffer layout (the caller's arrays back to back): res [J][4] i64, members [J] i32,
-// present [J] u8, overflow [J] u8, each 16-B aligned.
-__host__ __device__ inline void agg_out_layout(int64_t J, int64_t off[4]) {
+// Output buffer layout (the caller's arrays back to back): res [J][nd] i64, members [J] i32,
+// present [J] (u8, or u16 for a key table), overflow [J] u8, each 16-B aligned.
+__host__ __device__ inline void agg_out_layout(int64_t J, int64_t off[4], AggKeys ak = AggKeys{}) {
   off[0] = 0;
-  off[1] = agg_r16(J * 32);
+  off[1] = agg_r16(J * 8 * ak.nd);
   off[2] = off[1] + agg_r16(J * 4);
-  off[3] = off[2] + agg_r16(J);
+  off[3] = off[2] + agg_r16(J * (ak.fb == 1 ? 1 : 2));
 }
 
 // ---- launch wrappers (return hipError_t of the launch)
@@ -100,14 +115,14 @@ __host__ __device__ inline void agg_out_layout(int64_t J, int64_t off[4]) {
 // it and stores flag_val (release, system scope) -- the host waits on the flag, not on the stream.
 hipError_t launch_pg_agg_segments(hipStream_t s, int mode, const uint8_t* blob, const int64_t* seg_off, int64_t nseg,
                                   int64_t nbytes0, uint8_t* out, int64_t J, uint32_t* flag, uint32_t flag_val,
-                                  uint32_t* done_ctr);
+                                  uint32_t* done_ctr, AggKeys ak = AggKeys{});
 // One segment of <= AGG_KARG_BYTES (a multiple of 16) passed by value in the kernel arguments.
 constexpr int64_t AGG_KARG_BYTES = 512;   // (a 3 KB argument block cost ~1.5 us more per launch call)
 struct AggKarg {
   alignas(16) uint8_t b[AGG_KARG_BYTES];
 };
 hipError_t launch_pg_agg_karg(hipStream_t s, int mode, const AggKarg& blob, int64_t nbytes, uint8_t* out, int64_t J,
-                              uint32_t* flag, uint32_t flag_val);
+                              uint32_t* flag, uint32_t flag_val, AggKeys ak = AggKeys{});
 hipError_t launch_pg_min_resources(hipStream_t s, int mode, int64_t n_jobs, const int32_t* job_group_off,
                                    const int32_t* min_member, const int32_t* group_replicas,
                                    const int32_t* group_cont_off, const int64_t* cont_req,

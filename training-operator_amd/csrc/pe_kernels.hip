@@ -11,6 +11,8 @@
 //   apply             scatter the resolver's residual updates back into the SoA
 //
 // Integer compare/reduce only: no MFMA (nothing is a contraction).  Roofline = HBM / VALU issue.
+#include <type_traits>
+
 #include "pe_kernels.h"
 #include "pe_wave.h"
 
@@ -30,20 +32,26 @@ __device__ __forceinline__ bool add_ovf(int64_t a, int64_t b, int64_t* r) { retu
 __device__ __forceinline__ bool mul_ovf(int64_t a, int64_t b, int64_t* r) { return __builtin_mul_overflow(a, b, r); }
 
 // One job of CalcPGMinResources (V1) / CoScheduling.Build (V2): groups [g0, g1) of replicas rep[],
-// containers of group g [gco[g], gco[g+1]) in req[][4] / fl[].  Generic pointers: the segmented
+// containers of group g [gco[g], gco[g+1]) in req[][ND] / fl[].  Generic pointers: the segmented
 // kernel runs it from LDS, the device-resident kernel from global memory.
+// Key layouts (pe_kernels.h AggKeys): the fixed four engine dimensions (ND 4, u8 flags = presence bits
+// 0-3 | kind << 4), or a per-call key table of up to 16 keys (ND 4 / 8 / 16, u32 flags = presence bits
+// 0-15 | kind << 16; keys past the call's n_keys are never present).  Every key is summed exactly alike.
+template <int ND>
 struct AggJob {
-  int64_t acc[D];
+  int64_t acc[ND];
   uint32_t pres, members;
   int32_t pod_cnt;
   bool ovf;
 };
 
-__device__ __forceinline__ AggJob agg_job(int mode, int32_t mm, int32_t g0, int32_t g1, const int32_t* rep,
-                                          const int32_t* gco, const int64_t* req, const uint8_t* fl) {
-  AggJob o;
+template <int ND, typename FT>
+__device__ __forceinline__ AggJob<ND> agg_job_t(int mode, int32_t mm, int32_t g0, int32_t g1, const int32_t* rep,
+                                                const int32_t* gco, const int64_t* req, const FT* fl) {
+  constexpr int KS = sizeof(FT) == 1 ? 4 : 16;   // kind shift
+  AggJob<ND> o;
 #pragma unroll
-  for (int d = 0; d < D; ++d) o.acc[d] = 0;
+  for (int d = 0; d < ND; ++d) o.acc[d] = 0;
   o.pres = 0;
   o.members = 0;
   o.pod_cnt = 0;
@@ -61,16 +69,18 @@ __device__ __forceinline__ AggJob agg_job(int mode, int32_t mm, int32_t g0, int3
       o.members += (uint32_t)r;
       k = r;
     }
-    int64_t side[D] = {0, 0, 0, 0}, initmax[D] = {0, 0, 0, 0}, main_[D] = {0, 0, 0, 0}, over[D] = {0, 0, 0, 0};
+    int64_t side[ND], initmax[ND], main_[ND], over[ND];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) side[d] = initmax[d] = main_[d] = over[d] = 0;
     uint32_t pp = 0;
     for (int32_t c = gco[g]; c < gco[g + 1]; ++c) {
       const uint32_t f = fl[c];
-      const uint32_t kind = (f >> 4) & 3u;
+      const uint32_t kind = (f >> KS) & 3u;
       if (mode == 1 && kind != 0) continue;  // v1 ignores init containers and overhead
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
+      for (int d = 0; d < ND; ++d) {
         if (!(f & (1u << d))) continue;
-        const int64_t v = req[(int64_t)c * D + d];
+        const int64_t v = req[(int64_t)c * ND + d];
         pp |= 1u << d;
         if (kind == 0) o.ovf |= add_ovf(main_[d], v, &main_[d]);
         else if (kind == 2) o.ovf |= add_ovf(side[d], v, &side[d]);
@@ -83,7 +93,7 @@ __device__ __forceinline__ AggJob agg_job(int mode, int32_t mm, int32_t g0, int3
       }
     }
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
+    for (int d = 0; d < ND; ++d) {
       if (!(pp & (1u << d))) continue;
       int64_t pod, t;
       o.ovf |= add_ovf(side[d], main_[d], &pod);          // v1: side/initmax/over are all 0
@@ -97,6 +107,11 @@ __device__ __forceinline__ AggJob agg_job(int mode, int32_t mm, int32_t g0, int3
   return o;
 }
 
+__device__ __forceinline__ AggJob<D> agg_job(int mode, int32_t mm, int32_t g0, int32_t g1, const int32_t* rep,
+                                             const int32_t* gco, const int64_t* req, const uint8_t* fl) {
+  return agg_job_t<D, uint8_t>(mode, mm, g0, g1, rep, gco, req, fl);
+}
+
 __global__ __launch_bounds__(256) void pg_min_resources_kernel(
     int mode, int64_t n_jobs, const int32_t* __restrict__ job_group_off, const int32_t* __restrict__ min_member,
     const int32_t* __restrict__ group_replicas, const int32_t* __restrict__ group_cont_off,
@@ -104,8 +119,8 @@ __global__ __launch_bounds__(256) void pg_min_resources_kernel(
     uint8_t* __restrict__ out_present, int32_t* __restrict__ out_members, uint8_t* __restrict__ out_overflow) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_jobs) return;
-  const AggJob o = agg_job(mode, mode == 1 ? min_member[j] : 0, job_group_off[j], job_group_off[j + 1],
-                           group_replicas, group_cont_off, cont_req, cont_flags);
+  const AggJob<D> o = agg_job(mode, mode == 1 ? min_member[j] : 0, job_group_off[j], job_group_off[j + 1],
+                              group_replicas, group_cont_off, cont_req, cont_flags);
 #pragma unroll
   for (int d = 0; d < D; ++d) out_res[j * D + d] = o.ovf ? 0 : o.acc[d];   // no int64 answer: defined as 0
   out_present[j] = (uint8_t)o.pres;
@@ -120,9 +135,11 @@ __global__ __launch_bounds__(256) void pg_min_resources_kernel(
 // One segment: stage [seg, seg + bytes) into LDS (8 16-B loads in flight per lane before the LDS
 // stores: a 48 KB segment is 2 PCIe round trips, not 12), lane t aggregates job t from LDS and writes
 // its outputs into `out`; with a flag, the last block to finish publishes the launch.
+template <int ND, typename FT>
 __device__ __forceinline__ void agg_segment(int mode, const uint8_t* seg, int64_t bytes, uint4* lds,
                                             uint8_t* __restrict__ out, int64_t J, uint32_t* flag, uint32_t flag_val,
                                             uint32_t* done_ctr) {
+  using PT = typename std::conditional<sizeof(FT) == 1, uint8_t, uint16_t>::type;   // presence bits out
   if (bytes <= AGG_SEG_BYTES) {   // stage in LDS (else read in place: one oversized job)
     const uint4* src = reinterpret_cast<const uint4*>(seg);
     const int n16 = (int)(bytes >> 4);
@@ -144,26 +161,28 @@ __device__ __forceinline__ void agg_segment(int mode, const uint8_t* seg, int64_
     seg = reinterpret_cast<const uint8_t*>(lds);
   }
   const AggSegHdr h = *reinterpret_cast<const AggSegHdr*>(seg);
+  const AggKeys ak{ND, (int)sizeof(FT)};
   int64_t off[7];
-  agg_seg_layout(h.nj, h.ng, h.nc, mode == 1, off);
+  agg_seg_layout(h.nj, h.ng, h.nc, mode == 1, off, ak);
   const int t = threadIdx.x;
   if (t < h.nj) {
     const int32_t* jgo = reinterpret_cast<const int32_t*>(seg + off[0]);
     const int32_t mm = mode == 1 ? reinterpret_cast<const int32_t*>(seg + off[1])[t] : 0;
     // the offsets are the caller's (absolute): rebase the group and container sections instead
-    const AggJob o = agg_job(mode, mm, jgo[t] - h.g0, jgo[t + 1] - h.g0, reinterpret_cast<const int32_t*>(seg + off[2]),
-                             reinterpret_cast<const int32_t*>(seg + off[3]),
-                             reinterpret_cast<const int64_t*>(seg + off[4]) - (int64_t)h.c0 * D, seg + off[5] - h.c0);
+    const AggJob<ND> o = agg_job_t<ND, FT>(mode, mm, jgo[t] - h.g0, jgo[t + 1] - h.g0,
+                                           reinterpret_cast<const int32_t*>(seg + off[2]),
+                                           reinterpret_cast<const int32_t*>(seg + off[3]),
+                                           reinterpret_cast<const int64_t*>(seg + off[4]) - (int64_t)h.c0 * ND,
+                                           reinterpret_cast<const FT*>(seg + off[5]) - h.c0);
     int64_t oo[4];
-    agg_out_layout(J, oo);
+    agg_out_layout(J, oo, ak);
     const int64_t j = h.j0 + t;
-    int64_t* res = reinterpret_cast<int64_t*>(out + oo[0]) + j * D;
-    const int64_t z0 = o.ovf ? 0 : o.acc[0], z1 = o.ovf ? 0 : o.acc[1], z2 = o.ovf ? 0 : o.acc[2],
-                  z3 = o.ovf ? 0 : o.acc[3];
-    reinterpret_cast<longlong2*>(res)[0] = longlong2{z0, z1};   // 32 B per lane, two 16-B stores
-    reinterpret_cast<longlong2*>(res)[1] = longlong2{z2, z3};
+    int64_t* res = reinterpret_cast<int64_t*>(out + oo[0]) + j * ND;
+#pragma unroll
+    for (int d = 0; d < ND; d += 2)   // ND x 8 B per lane in 16-B stores
+      reinterpret_cast<longlong2*>(res)[d / 2] = longlong2{o.ovf ? 0 : o.acc[d], o.ovf ? 0 : o.acc[d + 1]};
     reinterpret_cast<int32_t*>(out + oo[1])[j] = mode == 1 ? o.pod_cnt : (int32_t)o.members;
-    out[oo[2] + j] = (uint8_t)o.pres;
+    reinterpret_cast<PT*>(out + oo[2])[j] = (PT)o.pres;
     out[oo[3] + j] = o.ovf ? 1 : 0;
   }
   if (flag) {   // latency launch: publish the outputs; the LAST block to finish stores the flag
@@ -181,7 +200,7 @@ __device__ __forceinline__ void agg_segment(int mode, const uint8_t* seg, int64_
   }
 }
 
-
+template <int ND, typename FT>
 __global__ __launch_bounds__(AGG_SEG_JOBS) void pg_agg_seg_kernel(int mode, const uint8_t* __restrict__ blob,
                                                                  const int64_t* __restrict__ seg_off, int64_t nbytes0,
                                                                  uint8_t* __restrict__ out, int64_t J, uint32_t* flag,
@@ -192,35 +211,46 @@ __global__ __launch_bounds__(AGG_SEG_JOBS) void pg_agg_seg_kernel(int mode, cons
     a = seg_off[blockIdx.x];
     e = seg_off[blockIdx.x + 1];
   }
-  agg_segment(mode, blob + a, e - a, lds, out, J, flag, flag_val, done_ctr);
+  agg_segment<ND, FT>(mode, blob + a, e - a, lds, out, J, flag, flag_val, done_ctr);
 }
 
 // A one-segment call of <= AGG_KARG_BYTES travels IN the kernel arguments (the blob is the first
 // argument, so it sits at offset 0 of the kernarg segment): no zero-copy read of host memory, i.e.
 // one PCIe round trip less on the operator's one-job call.
+template <int ND, typename FT>
 __global__ __launch_bounds__(AGG_SEG_JOBS) void pg_agg_karg_kernel(AggKarg blob, int mode, int64_t nbytes,
                                                                   uint8_t* __restrict__ out, int64_t J, uint32_t* flag,
                                                                   uint32_t flag_val) {
   __shared__ uint4 lds[AGG_KARG_BYTES / 16];
   const uint8_t* kp = (const uint8_t*)__builtin_amdgcn_kernarg_segment_ptr();   // (address space 4 -> generic)
   (void)blob;
-  agg_segment(mode, kp, nbytes, lds, out, J, flag, flag_val, nullptr);
+  agg_segment<ND, FT>(mode, kp, nbytes, lds, out, J, flag, flag_val, nullptr);
 }
 
+// the kernel instance of a key layout: the fixed dimensions, or a key table of 4 / 8 / 16 keys
+#define PE_AGG_DISPATCH(ak, KERNEL, ...)                                                                 \
+  do {                                                                                                   \
+    if ((ak).fb == 1 && (ak).nd == 4) hipLaunchKernelGGL((KERNEL<4, uint8_t>), __VA_ARGS__);              \
+    else if ((ak).fb == 4 && (ak).nd == 4) hipLaunchKernelGGL((KERNEL<4, uint32_t>), __VA_ARGS__);        \
+    else if ((ak).fb == 4 && (ak).nd == 8) hipLaunchKernelGGL((KERNEL<8, uint32_t>), __VA_ARGS__);        \
+    else if ((ak).fb == 4 && (ak).nd == 16) hipLaunchKernelGGL((KERNEL<16, uint32_t>), __VA_ARGS__);      \
+    else return hipErrorInvalidValue;                                                                    \
+  } while (0)
+
 hipError_t launch_pg_agg_karg(hipStream_t s, int mode, const AggKarg& blob, int64_t nbytes, uint8_t* out, int64_t J,
-                              uint32_t* flag, uint32_t flag_val) {
+                              uint32_t* flag, uint32_t flag_val, AggKeys ak) {
   if (nbytes <= 0 || nbytes > AGG_KARG_BYTES || (nbytes & 15) || !flag) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pg_agg_karg_kernel, dim3(1), dim3(AGG_SEG_JOBS), 0, s, blob, mode, nbytes, out, J, flag, flag_val);
+  PE_AGG_DISPATCH(ak, pg_agg_karg_kernel, dim3(1), dim3(AGG_SEG_JOBS), 0, s, blob, mode, nbytes, out, J, flag, flag_val);
   return hipGetLastError();
 }
 
 hipError_t launch_pg_agg_segments(hipStream_t s, int mode, const uint8_t* blob, const int64_t* seg_off, int64_t nseg,
                                   int64_t nbytes0, uint8_t* out, int64_t J, uint32_t* flag, uint32_t flag_val,
-                                  uint32_t* done_ctr) {
+                                  uint32_t* done_ctr, AggKeys ak) {
   if (nseg <= 0) return hipSuccess;
   if ((!seg_off && nseg != 1) || (flag && nseg > 1 && !done_ctr)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pg_agg_seg_kernel, dim3((unsigned)nseg), dim3(AGG_SEG_JOBS), 0, s, mode, blob, seg_off, nbytes0,
-                     out, J, flag, flag_val, done_ctr);
+  PE_AGG_DISPATCH(ak, pg_agg_seg_kernel, dim3((unsigned)nseg), dim3(AGG_SEG_JOBS), 0, s, mode, blob, seg_off, nbytes0,
+                  out, J, flag, flag_val, done_ctr);
   return hipGetLastError();
 }
 
@@ -1736,13 +1766,29 @@ __global__ __launch_bounds__(MG_THREADS) void merge_shards_kernel(const uint8_t*
   // would invalidate L2 under every kernel on the GPU).  Headers once per block, through LDS.
   __shared__ uint64_t hl[MG_THREADS / 64];
   __shared__ int hn[MG_THREADS / 64];
+  __shared__ int bad;
+  if (tid == 0) {
+    s.total = 0;
+    bad = 0;
+  }
+  __syncthreads();
   if (tid < world) {
     const CandHdr* h = reinterpret_cast<const CandHdr*>(gath + tid * shard_bytes + (size_t)g * gb);
     hl[tid] = __hip_atomic_load(&h->limit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    hn[tid] = min(__hip_atomic_load(&h->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), K);
+    const int n = __hip_atomic_load(&h->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    hn[tid] = n < 0 ? 0 : (n > K ? K : n);
+    if (n < 0 || n > K) bad = 1;   // a shard list is corrupt: the merged group says so (never read past it)
   }
-  if (tid == 0) s.total = 0;
   __syncthreads();
+  if (bad) {
+    if (tid == 0) {
+      CandHdr* hp = reinterpret_cast<CandHdr*>(out + (size_t)g * gb);
+      hp->n = CAND_CORRUPT;
+      hp->limit = 0;
+      __hip_atomic_store(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return;
+  }
   uint64_t L = NO_KEY;
   for (int r = 0; r < world; ++r) L = umin64(L, hl[r]);
   for (int r = 0; r < world; ++r) {
@@ -1856,13 +1902,28 @@ __global__ __launch_bounds__(RM_THREADS) void merge_ranked_kernel(const uint8_t*
     }
     return;
   }
+  __shared__ int bad;
+  if (tid == 0) {
+    newlim = NO_KEY;
+    bad = 0;
+  }
+  __syncthreads();
   if (tid < world) {   // (system-scope loads: see merge_shards_kernel)
     const CandHdr* h = reinterpret_cast<const CandHdr*>(gath + tid * shard_bytes + (size_t)g * gb);
     hl[tid] = __hip_atomic_load(&h->limit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    hn[tid] = max(0, min(__hip_atomic_load(&h->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), K));
+    const int n = __hip_atomic_load(&h->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    hn[tid] = max(0, min(n, K));
+    if (n < 0 || n > K) bad = 1;   // (as merge_shards_kernel: a corrupt shard list marks the group)
   }
-  if (tid == 0) newlim = NO_KEY;
   __syncthreads();
+  if (bad) {
+    if (tid == 0) {
+      hp->n = CAND_CORRUPT;
+      hp->limit = 0;
+      __hip_atomic_store(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return;
+  }
   uint64_t L = NO_KEY;
   for (int r = 0; r < world; ++r) L = umin64(L, hl[r]);
   for (int r = 0; r < world; ++r) {
@@ -2387,12 +2448,16 @@ __global__ __launch_bounds__(WK_ROUND) void walk_kernel(const ReqRec* __restrict
         k[u] = node_key(w.ovl_res[i], w.ovl_res[w.sstride + i], w.ovl_res[2 * w.sstride + i],
                         w.ovl_res[3 * w.sstride + i], w.ovl_lab[i], q0, q1, q2, q3, need, id_base + (uint64_t)w.ovl[i]);
     }
+    // room for this step's appends BEFORE them: the walk leaves up to MG_CAP - WK_MULTI * WK_ROUND keys,
+    // and one overlay step appends up to OV * WK_ROUND (more than that room) -- keys past MG_CAP would be
+    // dropped, and the dropped ones may be the group's best (changed nodes are the tight ones).
+    // (Tcur is block-uniform; the step's keys wait in registers across the compaction.)
+    if (Tcur > MG_CAP - OV * WK_ROUND) compact();
     int* const cnt = step_begin();
 #pragma unroll
     for (int u = 0; u < OV; ++u) step_append(s, Tcur, cnt, k[u], k[u] < xstop);   // (NO_KEY never is)
     __syncthreads();
     step_end();
-    if (Tcur > MG_CAP - OV * WK_ROUND) compact();
   }
   __syncthreads();
   WPT(3);

@@ -302,10 +302,38 @@ void merge_shards(const std::vector<const GroupCands*>& parts, GroupCands& out) 
   out.n = out.own.size();
 }
 
+static std::string list_where(int w, int r) {
+  return "corrupt candidate list (group " + std::to_string(w) + ", shard " + std::to_string(r) + "): ";
+}
+
+// A header count the slot cannot hold: n < 0 (other than the exchange's timeout marker, handled by
+// the caller) or n > K would read outside the group's slot.
+static size_t checked_count(int32_t n, int K, int w, int r) {
+  if (n < 0 || n > K)
+    throw CorruptList(list_where(w, r) + "header count " + std::to_string(n) + " outside [0, " + std::to_string(K) + "]");
+  return (size_t)n;
+}
+
 void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands,
-                  bool copy_blob) {
+                  bool copy_blob, int64_t n_nodes) {
   const size_t gb = 16 + (size_t)K * 48;
   const size_t shard_bytes = (size_t)n_groups * gb;
+  // validate every header and record before anything is used (no partial window)
+  for (int r = 0; r < n_shards; ++r)
+    for (int w = 0; w < n_groups; ++w) {
+      const uint8_t* base = blob + (size_t)r * shard_bytes + (size_t)w * gb;
+      int32_t n;
+      std::memcpy(&n, base, 4);
+      const size_t m = checked_count(n, K, w, r);
+      const Cand* c = reinterpret_cast<const Cand*>(base + 16);
+      for (size_t i = 0; i < m; ++i) {
+        const uint64_t k = c[i].key;
+        if ((int64_t)(k & 0xFFFFFFull) >= n_nodes)
+          throw CorruptList(list_where(w, r) + "node id " + std::to_string(k & 0xFFFFFFull) + " outside the " +
+                            std::to_string(n_nodes) + "-node inventory");
+        if (i > 0 && k <= c[i - 1].key) throw CorruptList(list_where(w, r) + "keys not ascending at entry " + std::to_string(i));
+      }
+    }
   cands.resize((size_t)n_groups);
   std::vector<GroupCands> parts((size_t)n_shards);
   std::vector<const GroupCands*> pp((size_t)n_shards);
@@ -318,7 +346,7 @@ void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::v
       std::memcpy(&limit, base + 8, 8);
       GroupCands& gc = n_shards == 1 ? cands[w] : parts[r];
       gc.limit = limit;
-      gc.n = (size_t)std::max(n, 0);
+      gc.n = (size_t)n;   // (validated above)
       gc.data = reinterpret_cast<const Cand*>(base + 16);   // 16-B aligned records in the blob
       gc.keys = nullptr;
       gc.keyed = false;
@@ -333,15 +361,18 @@ void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::v
 }
 
 // One group of a one-shard key blob: the list points into the blob.
-static void parse_group_keys(const uint8_t* base, GroupCands& gc) {
+static void parse_group_keys(const uint8_t* base, int K, size_t w, GroupCands& gc) {
   int32_t n;
   uint64_t limit;
   std::memcpy(&n, base, 4);
   std::memcpy(&limit, base + 8, 8);
-  if (n < 0)   // (the zero-copy exchange wait timed out on a peer's list: pe_kernels.h launch_xwait)
+  if (n == -1)   // (the zero-copy exchange wait timed out on a peer's list: pe_kernels.h CAND_TIMEOUT)
     throw ExchangeError("host exchange: a rank's candidate lists never arrived (peer stalled or failed; rank " +
                         std::to_string((limit >> 32) & 0x7fffffffu) + "'s slot still held generation " +
                         std::to_string((uint32_t)limit) + ")");
+  if (n == -2)   // (a merge found a shard list whose header count was outside [0, K]: CAND_CORRUPT)
+    throw CorruptList(list_where((int)w, -1) + "a shard's header count was outside [0, " + std::to_string(K) +
+                      "] (merged group marked corrupt)");
   gc.keyed = true;
   gc.data = nullptr;
   gc.merged.clear();
@@ -349,7 +380,7 @@ static void parse_group_keys(const uint8_t* base, GroupCands& gc) {
   gc.part_n.clear();
   gc.limit = limit;
   gc.keys = reinterpret_cast<const uint64_t*>(base + 16);
-  gc.n = (size_t)std::max(n, 0);
+  gc.n = checked_count(n, K, (int)w, 0);
   for (int l = 0; l < 4; ++l) __builtin_prefetch(gc.keys + 8 * l);   // list heads, fresh from the device
 }
 
@@ -357,6 +388,7 @@ void WindowFeed::reset(const uint8_t* blob, int n_groups, int K, uint32_t gen, s
   blob_ = blob;
   n_ = (size_t)std::max(n_groups, 0);
   gb_ = 16 + (size_t)K * 8;
+  K_ = K;
   gen_ = gen;
   cands_ = cands;
   cands->resize(n_);
@@ -373,7 +405,7 @@ void WindowFeed::advance() {
   size_t p = parsed_.load(std::memory_order_relaxed);
   const size_t p0 = p;
   while (p < n_ && signalled(p)) {
-    parse_group_keys(blob_ + p * gb_, (*cands_)[p]);
+    parse_group_keys(blob_ + p * gb_, K_, p, (*cands_)[p]);
     ++p;
   }
   if (p != p0) parsed_.store(p, std::memory_order_release);
@@ -426,7 +458,7 @@ void parse_window_keys(const uint8_t* blob, int n_shards, int n_groups, int K, s
       std::memcpy(&limit, base + 8, 8);
       gc.limit = std::min(gc.limit, limit);
       gc.part.push_back(reinterpret_cast<const uint64_t*>(base + 16));
-      gc.part_n.push_back((size_t)std::max(n, 0));
+      gc.part_n.push_back(checked_count(n, K, w, r));
     }
     if (n_shards == 1) {
       gc.keys = gc.part[0];
@@ -531,9 +563,10 @@ void SeedScorer::pin(const cpu_set_t& set) {
 
 void SeedScorer::start(const DirtySet* seeds, const std::vector<int32_t>* groups,
                        const std::vector<GroupCands>* cands, const int64_t* scan_req, const uint32_t* need,
-                       const WindowFeed* feed, const NodeState* mirror) {
+                       const WindowFeed* feed, const NodeState* mirror, int64_t mirror_n) {
   seeds_ = seeds;
   mirror_ = mirror;
+  mirror_n_ = mirror ? mirror_n : 0;
   groups_ = groups;
   cands_ = cands;
   feed_ = feed;
@@ -643,8 +676,10 @@ void SeedScorer::loop() {
         const GroupCands& gc = (*cands_)[wi];
         if (gc.keys) {
           int64_t sink = 0;
-          for (size_t i = slots_[wi].top.head, e = std::min(gc.size(), i + (size_t)kWarmStates); i < e; ++i)
-            sink += mirror_[gc.keys[i] & 0xFFFFFFull].res[0];
+          for (size_t i = slots_[wi].top.head, e = std::min(gc.size(), i + (size_t)kWarmStates); i < e; ++i) {
+            const uint64_t id = gc.keys[i] & 0xFFFFFFull;
+            if (id < (uint64_t)mirror_n_) sink += mirror_[id].res[0];   // (an id outside: the resolver raises on it)
+          }
           warm_sink_ += sink;
         }
       }
@@ -867,7 +902,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         seeds_.upsert(u.gid, st);
       }
     }
-    scorer_.start(&seeds_, &groups, &cands, qeff_.data(), need_, feed, mirror_.nodes);
+    scorer_.start(&seeds_, &groups, &cands, qeff_.data(), need_, feed, mirror_.nodes, mirror_.n);
     for (size_t i = 0; i < seeds_.size(); ++i) any_set(seeds_.gid[i]);
   }
   if (feed) feed->advance();
@@ -1027,6 +1062,9 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         slot = -1;
       } else {
         if (gc.keyed) {   // clean: the mirror holds the snapshot state
+          if (__builtin_expect(gid >= mirror_.n, 0))   // (a device-written id: checked where it is used)
+            throw CorruptList(list_where((int)wi, -1) + "node id " + std::to_string(gid) + " outside the " +
+                              std::to_string(mirror_.n) + "-node inventory");
           st = mirror_.nodes[gid];
           // keep the next two clean entries' states on their way
 #ifndef PE_PLACE_PREFETCH

@@ -144,14 +144,25 @@ uint64_t key_of(const int64_t res[RD], uint32_t labels, const int64_t q[RD], uin
 // Merge per-shard candidate lists of one group into the global exact list (limit = min).
 void merge_shards(const std::vector<const GroupCands*>& parts, GroupCands& out);
 
+// A candidate list the resolver cannot trust: a header count outside [0, K] (it would read past the
+// group's slot), a listed node id outside the inventory, or (record blobs) keys out of order.  The
+// blobs may arrive over any transport (placement.h), so they are checked, never read past: the
+// pe_resolver_* ABI reports PE_EINVAL (before any update is written), pe_place_greedy PE_EHIP.
+struct CorruptList : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
 // Window blob = n_shards consecutive shard blocks, each n_groups x (16-B header {int32 n,
 // int32 flags, uint64 limit} + K x 48-B records {u64 key, i64 res[4], u64 labels}) -- exactly
 // what the merge kernel writes.  Parses and merges the shards into cands[n_groups].
 // With one shard and copy_blob = false the lists point INTO the blob, which must outlive them.
+// Every header and record is validated (CorruptList): 0 <= n <= K, node id (key bits 0-23) <
+// n_nodes, keys strictly ascending within a shard list.
 void parse_window(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands,
-                  bool copy_blob = false);
+                  bool copy_blob = false, int64_t n_nodes = (int64_t)1 << 24);
 // Key-only window blob (the engine's device format): per shard, per group a 16-B header + K u64
-// keys.  Lists point into the blob when n_shards == 1.
+// keys.  Lists point into the blob when n_shards == 1.  Headers are validated (0 <= n <= K); the
+// listed node ids are checked where the resolver reads their mirror state (Resolver::resolve).
 void parse_window_keys(const uint8_t* blob, int n_shards, int n_groups, int K, std::vector<GroupCands>& cands);
 
 // Pipelined walk windows (engine, one shard): the device writes each group's key list straight
@@ -195,6 +206,7 @@ class WindowFeed {
   std::vector<GroupCands>* cands_ = nullptr;
   std::atomic<size_t> parsed_{0};
   double spin_ms_ = 0;
+  int K_ = 0;
 };
 
 // Node id -> small index, open addressing (linear probing) sized to the live entries: the dirty
@@ -347,7 +359,7 @@ class SeedScorer {
   // until stop()).
   void start(const DirtySet* seeds, const std::vector<int32_t>* groups, const std::vector<GroupCands>* cands,
              const int64_t* scan_req, const uint32_t* need, const WindowFeed* feed = nullptr,
-             const NodeState* mirror = nullptr);
+             const NodeState* mirror = nullptr, int64_t mirror_n = 0);
   bool ready(size_t wi) const { return slots_[wi].gen.load(std::memory_order_acquire) == gen_; }
   const SeedTop& top(size_t wi) const { return slots_[wi].top; }
   // the resolver is at group wi: the helper skips what it would finish too late
@@ -389,6 +401,7 @@ class SeedScorer {
   // host mirror: the helper reads the states of each group's first non-seed list entries, so the
   // resolver finds those lines in a cache of its CCD (a cross-core hit) instead of in DRAM
   const NodeState* mirror_ = nullptr;
+  int64_t mirror_n_ = 0;
 #ifndef PE_WARM_STATES
 #define PE_WARM_STATES 4
 #endif

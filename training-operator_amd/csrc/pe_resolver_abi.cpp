@@ -14,6 +14,7 @@ struct pe_resolver {
   pe::Resolver* r = nullptr;
   std::vector<pe::GroupCands> cands;
   std::vector<pe::Update> updates;
+  int64_t n_nodes = PE_MAX_NODES;   // listed and seeded node ids must lie below (pe_resolver_set_nodes)
   ~pe_resolver() { delete r; }
 };
 
@@ -63,6 +64,12 @@ int pe_resolver_create(int64_t n_jobs, const int32_t* job_group_off, const int32
 
 void pe_resolver_destroy(pe_resolver* r) { delete r; }
 
+int pe_resolver_set_nodes(pe_resolver* r, int64_t n_nodes) {
+  if (!r || n_nodes < 0 || n_nodes > PE_MAX_NODES) return PE_EINVAL;
+  r->n_nodes = n_nodes;
+  return PE_OK;
+}
+
 int pe_resolver_done(const pe_resolver* r) { return r && r->r->done() ? 1 : 0; }
 
 int pe_resolver_next_window(pe_resolver* r, int32_t max_groups, int64_t max_pods, int32_t* out_groups,
@@ -90,13 +97,14 @@ int pe_resolver_resolve_seeded(pe_resolver* r, int32_t n_groups, const int32_t* 
   if (n_groups > 0 && (!groups || !blob)) return PE_EINVAL;
   if (n_seeds < 0 || (n_seeds > 0 && !seeds)) return PE_EINVAL;
   for (int64_t i = 0; i < n_seeds; ++i)
-    if (seeds[i * 6] < 0 || seeds[i * 6] >= PE_MAX_NODES || seeds[i * 6 + 5] < 0 || seeds[i * 6 + 5] > 0xFFFFFFFFll)
+    if (seeds[i * 6] < 0 || seeds[i * 6] >= r->n_nodes || seeds[i * 6 + 5] < 0 || seeds[i * 6 + 5] > 0xFFFFFFFFll)
       return PE_EINVAL;
   try {
     std::vector<int32_t> g(groups, groups + n_groups);
     for (int32_t x : g)
       if (x < 0 || x >= (int32_t)r->cnt.size()) return PE_EINVAL;
-    pe::parse_window(blob, n_shards, n_groups, topk, r->cands);
+    // every header, node id and key order is checked before the resolver moves (PE_EINVAL, no update)
+    pe::parse_window(blob, n_shards, n_groups, topk, r->cands, false, r->n_nodes);
     std::vector<pe::Update> seed((size_t)n_seeds);
     for (int64_t i = 0; i < n_seeds; ++i) {
       seed[i].gid = seeds[i * 6];
@@ -115,6 +123,10 @@ int pe_resolver_resolve_seeded(pe_resolver* r, int32_t n_groups, const int32_t* 
     return PE_OK;
   } catch (const std::bad_alloc&) {
     return PE_ENOMEM;
+  } catch (const pe::CorruptList&) {
+    return PE_EINVAL;
+  } catch (const std::exception&) {   // (nothing else may cross the C boundary)
+    return PE_EINVAL;
   }
 }
 

@@ -35,28 +35,39 @@ std::string Dims::name_of(int d) const {
 
 // ------------------------------------------------------------------ flattening
 
-static void add_record(const Dims& eng, const ResourceList* rl, int kind, Flat* out) {
-  int64_t v[PE_DIMS] = {0, 0, 0, 0};
-  uint8_t pres = 0;
+static void add_record(const ResourceList* rl, int kind, Flat* out) {
   if (rl) {
     for (const auto& kv : *rl) {
-      const int d = eng.dim_of(kv.first);
-      if (d < 0) throw Error{PE_EINVAL, "resource " + kv.first + " has no engine dimension"};
-      try {
-        v[d] = kv.second.Canonical(kv.first);
-      } catch (const QuantityError& e) {
-        throw Error{PE_EINVAL, e.msg};
+      if (kv.second.Negative()) throw Error{PE_EINVAL, kv.first + "=" + kv.second.String() + " is negative"};
+      auto it = out->key_id.find(kv.first);
+      if (it == out->key_id.end()) {
+        it = out->key_id.emplace(kv.first, (int32_t)out->keys.size()).first;
+        out->keys.push_back(kv.first);
       }
-      pres |= (uint8_t)(1u << d);
+      out->ent_key.push_back(it->second);
+      out->ent_q.push_back(kv.second);
     }
   }
-  out->cont_req.insert(out->cont_req.end(), v, v + PE_DIMS);
-  out->cont_flags.push_back((uint8_t)(pres | (kind << PE_KIND_SHIFT)));
+  out->cont_kind.push_back((uint8_t)kind);
+  out->ent_off.push_back((int32_t)out->ent_key.size());
+}
+
+std::vector<int> Flat::Scales() const {
+  std::vector<int> sc(keys.size(), 0);
+  std::vector<bool> seen(keys.size(), false);
+  for (size_t e = 0; e < ent_key.size(); ++e) {
+    if (ent_q[e].IsZero()) continue;
+    const int k = ent_key[e];
+    const int x = ent_q[e].Exp10();
+    sc[k] = seen[k] ? std::min(sc[k], x) : x;
+    seen[k] = true;
+  }
+  return sc;
 }
 
 static void end_group(int32_t replicas, Flat* out) {
   out->group_replicas.push_back(replicas);
-  out->group_cont_off.push_back((int32_t)out->cont_flags.size());
+  out->group_cont_off.push_back((int32_t)out->cont_kind.size());
 }
 
 static void end_job(int32_t min_member, Flat* out) {
@@ -105,20 +116,23 @@ struct FlatTxn {
   size_t j, g, c, r;
   bool done = false;
   explicit FlatTxn(Flat* out)
-      : f(out), j(out->job_group_off.size()), g(out->group_replicas.size()), c(out->cont_flags.size()),
-        r(out->cont_req.size()) {}
+      : f(out), j(out->job_group_off.size()), g(out->group_replicas.size()), c(out->cont_kind.size()),
+        r(out->ent_key.size()) {}
   ~FlatTxn() {
     if (done) return;
     f->job_group_off.resize(j);
     f->min_member.resize(j - 1);
     f->group_replicas.resize(g);
     f->group_cont_off.resize(g + 1);
-    f->cont_flags.resize(c);
-    f->cont_req.resize(r);
+    f->cont_kind.resize(c);
+    f->ent_off.resize(c + 1);
+    f->ent_key.resize(r);
+    f->ent_q.resize(r);
+    // (a key first seen in the rolled-back records stays in the table: it is simply never present)
   }
 };
 
-void FlattenV1Job(const Dims& eng, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
+void FlattenV1Job(int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
                   const PriorityClassGetFunc& pcGetFunc, Flat* out, const V1OrderPolicy& order) {
   FlatTxn txn(out);
   for (const ReplicaType& t : ReplicaOrderV1(replicas, pcGetFunc, order)) {
@@ -126,7 +140,7 @@ void FlattenV1Job(const Dims& eng, int32_t minMember, const std::map<ReplicaType
     for (const Container& c : spec.template_spec.containers) {
       // AddResourceList (util.go:79-104): Requests keys, or Limits only when Requests is nil
       const ResourceList* rl = c.requests ? &*c.requests : (c.limits ? &*c.limits : nullptr);
-      add_record(eng, rl, PE_KIND_CONTAINER, out);
+      add_record(rl, PE_KIND_CONTAINER, out);
     }
     end_group(spec.replicas ? *spec.replicas : -1, out);
   }
@@ -134,22 +148,22 @@ void FlattenV1Job(const Dims& eng, int32_t minMember, const std::map<ReplicaType
   txn.done = true;
 }
 
-void FlattenV2PodGroup(const Dims& eng, int32_t replicas, const PodSpec& pod, Flat* out) {
+void FlattenV2PodGroup(int32_t replicas, const PodSpec& pod, Flat* out) {
   FlatTxn txn(out);
   for (const Container& c : pod.init_containers) {
     const bool sidecar = c.restart_policy && *c.restart_policy == "Always";
-    add_record(eng, c.requests ? &*c.requests : nullptr, sidecar ? PE_KIND_SIDECAR : PE_KIND_INIT, out);
+    add_record(c.requests ? &*c.requests : nullptr, sidecar ? PE_KIND_SIDECAR : PE_KIND_INIT, out);
   }
-  for (const Container& c : pod.containers) add_record(eng, c.requests ? &*c.requests : nullptr, PE_KIND_CONTAINER, out);
-  if (pod.overhead) add_record(eng, &*pod.overhead, PE_KIND_OVERHEAD, out);
+  for (const Container& c : pod.containers) add_record(c.requests ? &*c.requests : nullptr, PE_KIND_CONTAINER, out);
+  if (pod.overhead) add_record(&*pod.overhead, PE_KIND_OVERHEAD, out);
   end_group(replicas, out);
   txn.done = true;
 }
 
-void FlattenV2Info(const Dims& eng, const Info& info, Flat* out) {
+void FlattenV2Info(const Info& info, Flat* out) {
   FlatTxn txn(out);
   for (const auto& kv : info.scheduler.total_requests) {
-    add_record(eng, &kv.second.pod_requests, PE_KIND_CONTAINER, out);
+    add_record(&kv.second.pod_requests, PE_KIND_CONTAINER, out);
     end_group(kv.second.replicas, out);
   }
   end_job(0, out);
@@ -159,37 +173,80 @@ void FlattenV2Info(const Dims& eng, const Info& info, Flat* out) {
 // ------------------------------------------------------------------ aggregation through the ABI
 
 struct AggOut {
-  std::vector<int64_t> res;
-  std::vector<uint8_t> present, overflow;
+  std::vector<std::string> keys;
+  std::vector<int> scale;        // per key: results are counts of 10^scale
+  std::vector<int64_t> res;      // [J][keys]
+  std::vector<uint8_t> present;  // [J][keys] 0 / 1
+  std::vector<uint8_t> overflow;
   std::vector<int32_t> members;
 };
 
+// One pe_pg_min_resources_keys call per slice of <= PE_MAX_KEYS keys (keys never interact; every
+// slice returns the same members).  A value with no int64 at its key's scale marks its job overflowed
+// on the host (its records carry 0), exactly like a sum the kernel flags.
 static AggOut run_agg(Engine& eng, int mode, const Flat& f) {
   const int64_t J = (int64_t)f.job_group_off.size() - 1;
+  const int64_t C = (int64_t)f.cont_kind.size();
+  const int nk = (int)f.keys.size();
   AggOut o;
-  o.res.assign((size_t)J * PE_DIMS, 0);
-  o.present.assign((size_t)J, 0);
+  o.keys = f.keys;
+  o.scale = f.Scales();
+  o.res.assign((size_t)J * nk, 0);
+  o.present.assign((size_t)J * nk, 0);
   o.overflow.assign((size_t)J, 0);
   o.members.assign((size_t)J, 0);
   if (J == 0) return o;
-  const int rc = pe_pg_min_resources(eng.ctx(), mode, J, f.job_group_off.data(), f.min_member.data(),
-                                     f.group_replicas.data(), f.group_cont_off.data(), f.cont_req.data(),
-                                     f.cont_flags.data(), o.res.data(), o.present.data(), o.members.data(),
-                                     o.overflow.data());
-  if (rc != PE_OK && rc != PE_EOVERFLOW) throw Error{rc, pe_last_error(eng.ctx())};
+  std::vector<int64_t> val(f.ent_q.size(), 0);
+  for (int64_t j = 0; j < J; ++j)
+    for (int32_t g = f.job_group_off[j]; g < f.job_group_off[j + 1]; ++g)
+      for (int32_t c = f.group_cont_off[g]; c < f.group_cont_off[g + 1]; ++c)
+        for (int32_t e = f.ent_off[c]; e < f.ent_off[c + 1]; ++e) {
+          const std::optional<int64_t> v = f.ent_q[e].Scaled(o.scale[f.ent_key[e]]);
+          if (v) val[e] = *v;
+          else o.overflow[j] = 1;
+        }
+  std::vector<int64_t> req, res((size_t)J * PE_MAX_KEYS);
+  std::vector<uint32_t> flags((size_t)C);
+  std::vector<uint16_t> pres((size_t)J);
+  std::vector<uint8_t> ovf((size_t)J);
+  for (int lo = 0; lo < std::max(nk, 1); lo += PE_MAX_KEYS) {
+    const int n = std::max(1, std::min(PE_MAX_KEYS, nk - lo));   // (no key at all: one empty key for members)
+    req.assign((size_t)C * n, 0);
+    for (int64_t c = 0; c < C; ++c) {
+      uint32_t fl = (uint32_t)f.cont_kind[c] << PE_KEYS_KIND_SHIFT;
+      for (int32_t e = f.ent_off[c]; e < f.ent_off[c + 1]; ++e) {
+        const int k = f.ent_key[e] - lo;
+        if (k < 0 || k >= n || lo + k >= nk) continue;
+        req[(size_t)c * n + k] = val[e];
+        fl |= 1u << k;
+      }
+      flags[c] = fl;
+    }
+    const int rc = pe_pg_min_resources_keys(eng.ctx(), mode, J, n, f.job_group_off.data(), f.min_member.data(),
+                                            f.group_replicas.data(), f.group_cont_off.data(), req.data(),
+                                            flags.data(), res.data(), pres.data(), o.members.data(), ovf.data());
+    if (rc != PE_OK && rc != PE_EOVERFLOW) throw Error{rc, pe_last_error(eng.ctx())};
+    for (int64_t j = 0; j < J; ++j) {
+      o.overflow[j] |= ovf[j];
+      for (int k = 0; k < n && lo + k < nk; ++k) {
+        o.res[(size_t)j * nk + lo + k] = res[(size_t)j * n + k];
+        o.present[(size_t)j * nk + lo + k] = (uint8_t)(pres[j] >> k & 1);
+      }
+    }
+  }
   return o;
 }
 
-static ResourceList to_list(const Dims& eng, const AggOut& o, int64_t j,
-                            const std::map<std::string, Format>* formats = nullptr) {
+static ResourceList to_list(const AggOut& o, int64_t j, const std::map<std::string, Format>* formats = nullptr) {
   if (o.overflow[j]) throw Error{PE_EOVERFLOW, "int64 overflow: the reference would switch to inf.Dec"};
   ResourceList rl;
-  for (int d = 0; d < PE_DIMS; ++d) {
-    if (!(o.present[j] & (1u << d))) continue;
-    const std::string key = eng.name_of(d);
+  const size_t nk = o.keys.size();
+  for (size_t k = 0; k < nk; ++k) {
+    if (!o.present[j * nk + k]) continue;
+    const std::string& key = o.keys[k];
     const auto f = formats ? formats->find(key) : std::map<std::string, Format>::const_iterator{};
-    rl[key] = formats && f != formats->end() ? Quantity::FromCanonical(key, o.res[j * PE_DIMS + d], f->second)
-                                             : Quantity::FromCanonical(key, o.res[j * PE_DIMS + d]);
+    const Format fmt = formats && f != formats->end() ? f->second : key == "cpu" ? Format::kDecimalSI : Format::kBinarySI;
+    rl[key] = Quantity::FromScaled(o.res[j * nk + k], o.scale[k], fmt);
   }
   return rl;
 }
@@ -247,20 +304,20 @@ std::map<std::string, Format> MinResourcesFormatsV1(int32_t minMember, const std
 ResourceList CalcPGMinResources(Engine& eng, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
                                 const PriorityClassGetFunc& pcGetFunc, const V1OrderPolicy& order) {
   Flat f;
-  FlattenV1Job(eng.dims(), minMember, replicas, pcGetFunc, &f, order);
+  FlattenV1Job(minMember, replicas, pcGetFunc, &f, order);
   const auto formats = MinResourcesFormatsV1(minMember, replicas, pcGetFunc, order);
-  return to_list(eng.dims(), run_agg(eng, PE_MODE_V1, f), 0, &formats);
+  return to_list(run_agg(eng, PE_MODE_V1, f), 0, &formats);
 }
 
 std::vector<ResourceList> CalcPGMinResourcesBatch(Engine& eng, const std::vector<V1Job>& jobs,
                                                   const PriorityClassGetFunc& pcGetFunc, const V1OrderPolicy& order) {
   Flat f;
-  for (const V1Job& j : jobs) FlattenV1Job(eng.dims(), j.min_member, j.replicas, pcGetFunc, &f, order);
+  for (const V1Job& j : jobs) FlattenV1Job(j.min_member, j.replicas, pcGetFunc, &f, order);
   AggOut o = run_agg(eng, PE_MODE_V1, f);
   std::vector<ResourceList> out;
   for (size_t j = 0; j < jobs.size(); ++j) {
     const auto formats = MinResourcesFormatsV1(jobs[j].min_member, jobs[j].replicas, pcGetFunc, order);
-    out.push_back(to_list(eng.dims(), o, (int64_t)j, &formats));
+    out.push_back(to_list(o, (int64_t)j, &formats));
   }
   return out;
 }
@@ -287,7 +344,7 @@ Info NewInfo(Engine& eng, const InfoOptions& opts) {
   if (opts.pod_spec_replicas.empty()) return info;
   Flat f;
   for (const PodSpecReplica& r : opts.pod_spec_replicas) {
-    FlattenV2PodGroup(eng.dims(), 1, r.pod_spec, &f);   // per-pod requests: one group of 1 replica per job
+    FlattenV2PodGroup(1, r.pod_spec, &f);   // per-pod requests: one group of 1 replica per job
     end_job(0, &f);
   }
   AggOut o = run_agg(eng, PE_MODE_V2, f);
@@ -306,7 +363,7 @@ Info NewInfo(Engine& eng, const InfoOptions& opts) {
     if (r.pod_spec.overhead)
       for (const auto& kv : *r.pod_spec.overhead) acc.add(kv.first, kv.second, true);
     info.scheduler.total_requests[r.name] =
-        TotalResourceRequest{r.replicas, to_list(eng.dims(), o, (int64_t)i, &acc.fmt)};
+        TotalResourceRequest{r.replicas, to_list(o, (int64_t)i, &acc.fmt)};
   }
   return info;
 }
@@ -384,7 +441,7 @@ std::vector<CoScheduling::BuildResult> CoScheduling::BuildBatch(const std::vecto
         !trainJobs[i])
       continue;  // coscheduling.go:104-106: (nil, nil)
     try {
-      FlattenV2Info(eng_.dims(), *info, &f);
+      FlattenV2Info(*info, &f);
       idx.push_back(i);
     } catch (const Error& e) {
       out[i].error = e;
@@ -404,7 +461,7 @@ std::vector<CoScheduling::BuildResult> CoScheduling::BuildBatch(const std::vecto
     pg.ns = trainJobs[i]->ns;
     pg.min_member = o.members[n];
     try {
-      pg.min_resources = to_list(eng_.dims(), o, (int64_t)n);
+      pg.min_resources = to_list(o, (int64_t)n);
     } catch (const Error& e) {
       out[i].error = e;
       continue;
@@ -414,15 +471,13 @@ std::vector<CoScheduling::BuildResult> CoScheduling::BuildBatch(const std::vecto
     FormatAcc acc;
     for (const auto& kv : infos[i]->scheduler.total_requests)
       for (const auto& q : kv.second.pod_requests) {
-        Quantity scaled = q.second.IsZero() || kv.second.replicas == 0
-                              ? Quantity::FromCanonical(q.first, 0, q.second.format())
-                              : q.second;
+        Quantity scaled = q.second.IsZero() || kv.second.replicas == 0 ? Quantity::FromScaled(0, 0, q.second.format())
+                                                                       : q.second;
         acc.add(q.first, scaled, false);
       }
     for (auto& kv : pg.min_resources) {
       auto f = acc.fmt.find(kv.first);
-      if (f != acc.fmt.end())
-        kv.second = Quantity::FromCanonical(kv.first, kv.second.Canonical(kv.first), f->second);
+      if (f != acc.fmt.end()) kv.second = kv.second.WithFormat(f->second);
     }
     pg.schedule_timeout_seconds = infos[i]->runtime_policy.pod_group_policy->coscheduling->schedule_timeout_seconds;
     pg.owner_api_version = "kubeflow.org/v2alpha1";   // SetControllerReference (coscheduling.go:134)

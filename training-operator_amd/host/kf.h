@@ -195,8 +195,9 @@ std::vector<ReplicaType> ReplicaOrderV1(const std::map<ReplicaType, ReplicaSpec>
 
 int32_t GetTotalReplicas(const std::map<ReplicaType, ReplicaSpec>& replicas);
 
-// util.go:108.  Throws kf::Error when a quantity has no exact int64 canonical form, a resource key
-// has no engine dimension, or the sum overflows int64 (Go would switch to inf.Dec).
+// util.go:108.  Any resource key (a per-call key table, pe_pg_min_resources_keys).  Throws kf::Error
+// {PE_EOVERFLOW} when a sum or a value has no int64 at its key's scale (Go would switch to inf.Dec:
+// the one case a caller hands to the reference), {PE_EINVAL} on a negative quantity.
 ResourceList CalcPGMinResources(Engine& eng, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
                                 const PriorityClassGetFunc& pcGetFunc, const V1OrderPolicy& order = {});
 
@@ -374,15 +375,26 @@ class NodeInventory {
 
 // ------------------------------------------------------------------ flattening (exposed for tests)
 
+// The CSR of one pe_pg_min_resources_keys batch over a per-call KEY TABLE: every ResourceName the
+// containers name (the reference sums any key: util.go:80-103, coscheduling.go:112-116), numbered in
+// first-seen order.  The quantities stay exact here; run time picks each key's decimal scale (the
+// finest exponent its nonzero quantities need, Quantity::Exp10) and converts them to int64 counts of
+// 10^scale units -- a value with no int64 at its key's scale makes its job an overflow (inf.Dec in Go).
 struct Flat {
   std::vector<int32_t> job_group_off{0}, min_member, group_replicas, group_cont_off{0};
-  std::vector<int64_t> cont_req;
-  std::vector<uint8_t> cont_flags;
+  std::vector<uint8_t> cont_kind;          // PE_KIND_*
+  std::vector<int32_t> ent_off{0};         // container c's entries: [ent_off[c], ent_off[c + 1])
+  std::vector<int32_t> ent_key;            // key id of each entry
+  std::vector<Quantity> ent_q;
+  std::vector<std::string> keys;           // key id -> ResourceName
+  std::map<std::string, int32_t> key_id;
+  std::vector<int> Scales() const;         // per key id
 };
-// Each call appends exactly one job (V1Job / Info) or one group (V2PodGroup) or nothing (throws).
-void FlattenV1Job(const Dims& dims, int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
+// Each call appends exactly one job (V1Job / Info) or one group (V2PodGroup) or nothing (throws
+// Error{PE_EINVAL} on a negative quantity).
+void FlattenV1Job(int32_t minMember, const std::map<ReplicaType, ReplicaSpec>& replicas,
                   const PriorityClassGetFunc& pcGetFunc, Flat* out, const V1OrderPolicy& order = {});
-void FlattenV2PodGroup(const Dims& dims, int32_t replicas, const PodSpec& pod, Flat* out);
-void FlattenV2Info(const Dims& dims, const Info& info, Flat* out);
+void FlattenV2PodGroup(int32_t replicas, const PodSpec& pod, Flat* out);
+void FlattenV2Info(const Info& info, Flat* out);
 
 }  // namespace kf

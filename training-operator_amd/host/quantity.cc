@@ -130,6 +130,56 @@ Quantity Quantity::FromCanonical(const std::string& resource, int64_t v, Format 
   return q;
 }
 
+int Quantity::Exp10() const {
+  if (mant_ == 0) return 0;
+  // value = mant * 2^e2 * 10^e10 (e2 >= 0): trailing zeros of mant * 2^e2 = min(2s, 5s) of it
+  __int128 m = mant_ < 0 ? -mant_ : mant_;
+  int twos = e2_, fives = 0;
+  while (m % 2 == 0) {
+    m /= 2;
+    ++twos;
+  }
+  while (m % 5 == 0) {
+    m /= 5;
+    ++fives;
+  }
+  return e10_ + (twos < fives ? twos : fives);
+}
+
+std::optional<int64_t> Quantity::Scaled(int s) const {
+  if (mant_ < 0) return std::nullopt;
+  if (mant_ == 0) return 0;
+  if (s > Exp10()) return std::nullopt;   // (not an integer count of 10^s)
+  __int128 x = mant_;
+  int k = e10_ - s;                       // value / 10^s = mant * 2^e2 * 10^k
+  while (k < 0 && x % 10 == 0) {          // the exact divisions first: x never grows past the result
+    x /= 10;
+    ++k;
+  }
+  for (int i = 0; i < e2_; ++i) {
+    if (x > (__int128)INT64_MAX) return std::nullopt;
+    x *= 2;
+  }
+  while (k < 0) {                         // (the 2s of 2^e2 pair with the 5s left in x)
+    x /= 10;
+    ++k;
+  }
+  for (; k > 0; --k) {
+    if (x > (__int128)INT64_MAX) return std::nullopt;
+    x *= 10;
+  }
+  if (x > (__int128)INT64_MAX) return std::nullopt;
+  return (int64_t)x;
+}
+
+Quantity Quantity::FromScaled(int64_t v, int s, Format f) {
+  Quantity q;
+  q.mant_ = v;
+  q.e10_ = s;
+  q.format_ = f;
+  return q;
+}
+
 bool Quantity::Equal(const Quantity& o) const {
   __int128 m1, m2;
   int a1, b1, a2, b2;

@@ -31,6 +31,19 @@ class Quantity {
 
   // canonical int64 for `resource` (cpu: milli); throws QuantityError when inexact / negative / > int64
   int64_t Canonical(const std::string& resource) const;
+  // Key tables (placement.h pe_pg_min_resources_keys): the value as an exact count of 10^s units.
+  // Exp10(): the exponent e of value = m * 10^e, m an integer not divisible by 10 (0 for zero) -- the
+  // finest scale the value needs.  Scaled(s): value / 10^s when that is an exact int64 in [0, INT64_MAX]
+  // (s <= Exp10()), else nullopt (negative, or no int64: Go would hold the sum in inf.Dec).
+  int Exp10() const;
+  std::optional<int64_t> Scaled(int s) const;
+  static Quantity FromScaled(int64_t v, int s, Format f);
+  Quantity WithFormat(Format f) const {
+    Quantity q = *this;
+    q.format_ = f;
+    return q;
+  }
+  bool Negative() const { return mant_ < 0; }
   // Cmp == 0 semantics
   bool Equal(const Quantity& o) const;
   bool IsZero() const { return mant_ == 0; }

@@ -212,6 +212,30 @@ class Engine:
         self._chk(rc, "pe_pg_min_resources", ok=(0, _abi.PE_EOVERFLOW) if allow_overflow else (0,))
         return out, pres, mem, ovf
 
+    def pg_min_resources_keys(self, mode, job_group_off, min_member, group_replicas, group_cont_off, cont_req,
+                              cont_flags, allow_overflow=True):
+        """pe_pg_min_resources_keys: cont_req [C][n_keys] int64 (each key at the caller's decimal scale),
+        cont_flags [C] u32 = presence bits 0..n_keys-1 | kind << PE_KEYS_KIND_SHIFT.  Returns
+        (min_res [J][n_keys], present [J] u16, members, overflow)."""
+        jgo = _c(job_group_off, np.int32)
+        J = len(jgo) - 1
+        mm = None if min_member is None else _c(min_member, np.int32)
+        rep = _c(group_replicas, np.int32)
+        gco = _c(group_cont_off, np.int32)
+        req = np.ascontiguousarray(cont_req, dtype=np.int64)
+        if req.ndim != 2:
+            raise ValueError("cont_req must be [C][n_keys]")
+        nk = req.shape[1]
+        fl = _c(cont_flags, np.uint32)
+        out = np.zeros((J, nk), dtype=np.int64)
+        pres = np.zeros(J, dtype=np.uint16)
+        mem = np.zeros(J, dtype=np.int32)
+        ovf = np.zeros(J, dtype=np.uint8)
+        rc = self.lib.pe_pg_min_resources_keys(self.h, mode, J, nk, _p(jgo), _p(mm), _p(rep), _p(gco), _p(req), _p(fl),
+                                               _p(out), _p(pres), _p(mem), _p(ovf))
+        self._chk(rc, "pe_pg_min_resources_keys", ok=(0, _abi.PE_EOVERFLOW) if allow_overflow else (0,))
+        return out, pres, mem, ovf
+
     # ------------------------------------------------------------ fit mask
     def jobs_upload(self, req, need=None):
         req = _c(req, np.int64).reshape(-1, 4)
@@ -312,6 +336,12 @@ class Resolver:
         if getattr(self, "h", None):
             self.lib.pe_resolver_destroy(self.h)
             self.h = None
+
+    def set_nodes(self, n_nodes: int):
+        """pe_resolver_set_nodes: listed / seeded node ids must lie below n_nodes (PE_EINVAL otherwise)."""
+        rc = self.lib.pe_resolver_set_nodes(self.h, int(n_nodes))
+        if rc != 0:
+            raise PlacementError(rc, "pe_resolver_set_nodes")
 
     def done(self) -> bool:
         return bool(self.lib.pe_resolver_done(self.h))

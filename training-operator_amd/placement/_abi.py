@@ -20,6 +20,8 @@ PE_NODE_SET, PE_NODE_REMOVE = 0, 1
 PE_JOB_PLACED, PE_JOB_UNSCHEDULABLE = 0, 1
 PE_KIND_CONTAINER, PE_KIND_INIT, PE_KIND_SIDECAR, PE_KIND_OVERHEAD = 0, 1, 2, 3
 PE_KIND_SHIFT = 4
+PE_MAX_KEYS = 16
+PE_KEYS_KIND_SHIFT = 16
 PE_COMM_ID_BYTES = 128
 PE_DIMS = 4
 
@@ -71,6 +73,7 @@ SIGNATURES = {
     "pe_comm_ranks": (ctypes.c_int, [P, ctypes.POINTER(i32)]),
     "pe_read_residuals": (ctypes.c_int, [P, P]),
     "pe_pg_min_resources": (ctypes.c_int, [P, i32, i64, P, P, P, P, P, P, P, P, P, P]),
+    "pe_pg_min_resources_keys": (ctypes.c_int, [P, i32, i64, i32, P, P, P, P, P, P, P, P, P, P]),
     "pe_fit_mask": (ctypes.c_int, [P, i64, P, P, P, ctypes.POINTER(P), ctypes.POINTER(i64)]),
     "pe_jobs_upload": (ctypes.c_int, [P, i64, P, P]),
     "pe_fit_mask_run": (ctypes.c_int, [P]),
@@ -81,6 +84,7 @@ SIGNATURES = {
     "pe_place_greedy": (ctypes.c_int, [P, i64, P, P, P, P, P, P, P]),
     "pe_resolver_create": (ctypes.c_int, [i64, P, P, P, P, P, ctypes.POINTER(P)]),
     "pe_resolver_destroy": (None, [P]),
+    "pe_resolver_set_nodes": (ctypes.c_int, [P, i64]),
     "pe_resolver_done": (ctypes.c_int, [P]),
     "pe_resolver_next_window": (ctypes.c_int, [P, i32, i64, P, ctypes.POINTER(i32)]),
     "pe_resolver_resolve": (ctypes.c_int, [P, i32, P, P, i32, i32, P, i64, ctypes.POINTER(i64),
