@@ -270,6 +270,11 @@ def profile_check(path: str, n_nodes: int, n_jobs: int, kern_ms: float, src_hash
     if summ is None:
         return out
     out["profile"] = f"profiles/{tag}/summary.json"
+    # every candidate of these sources with its step, so a reader sees which one matched and the spread
+    # the choice was made from (advice r5: the best of N is an easier match than one profile)
+    out["profile_candidates"] = [{"profile": f"profiles/{t}/summary.json", "step_ms": step_ms(sm)} for t, sm in pool]
+    steps = [c["step_ms"] for c in out["profile_candidates"] if c["step_ms"]]
+    out["profile_candidates_spread"] = (max(steps) / min(steps) - 1.0) if len(steps) > 1 else 0.0
     kernels = summ.get("kernels", {})
     if names[0] not in kernels:
         return out
@@ -304,23 +309,23 @@ def agg_profile_ms(src_hash: str):
     return k["total_ns"] / AGG_PROFILE_CALLS / 1e6 if k else None
 
 
-def agg_roofline(in_bytes: int, out_bytes: int, events_ms: float, profile_ms, pcie):
-    """Roofline of the 1M-job aggregation call's kernel.  The batch crosses PCIe: the packed batch is
-    read zero-copy (in_bytes, host to device) while the outputs are written into pinned memory
-    (out_bytes, device to host) -- the two directions of a full-duplex link, so peak = the box's
-    measured pinned H2D + D2H rates, and h2d_frac prices the input stream alone.  Kernel time = the
-    committed profile's (the sum of the call's chunk launches) when it matches the sources, else
-    hipEvents around the whole call (which also cover the host packing its first chunk)."""
-    ms = profile_ms if profile_ms else events_ms
-    ach = (in_bytes + out_bytes) / (ms * 1e-3) / 1e9
-    peak = (pcie["h2d_gbs"] + pcie["d2h_gbs"]) if pcie else None
-    return {"bound": "pcie", "kernel": "pe::pg_agg_seg_kernel", "kernel_ms": ms,
-            "time_source": "rocprof profile (sum of the call's chunk launches)" if profile_ms else
-                           "hipEvents around the call (host packing of the first chunk included)",
-            "events_call_ms": events_ms, "profile_kernel_ms": profile_ms, "in_bytes": in_bytes, "out_bytes": out_bytes,
-            "achieved": ach, "unit": "GB/s", "peak": peak, "frac": ach / peak if peak else None,
-            "h2d_frac": in_bytes / (ms * 1e-3) / 1e9 / pcie["h2d_gbs"] if pcie else None,
-            "hbm_frac": ach / HBM_PEAK_GBS}
+def agg_roofline(in_bytes: int, out_bytes: int, call_ms: float, events_ms: float, profile_ms, pcie):
+    """Roofline of the 1M-job aggregation call.  The batch crosses PCIe: the packed input host to device
+    (a DMA per chunk, pe_engine.cpp) while the kernels write the outputs into pinned memory device to
+    host -- the two directions of a full-duplex link, each at the box's measured pinned rate.  The bound
+    is the slower direction's time, max(in / h2d, out / d2h) (the input, 3x the output); frac = that
+    bound / the whole call's wall time (planning, packing, DMA, kernels, copy-out: what the caller
+    waits for).  full_duplex_frac prices (in + out) against h2d + d2h together -- out of reach by
+    construction (<= 0.65 here: the output direction idles 3/4 of the time)."""
+    bound = max(in_bytes / pcie["h2d_gbs"], out_bytes / pcie["d2h_gbs"]) / 1e6 if pcie else None
+    ach = in_bytes / (call_ms * 1e-3) / 1e9
+    return {"bound": "pcie (host to device: the packed batch)", "kernel": "pe::pg_agg_seg_kernel",
+            "call_ms": call_ms, "bound_ms": bound, "events_call_ms": events_ms, "profile_kernel_ms": profile_ms,
+            "in_bytes": in_bytes, "out_bytes": out_bytes, "achieved": ach, "unit": "GB/s",
+            "peak": pcie["h2d_gbs"] if pcie else None, "frac": bound / call_ms if bound else None,
+            "full_duplex_frac": (in_bytes + out_bytes) / (call_ms * 1e-3) / 1e9 / (pcie["h2d_gbs"] + pcie["d2h_gbs"])
+            if pcie else None,
+            "hbm_frac": (in_bytes + out_bytes) / (call_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
 def greedy_profile(src_hash: str):
@@ -575,6 +580,35 @@ def main(argv=None):
             holder[0].load_nodes(node_inv.cap, node_inv.used, node_inv.labels, node_inv.island)
         raise AssertionError("unreachable")
 
+    # PE_BENCH_INTERLEAVE_ONE=1 (multi-rank rehearsals, tests/test_gpu_multirank.py): after every timed
+    # sharded greedy batch, rank 0 places the same batch alone on an unsharded context of the whole
+    # inventory while the other ranks wait at a barrier -- a 1-rank reference timed on the same box in
+    # the same minutes (interleaved), so a 2-rank / 1-rank bound does not compare two bench launches
+    interleave = world > 1 and os.environ.get("PE_BENCH_INTERLEAVE_ONE") == "1"
+
+    def solo_engine(kw, node_inv, batch):
+        if not interleave or rank != 0:
+            return None
+        se = Engine(device, **kw)
+        se.load_nodes(node_inv.cap, node_inv.used, node_inv.labels, node_inv.island)
+        se.place_batch(batch)   # warm-up
+        return se
+
+    def solo_timed(se, batch):
+        """rank 0 alone on its unsharded context (the other ranks at the barrier): seconds, or None"""
+        if not interleave:
+            return None
+        barrier()
+        t = None
+        if se is not None:
+            se.reset_residuals()
+            se.synchronize()
+            g0 = time.perf_counter()
+            se.place_batch(batch)
+            t = time.perf_counter() - g0
+        barrier()
+        return t
+
     N = args.nodes
     J = args.fit_jobs * (world if args.scaling == "weak" else 1)
     inv = synth.make_inventory(N, synth.SEED["cfg5"], gpu_frac=0.2)
@@ -782,8 +816,10 @@ def main(argv=None):
             "pcie": pcie,
             "pcie_bound_ms": (mb / pcie["h2d_gbs"] / 1e6) if pcie else None,
             "latency_us": lat, "ctypes_call_us": ctypes_us,
-            "roofline": agg_roofline(mb - 38 * (hi_j - lo_j), 38 * (hi_j - lo_j), kms, agg_profile_ms(source_hash(ROOT)),
-                                     pcie),
+            "pcie_bound_duplex_ms": (max((mb - 38 * (hi_j - lo_j)) / pcie["h2d_gbs"], 38 * (hi_j - lo_j) / pcie["d2h_gbs"])
+                                     / 1e6) if pcie else None,
+            "roofline": agg_roofline(mb - 38 * (hi_j - lo_j), 38 * (hi_j - lo_j), at * 1e3, kms,
+                                     agg_profile_ms(source_hash(ROOT)), pcie),
             "note": "latency_us: one pe_pg_min_resources call on the first J jobs (median / p90 of 400, ctypes pointers "
                     "built once; ctypes_call_us = the dispatch cost of an empty ABI call, included); r2_path = the "
                     "round-2 call path (PE_AGG_DEVICE=1: six H2D + four D2H copies + stream sync) on the same box; "
@@ -797,8 +833,9 @@ def main(argv=None):
         eng.reset_residuals()
         place_timed(holder, batch, eng_kw, inv)     # warm-up pass (allocations, code paths)
         eng = holder[0]
+        solo = solo_engine(eng_kw, inv, batch)
         eng.reset_stats()
-        times = []
+        times, solo_t = [], []
         placed = 0
         for _ in range(args.greedy_steps):
             eng.reset_residuals()
@@ -809,6 +846,11 @@ def main(argv=None):
                 times = []
             times.append(t)
             placed = int((st == 0).sum())
+            t1 = solo_timed(solo, batch)
+            if t1 is not None:
+                solo_t.append(t1)
+        if solo is not None:
+            solo.close()
         s = eng.stats()
         gt = float(np.median(times))
         gs = args.greedy_steps
@@ -821,6 +863,8 @@ def main(argv=None):
                          "zero_copy_exchange_windows_per_batch": s["xchg_zc_windows"] / gs,
                          "exchange_us_per_window": exchange_cost(s),
                          "naive_pod_x_node_evals_per_s": batch.n_pods * float(N) / gt}
+        if solo_t:
+            out["greedy"]["interleaved_one_rank_ms_per_batch"] = float(np.median(solo_t)) * 1e3
         if s["walk_groups"] > 0:
             # greedy roofline of the walk kernel.  Bytes it reads per batch (engine counters of the timed
             # batches): per group the round summaries (first key 8 B, max residual 32 B, label OR 4 B per
@@ -912,9 +956,10 @@ def main(argv=None):
             ch = [make_engine(**ckw)]
             ch[0].load_nodes(cinv.cap, cinv.used, cinv.labels, cinv.island)
             place_timed(ch, cb, ckw, cinv)           # warm-up
+            solo = solo_engine(ckw, cinv, cb)
             ce = ch[0]
             ce.reset_stats()
-            ts = []
+            ts, solo_t = [], []
             for _ in range(3):
                 ce.reset_residuals()
                 ce.synchronize()
@@ -923,6 +968,11 @@ def main(argv=None):
                     ce = ch[0]
                     ts = []
                 ts.append(t)
+                t1 = solo_timed(solo, cb)
+                if t1 is not None:
+                    solo_t.append(t1)
+            if solo is not None:
+                solo.close()
             ct = float(np.median(ts))
             cs = ce.stats()
             out["configs"][cfg] = {"workload": what, "nodes": n_nodes, "jobs": n_jobs, "pods": cb.n_pods,
@@ -933,6 +983,8 @@ def main(argv=None):
                                    "device_wait_ms_per_batch": cs["greedy_wait_ms"] / 3.0,
                                    "zero_copy_exchange_windows_per_batch": cs["xchg_zc_windows"] / 3.0,
                                    "exchange_us_per_window": exchange_cost(cs)}
+            if solo_t:
+                out["configs"][cfg]["interleaved_one_rank_ms_per_batch"] = float(np.median(solo_t)) * 1e3
             ce.close()
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -74,7 +74,8 @@ def main():
     res2 = e.read_residuals()
     s = e.stats()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), pods=pods, st=st, res=res, pods2=pods2, st2=st2, res2=res2,
-             b=b, e=en, windows=s["windows"], zc=s["xchg_zc_windows"], rescans=s["rescans"])
+             b=b, e=en, windows=s["windows"], zc=s["xchg_zc_windows"], rescans=s["rescans"],
+             xmerge_ms=s["xchg_merge_ms"], xwait_ms=s["xchg_wait_ms"], host_ms=s["greedy_host_ms"])
     e.close()
     dist.destroy_process_group()
 

@@ -137,8 +137,9 @@ def test_greedy_and_aggregation_profile_lookups(tmp_path, monkeypatch):
     assert g["warm"] == 30000.0 and g["cold"] == 45000.0 and g["profile"].endswith("p/summary.json")
     assert bench.greedy_profile("other") == {}
     assert abs(bench.agg_profile_ms("abc") - 2.8) < 1e-9 and bench.agg_profile_ms("other") is None
-    r = bench.agg_roofline(42_000_000, 14_000_000, 4.0, 2.8, {"h2d_gbs": 56.0, "d2h_gbs": 55.0})
-    assert r["bound"] == "pcie" and abs(r["achieved"] - 20.0) < 1e-9 and abs(r["frac"] - 20.0 / 111.0) < 1e-9
-    assert abs(r["h2d_frac"] - 15.0 / 56.0) < 1e-9
-    r = bench.agg_roofline(42_000_000, 14_000_000, 4.0, None, None)
-    assert r["kernel_ms"] == 4.0 and r["frac"] is None and "hipEvents" in r["time_source"]
+    # the call's wall time against the slower direction of the link: 42 MB in at 56 GB/s = 0.75 ms
+    r = bench.agg_roofline(42_000_000, 14_000_000, 1.5, 1.4, 2.8, {"h2d_gbs": 56.0, "d2h_gbs": 55.0})
+    assert r["bound"].startswith("pcie") and abs(r["achieved"] - 28.0) < 1e-9 and abs(r["bound_ms"] - 0.75) < 1e-9
+    assert abs(r["frac"] - 0.5) < 1e-9 and abs(r["full_duplex_frac"] - 56.0 / 1.5 / 111.0) < 1e-9
+    r = bench.agg_roofline(42_000_000, 14_000_000, 4.0, 3.9, None, None)
+    assert r["call_ms"] == 4.0 and r["frac"] is None and r["peak"] is None

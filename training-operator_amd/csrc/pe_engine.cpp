@@ -32,6 +32,7 @@
 
 #include "pe_hostx.h"
 #include "pe_kernels.h"
+#include "pe_merge.h"
 #include "pe_resolver.h"
 #include "placement.h"
 
@@ -223,59 +224,6 @@ class SpinQueue {
   std::thread th_;   // last: starts after the members above exist
 };
 
-// Two ascending u64 lists (unique keys) merged: the first `want` keys of their union into out (which
-// holds want rounded up to 8, + 8).  AVX-512 bitonic merge, 8 keys per step (the host-merged
-// zero-copy exchange's two-shard case; the scalar merge is a chain of dependent loads and compares,
-// ~7 cycles per key).
-#define PE_AVX512 __attribute__((target("avx512f")))
-PE_AVX512 static inline __m512i bitonic8(__m512i v) {   // a bitonic 8-vector, sorted ascending
-  const __m512i p4 = _mm512_set_epi64(3, 2, 1, 0, 7, 6, 5, 4), p2 = _mm512_set_epi64(5, 4, 7, 6, 1, 0, 3, 2),
-                p1 = _mm512_set_epi64(6, 7, 4, 5, 2, 3, 0, 1);
-  __m512i q = _mm512_permutexvar_epi64(p4, v);
-  v = _mm512_mask_blend_epi64(0xF0, _mm512_min_epu64(v, q), _mm512_max_epu64(v, q));
-  q = _mm512_permutexvar_epi64(p2, v);
-  v = _mm512_mask_blend_epi64(0xCC, _mm512_min_epu64(v, q), _mm512_max_epu64(v, q));
-  q = _mm512_permutexvar_epi64(p1, v);
-  return _mm512_mask_blend_epi64(0xAA, _mm512_min_epu64(v, q), _mm512_max_epu64(v, q));
-}
-PE_AVX512 static inline void merge16(__m512i& lo, __m512i& hi, __m512i a, __m512i b) {   // a, b sorted
-  const __m512i rev = _mm512_set_epi64(0, 1, 2, 3, 4, 5, 6, 7);
-  const __m512i rb = _mm512_permutexvar_epi64(rev, b);
-  lo = bitonic8(_mm512_min_epu64(a, rb));
-  hi = bitonic8(_mm512_max_epu64(a, rb));
-}
-PE_AVX512 static inline __m512i load8pad(const uint64_t* p, int i, int n) {   // p[i .. i+8), ~0 past n
-  const int k = std::max(0, std::min(8, n - i));
-  return _mm512_mask_loadu_epi64(_mm512_set1_epi64(-1), (__mmask8)((1u << k) - 1u), p + i);
-}
-PE_AVX512 static int merge2_avx512(const uint64_t* a, int na, const uint64_t* b, int nb, int want, uint64_t* out) {
-  __m512i lo, hi;
-  merge16(lo, hi, load8pad(a, 0, na), load8pad(b, 0, nb));
-  int ia = 8, ib = 8, m = 0;
-  _mm512_storeu_si512(out, lo);
-  m = 8;
-  while (m < want) {
-    const uint64_t xa = ia < na ? a[ia] : ~0ull, xb = ib < nb ? b[ib] : ~0ull;
-    __m512i nx;
-    if (xa == ~0ull && xb == ~0ull) {
-      _mm512_storeu_si512(out + m, hi);
-      m += 8;
-      break;
-    }
-    if (xa < xb) {
-      nx = load8pad(a, ia, na);
-      ia += 8;
-    } else {
-      nx = load8pad(b, ib, nb);
-      ib += 8;
-    }
-    merge16(lo, hi, hi, nx);
-    _mm512_storeu_si512(out + m, lo);
-    m += 8;
-  }
-  return std::min(m, want);
-}
-static const bool kHaveAvx512 = __builtin_cpu_supports("avx512f");
 
 struct PeError {
   int code;
@@ -350,6 +298,7 @@ double rccl_timeout_s() {
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // pe_config.fit_path_mask bits
+constexpr int kMaxMergers = 7;   // zero-copy exchange: merge helper threads per rank (at most)
 constexpr int PATH_I64 = 1, PATH_I32 = 2, PATH_CODED = 4, PATH_NO_THERM = 8, PATH_PLANES = 16, PATH_PLANES_BLOCKS = 32,
               PATH_LDS = 64;
 constexpr int PATHS_ALL = PATH_I64 | PATH_I32 | PATH_CODED | PATH_PLANES | PATH_LDS;
@@ -444,6 +393,9 @@ struct pe_ctx {
   // aggregation: segmented batch and outputs in pinned, device-mapped host memory (pe_kernels.h
   // AggSegHdr); the device-resident arrays below only serve the PE_AGG_DEVICE=1 A/B path
   HostBuf<uint8_t> a_stage, a_outh;
+  DevBuf<uint8_t> a_dstage;              // large batches: the packed batch DMA'd to the device chunk by chunk
+  hipStream_t a_h2d = nullptr;           // ... on this copy stream (the kernels wait on its events)
+  std::vector<hipEvent_t> a_ev_h2d;
   HostBuf<int64_t> a_segoff;
   HostBuf<uint32_t> a_flag;
   std::vector<hipEvent_t> a_ev;   // large batches: one per chunk (its outputs are copied out when it is done)
@@ -517,6 +469,10 @@ struct pe_ctx {
     lds_spec_d.release(); lds_vals.release(); lds_codes.release(); lds_ranks.release(); lds_aux.release(); lds_slots.release(); lds_rows.release();
     a_stage.release(); a_outh.release(); a_segoff.release(); a_flag.release(); a_ctr.release();
     for (hipEvent_t e : a_ev) (void)hipEventDestroy(e);
+    if (a_h2d) (void)hipStreamSynchronize(a_h2d);
+    for (hipEvent_t e : a_ev_h2d) (void)hipEventDestroy(e);
+    if (a_h2d) (void)hipStreamDestroy(a_h2d);
+    a_dstage.release();
     a_jgo.release(); a_mm.release(); a_rep.release(); a_gco.release(); a_mem.release();
     a_req.release(); a_out.release(); a_fl.release(); a_pres.release(); a_ovf.release();
     g_groups.release(); g_cand.release(); g_bound.release(); g_cnt.release(); g_out.release(); g_gath.release();
@@ -1304,19 +1260,35 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
           t_wait = std::chrono::duration<double, std::milli>(now() - tw).count();
         }
       } else {
-        // chunks of segments, each packed by the planning pool and launched at once: the kernel of
-        // chunk k reads its segments over PCIe while the host packs chunk k + 1, and chunk k - 1's
-        // outputs are copied out once its kernel is done (an event per chunk)
+        // chunks of segments, each packed by the planning pool and launched at once: chunk k's
+        // segments cross PCIe while the host packs chunk k + 1, and chunk k - 1's outputs are copied
+        // out once its kernel is done (an event per chunk).  The input crosses as one DMA per chunk
+        // (a copy engine on its own stream, pinned -> device; the chunk's kernel waits on its event and
+        // reads the segments from HBM): the copy engine streams the link at its rate, where the kernels'
+        // own zero-copy reads reached ~2/3 of it beside their output writes (round 5: 3.35 ms of kernel
+        // for a 2.2 ms input stream).  Outputs stay zero-copy writes into pinned memory: the link's
+        // other direction.  PE_AGG_ZEROCOPY=1: the kernels read the pinned batch directly (A/B).
         static const int64_t kChunks = [] {   // PE_AGG_CHUNKS (1..64, default 8): pipeline depth
           const char* e = std::getenv("PE_AGG_CHUNKS");
           return e ? std::max<int64_t>(1, std::min<int64_t>(64, std::atoll(e))) : 8;
         }();
         const int64_t C = T == 1 ? 1 : kChunks;
+        const bool dma = !std::getenv("PE_AGG_ZEROCOPY");
         while ((int64_t)ctx->a_ev.size() < C) {
           hipEvent_t e;
           hipchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
           ctx->a_ev.push_back(e);
         }
+        if (dma) {
+          hipchk(ctx->a_dstage.ensure((size_t)total), "alloc device aggregation batch");
+          if (!ctx->a_h2d) hipchk(hipStreamCreateWithFlags(&ctx->a_h2d, hipStreamNonBlocking), "stream");
+          while ((int64_t)ctx->a_ev_h2d.size() < C) {
+            hipEvent_t e;
+            hipchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+            ctx->a_ev_h2d.push_back(e);
+          }
+        }
+        const uint8_t* const blob = dma ? ctx->a_dstage.p : ctx->a_stage.dev;
         int64_t prev_s0 = -1, prev_s1 = -1, prev_c = -1;   // prev_c: event of the last launched chunk
         auto job_end = [&](int64_t s1) { return all[(size_t)s1 - 1].j0 + all[(size_t)s1 - 1].nj; };
         for (int64_t c = 0; c < C && first_neg == INT64_MAX; ++c) {
@@ -1328,7 +1300,14 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
           t_pack += std::chrono::duration<double, std::milli>(now() - tp).count();
           first_neg = *std::min_element(bad, bad + T);
           if (first_neg != INT64_MAX) break;
-          hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, ctx->a_stage.dev, ctx->a_segoff.dev + s0, s1 - s0, 0, od,
+          if (dma) {   // the chunk's bytes at the same offsets in the device copy (seg_off stays valid)
+            hipchk(hipMemcpyAsync(ctx->a_dstage.p + so[s0], ctx->a_stage.p + so[s0], (size_t)(so[s1] - so[s0]),
+                                  hipMemcpyHostToDevice, ctx->a_h2d),
+                   "H2D aggregation chunk");
+            hipchk(hipEventRecord(ctx->a_ev_h2d[(size_t)c], ctx->a_h2d), "event record");
+            hipchk(hipStreamWaitEvent(ctx->stream, ctx->a_ev_h2d[(size_t)c], 0), "stream wait");
+          }
+          hipchk(pe::launch_pg_agg_segments(ctx->stream, mode, blob, ctx->a_segoff.dev + s0, s1 - s0, 0, od,
                                             n_jobs, nullptr, 0, nullptr, ak),
                  "launch pg_agg_segments");
           hipchk(hipEventRecord(ctx->a_ev[(size_t)c], ctx->stream), "event record");
@@ -2483,24 +2462,29 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
                                  ctx->g_lo.p),
            "launch prep_nodes");
     const bool walk = ctx->walk && ctx->Ns > 0;
-    // Candidate lists that grow after a rescan (one GPU, sorted walk): windows start with lists of
-    // topk keys; once a window's lists ran out (a rescan: its groups consumed more list entries than
-    // it had -- whole-node gangs, all of a window's groups after the same few nodes), the rest of the
-    // batch walks lists of 2 x topk.  Longer lists cost walk time (cfg3: 0.58 -> 1.25 ms of device
-    // wait at 512), rescans cost a drained pipeline each (cfg4: 41 rescans at 256, none at 384).
-    // The blob stride is the grown length from the start.  Sharded runs grow too when they exchange
-    // through a node's shared-memory segment whose slots hold the grown stride (every rank resolves
-    // alike, so all switch at the same window; the host merge cuts at the window's length); the RCCL
-    // transport keeps topk (its all-gather moves whole strides).  PE_NO_LIST_GROWTH=1 keeps topk
-    // throughout (A/B; read per call).
-    const bool no_growth = std::getenv("PE_NO_LIST_GROWTH") != nullptr;
+    // Candidate lists that grow after a rescan (sorted walk): windows start with lists of topk keys;
+    // once a window's lists ran out (a rescan: its groups consumed more list entries than it had --
+    // whole-node gangs, all of a window's groups after the same few nodes), the rest of the batch walks
+    // lists of 2 x topk.  Longer lists cost walk time (cfg3: 0.58 -> 1.25 ms of device wait at 512),
+    // rescans cost a drained pipeline each (cfg4: 41 rescans at 256, none at 384).  The blob capacity
+    // is the grown length from the start.  Sharded runs grow alike on every rank (each resolves every
+    // window identically, so all switch at the same window): over a node's shared-memory segment when
+    // its slots hold the grown stride (the host merge cuts at the window's length), and over RCCL, whose
+    // windows are written, gathered and merged at the window's own list length (rccl_grow: the
+    // all-gather moves k_win keys per group, not the capacity).  The decision depends on nothing a rank
+    // holds alone (its shard may be empty): ctx->walk, the segment, the communicator.
+    // PE_NO_LIST_GROWTH=1 keeps topk throughout on an UNSHARDED context (A/B; read per call) -- a
+    // per-process variable cannot steer sharded ranks, which must agree on the stride.
+    const bool rccl_path = ctx->comm && !(ctx->exchange && !(ctx->world == 1 && !ctx->comm));
+    const bool no_growth = ctx->world == 1 && !ctx->comm && std::getenv("PE_NO_LIST_GROWTH") != nullptr;
     const int K0 = ctx->topk;
     const int Kg = std::max(K0, std::min(2 * K0, pe::WK_ROUND - 1));
     pe_host_exchange* const hx_grow = ctx->world > 1 && pe::hx_is(ctx->exchange)
                                           ? static_cast<pe_host_exchange*>(ctx->exchange_user) : nullptr;
-    const bool kgrow = walk && !no_growth &&
-                       ((ctx->world == 1 && !ctx->comm) ||
+    const bool kgrow = ctx->walk && !no_growth &&
+                       ((ctx->world == 1 && !ctx->comm) || rccl_path ||
                         (hx_grow && (size_t)ctx->window_groups * pe::cand_group_bytes(Kg) <= pe::hx_slot_bytes(hx_grow)));
+    const bool rccl_grow = kgrow && rccl_path;
     const int K = kgrow ? Kg : K0;   // blob stride (list capacity)
     int k_win = K0;                  // list length walked (changed only while the helper threads are idle)
     // PE_ASYNC_RESORT=0: rebuild the walk index in line, on the main stream (A/B; read per call).
@@ -2673,9 +2657,13 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // wider sharded runs take the host merge)
     const bool dev_merge = !direct_out && (int64_t)ctx->world * K <= pe::MG_CAP &&
                            ctx->world <= pe::MG_THREADS / 64 && !std::getenv("PE_HOST_MERGE");
-    // the shard merge kernel: PE_MERGE_RANKED=1 the rank merge (256-thread blocks, no sort; A/B)
-    const bool ranked = std::getenv("PE_MERGE_RANKED") && ctx->world <= pe::RM_MAX_WORLD &&
-                        (int64_t)ctx->world * K * 8 <= 64 * 1024;
+    // the shard merge kernel: at 1-2 ranks the rank merge (256-thread blocks, a cut of each list ranked,
+    // no sort), from 3 ranks the top-K sort merge (1024-thread blocks) -- measured alone on one MI355X,
+    // 112 groups of K = 256 (tools/bench_merge_dev.cc, profiles/r23_merge_dev.txt): rank 13.7 / 19.9 /
+    // 35.0 / 102 us per window at 2 / 4 / 8 / 16 ranks, sort 18.0 / 14.8 / 15.2 / 19.3 us.
+    // PE_MERGE_RANKED=1 / PE_MERGE_SORT=1 force one (A/B; the rank merge only where its LDS holds the lists).
+    const bool ranked = (std::getenv("PE_MERGE_RANKED") || (ctx->world <= 2 && !std::getenv("PE_MERGE_SORT"))) &&
+                        ctx->world <= pe::RM_MAX_WORLD && pe::merge_ranked_lds(ctx->world, K) <= pe::RM_MAX_LDS;
     auto* const merge_fn = ranked ? &pe::launch_merge_ranked : &pe::launch_merge_shards;
     const bool signalled = pipelined && !std::getenv("PE_NO_GROUP_SIGNAL") && (direct_out ? walk : dev_merge);
     // Zero-copy shared-memory exchange (pe_hostx.h): decided first, the pipeline depth depends on it.
@@ -2720,6 +2708,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     const uint8_t* last_blob = nullptr;   // the parsed blob of the window being resolved (one list per group
                                           // unless the shards are merged on the host)
     uint32_t buf_gen[4] = {0, 0, 0, 0};
+    int buf_k[4] = {K, K, K, K};   // the list stride each blob buffer's window was written with
     pe::WindowFeed feed;
     struct StreamIdle {
       hipStream_t s;
@@ -2744,6 +2733,10 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // never completes keeps the stream busy, which the idle test above cannot tell from a slow walk
     const double coll_tmo = !use_exchange && ctx->comm ? rccl_timeout_s() : 0.0;
     feed.timeout_s = coll_tmo;
+    // a timed-out window starts the communicator's abort where it is detected, before the unwinding
+    // (the launch helper's and the events' clean-up) could wait on anything the stuck collective holds
+    feed.on_timeout = [](void* u) { rccl_abort(static_cast<pe_ctx*>(u)); };
+    feed.timeout_user = ctx;
     auto sync_stream = [&](const char* what) {
       if (coll_tmo <= 0) return hipchk(hipStreamSynchronize(s), what);
       const auto ts = std::chrono::steady_clock::now();
@@ -2752,10 +2745,12 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         if (e != hipErrorNotReady) return hipchk(e, what);
         if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
         if ((spin & 63) == 0 &&
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count() > coll_tmo)
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count() > coll_tmo) {
+          rccl_abort(ctx);   // (at the throw site: see feed.on_timeout)
           throw pe::CollectiveTimeout(std::string(what) + ": the stream did not drain within " +
                                       std::to_string(coll_tmo) +
                                       " s -- a window's all-gather is stuck (a peer stalled or was lost; PE_RCCL_TIMEOUT_S)");
+        }
       }
     };
     // PE_TEST_STALL_WINDOW=n, PE_TEST_STALL_MS=m (test knob, RCCL transport): a one-thread kernel that
@@ -2793,10 +2788,26 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     const bool split_x =
         use_exchange && pipelined && signalled && walk && !zc_dev && !std::getenv("PE_NO_SPLIT_EXCHANGE");
     std::unique_ptr<SpinQueue> xworker;
+    // Zero-copy windows of 3+ ranks: the exchange thread's host merge grows with the world (8 ranks:
+    // ~1-2 us per group against ~0.5 us of resolve; tools/bench_merge.cc), so the window's groups are
+    // shared among the exchange thread and helpers, group w on thread w mod T (T = 1 + helpers: 2 up to
+    // 4 ranks, 4 above; PE_XCHG_THREADS overrides).  The resolver still takes the groups in order.
+    std::vector<std::unique_ptr<SpinWorker>> xmergers;
     if (split_x) {
       xworker.reset(new SpinQueue(ctx->device));
       if (pin.on) xworker->pin(pin.l3);
       stream_idle.x = xworker.get();
+      if (zc && !std::getenv("PE_ZC_DEV_MERGE")) {
+        int T = ctx->world <= 2 ? 1 : ctx->world <= 4 ? 2 : 4;
+        if (const char* e = std::getenv("PE_XCHG_THREADS")) T = std::atoi(e);
+        T = std::max(1, std::min(T, kMaxMergers + 1));
+        for (int t = 1; t < T; ++t) {
+          xmergers.emplace_back(new SpinWorker(ctx->device));
+          if (pin.on) xmergers.back()->pin(pin.l3);
+          xmergers.back()->post(&pe::merge_warm);   // (waited for before the first window's share)
+        }
+        xworker->post(&pe::merge_warm);
+      }
     }
     struct XWait {   // every exit: the exchange thread's task is over before the buffers it uses go
       std::unique_ptr<SpinQueue>& w;
@@ -2825,77 +2836,21 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       static_assert(pe::HX_ZC_MAX_WORLD >= pe::RM_MAX_WORLD, "zero-copy merge arrays");
       const uint64_t* lists[pe::HX_ZC_MAX_WORLD];   // (zero-copy windows: world <= HX_ZC_MAX_WORLD)
       int ns[pe::HX_ZC_MAX_WORLD];
+      bool bad = false;
       for (int r = 0; r < W; ++r) {
         const uint8_t* g = gath + (size_t)r * stride + (size_t)w * gb;
         pe::CandHdr h;
         std::memcpy(&h, g, sizeof(h));
         L = std::min(L, h.limit);
         lists[r] = reinterpret_cast<const uint64_t*>(g + sizeof(h));
+        bad |= h.n < 0 || h.n > K;   // a corrupt rank list: the merged group says so (never read past it)
         ns[r] = std::max(0, std::min(h.n, K));
       }
-      for (int r = 0; r < W; ++r)   // keys below L only (ascending lists: cut each at L)
-        ns[r] = (int)(std::lower_bound(lists[r], lists[r] + ns[r], L) - lists[r]);
-      int m = 0;
       uint64_t lim = L;
-      if (W >= 2 && kHaveAvx512) {   // pairwise: the K + 1 smallest of shards 0..r, merged with shard r + 1
-        alignas(64) uint64_t tmp[2][pe::MG_CAP + 16];
-        const uint64_t* acc = lists[0];
-        int na = std::min(ns[0], Kc + 1);
-        for (int r = 1; r < W; ++r) {
-          const int want = std::min(Kc + 1, na + ns[r]);
-          uint64_t* o = tmp[r & 1];
-          na = want > 0 ? merge2_avx512(acc, na, lists[r], ns[r], want, o) : 0;
-          acc = o;
-        }
-        m = na;
-        std::memcpy(dst, acc, (size_t)std::min(m, Kc) * 8);
-        if (m > Kc) lim = acc[Kc];
-      } else if (W == 2) {
-        const uint64_t *a = lists[0], *b = lists[1];
-        const int na = ns[0], nb = ns[1];
-        int i = 0, j = 0;
-        const int want = std::min(Kc + 1, na + nb);
-        while (m < want && i < na && j < nb) {
-          const uint64_t x = a[i], y = b[j];
-          const bool t = x < y;
-          const uint64_t v = t ? x : y;
-          if (m < Kc) dst[m] = v;
-          else lim = v;   // (the (K+1)-th key is the merged list's limit)
-          ++m;
-          i += t;
-          j += !t;
-        }
-        for (; m < want && i < na; ++m, ++i) {
-          if (m < Kc) dst[m] = a[i];
-          else lim = a[i];
-        }
-        for (; m < want && j < nb; ++m, ++j) {
-          if (m < Kc) dst[m] = b[j];
-          else lim = b[j];
-        }
-      } else {
-        int hd[pe::HX_ZC_MAX_WORLD] = {0};
-        for (;;) {
-          int br = -1;
-          uint64_t bk = pe::NO_KEY;
-          for (int r = 0; r < W; ++r)
-            if (hd[r] < ns[r] && lists[r][hd[r]] < bk) {
-              bk = lists[r][hd[r]];
-              br = r;
-            }
-          if (br < 0) break;
-          ++hd[br];
-          if (m == Kc) {
-            lim = bk;
-            ++m;
-            break;
-          }
-          dst[m++] = bk;
-        }
-      }
+      const int m = bad ? pe::CAND_CORRUPT : pe::merge_rank_lists(lists, ns, W, L, Kc, dst, &lim);
       pe::CandHdr* hp = reinterpret_cast<pe::CandHdr*>(og);
-      hp->n = std::min(m, Kc);
-      hp->limit = m > Kc ? lim : L;
+      hp->n = m;
+      hp->limit = bad ? 0 : lim;
       __atomic_store_n(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE);   // the group's signal, last
     };
     auto host_merge_group = [&](const uint8_t* gath, int Wg, int w, uint8_t* out, uint32_t gen) {
@@ -2907,19 +2862,21 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       ns.resize((size_t)W);
       hd.assign((size_t)W, 0);
       uint64_t L = pe::NO_KEY;
+      bool bad = false;
       for (int r = 0; r < W; ++r) {
         const uint8_t* g = gath + ((size_t)r * Wg + w) * gb;
         pe::CandHdr h;
         std::memcpy(&h, g, sizeof(h));
         L = std::min(L, h.limit);
         lists[(size_t)r] = reinterpret_cast<const uint64_t*>(g + sizeof(h));
+        bad |= h.n < 0 || h.n > K;   // a corrupt rank list: no key is taken, the group is marked below
         ns[(size_t)r] = std::max(0, std::min(h.n, K));
       }
       uint8_t* og = out + (size_t)w * gb;
       uint64_t* dst = reinterpret_cast<uint64_t*>(og + sizeof(pe::CandHdr));
-      int m = 0;
+      int m = bad ? pe::CAND_CORRUPT : 0;
       uint64_t lim = L;
-      for (;;) {
+      for (; !bad;) {
         int br = -1;
         uint64_t bk = L;   // (only keys below the smallest limit count)
         for (int r = 0; r < W; ++r)
@@ -2946,51 +2903,89 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       if (zc_host) {   // every rank's lists are in the segment: merge each group as all ranks signalled it
         const double tmo = pe::hx_timeout_s();
         const auto t0 = std::chrono::steady_clock::now();
-        double spun = 0, merged = 0;
-        double waited = 0;   // (stats: the clock is read only around a wait that happens)
-        for (int w = 0; w < Wg; ++w) {
-          const auto ts = trace ? std::chrono::steady_clock::now() : t0;
-          for (int r = 0; r < ctx->world; ++r) {
-            const pe::CandHdr* h = reinterpret_cast<const pe::CandHdr*>(hw->host + (size_t)r * hw->slot + (size_t)w * gb);
-            if (__atomic_load_n(&h->flags, __ATOMIC_ACQUIRE) == (int32_t)hw->gen) continue;
-            const auto tw = std::chrono::steady_clock::now();
-            for (unsigned spin = 1; __atomic_load_n(&h->flags, __ATOMIC_ACQUIRE) != (int32_t)hw->gen; ++spin) {
-              _mm_pause();
-              if ((spin & 4095) == 0) {
-                const hipError_t e = hipStreamQuery(s);   // a faulted walk of this rank: its own error
-                if (e != hipErrorNotReady) hipchk(e, "walk window stream");
-                if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > tmo)
-                  throw pe::ExchangeError("host exchange: rank " + std::to_string(r) +
-                                          "'s candidate lists never arrived (peer stalled or failed; PE_HX_TIMEOUT_S)");
-              }
-            }
-            waited += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
-          }
-          const auto tm = trace ? std::chrono::steady_clock::now() : t0;
-          // the next groups' lists on their way from DRAM (the device wrote them past the CPU caches;
-          // a line fetched before the device's write is snooped out again, harmless) and the output
-          // lines owned for writing: the merge is otherwise a chain of cache misses
-          for (int a = 1; a <= 2 && w + a < Wg; ++a) {
+        const int T = 1 + (int)xmergers.size();   // the exchange thread + its merge helpers, groups w = t mod T
+        const size_t pf_bytes = pe::merge_read_bytes(ctx->world, k_win, gb);
+        // one share of the window: groups t, t + T, ... (waited / merged / spun: this share's times)
+        auto share = [&, hw, b, gen, Wg](int t, double* waited, double* spun, double* merged) {
+          for (int w = t; w < Wg; w += T) {
+            const auto ts = trace ? std::chrono::steady_clock::now() : t0;
             for (int r = 0; r < ctx->world; ++r) {
-              const uint8_t* gl = hw->host + (size_t)r * hw->slot + (size_t)(w + a) * gb;
-              for (size_t o = 0; o < gb; o += 64) __builtin_prefetch(gl + o, 0, 3);
+              const pe::CandHdr* h = reinterpret_cast<const pe::CandHdr*>(hw->host + (size_t)r * hw->slot + (size_t)w * gb);
+              if (__atomic_load_n(&h->flags, __ATOMIC_ACQUIRE) == (int32_t)hw->gen) continue;
+              const auto tw = std::chrono::steady_clock::now();
+              for (unsigned spin = 1; __atomic_load_n(&h->flags, __ATOMIC_ACQUIRE) != (int32_t)hw->gen; ++spin) {
+                _mm_pause();
+                if ((spin & 4095) == 0) {
+                  if (t == 0) {   // (HIP calls from the exchange thread only) a faulted walk of this rank: its own error
+                    const hipError_t e = hipStreamQuery(s);
+                    if (e != hipErrorNotReady) hipchk(e, "walk window stream");
+                  }
+                  if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > tmo)
+                    throw pe::ExchangeError("host exchange: rank " + std::to_string(r) +
+                                            "'s candidate lists never arrived (peer stalled or failed; PE_HX_TIMEOUT_S)");
+                }
+              }
+              *waited += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
             }
-            uint8_t* ol = outbuf(b) + (size_t)(w + a) * gb;
-            for (size_t o = 0; o < gb; o += 64) __builtin_prefetch(ol + o, 1, 3);
+            const auto tm = trace ? std::chrono::steady_clock::now() : t0;
+            // this share's next groups on their way from DRAM (the device wrote them past the CPU caches;
+            // a line fetched before the device's write is snooped out again, harmless) -- the heads the
+            // merge reads, not whole slots -- and the output lines owned for writing
+            for (int a = 1; a <= 2 && w + a * T < Wg; ++a) {
+              const int wn = w + a * T;
+              for (int r = 0; r < ctx->world; ++r) {
+                const uint8_t* gl = hw->host + (size_t)r * hw->slot + (size_t)wn * gb;
+                for (size_t o = 0; o < pf_bytes; o += 64) __builtin_prefetch(gl + o, 0, 3);
+              }
+              uint8_t* ol = outbuf(b) + (size_t)wn * gb;
+              for (size_t o = 0; o < gb; o += 64) __builtin_prefetch(ol + o, 1, 3);
+            }
+            host_merge_zc(hw->host, hw->slot, w, outbuf(b), gen);
+            if (trace) {
+              *spun += std::chrono::duration<double, std::micro>(tm - ts).count();
+              *merged += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tm).count();
+            }
           }
-          host_merge_zc(hw->host, hw->slot, w, outbuf(b), gen);
-          if (trace) {
-            spun += std::chrono::duration<double, std::micro>(tm - ts).count();
-            merged += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tm).count();
+        };
+        struct Times {
+          double waited = 0, spun = 0, merged = 0, busy = 0;   // busy: the share's wall time less its waits
+        };
+        Times tt[kMaxMergers + 1];
+        auto timed_share = [&share](int t, Times* x) {
+          const auto a = std::chrono::steady_clock::now();
+          share(t, &x->waited, &x->spun, &x->merged);
+          x->busy = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count() - x->waited;
+        };
+        for (int t = 1; t < T; ++t) {
+          Times* x = &tt[t];
+          xmergers[(size_t)t - 1]->wait();   // (the warm-up task, before the first window)
+          xmergers[(size_t)t - 1]->post([&timed_share, t, x] { timed_share(t, x); });
+        }
+        std::exception_ptr err;
+        try {
+          timed_share(0, &tt[0]);
+        } catch (...) {
+          err = std::current_exception();
+        }
+        for (int t = 1; t < T; ++t) try {   // every helper is done with the window before it is released
+            xmergers[(size_t)t - 1]->wait();
+          } catch (...) {
+            if (!err) err = std::current_exception();
           }
+        if (err) std::rethrow_exception(err);
+        double busy = 0, spun = 0, merged = 0;
+        for (int t = 0; t < T; ++t) {
+          busy = std::max(busy, tt[t].busy);   // the merge's critical path: the busiest share (they run side by side)
+          spun += tt[t].spun;
+          merged += tt[t].merged;
         }
         if (trace) {
           tr_xspin.push_back(spun);
           tr_xmerge.push_back(merged);
         }
         const double all_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        ctx->stats.xchg_wait_ms += waited;
-        ctx->stats.xchg_merge_ms += all_ms - waited;
+        ctx->stats.xchg_merge_ms += busy;
+        ctx->stats.xchg_wait_ms += std::max(0.0, all_ms - busy);   // the rest of the window's exchange: waiting
         pe::hx_zc_consumed(hx, *hw);
         return;
       }
@@ -3022,7 +3017,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         for (int w = 0; w < Wg; ++w) host_merge_group(ctx->h_xg[b].p, Wg, w, outbuf(b), gen);
         ctx->stats.xchg_merge_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tm).count();
       } else if (dev_merge) {   // the gathered lists (pinned) merged on the device, signalled per group
-        hipchk(merge_fn(s, ctx->h_xg[b].dev, ctx->world, Wg, K, outbufdev(b), gen, 0, nullptr),
+        hipchk(merge_fn(s, ctx->h_xg[b].dev, ctx->world, Wg, K, outbufdev(b), gen, 0, nullptr, true),
                "launch merge_shards");
       }
     };
@@ -3032,6 +3027,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
                               const pe::HxWindow* hw_in = nullptr) {
       const int Wg = (int)groups.size();
       const int Wgp = (int)round_up(Wg, pe::SC_GT);
+      const int Kw = rccl_grow ? k_win : K;   // the window's list stride (RCCL: its length, see rccl_grow)
       auto& hg = hgroups(b);
       for (int w = 0; w < Wgp; ++w) {
         const int g = groups[std::min(w, Wg - 1)];
@@ -3058,6 +3054,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         gen = ctx->walk_gen;
       }
       buf_gen[b] = gen;
+      buf_k[b] = Kw;
       if (walk) {   // one 64-B request per block: read from pinned host memory, no H2D copy
         // PE_WALK_SWITCH_DELAY=n (test knob): take a finished rebuild over only after n windows ran
         // with it pending, so the dual overlay writes of those windows' applies are exercised
@@ -3077,7 +3074,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           hipchk(hipEventRecord(evp.first, s), "event record");
         }
         hipchk(pe::launch_walk(s, hg.dev, Wg, k_win, walk_index(ctx), ctx->res.p, ctx->stride, ctx->labels.p, ctx->Ns,
-                               (uint64_t)ctx->begin, dst, zc ? hw.gen : direct_out || own_direct ? gen : 0u, K),
+                               (uint64_t)ctx->begin, dst, zc ? hw.gen : direct_out || own_direct ? gen : 0u, Kw),
                "launch walk");
         if (wev) hipchk(hipEventRecord(evp.second, s), "event record");
         walk_launch_groups += Wg;
@@ -3090,12 +3087,13 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         hipchk(pe::launch_merge(s, ctx->g_cand.p, ctx->g_cnt.p, ctx->g_bound.p, nwaves, K, dst, Wg),
                "launch merge");
       } else if (zc) {   // an empty shard: empty lists, signalled in stream order like a walk's
-        hipchk(pe::launch_empty_groups(s, Wg, K, dst, hw.gen), "launch empty groups");
+        hipchk(pe::launch_empty_groups(s, Wg, Kw, dst, hw.gen), "launch empty groups");
       } else {
-        std::vector<uint8_t> empty((size_t)Wg * gb, 0);
+        const size_t gbw = pe::cand_group_bytes(Kw);
+        std::vector<uint8_t> empty((size_t)Wg * gbw, 0);
         for (int w = 0; w < Wg; ++w) {
           pe::CandHdr h{0, 0, pe::NO_KEY};
-          std::memcpy(empty.data() + (size_t)w * gb, &h, sizeof(h));
+          std::memcpy(empty.data() + (size_t)w * gbw, &h, sizeof(h));
         }
         if (direct_out) {
           std::memcpy(outbuf(b), empty.data(), empty.size());
@@ -3104,7 +3102,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           hipchk(hipStreamSynchronize(s), "sync empty");
         }
       }
-      const size_t bytes = (size_t)Wg * gb;
+      const size_t bytes = (size_t)Wg * pe::cand_group_bytes(Kw);
       if (direct_out) {
         // written in place
       } else if (zc_host) {   // the exchange thread (or, not deferred, this thread) merges on the host
@@ -3115,7 +3113,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         hipchk(pe::launch_xwait(s, hw.dev, ctx->world, Wg, K, (int64_t)hw.slot, hw.gen, zc_ticks, ctx->g_xstatus.p),
                "launch exchange wait");
         hipchk(merge_fn(s, hw.dev, ctx->world, Wg, K, outbufdev(b), gen, (int64_t)hw.slot,
-                                       ctx->g_xstatus.p),
+                                       ctx->g_xstatus.p, true),
                "launch merge_shards");
       } else if (use_exchange) {
         if (!pipelined)
@@ -3127,7 +3125,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           hipchk(pe::launch_stall(s, stall_ticks), "launch stall (test knob)");
         ncclchk(ncclAllGather(ctx->g_out.p, ctx->g_gath.p, bytes, ncclUint8, ctx->comm, s), "ncclAllGather");
         if (dev_merge)
-          hipchk(merge_fn(s, ctx->g_gath.p, ctx->world, Wg, K, outbufdev(b), gen, 0, nullptr), "launch merge_shards");
+          hipchk(merge_fn(s, ctx->g_gath.p, ctx->world, Wg, Kw, outbufdev(b), gen, 0, nullptr, false),   // (device lists)
+                 "launch merge_shards");
         else
           hipchk(hipMemcpyAsync(outbuf(b), ctx->g_gath.p, bytes * ctx->world, hipMemcpyDeviceToHost, s),
                  "D2H gathered");
@@ -3143,7 +3142,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       const auto tw = std::chrono::steady_clock::now();
       if (signalled && buf_gen[b] != 0) {   // the first group's list (and so every earlier launch) is done
         last_blob = outbuf(b);
-        feed.reset(outbuf(b), Wg, K, buf_gen[b], &cands);
+        feed.reset(outbuf(b), Wg, buf_k[b], buf_gen[b], &cands);
         feed.wait(0);
         feed_spin_seen = feed.spin_ms();
         const auto th = std::chrono::steady_clock::now();
@@ -3159,7 +3158,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           raise(PE_ERCCL, "exchange callback failed");
         ctx->stats.xchg_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tx).count();
         if (dev_merge) {   // the gathered blob (pinned) merged by the device into h_merged
-          hipchk(merge_fn(s, outbufdev(b), ctx->world, Wg, K, ctx->h_merged.dev, 0u, 0, nullptr),
+          hipchk(merge_fn(s, outbufdev(b), ctx->world, Wg, K, ctx->h_merged.dev, 0u, 0, nullptr, true),
                  "launch merge_shards");
           sync_stream("sync merge");
           last_blob = ctx->h_merged.p;
@@ -3168,7 +3167,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       const auto th = std::chrono::steady_clock::now();
       ctx->stats.greedy_wait_ms += std::chrono::duration<double, std::milli>(th - tw).count();
       if (trace) tr_wait.push_back(std::chrono::duration<double, std::micro>(th - tw).count());
-      pe::parse_window_keys(last_blob, dev_merge ? 1 : ctx->world, Wg, K, cands);   // lists point into the blob
+      pe::parse_window_keys(last_blob, dev_merge ? 1 : ctx->world, Wg, buf_k[b], cands);   // lists point into the blob
 
       ctx->stats.greedy_host_ms +=
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();

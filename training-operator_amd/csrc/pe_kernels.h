@@ -371,19 +371,24 @@ hipError_t launch_walk_build(hipStream_t s, const int64_t* res, int64_t stride, 
 // shared-memory exchange's slots are further apart).  xstatus (zero-copy exchange, device word
 // written by launch_xwait before it on the stream): nonzero = a rank's lists never arrived, every
 // group is written with n = -1 and limit = *xstatus (signalled) instead of a list.
+// sys_scope: the lists may sit in host memory other processes write (this kernel always reads so).
 hipError_t launch_merge_shards(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen,
-                               int64_t rank_stride = 0, const uint64_t* xstatus = nullptr);
+                               int64_t rank_stride = 0, const uint64_t* xstatus = nullptr, bool sys_scope = true);
 // Zero-copy exchange: one block waits until every rank's header of every group (slot r at gath +
 // r * rank_stride) carries in_gen, at most timeout_ticks of wall_clock64 (100 MHz); *xstatus = 0,
 // or 1 << 63 | rank << 32 | the generation that rank's slot still held.
 constexpr int XW_THREADS = 256;
 hipError_t launch_xwait(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, int64_t rank_stride,
                         uint32_t in_gen, int64_t timeout_ticks, uint64_t* xstatus);
-// The same merge by rank (merge_ranked_kernel): 256-thread blocks, the lists in LDS (world x K x 8 B
-// of dynamic LDS, at most 64 KiB), no sort
+// The same merge by rank (merge_ranked_kernel, the default): 256-thread blocks, the lists and the
+// merged list in LDS (merge_ranked_lds bytes of dynamic LDS, at most RM_MAX_LDS), a cut of each list
+// ranked by lock-step binary searches, no sort.  sys_scope = false: gath is device memory written by
+// an earlier kernel of the stream (the RCCL all-gather), read with plain loads.
 constexpr int RM_THREADS = 256, RM_MAX_WORLD = 16;
+constexpr size_t RM_MAX_LDS = 64 * 1024;
+size_t merge_ranked_lds(int world, int K);
 hipError_t launch_merge_ranked(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen,
-                               int64_t rank_stride = 0, const uint64_t* xstatus = nullptr);
+                               int64_t rank_stride = 0, const uint64_t* xstatus = nullptr, bool sys_scope = true);
 // Wg empty lists (n = 0, limit = NO_KEY), signalled with gen
 hipError_t launch_empty_groups(hipStream_t s, int Wg, int K, uint8_t* out, uint32_t gen);
 // Test knob (PE_TEST_STALL_*): one thread that holds the stream for `ticks` of wall_clock64 (100 MHz),

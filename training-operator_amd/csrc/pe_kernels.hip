@@ -1808,7 +1808,7 @@ __global__ __launch_bounds__(MG_THREADS) void merge_shards_kernel(const uint8_t*
 }
 
 hipError_t launch_merge_shards(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen,
-                               int64_t rank_stride, const uint64_t* xstatus) {
+                               int64_t rank_stride, const uint64_t* xstatus, bool /*sys_scope: always*/) {
   if (Wg <= 0) return hipSuccess;
   if (world < 1 || world > MG_THREADS / 64 || K < 1 || (int64_t)world * K > MG_CAP) return hipErrorInvalidValue;
   hipLaunchKernelGGL(merge_shards_kernel, dim3(Wg), dim3(MG_THREADS), 0, s, gath, world, Wg, K, out, gen, rank_stride,
@@ -1860,12 +1860,20 @@ hipError_t launch_xwait(hipStream_t s, const uint8_t* gath, int world, int Wg, i
   return hipGetLastError();
 }
 
-// Rank merge (same output as merge_shards_kernel): one 256-thread block per group holds the shards'
-// lists in LDS (world x K keys) and places every key below L by its rank in the union -- its index
-// in its own list plus, per other shard, the number of that shard's keys below it (binary search;
-// keys are unique across shards: the node id is in their low bits).  Ranks < K are the output, rank
-// K is the limit.  No sort, no histogram: a small block that fits beside a walk's 1024-thread block
-// on one CU, and one pass over host-memory lists.
+// Rank merge (same output as merge_shards_kernel), the default shard merge: one 256-thread block
+// per group holds the shards' lists in LDS (world x K keys) and places the merged list's keys by
+// their rank in the union.  Only a cut of each list is ranked: with c = ceil((K+1) / world), every
+// list's first min(c, keys below L) keys hold >= K + 1 keys in all (unless the lists have fewer below
+// L than that, when every key below L is ranked), so the K + 1 smallest are at or below U = the
+// largest of those heads -- the candidates are each list's keys <= U (a downward-closed set: ~1.3
+// (K+1) keys at 8 ranks instead of 8 K).  A candidate's rank is its index in its own list plus, per
+// other list, the count of that list's candidates below it: lock-step branchless binary searches
+// over every other list, one step of each per round (independent LDS reads in flight, no sort, no
+// histogram, one barrier).  Keys are unique across shards (the node id is in their low bits).
+// Ranks < K land in an LDS output list copied out coalesced; rank K is the new limit.
+// SYS: the lists sit in host memory written by other processes' kernels (host exchange): read with
+// system-scope relaxed loads (see merge_shards_kernel).  !SYS: the all-gather's device buffer,
+// written by an earlier kernel of the stream -- plain loads.
 __device__ __forceinline__ int lds_lower_bound(const uint64_t* a, int n, uint64_t k) {
   int lo = 0;
   while (n > 0) {
@@ -1880,14 +1888,21 @@ __device__ __forceinline__ int lds_lower_bound(const uint64_t* a, int n, uint64_
   return lo;
 }
 
+template <bool SYS>
+__device__ __forceinline__ uint64_t merge_load(const uint64_t* p) {
+  if constexpr (SYS) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return *p;
+}
+
+template <bool SYS>
 __global__ __launch_bounds__(RM_THREADS) void merge_ranked_kernel(const uint8_t* __restrict__ gath, int world, int Wg,
                                                                   int K, uint8_t* __restrict__ out, uint32_t gen,
                                                                   int64_t rank_stride,
                                                                   const uint64_t* __restrict__ xstatus) {
-  extern __shared__ uint64_t lk[];   // shard r's keys at lk[r * K ...]
+  extern __shared__ uint64_t lk[];   // shard r's keys at lk[r * K ...]; the merged list at lk[world * K ...]
   __shared__ uint64_t hl[RM_MAX_WORLD];
-  __shared__ int hn[RM_MAX_WORLD], cnt[RM_MAX_WORLD];
-  __shared__ uint64_t newlim;
+  __shared__ int hn[RM_MAX_WORLD], cnt[RM_MAX_WORLD], mc[RM_MAX_WORLD];
+  __shared__ int bad;
   const int g = blockIdx.x;
   const int tid = threadIdx.x;
   const size_t gb = cand_group_bytes(K);
@@ -1902,16 +1917,18 @@ __global__ __launch_bounds__(RM_THREADS) void merge_ranked_kernel(const uint8_t*
     }
     return;
   }
-  __shared__ int bad;
-  if (tid == 0) {
-    newlim = NO_KEY;
-    bad = 0;
-  }
+  if (tid == 0) bad = 0;
   __syncthreads();
-  if (tid < world) {   // (system-scope loads: see merge_shards_kernel)
+  if (tid < world) {
     const CandHdr* h = reinterpret_cast<const CandHdr*>(gath + tid * shard_bytes + (size_t)g * gb);
-    hl[tid] = __hip_atomic_load(&h->limit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const int n = __hip_atomic_load(&h->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    int n;
+    if constexpr (SYS) {
+      hl[tid] = __hip_atomic_load(&h->limit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      n = __hip_atomic_load(&h->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      hl[tid] = h->limit;
+      n = h->n;
+    }
     hn[tid] = max(0, min(n, K));
     if (n < 0 || n > K) bad = 1;   // (as merge_shards_kernel: a corrupt shard list marks the group)
   }
@@ -1924,45 +1941,100 @@ __global__ __launch_bounds__(RM_THREADS) void merge_ranked_kernel(const uint8_t*
     }
     return;
   }
+  // every list into LDS: 8 loads per thread in flight at once (the lists are at most K keys each)
+  const int span = world * K;
+  for (int base = 0; base < span; base += 8 * RM_THREADS) {
+    uint64_t v[8];
+    int at[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * RM_THREADS + tid;
+      const int r = i / K, j = i - r * K;
+      at[u] = i < span && j < hn[r] ? i : -1;
+      v[u] = at[u] >= 0 ? merge_load<SYS>(reinterpret_cast<const uint64_t*>(gath + r * shard_bytes + (size_t)g * gb +
+                                                                               sizeof(CandHdr)) + j)
+                        : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (at[u] >= 0) lk[at[u]] = v[u];
+  }
   uint64_t L = NO_KEY;
   for (int r = 0; r < world; ++r) L = umin64(L, hl[r]);
-  for (int r = 0; r < world; ++r) {
-    const uint64_t* keys = reinterpret_cast<const uint64_t*>(gath + r * shard_bytes + (size_t)g * gb + sizeof(CandHdr));
-    for (int i = tid; i < hn[r]; i += RM_THREADS)
-      lk[r * K + i] = __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
   __syncthreads();
   if (tid < world) cnt[tid] = lds_lower_bound(lk + tid * K, hn[tid], L);   // keys below L
   __syncthreads();
-  int T = 0;
-  for (int r = 0; r < world; ++r) T += cnt[r];
-  uint64_t* dst = reinterpret_cast<uint64_t*>(og + sizeof(CandHdr));
-  for (int r = 0; r < world; ++r)
-    for (int i = tid; i < cnt[r]; i += RM_THREADS) {
-      const uint64_t k = lk[r * K + i];
-      int rank = i;
-      for (int r2 = 0; r2 < world; ++r2)
-        if (r2 != r) rank += lds_lower_bound(lk + r2 * K, cnt[r2], k);
-      if (rank < K) dst[rank] = k;
-      else if (rank == K) newlim = k;
-    }
+  const int c = (K + 1 + world - 1) / world;
+  int T = 0, have = 0;
+  uint64_t U = 0;
+  for (int r = 0; r < world; ++r) {
+    const int hd = min(cnt[r], c);
+    T += cnt[r];
+    have += hd;
+    if (hd > 0) U = umax64(U, lk[r * K + hd - 1]);
+  }
+  if (tid < world)   // the candidates: keys <= U (when the heads hold K + 1 keys), else every key below L
+    mc[tid] = have >= K + 1 ? lds_lower_bound(lk + tid * K, cnt[tid], U + 1) : cnt[tid];
   __syncthreads();
+  int M = 0, mx = 0, mq[RM_MAX_WORLD];
+#pragma unroll
+  for (int q = 0; q < RM_MAX_WORLD; ++q) {
+    mq[q] = q < world ? mc[q] : 0;
+    M += mq[q];
+    mx = max(mx, mq[q]);
+  }
+  int top = 1;   // the largest power of two <= mx (the binary searches' first step)
+  while (top * 2 <= mx) top *= 2;
+  uint64_t* ok = lk + (size_t)world * K;   // the merged list (K + 1 keys: the list and the new limit)
+  for (int t = tid; t < M; t += RM_THREADS) {
+    int r = 0, idx = t;
+    while (idx >= mc[r]) {   // (t < M: some list holds it; LDS, not the register copy: r is not static)
+      idx -= mc[r];
+      ++r;
+    }
+    const uint64_t k = lk[r * K + idx];
+    int pos[RM_MAX_WORLD];
+#pragma unroll
+    for (int q = 0; q < RM_MAX_WORLD; ++q) pos[q] = 0;
+    for (int st = top; st > 0; st >>= 1) {
+#pragma unroll
+      for (int q = 0; q < RM_MAX_WORLD; ++q) {
+        const int p = pos[q] + st;
+        if (q < world && q != r && p <= mq[q] && lk[q * K + p - 1] < k) pos[q] = p;
+      }
+    }
+    int rank = idx;
+#pragma unroll
+    for (int q = 0; q < RM_MAX_WORLD; ++q) rank += pos[q];
+    if (rank <= K) ok[rank] = k;
+  }
+  __syncthreads();
+  const int nout = T < K ? T : K;
+  uint64_t* dst = reinterpret_cast<uint64_t*>(og + sizeof(CandHdr));
+  for (int i = tid; i < nout; i += RM_THREADS) dst[i] = ok[i];
   if (tid == 0) {
-    hp->n = T < K ? T : K;
-    hp->limit = T > K ? newlim : L;
+    hp->n = nout;
+    hp->limit = T > K ? ok[K] : L;
+    if (gen == 0) hp->flags = 0;
   }
   // as write_group: every store has left the CU, the block agrees, then the signal (release)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) __hip_atomic_store(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid == 0 && gen != 0) __hip_atomic_store(&hp->flags, (int32_t)gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+size_t merge_ranked_lds(int world, int K) { return ((size_t)world * K + K + 1) * sizeof(uint64_t); }
+
 hipError_t launch_merge_ranked(hipStream_t s, const uint8_t* gath, int world, int Wg, int K, uint8_t* out, uint32_t gen,
-                               int64_t rank_stride, const uint64_t* xstatus) {
+                               int64_t rank_stride, const uint64_t* xstatus, bool sys_scope) {
   if (Wg <= 0) return hipSuccess;
-  if (world < 1 || world > RM_MAX_WORLD || K < 1 || (int64_t)world * K * 8 > 64 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(merge_ranked_kernel, dim3(Wg), dim3(RM_THREADS), (size_t)world * K * 8, s, gath, world, Wg, K, out,
-                     gen, rank_stride, xstatus);
+  if (world < 1 || world > RM_MAX_WORLD || K < 1 || merge_ranked_lds(world, K) > RM_MAX_LDS) return hipErrorInvalidValue;
+  if (sys_scope)
+    hipLaunchKernelGGL(merge_ranked_kernel<true>, dim3(Wg), dim3(RM_THREADS), merge_ranked_lds(world, K), s, gath, world,
+                       Wg, K, out, gen, rank_stride, xstatus);
+  else
+    hipLaunchKernelGGL(merge_ranked_kernel<false>, dim3(Wg), dim3(RM_THREADS), merge_ranked_lds(world, K), s, gath, world,
+                       Wg, K, out, gen, rank_stride, xstatus);
   return hipGetLastError();
 }
 

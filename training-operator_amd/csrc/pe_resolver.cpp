@@ -429,10 +429,12 @@ void WindowFeed::wait(size_t w) {
         throw std::runtime_error("walk window: group " + std::to_string(w) + " was never signalled");
       }
       if (timeout_s > 0 &&
-          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+        if (on_timeout) on_timeout(timeout_user);
         throw CollectiveTimeout("RCCL window: group " + std::to_string(w) + " not merged within " +
                                 std::to_string(timeout_s) +
                                 " s -- its all-gather is stuck (a peer stalled or was lost; PE_RCCL_TIMEOUT_S)");
+      }
     }
   }
   spin_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -195,8 +195,12 @@ class WindowFeed {
   bool (*idle)(void*) = nullptr;
   void* idle_user = nullptr;
   // > 0: wait() gives up after this many seconds blocked on one group, busy device or not, and
-  // throws CollectiveTimeout (the RCCL transport; the other transports have bounds of their own)
+  // throws CollectiveTimeout (the RCCL transport; the other transports have bounds of their own).
+  // on_timeout(timeout_user), when set, runs first, at the throw site: the engine starts the
+  // communicator's abort there, before the unwinding waits for anything (advice r5)
   double timeout_s = 0;
+  void (*on_timeout)(void*) = nullptr;
+  void* timeout_user = nullptr;
   double spin_ms() const { return spin_ms_; }   // time spent blocked in wait() since reset
  private:
   bool signalled(size_t w) const;
