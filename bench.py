@@ -309,14 +309,17 @@ def agg_profile_ms(src_hash: str):
     return k["total_ns"] / AGG_PROFILE_CALLS / 1e6 if k else None
 
 
-def agg_roofline(in_bytes: int, out_bytes: int, call_ms: float, events_ms: float, profile_ms, pcie):
+def agg_roofline(in_bytes: int, out_bytes: int, call_ms: float, events_ms: float, profile_ms, pcie, wire_bytes=None):
     """Roofline of the 1M-job aggregation call.  The batch crosses PCIe: the packed input host to device
     (a DMA per chunk, pe_engine.cpp) while the kernels write the outputs into pinned memory device to
     host -- the two directions of a full-duplex link, each at the box's measured pinned rate.  The bound
     is the slower direction's time, max(in / h2d, out / d2h) (the input, 3x the output); frac = that
     bound / the whole call's wall time (planning, packing, DMA, kernels, copy-out: what the caller
     waits for).  full_duplex_frac prices (in + out) against h2d + d2h together -- out of reach by
-    construction (<= 0.65 here: the output direction idles 3/4 of the time)."""
+    construction (<= 0.65 here: the output direction idles 3/4 of the time).  wire_bytes: the packed
+    segments that actually crossed (requests narrowed to 32 bits above a per-key shift where that is
+    exact), priced as wire_frac = (wire_bytes / h2d) / call_ms -- the link's busy share; the bound and
+    frac above stay priced on the caller's arrays, so frac can pass 1 when the wire carries less."""
     bound = max(in_bytes / pcie["h2d_gbs"], out_bytes / pcie["d2h_gbs"]) / 1e6 if pcie else None
     ach = in_bytes / (call_ms * 1e-3) / 1e9
     return {"bound": "pcie (host to device: the packed batch)", "kernel": "pe::pg_agg_seg_kernel",
@@ -325,7 +328,9 @@ def agg_roofline(in_bytes: int, out_bytes: int, call_ms: float, events_ms: float
             "peak": pcie["h2d_gbs"] if pcie else None, "frac": bound / call_ms if bound else None,
             "full_duplex_frac": (in_bytes + out_bytes) / (call_ms * 1e-3) / 1e9 / (pcie["h2d_gbs"] + pcie["d2h_gbs"])
             if pcie else None,
-            "hbm_frac": (in_bytes + out_bytes) / (call_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            "hbm_frac": (in_bytes + out_bytes) / (call_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "wire_bytes": wire_bytes,
+            "wire_frac": wire_bytes / pcie["h2d_gbs"] / 1e6 / call_ms if pcie and wire_bytes else None}
 
 
 def greedy_profile(src_hash: str):
@@ -777,6 +782,7 @@ def main(argv=None):
         assert mcall() in (0, -2)
         e0, e1 = ev.create(), ev.create()
         ts, ks = [], []
+        st0 = eng.stats()
         for _ in range(5):
             barrier()
             t0 = time.perf_counter()
@@ -785,6 +791,9 @@ def main(argv=None):
             ev.record(e1, stream)
             ts.append(allmax(time.perf_counter() - t0))
             ks.append(ev.elapsed_ms(e0, e1))
+        st1 = eng.stats()
+        # the packed segments that crossed per call (requests narrowed where exact: pe_kernels.h agg_seg_layout)
+        wire = {k: (st1[k] - st0[k]) / 5 for k in ("agg_wire_bytes", "agg_segments", "agg_narrow_segments")}
         at = float(np.median(ts))
         kms = float(np.median(ks))
         wts = []
@@ -819,7 +828,9 @@ def main(argv=None):
             "pcie_bound_duplex_ms": (max((mb - 38 * (hi_j - lo_j)) / pcie["h2d_gbs"], 38 * (hi_j - lo_j) / pcie["d2h_gbs"])
                                      / 1e6) if pcie else None,
             "roofline": agg_roofline(mb - 38 * (hi_j - lo_j), 38 * (hi_j - lo_j), at * 1e3, kms,
-                                     agg_profile_ms(source_hash(ROOT)), pcie),
+                                     agg_profile_ms(source_hash(ROOT)), pcie, wire["agg_wire_bytes"]),
+            "wire_bytes_per_call": wire["agg_wire_bytes"], "segments_per_call": wire["agg_segments"],
+            "narrowed_segments_per_call": wire["agg_narrow_segments"],
             "note": "latency_us: one pe_pg_min_resources call on the first J jobs (median / p90 of 400, ctypes pointers "
                     "built once; ctypes_call_us = the dispatch cost of an empty ABI call, included); r2_path = the "
                     "round-2 call path (PE_AGG_DEVICE=1: six H2D + four D2H copies + stream sync) on the same box; "

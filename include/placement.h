@@ -162,6 +162,12 @@ typedef struct {
      time it spent merging them on the host (zero-copy windows) */
   double xchg_wait_ms;
   double xchg_merge_ms;
+  /* (ABI 7) aggregation calls above 8192 jobs (the chunked path): segments packed, how many of them crossed with
+     narrowed request records (value >> per-key shift in 32 bits), and the packed bytes that crossed to
+     the device, cumulative */
+  int64_t agg_segments;
+  int64_t agg_narrow_segments;
+  int64_t agg_wire_bytes;
 } pe_stats;
 
 int pe_abi_version(void);

@@ -141,5 +141,9 @@ def test_greedy_and_aggregation_profile_lookups(tmp_path, monkeypatch):
     r = bench.agg_roofline(42_000_000, 14_000_000, 1.5, 1.4, 2.8, {"h2d_gbs": 56.0, "d2h_gbs": 55.0})
     assert r["bound"].startswith("pcie") and abs(r["achieved"] - 28.0) < 1e-9 and abs(r["bound_ms"] - 0.75) < 1e-9
     assert abs(r["frac"] - 0.5) < 1e-9 and abs(r["full_duplex_frac"] - 56.0 / 1.5 / 111.0) < 1e-9
+    assert r["wire_frac"] is None
+    # narrowed requests: 28 MB on the wire at 56 GB/s = 0.5 ms of the 1.5 ms call
+    r = bench.agg_roofline(42_000_000, 14_000_000, 1.5, 1.4, 2.8, {"h2d_gbs": 56.0, "d2h_gbs": 55.0}, 28_000_000)
+    assert abs(r["wire_frac"] - 0.5 / 1.5) < 1e-9 and r["wire_bytes"] == 28_000_000
     r = bench.agg_roofline(42_000_000, 14_000_000, 4.0, 3.9, None, None)
     assert r["call_ms"] == 4.0 and r["frac"] is None and r["peak"] is None

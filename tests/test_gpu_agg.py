@@ -84,6 +84,18 @@ def test_agg_oversized_segments(eng, mode):
         _check(eng, mode, arrs)
 
 
+@pytest.mark.parametrize("mode", [V1, V2])
+def test_agg_chunked_batch_with_oversized_jobs(eng, mode):
+    """Batches above 32k jobs are planned, packed and DMA'd chunk by chunk (the staging sized from a
+    bound before the first chunk is planned): oversized jobs inside and between chunks, and a batch
+    of mostly oversized jobs (the most segments per byte the bound allows for)."""
+    big_c = _one_job_csr(4, 600, 11)
+    big_g = _one_job_csr(9000, 0, 12)
+    _check(eng, mode, _concat([random_csr(40000, 13), big_c, random_csr(20000, 14), big_g, big_c,
+                               random_csr(30000, 15, big=True)]))
+    _check(eng, mode, _concat([big_c] * 40 + [random_csr(33000, 16)] + [big_c] * 40))
+
+
 def test_agg_alternating_calls(eng):
     """Small (flag) and large (stream sync) calls interleaved: buffers grow and are reused, flag
     generations advance."""
@@ -210,3 +222,60 @@ def test_agg_keys_wide_golden(eng, golden_dir):
             assert ovf[j] == int(case.get("overflow", False)), case["name"]
             if not ovf[j]:
                 assert W.same(res[j], W.want_list(want)), (case["name"], res[j])
+
+
+def narrow_values(rng, shape, span_bits, p_zero=0.3):
+    """Request values as canonical quantities come: per key a common power-of-two factor (2^0..2^30) times
+    an integer below 2^span_bits -- a segment's key narrows to 32 bits exactly when its values span <= 32
+    bits above their common trailing zeros."""
+    sh = rng.integers(0, 31, shape[1])
+    v = rng.integers(0, 2**span_bits, shape, dtype=np.int64) << sh
+    v[rng.random(shape) < p_zero] = 0
+    return v
+
+
+@pytest.mark.parametrize("mode", [V1, V2])
+@pytest.mark.parametrize("J", [1, 300, 9000, 40000])
+def test_agg_narrowed_requests(eng, mode, J):
+    """The packed segments carry their requests narrowed (value >> per-key shift in 32 bits) when every
+    key of the segment allows it: values spanning exactly 32 bits, keys that are zero throughout, and
+    segments one 33-bit value keeps wide, on every call path, bit-exact vs the oracle; the chunked path
+    reports narrowed segments in pe_stats."""
+    rng = np.random.default_rng(900 + J + mode)
+    jgo, mm, rep, gco, _, fl = random_csr(J, 910 + J + mode)
+    C = int(gco[-1])
+    req = narrow_values(rng, (C, 4), 32)
+    req[:, 3] = 0                                        # a key absent from every container
+    if C > 0:
+        req[:: max(1, C // 7), 1] = (2**32) << 5         # 33 bits above the shift: that segment stays wide
+        req[0, 0] = (2**32 - 1) << 29                    # exactly 32 bits
+    eng.reset_stats()
+    _check(eng, mode, (jgo, mm, rep, gco, req, fl))
+    st = eng.stats()
+    if J > 8192:
+        assert st["agg_narrow_segments"] > 0 and st["agg_narrow_segments"] < st["agg_segments"], st
+        assert 0 < st["agg_wire_bytes"]
+
+
+@pytest.mark.parametrize("n_keys", [1, 4, 5, 9, 16])
+def test_agg_keys_narrowed(eng, n_keys):
+    """Key tables (4 / 8 / 16-wide kernels) with narrowable values, and with a span of 33 bits."""
+    for span, J in ((32, 40000), (33, 9000), (20, 300)):
+        arrs = list(random_keys_csr(J, n_keys, 60 + n_keys + span))
+        rng = np.random.default_rng(70 + n_keys + span)
+        arrs[4] = narrow_values(rng, arrs[4].shape, span)
+        for mode in (V1, V2):
+            _check_keys(eng, mode, tuple(arrs))
+
+
+def test_agg_realistic_batch_narrowed(eng):
+    """bench.py's batch (synth.make_pg_batch: milli-cpu, memory in MiB multiples, gpu counts): every
+    segment narrowed, the packed batch over a quarter smaller than the caller's arrays."""
+    from placement import synth
+    agg = synth.make_pg_batch(100_000, synth.SEED["cfg3"])
+    eng.reset_stats()
+    _check(eng, V1, agg)
+    st = eng.stats()
+    assert st["agg_narrow_segments"] == st["agg_segments"] > 0, st
+    caller = sum(a.nbytes for a in agg)
+    assert st["agg_wire_bytes"] < 0.75 * caller, (st["agg_wire_bytes"], caller)

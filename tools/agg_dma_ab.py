@@ -3,7 +3,8 @@
 it) under call-path settings, each in a child process (the engine reads PE_AGG_CHUNKS once):
 median of 9 calls after 3 warm-ups, interleaved over 2 reps, beside the box's PCIe rates and the
 batch's bound (max(in / h2d, out / d2h)) and the round-2 path (PE_AGG_DEVICE=1).
-    python tools/agg_dma_ab.py "dma,8" "dma,16" "zc,8" ..."""
+    python tools/agg_dma_ab.py "dma,8" "dma,16" "zc,8" "dma,8,PE_AGG_ONE_PLAN=1" ...
+(a third field: environment settings of that child, K=V joined by +)"""
 import json
 import os
 import subprocess
@@ -31,8 +32,11 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "training-operator_amd")]
 res = {}
 for rep in range(2):
     for cfg in sys.argv[1:] + ["r2,8"]:
-        mode, ch = cfg.split(",")
+        mode, ch, *extra = cfg.split(",")
         env = dict(os.environ, PE_AGG_CHUNKS=ch)
+        for kv in (extra[0].split("+") if extra else []):   # "dma,8,PE_AGG_ONE_PLAN=1+PE_POOL_SPIN_US=0"
+            k, v = kv.split("=")
+            env[k] = v
         env.pop("PE_AGG_ZEROCOPY", None)
         env.pop("PE_AGG_DEVICE", None)
         if mode == "zc":

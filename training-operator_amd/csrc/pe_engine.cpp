@@ -308,6 +308,8 @@ struct AggSeg {
   int64_t j0;
   int32_t nj, ng, nc;
   int64_t bytes;
+  bool narrow;            // the request section narrowed (pe_kernels.h agg_seg_layout), shifts in sh
+  uint8_t sh[pe::AGG_MAX_KEYS];
 };
 
 }  // namespace
@@ -591,6 +593,7 @@ class PlanPool {
         want_ = n - 1;
         left_ = n - 1;
         ++gen_;
+        agen_.store(gen_, std::memory_order_release);
       }
       cv_.notify_all();
       try {
@@ -613,16 +616,35 @@ class PlanPool {
   }
 
  private:
+  // A worker that just finished spins for up to spin_us() before it sleeps on the condition variable:
+  // a chunked call dispatches plan / pack / copy-out back to back (24 dispatches in a 1M-job
+  // aggregation), and a futex wake-up per dispatch cost ~50 us each.
+  static int spin_us() {   // PE_POOL_SPIN_US (0..2000, default 150; A/B)
+    static const int v = [] {
+      const char* e = std::getenv("PE_POOL_SPIN_US");
+      return e ? std::max(0, std::min(2000, std::atoi(e))) : 150;
+    }();
+    return v;
+  }
   void loop(int id) {
     uint64_t seen = 0;
+    bool ran = false;
     for (;;) {
       const std::function<void(int)>* f;
       std::vector<std::exception_ptr>* errs;
+      if (ran && spin_us() > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned i = 1; agen_.load(std::memory_order_acquire) == seen; ++i) {
+          _mm_pause();
+          if ((i & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us())) break;
+        }
+      }
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
-        if (id >= want_) continue;   // not needed for this call
+        ran = id < want_;
+        if (!ran) continue;   // not needed for this call
         f = task_;
         errs = errs_;
       }
@@ -642,6 +664,7 @@ class PlanPool {
   std::vector<std::exception_ptr>* errs_ = nullptr;
   int want_ = 0, left_ = 0;
   uint64_t gen_ = 0;
+  std::atomic<uint64_t> agen_{0};   // gen_, for the spinning workers (written under mu_)
 };
 
 // The first index in [0, n) where bad(i) holds, or n: chunks of 4096 reduced branch-free (the
@@ -1012,6 +1035,29 @@ void agg_device_path(pe_ctx* ctx, int32_t mode, int64_t n_jobs, int64_t G, int64
   hipchk(hipStreamSynchronize(s), "sync pg_min_resources");
 }
 
+// Per-key OR of rows x 4 int64 request records (the narrowing test of a segment, below)
+__attribute__((target("avx2"))) void or_rows4(const int64_t* q, int64_t rows, uint64_t orv[4]) {
+  __m256i a = _mm256_setzero_si256(), b = _mm256_setzero_si256();
+  int64_t r = 0;
+  for (; r + 2 <= rows; r += 2) {
+    a = _mm256_or_si256(a, _mm256_loadu_si256(reinterpret_cast<const __m256i*>(q + r * 4)));
+    b = _mm256_or_si256(b, _mm256_loadu_si256(reinterpret_cast<const __m256i*>(q + r * 4 + 4)));
+  }
+  if (r < rows) a = _mm256_or_si256(a, _mm256_loadu_si256(reinterpret_cast<const __m256i*>(q + r * 4)));
+  _mm256_storeu_si256(reinterpret_cast<__m256i*>(orv), _mm256_or_si256(a, b));
+}
+
+// rows x 4 int64 records -> rows x 4 u32 of value >> sh[key] (the values are known to fit)
+__attribute__((target("avx2"))) void narrow_rows4(uint32_t* dst, const int64_t* q, int64_t rows, const uint8_t sh[4]) {
+  const __m256i vs = _mm256_set_epi64x(sh[3], sh[2], sh[1], sh[0]);
+  const __m256i even = _mm256_set_epi32(7, 5, 3, 1, 6, 4, 2, 0);
+  for (int64_t r = 0; r < rows; ++r) {
+    const __m256i v = _mm256_srlv_epi64(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(q + r * 4)), vs);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + r * 4),
+                     _mm256_castsi256_si128(_mm256_permutevar8x32_epi32(v, even)));
+  }
+}
+
 // dst[0, n) = src[0, n) and the OR of all values (its sign says whether any is negative), in one
 // pass: the aggregation's request records are validated while they are packed.
 __attribute__((target("avx2"))) int64_t copy_or_i64(int64_t* dst, const int64_t* src, int64_t n) {
@@ -1040,11 +1086,12 @@ void ensure_pinned(HostBuf<T>& b, size_t count, const char* what) {
 }
 
 // Call path (pe_kernels.h AggSegHdr): validate + pack the batch into segments of <= 256 jobs in a
-// pinned, device-mapped staging buffer (on the planning pool for large batches), one launch (one
-// block per segment: the segment comes into LDS over PCIe in one round of coalesced 16-B loads),
-// outputs written by the kernel straight into a pinned buffer in the caller's layout, then copied
-// out.  One segment (the operator's per-reconcile call: one job) waits on a flag the kernel stores
-// in pinned memory instead of a stream synchronisation.  No input ever goes through a DMA copy.
+// pinned, device-mapped staging buffer (on the planning pool for large batches), one block per
+// segment (the segment comes into LDS in one round of coalesced 16-B loads), outputs written by the
+// kernel straight into a pinned buffer in the caller's layout, then copied out.  Up to 8192 jobs: one
+// launch reading the pinned segments over PCIe, the host waiting on a flag the kernel stores in pinned
+// memory (the operator's per-reconcile call: one job).  Larger batches: chunks planned, packed, DMA'd
+// to the device and launched one after another (below).
 // ak / n_keys: the fixed four dimensions ({4, 1}, n_keys 4) or a per-call key table of n_keys <= 16
 // keys padded to ak.nd (pe_pg_min_resources_keys); cont_flags / out_present are u8 or u32 / u16.
 int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_keys, const int32_t* job_group_off,
@@ -1111,15 +1158,54 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
       constexpr int64_t kLatJobs = 8192;
       int64_t seg_jobs = n_jobs <= 2048 ? 32 : pe::AGG_SEG_JOBS;   // (8192 jobs: 94 us with 256, 112 with 32)
       if (const char* e = std::getenv("PE_AGG_SEG_JOBS")) seg_jobs = std::max<int64_t>(1, std::min<int64_t>(pe::AGG_SEG_JOBS, std::atoll(e)));
+      // Large batches run in chunks (PE_AGG_CHUNKS, 1..64, default 8): chunk k's segments are planned
+      // and packed by the planning pool while chunk k - 1 crosses PCIe, so the link starts after the
+      // first chunk's plan and pack instead of the whole batch's plan (0.3 ms of a 1M-job call).
+      static const int64_t kChunks = [] {
+        const char* e = std::getenv("PE_AGG_CHUNKS");
+        return e ? std::max<int64_t>(1, std::min<int64_t>(64, std::atoll(e))) : 8;
+      }();
+      const int64_t CH = n_jobs > kLatJobs && T > 1 ? kChunks : 1;
+      // PE_AGG_ONE_PLAN=1 (A/B): the whole batch planned before the first chunk is packed
+      static const bool one_plan = std::getenv("PE_AGG_ONE_PLAN") != nullptr;
       auto& segs = ctx->agg_segs;
       if (segs.size() < (size_t)T) segs.resize((size_t)T);
-      auto plan = [&](int t) {
-        const int64_t ja = n_jobs * t / T, jb = n_jobs * (t + 1) / T;
+      // A segment's requests cross narrowed (pe_kernels.h agg_seg_layout) when every key's values span
+      // <= 32 bits above their common trailing zeros, none is negative, and it saves bytes; else as the
+      // caller's int64 records.  PE_AGG_WIDE=1: never narrowed (A/B).
+      static const bool no_narrow = std::getenv("PE_AGG_WIDE") != nullptr;
+      auto narrow_seg = [&](AggSeg& sg) {
+        sg.narrow = false;
+        if (no_narrow || sg.nc == 0 ||
+            pe::agg_req_bytes(sg.nc, ND, true) >= pe::agg_req_bytes(sg.nc, ND, false))
+          return;
+        const int64_t* q = cont_req + (int64_t)gco[job_group_off[sg.j0]] * n_keys;
+        uint64_t orv[pe::AGG_MAX_KEYS] = {0};
+        if (n_keys == 4) {
+          or_rows4(q, sg.nc, orv);
+        } else {
+          for (int64_t c = 0; c < sg.nc; ++c)
+            for (int k = 0; k < n_keys; ++k) orv[k] |= (uint64_t)q[c * n_keys + k];
+        }
+        for (int k = 0; k < ND; ++k) {
+          const uint64_t v = k < n_keys ? orv[k] : 0;
+          if (v >> 63) return;   // a negative request: the wide pack reports it
+          const int tz = v ? __builtin_ctzll(v) : 0;
+          if (v && 63 - __builtin_clzll(v) - tz > 31) return;
+          sg.sh[k] = (uint8_t)tz;
+        }
+        sg.narrow = true;
+        int64_t off[7];
+        pe::agg_seg_layout(sg.nj, sg.ng, sg.nc, v1, off, ak, true);
+        sg.bytes = off[6];
+      };
+      auto plan = [&](int t, int64_t pa, int64_t pb) {   // thread t's share of jobs [pa, pb)
+        const int64_t ja = pa + (pb - pa) * t / T, jb = pa + (pb - pa) * (t + 1) / T;
         auto& out = segs[(size_t)t];
         out.clear();
         int64_t off[7];
         for (int64_t j = ja; j < jb;) {
-          AggSeg sg{j, 0, 0, 0, 0};
+          AggSeg sg{j, 0, 0, 0, 0, false, {}};
           while (j < jb && sg.nj < seg_jobs) {
             const int64_t g0 = job_group_off[j], g1 = job_group_off[j + 1];
             const int64_t nc = gco ? (int64_t)gco[g1] - gco[g0] : 0;
@@ -1131,20 +1217,45 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
             sg.bytes = off[6];
             ++j;
           }
+          narrow_seg(sg);
           out.push_back(sg);
         }
       };
-      if (T == 1) plan(0);
-      else PlanPool::get().run(T, plan);
-      size_t first[PlanPool::kMax + 1] = {0};
-      for (int t = 0; t < T; ++t) first[t + 1] = first[t] + segs[t].size();
-      const int64_t nseg = (int64_t)first[T];
-      ensure_pinned(ctx->a_segoff, (size_t)nseg + 1, "alloc pinned segment offsets");
-      int64_t* so = ctx->a_segoff.p;
-      so[0] = 0;
-      for (int t = 0, k = 0; t < T; ++t)
-        for (const AggSeg& sg : segs[t]) so[k + 1] = so[k] + sg.bytes, ++k;
-      const int64_t total = so[nseg];
+      auto& all = ctx->agg_all;   // every planned segment so far, in job order
+      all.clear();
+      // chunk c: plan jobs [n c / CH, n (c + 1) / CH), its segments appended to all and their offsets to so
+      int64_t* so = nullptr;
+      auto plan_chunk = [&](int64_t c) {   // (c = -1: every job, in one pass)
+        const int64_t pa = c < 0 ? 0 : n_jobs * c / CH, pb = c < 0 ? n_jobs : n_jobs * (c + 1) / CH;
+        if (T == 1) plan(0, pa, pb);
+        else PlanPool::get().run(T, [&](int t) { plan(t, pa, pb); });
+        const size_t k0 = all.size();
+        for (int t = 0; t < T; ++t) all.insert(all.end(), segs[t].begin(), segs[t].end());
+        if (so)
+          for (size_t k = k0; k < all.size(); ++k) so[k + 1] = so[k] + all[k].bytes;
+      };
+      // Pinned staging sized before the first chunk is planned (a chunked call writes chunk 0 before the
+      // rest is planned): raw section bytes plus at most 8 + 5 x 15 B of padding and a header per
+      // segment; a segment ends at 256 jobs, at a chunk or thread boundary, or where it and the next
+      // job would pass AGG_SEG_BYTES -- each job's bytes are in at most two such sums.
+      const int64_t raw = n_jobs * 8 + G * 8 + C * (8 * ND + ak.fb);
+      const int64_t seg_cap = n_jobs / pe::AGG_SEG_JOBS + 2 * raw / (pe::AGG_SEG_BYTES - 128) + CH * T + 2;
+      const int64_t seg_over = (int64_t)sizeof(pe::AggSegHdr) + 8 + 5 * 15;
+      int64_t nseg = 0, total = 0;
+      if (CH == 1 || one_plan) {
+        plan_chunk(-1);
+        nseg = (int64_t)all.size();
+        ensure_pinned(ctx->a_segoff, (size_t)nseg + 1, "alloc pinned segment offsets");
+        so = ctx->a_segoff.p;
+        so[0] = 0;
+        for (int64_t k = 0; k < nseg; ++k) so[k + 1] = so[k] + all[(size_t)k].bytes;
+        total = so[nseg];
+      } else {
+        ensure_pinned(ctx->a_segoff, (size_t)seg_cap + 1, "alloc pinned segment offsets");
+        so = ctx->a_segoff.p;
+        so[0] = 0;
+        total = raw + seg_cap * seg_over;   // (an upper bound: the staging capacity)
+      }
       int64_t oo[4];
       pe::agg_out_layout(n_jobs, oo, ak);
       const int64_t out_bytes = oo[3] + pe::agg_r16(n_jobs);
@@ -1163,9 +1274,6 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
       }
       const auto tt1 = now();
       // 2. pack (and the negative-request check, on the copied values); 3. launch
-      auto& all = ctx->agg_all;
-      all.clear();
-      for (int t = 0; t < T; ++t) all.insert(all.end(), segs[t].begin(), segs[t].end());
       int64_t bad[PlanPool::kMax];
       std::fill(bad, bad + PlanPool::kMax, INT64_MAX);
       auto pack = [&](int64_t s0, int64_t s1, int64_t& badv) {
@@ -1180,9 +1288,10 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
           const int32_t g0 = job_group_off[sg.j0];
           h.g0 = g0;
           h.c0 = sg.ng > 0 ? gco[g0] : 0;
+          h.narrow = sg.narrow ? 1 : 0;
           std::memcpy(b, &h, sizeof(h));
           int64_t off[7];
-          pe::agg_seg_layout(sg.nj, sg.ng, sg.nc, v1, off, ak);
+          pe::agg_seg_layout(sg.nj, sg.ng, sg.nc, v1, off, ak, sg.narrow);
           // offsets copied as they are (the kernel rebases by h.g0 / h.c0): every section is a memcpy
           std::memcpy(b + off[0], job_group_off + sg.j0, (size_t)(sg.nj + 1) * 4);
           if (v1) std::memcpy(b + off[1], min_member + sg.j0, (size_t)sg.nj * 4);
@@ -1194,7 +1303,20 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
               const int64_t* q = cont_req + (int64_t)c0 * n_keys;
               const int64_t nq = (int64_t)sg.nc * n_keys;
               int64_t any;
-              if (n_keys == ND) {
+              if (sg.narrow) {   // (no negative value: narrow_seg checked)
+                std::memcpy(b + off[4], sg.sh, 16);
+                uint32_t* d = reinterpret_cast<uint32_t*>(b + off[4] + 16);
+                if (n_keys == 4 && ND == 4) {
+                  narrow_rows4(d, q, sg.nc, sg.sh);
+                } else {
+                  for (int32_t c = 0; c < sg.nc; ++c) {
+                    for (int k = 0; k < n_keys; ++k)
+                      d[(int64_t)c * ND + k] = (uint32_t)((uint64_t)q[(int64_t)c * n_keys + k] >> sg.sh[k]);
+                    for (int k = n_keys; k < ND; ++k) d[(int64_t)c * ND + k] = 0;
+                  }
+                }
+                any = 0;
+              } else if (n_keys == ND) {
                 any = copy_or_i64(reinterpret_cast<int64_t*>(b + off[4]), q, nq);   // one pass
               } else {   // a key table narrower than its kernel: rows padded with zeros (never present)
                 int64_t* d = reinterpret_cast<int64_t*>(b + off[4]);
@@ -1260,21 +1382,16 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
           t_wait = std::chrono::duration<double, std::milli>(now() - tw).count();
         }
       } else {
-        // chunks of segments, each packed by the planning pool and launched at once: chunk k's
-        // segments cross PCIe while the host packs chunk k + 1, and chunk k - 1's outputs are copied
-        // out once its kernel is done (an event per chunk).  The input crosses as one DMA per chunk
-        // (a copy engine on its own stream, pinned -> device; the chunk's kernel waits on its event and
-        // reads the segments from HBM): the copy engine streams the link at its rate, where the kernels'
-        // own zero-copy reads reached ~2/3 of it beside their output writes (round 5: 3.35 ms of kernel
-        // for a 2.2 ms input stream).  Outputs stay zero-copy writes into pinned memory: the link's
-        // other direction.  PE_AGG_ZEROCOPY=1: the kernels read the pinned batch directly (A/B).
-        static const int64_t kChunks = [] {   // PE_AGG_CHUNKS (1..64, default 8): pipeline depth
-          const char* e = std::getenv("PE_AGG_CHUNKS");
-          return e ? std::max<int64_t>(1, std::min<int64_t>(64, std::atoll(e))) : 8;
-        }();
-        const int64_t C = T == 1 ? 1 : kChunks;
+        // chunks of segments, each planned and packed by the planning pool and launched at once: chunk
+        // k's segments cross PCIe while the host plans and packs chunk k + 1, and chunk k - 1's outputs
+        // are copied out once its kernel is done (an event per chunk).  The input crosses as one DMA per
+        // chunk (a copy engine on its own stream, pinned -> device; the chunk's kernel waits on its event
+        // and reads the segments from HBM): the copy engine streams the link at its rate, where the
+        // kernels' own zero-copy reads reached ~2/3 of it beside their output writes (round 5: 3.35 ms
+        // of kernel for a 2.2 ms input stream).  Outputs stay zero-copy writes into pinned memory: the
+        // link's other direction.  PE_AGG_ZEROCOPY=1: the kernels read the pinned batch directly (A/B).
         const bool dma = !std::getenv("PE_AGG_ZEROCOPY");
-        while ((int64_t)ctx->a_ev.size() < C) {
+        while ((int64_t)ctx->a_ev.size() < CH) {
           hipEvent_t e;
           hipchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
           ctx->a_ev.push_back(e);
@@ -1282,7 +1399,7 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
         if (dma) {
           hipchk(ctx->a_dstage.ensure((size_t)total), "alloc device aggregation batch");
           if (!ctx->a_h2d) hipchk(hipStreamCreateWithFlags(&ctx->a_h2d, hipStreamNonBlocking), "stream");
-          while ((int64_t)ctx->a_ev_h2d.size() < C) {
+          while ((int64_t)ctx->a_ev_h2d.size() < CH) {
             hipEvent_t e;
             hipchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
             ctx->a_ev_h2d.push_back(e);
@@ -1291,10 +1408,15 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
         const uint8_t* const blob = dma ? ctx->a_dstage.p : ctx->a_stage.dev;
         int64_t prev_s0 = -1, prev_s1 = -1, prev_c = -1;   // prev_c: event of the last launched chunk
         auto job_end = [&](int64_t s1) { return all[(size_t)s1 - 1].j0 + all[(size_t)s1 - 1].nj; };
-        for (int64_t c = 0; c < C && first_neg == INT64_MAX; ++c) {
-          const int64_t s0 = nseg * c / C, s1 = nseg * (c + 1) / C;
-          if (s1 == s0) continue;
+        for (int64_t c = 0; c < CH && first_neg == INT64_MAX; ++c) {
           const auto tp = now();
+          const bool planned = CH == 1 || one_plan;   // (every chunk planned above)
+          const int64_t s0 = planned ? nseg * c / CH : (int64_t)all.size();
+          if (!planned) plan_chunk(c);
+          const int64_t s1 = planned ? nseg * (c + 1) / CH : (int64_t)all.size();
+          if (!planned && (s1 > seg_cap || so[s1] > total))   // (the bounds above hold by construction)
+            raise(PE_ENOMEM, "aggregation staging bound exceeded");
+          if (s1 == s0) continue;
           if (T == 1) pack(s0, s1, bad[0]);
           else PlanPool::get().run(T, [&](int t) { pack(s0 + (s1 - s0) * t / T, s0 + (s1 - s0) * (t + 1) / T, bad[t]); });
           t_pack += std::chrono::duration<double, std::milli>(now() - tp).count();
@@ -1321,7 +1443,11 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
           prev_s1 = s1;
           prev_c = c;
         }
-        hipchk(hipStreamSynchronize(ctx->stream), "sync pg_agg_segments");   // (also before an EINVAL:
+        nseg = (int64_t)all.size();
+        hipchk(hipStreamSynchronize(ctx->stream), "sync pg_agg_segments");
+        ctx->stats.agg_segments += nseg;
+        ctx->stats.agg_wire_bytes += nseg > 0 ? so[nseg] : 0;
+        for (int64_t k = 0; k < nseg; ++k) ctx->stats.agg_narrow_segments += all[(size_t)k].narrow ? 1 : 0;   // (also before an EINVAL:
                                                                              // launched chunks read the batch)
       }
       if (first_neg != INT64_MAX) raise(PE_EINVAL, "cont_req: negative request at index " + std::to_string(first_neg));

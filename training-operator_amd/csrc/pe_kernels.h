@@ -72,7 +72,7 @@ struct AggSegHdr {
   int32_t nj, ng, nc;    // jobs, groups, containers
   int32_t g0, c0;        // the segment's first group / container: its jgo / gco sections hold the caller's
                          // absolute offsets (copied as they are), the kernel rebases
-  int32_t pad_;
+  int32_t narrow;        // 1: the request section is narrowed (agg_seg_layout), 0: nc x nd i64
 };
 static_assert(sizeof(AggSegHdr) == 32, "AggSegHdr must be 32 B");
 __host__ __device__ inline int64_t agg_r16(int64_t x) { return (x + 15) & ~int64_t(15); }
@@ -87,15 +87,22 @@ struct AggKeys {
 constexpr int AGG_MAX_KEYS = 16;
 // byte offsets of the sections in a segment: [0] jgo (nj+1 i32, absolute group ids), [1] min_member
 // (nj i32, V1 only), [2] replicas (ng i32), [3] gco (ng+1 i32, absolute container ids), [4] req
-// (nc x nd i64), [5] flags (nc x fb), [6] = size
+// (nc x nd i64; narrowed: 16 shift bytes, then nc x nd u32), [5] flags (nc x fb), [6] = size.
+// A narrowed request section holds value >> shift[key] in 32 bits, shift[key] = the fewest trailing
+// zero bits of the key's values in the segment -- exact whenever every value of a key spans <= 32 bits
+// above its shift (quantities in canonical units are: milli-cpu, memory in multiples of 2^k bytes),
+// and half the bytes over PCIe.  The host narrows a segment only when it can, and when it pays.
+__host__ __device__ inline int64_t agg_req_bytes(int64_t nc, int nd, bool narrow) {
+  return narrow ? 16 + agg_r16(nc * 4 * nd) : nc * 8 * nd;
+}
 __host__ __device__ inline void agg_seg_layout(int64_t nj, int64_t ng, int64_t nc, bool v1, int64_t off[7],
-                                               AggKeys ak = AggKeys{}) {
+                                               AggKeys ak = AggKeys{}, bool narrow = false) {
   off[0] = (int64_t)sizeof(AggSegHdr);
   off[1] = off[0] + agg_r16((nj + 1) * 4);
   off[2] = off[1] + (v1 ? agg_r16(nj * 4) : 0);
   off[3] = off[2] + agg_r16(ng * 4);
   off[4] = off[3] + agg_r16((ng + 1) * 4);
-  off[5] = off[4] + nc * 8 * ak.nd;
+  off[5] = off[4] + agg_req_bytes(nc, ak.nd, narrow);
   off[6] = off[5] + agg_r16(nc * ak.fb);
 }
 // Output buffer layout (the caller's arrays back to back): res [J][nd] i64, members [J] i32,

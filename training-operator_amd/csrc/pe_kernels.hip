@@ -45,9 +45,25 @@ struct AggJob {
   bool ovf;
 };
 
-template <int ND, typename FT>
+// Request readers: container c's value of key d.  ReqWide: the caller's int64 records; ReqNarrow: a
+// narrowed segment section (pe_kernels.h agg_seg_layout), value = u32 << shift[d].
+template <int ND>
+struct ReqWide {
+  const int64_t* p;
+  __device__ __forceinline__ int64_t operator()(int64_t c, int d) const { return p[c * ND + d]; }
+};
+template <int ND>
+struct ReqNarrow {
+  const uint32_t* p;
+  const uint8_t* sh;
+  __device__ __forceinline__ int64_t operator()(int64_t c, int d) const {
+    return (int64_t)((uint64_t)p[c * ND + d] << sh[d]);
+  }
+};
+
+template <int ND, typename FT, typename RV = ReqWide<ND>>
 __device__ __forceinline__ AggJob<ND> agg_job_t(int mode, int32_t mm, int32_t g0, int32_t g1, const int32_t* rep,
-                                                const int32_t* gco, const int64_t* req, const FT* fl) {
+                                                const int32_t* gco, const RV req, const FT* fl) {
   constexpr int KS = sizeof(FT) == 1 ? 4 : 16;   // kind shift
   AggJob<ND> o;
 #pragma unroll
@@ -80,7 +96,7 @@ __device__ __forceinline__ AggJob<ND> agg_job_t(int mode, int32_t mm, int32_t g0
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
         if (!(f & (1u << d))) continue;
-        const int64_t v = req[(int64_t)c * ND + d];
+        const int64_t v = req(c, d);
         pp |= 1u << d;
         if (kind == 0) o.ovf |= add_ovf(main_[d], v, &main_[d]);
         else if (kind == 2) o.ovf |= add_ovf(side[d], v, &side[d]);
@@ -109,7 +125,7 @@ __device__ __forceinline__ AggJob<ND> agg_job_t(int mode, int32_t mm, int32_t g0
 
 __device__ __forceinline__ AggJob<D> agg_job(int mode, int32_t mm, int32_t g0, int32_t g1, const int32_t* rep,
                                              const int32_t* gco, const int64_t* req, const uint8_t* fl) {
-  return agg_job_t<D, uint8_t>(mode, mm, g0, g1, rep, gco, req, fl);
+  return agg_job_t<D, uint8_t>(mode, mm, g0, g1, rep, gco, ReqWide<D>{req}, fl);
 }
 
 __global__ __launch_bounds__(256) void pg_min_resources_kernel(
@@ -163,17 +179,24 @@ __device__ __forceinline__ void agg_segment(int mode, const uint8_t* seg, int64_
   const AggSegHdr h = *reinterpret_cast<const AggSegHdr*>(seg);
   const AggKeys ak{ND, (int)sizeof(FT)};
   int64_t off[7];
-  agg_seg_layout(h.nj, h.ng, h.nc, mode == 1, off, ak);
+  agg_seg_layout(h.nj, h.ng, h.nc, mode == 1, off, ak, h.narrow != 0);
   const int t = threadIdx.x;
   if (t < h.nj) {
     const int32_t* jgo = reinterpret_cast<const int32_t*>(seg + off[0]);
     const int32_t mm = mode == 1 ? reinterpret_cast<const int32_t*>(seg + off[1])[t] : 0;
     // the offsets are the caller's (absolute): rebase the group and container sections instead
-    const AggJob<ND> o = agg_job_t<ND, FT>(mode, mm, jgo[t] - h.g0, jgo[t + 1] - h.g0,
-                                           reinterpret_cast<const int32_t*>(seg + off[2]),
-                                           reinterpret_cast<const int32_t*>(seg + off[3]),
-                                           reinterpret_cast<const int64_t*>(seg + off[4]) - (int64_t)h.c0 * ND,
-                                           reinterpret_cast<const FT*>(seg + off[5]) - h.c0);
+    const int32_t* rep = reinterpret_cast<const int32_t*>(seg + off[2]);
+    const int32_t* gco = reinterpret_cast<const int32_t*>(seg + off[3]);
+    const FT* fl = reinterpret_cast<const FT*>(seg + off[5]) - h.c0;
+    const AggJob<ND> o =
+        h.narrow ? agg_job_t<ND, FT>(mode, mm, jgo[t] - h.g0, jgo[t + 1] - h.g0, rep, gco,
+                                     ReqNarrow<ND>{reinterpret_cast<const uint32_t*>(seg + off[4] + 16) -
+                                                       (int64_t)h.c0 * ND,
+                                                   seg + off[4]},
+                                     fl)
+                 : agg_job_t<ND, FT>(mode, mm, jgo[t] - h.g0, jgo[t + 1] - h.g0, rep, gco,
+                                     ReqWide<ND>{reinterpret_cast<const int64_t*>(seg + off[4]) - (int64_t)h.c0 * ND},
+                                     fl);
     int64_t oo[4];
     agg_out_layout(J, oo, ak);
     const int64_t j = h.j0 + t;

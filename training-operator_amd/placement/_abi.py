@@ -50,7 +50,9 @@ class PeStats(ctypes.Structure):
                 ("walk_overlay", ctypes.c_int64), ("walk_groups", ctypes.c_int64), ("walk_prepass", ctypes.c_int64),
                 ("walk_ms", ctypes.c_double), ("walk_pend_updates", ctypes.c_int64),
                 ("xchg_zc_windows", ctypes.c_int64), ("xchg_wait_ms", ctypes.c_double),
-                ("xchg_merge_ms", ctypes.c_double)]
+                ("xchg_merge_ms", ctypes.c_double),
+                ("agg_segments", ctypes.c_int64), ("agg_narrow_segments", ctypes.c_int64),
+                ("agg_wire_bytes", ctypes.c_int64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
