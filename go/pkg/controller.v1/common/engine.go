@@ -32,6 +32,7 @@ import (
 	apiv1 "github.com/kubeflow/training-operator/pkg/apis/kubeflow.org/v1"
 	"github.com/kubeflow/training-operator/pkg/placement/hip"
 	v1 "k8s.io/api/core/v1"
+	"k8s.io/apimachinery/pkg/api/resource"
 )
 
 // flattenV1 builds the one-job v1 CSR of CalcPGMinResources(minMember, replicas, pcGetFunc), and the
@@ -100,9 +101,36 @@ func effectiveList(c v1.Container) v1.ResourceList {
 }
 
 // EngineErrors counts the engine failures (PE_EHIP, PE_ENODEV, a lost device ...) the v1-signature
-// adapter below could not return to its caller.  Monitor it: every count is a PodGroup written with an
-// empty MinResources and a log line, never an answer computed some other way.
+// adapter below could not return to its caller.  Monitor it: every count is a log line and a PodGroup
+// written with EngineErrorMinResources' answer, never an answer computed some other way.
 var EngineErrors uint64
+
+// EngineErrorResource is the resource the fail-closed answer asks for: no node offers it, so a gang
+// scheduler that checks MinResources admits no gang of that PodGroup until a later reconcile (the
+// operator resyncs, and SyncPodGroup always rewrites the PodGroup, job.go:308-313) computes the real
+// minimum.
+const EngineErrorResource v1.ResourceName = "placement.kubeflow.org/engine-error"
+
+// EngineErrorMinResources is what CalcPGMinResourcesEngine answers for a job whose aggregation failed
+// in the engine.  Default FailClosed: {EngineErrorResource: 1}, a minimum no cluster meets -- the gang
+// waits instead of being admitted unchecked.  FailOpen (opt-in): an empty list, i.e. no minimum (the
+// gang scheduler then checks nothing and may admit a gang that does not fit).  Production wiring
+// returns the error instead: CalcPGMinResourcesEngineE or PGMinResourcesBatch (INTEGRATION.md section 2).
+type EngineErrorPolicy int
+
+const (
+	FailClosed EngineErrorPolicy = iota
+	FailOpen
+)
+
+var EngineErrorMinResources = FailClosed
+
+func engineErrorAnswer() *v1.ResourceList {
+	if EngineErrorMinResources == FailOpen {
+		return &v1.ResourceList{}
+	}
+	return &v1.ResourceList{EngineErrorResource: *resource.NewQuantity(1, resource.DecimalSI)}
+}
 
 // CalcPGMinResourcesEngineE is CalcPGMinResources with the pod counting and the resource sums on the
 // GPU, and the engine's failures returned.  Only an int64 OVERFLOW goes to the reference's
@@ -133,9 +161,10 @@ func CalcPGMinResourcesEngineE(eng *hip.Engine, gpuName string) func(int32, map[
 
 // CalcPGMinResourcesEngine keeps util.go:108's signature (no error result) for a one-line swap of
 // jc.calcPGMinResourcesFn.  Like the reference it never returns nil.  An engine error cannot be
-// returned through that signature, so it is counted in EngineErrors, logged, and answered with an
-// EMPTY list (the gang scheduler then checks no minimum) -- not with the reference's CPU result.
-// Wire CalcPGMinResourcesEngineE instead where job.go can return the error (INTEGRATION.md section 2).
+// returned through that signature, so it is counted in EngineErrors, logged, and answered per
+// EngineErrorMinResources -- by default a minimum no node meets (fail closed), an empty list only when
+// FailOpen is chosen -- never with the reference's CPU result.  Wire CalcPGMinResourcesEngineE instead
+// where job.go can return the error (INTEGRATION.md section 2).
 func CalcPGMinResourcesEngine(eng *hip.Engine, gpuName string) func(int32, map[apiv1.ReplicaType]*apiv1.ReplicaSpec,
 	PriorityClassGetFunc) *v1.ResourceList {
 	calc := CalcPGMinResourcesEngineE(eng, gpuName)
@@ -143,9 +172,9 @@ func CalcPGMinResourcesEngine(eng *hip.Engine, gpuName string) func(int32, map[a
 		rl, err := calc(minMember, replicas, pcGetFunc)
 		if err != nil {
 			atomic.AddUint64(&EngineErrors, 1)
-			log.Errorf("CalcPGMinResources: %v (PodGroup MinResources left empty; EngineErrors=%d)", err,
-				atomic.LoadUint64(&EngineErrors))
-			return &v1.ResourceList{}
+			log.Errorf("CalcPGMinResources: %v (PodGroup MinResources answered per EngineErrorMinResources=%d; "+
+				"EngineErrors=%d)", err, EngineErrorMinResources, atomic.LoadUint64(&EngineErrors))
+			return engineErrorAnswer()
 		}
 		return rl
 	}

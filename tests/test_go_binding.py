@@ -108,7 +108,10 @@ def test_cgo_preamble_and_package():
              "func PGMinResourcesBatch(", "batch.AppendJobs(csr)", "agg.Unflatten(i, formats[i].Formats())",
              # engine errors are returned (E form, batch) or counted + logged, never answered by the reference
              "func CalcPGMinResourcesEngineE(", "var EngineErrors uint64", "atomic.AddUint64(&EngineErrors, 1)",
-             "return nil, fmt.Errorf(\"placement engine: CalcPGMinResources: %w\", err)"]),
+             "return nil, fmt.Errorf(\"placement engine: CalcPGMinResources: %w\", err)",
+             # the signature-preserving form fails CLOSED by default (advice r5): a minimum no node meets
+             "var EngineErrorMinResources = FailClosed", "return engineErrorAnswer()",
+             "EngineErrorResource: *resource.NewQuantity(1, resource.DecimalSI)"]),
     (FLATTEN_GO, ["type FormatAcc struct", "func (a *FormatAcc) Add(", "func (a *FormatAcc) Formats()",
                   "if !a.nonzero[d] {", "func (b *CSR) AppendJobs(o *CSR)", "BatchCrossoverJobs",
                   # key tables (ABI 7): any key, per-key decimal scale, key ids remapped on append
