@@ -174,7 +174,7 @@ static inline uint64_t key_bf(int64_t x0, int64_t x1, int64_t x2, int64_t x3, ui
 }
 
 void DirtySet::keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
-                    std::vector<int32_t>& idx) const {   // limit: keys >= it may be left out
+                    IdxVec& idx) const {   // limit: keys >= it may be left out
   const size_t n = n_;
   if (out.size() < n) out.resize(n);   // only the slots listed in idx are read
   idx.clear();
@@ -224,7 +224,10 @@ __attribute__((target("avx512f,avx512dq,avx512vl,avx512bw"))) static uint64_t ke
     const __mmask8 m = n - i >= 8 ? (__mmask8)0xFF : (__mmask8)((1u << (n - i)) - 1);
     const __m512i k = _mm512_maskz_loadu_epi64(m, kn + i);
     __mmask8 fit = m & (_mm512_cmplt_epu64_mask(_mm512_sub_epi64(k, vlo), vspan) | _mm512_cmpeq_epi64_mask(k, ones));
-    if (!fit) continue;   // (out is read at the slots listed in idx only)
+    // (out is read at the slots listed in idx only.  Measured in the box replay, round 6: scoring every
+    // group without this skip, +20 %; a range pass compacting the hits, then the hits through
+    // gathers, +15 % -- ~9.6 of ~235 dirty nodes pass the range test per group)
+    if (!fit) continue;
     const __m512i x0 = _mm512_maskz_loadu_epi64(m, x0p + i), x1 = _mm512_maskz_loadu_epi64(m, x1p + i),
                   x2 = _mm512_maskz_loadu_epi64(m, x2p + i), x3 = _mm512_maskz_loadu_epi64(m, x3p + i);
     const __m512i l = _mm512_cvtepu32_epi64(_mm256_maskz_loadu_epi32(m, lab + i));
@@ -249,7 +252,7 @@ __attribute__((target("avx512f,avx512dq,avx512vl,avx512bw"))) static uint64_t ke
 }
 
 uint64_t DirtySet::keys_all(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
-                            std::vector<int32_t>& idx) const {
+                            IdxVec& idx) const {
   // PE_NO_AVX512=1 forces the AVX2 path (tests cover both)
   static const bool avx512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") &&
                              __builtin_cpu_supports("avx512vl") && __builtin_cpu_supports("avx512bw") &&
@@ -259,7 +262,7 @@ uint64_t DirtySet::keys_all(const int64_t q[RD], uint32_t need, uint64_t limit, 
   if (!avx512) {
     keys(q, need, limit, out, idx);
     uint64_t mk = kNoKey;
-    std::vector<int32_t> fit;
+    IdxVec fit;
     for (int32_t j : idx)
       if (out[j] != kNoKey) fit.push_back(j);
     std::vector<uint8_t> seen(n, 0);
@@ -522,7 +525,7 @@ int l3_pick(const cpu_set_t& allowed, int k) {
 }
 
 void SeedScorer::compute(const DirtySet& seeds, const GroupCands& gc, const int64_t q[RD], uint32_t need,
-                         SeedTop& top, std::vector<uint64_t>& out, std::vector<int32_t>& idx) {
+                         SeedTop& top, std::vector<uint64_t>& out, IdxVec& idx) {
   size_t h = 0;   // (plain key arrays only: a lazily merged shard list is the resolver's to read)
   if (gc.keys)
     while (h < gc.size() && seeds.contains((int64_t)(gc.keys[h] & 0xFFFFFFull))) ++h;
@@ -924,7 +927,7 @@ bool Resolver::resolve(const std::vector<int32_t>& groups, const std::vector<Gro
         __builtin_prefetch(&mirror_.nodes[cands[w].key(i) & 0xFFFFFFull]);
   size_t wi = 0;
   std::vector<uint64_t>& dk = dk_;  // keys of the dirty nodes for the current group
-  std::vector<int32_t>& dki = dki_;  // the slots among them that can hold a key
+  IdxVec& dki = dki_;  // the slots among them that can hold a key
   auto argmin = [&dk, &dki]() -> int32_t {
     int32_t b = -1;
     uint64_t bk = kNoKey;

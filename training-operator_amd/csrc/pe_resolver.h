@@ -278,6 +278,28 @@ class IdMap {
   size_t mask_ = 0, n_ = 0;
 };
 
+// A vector whose resize() leaves new elements uninitialised: the key scans write every slot they
+// report, and re-growing the slot list to the dirty set's size zero-filled ~1 KB per group.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+using IdxVec = std::vector<int32_t, NoInitAlloc<int32_t>>;
+
 // Nodes modified since the window's snapshot, as flat struct-of-arrays so the per-group re-score
 // is one branch-free (vectorisable) loop; gid -> slot is a small hash map.  The columns share one
 // allocation, one count and one capacity: an append is one capacity test and seven stores (seven
@@ -310,14 +332,13 @@ class DirtySet {
   // >= `limit` may be reported as NO_KEY: a node whose node-only key K(n) (below) rules out a key
   // < limit is not scored (K(n) >= (s(q) << 24) for a fit, key >= K(n) - ((s(q) + 2) << 24)).
   // `idx` receives the slots that were scored (the rest are NO_KEY in out).
-  void keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
-            std::vector<int32_t>& idx) const;
+  void keys(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out, IdxVec& idx) const;
   // the fitting slots' keys for (q, need): their slots -> idx, their keys -> out at those slots
   // (out elsewhere is left as it was; the K(n) range test above leaves out nodes that cannot have a
   // key < limit); returns the smallest.  AVX-512 where the CPU has it (8 nodes per step), else
   // keys() + a scalar pass.
   uint64_t keys_all(const int64_t q[RD], uint32_t need, uint64_t limit, std::vector<uint64_t>& out,
-                    std::vector<int32_t>& idx) const;
+                    IdxVec& idx) const;
   uint64_t key_at(int32_t i, const int64_t q[RD], uint32_t need) const;
   // the columns, size() entries each
   int64_t *gid = nullptr, *r0 = nullptr, *r1 = nullptr, *r2 = nullptr, *r3 = nullptr;
@@ -374,7 +395,7 @@ class SeedScorer {
   void pin(const cpu_set_t& set);
   // one group's top (any thread; out / idx are the caller's scratch)
   static void compute(const DirtySet& seeds, const GroupCands& gc, const int64_t q[RD], uint32_t need, SeedTop& top,
-                      std::vector<uint64_t>& out, std::vector<int32_t>& idx);
+                      std::vector<uint64_t>& out, IdxVec& idx);
 
  private:
   void loop();
@@ -414,7 +435,7 @@ class SeedScorer {
   const int64_t* req_ = nullptr;
   const uint32_t* need_ = nullptr;
   std::vector<uint64_t> out_;
-  std::vector<int32_t> idx_;
+  IdxVec idx_;
 };
 
 class Resolver {
@@ -479,7 +500,7 @@ class Resolver {
   // window state
   DirtySet dirty_;
   std::vector<uint64_t> dk_;
-  std::vector<int32_t> dki_;   // dirty slots with a key for the current group (argmin runs over these)
+  IdxVec dki_;   // dirty slots with a key for the current group (argmin runs over these)
   std::vector<size_t> head_;   // per window group: its list's first entry not known to be dirty
   // pipelined windows: the seeds live here (not in dirty_, which then holds the window's own
   // changes only); their per-group keys come from the scorer's helper thread
@@ -501,7 +522,7 @@ class Resolver {
     return w < any_.size() && (any_[w] >> (g & 63) & 1);
   }
   std::vector<uint64_t> sk_out_;
-  std::vector<int32_t> sk_idx_;
+  IdxVec sk_idx_;
   std::vector<uint64_t> sfull_;      // a group's every seed key below the limit (truncated top)
   SeedScorer scorer_;                // declared after what its thread reads: stopped first
   // A failed job's nodes are restored from their CURRENT states, looked up only then (rollbacks are
