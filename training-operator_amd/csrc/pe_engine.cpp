@@ -1048,24 +1048,46 @@ __attribute__((target("avx2"))) void or_rows4(const int64_t* q, int64_t rows, ui
 }
 
 // rows x 4 int64 records -> rows x 4 u32 of value >> sh[key] (the values are known to fit)
+// NT: non-temporal stores (dst 16-B aligned): the staging buffer is written once and read by the DMA
+// engine, so no line of it is read for ownership first (the pack's host-memory traffic is otherwise
+// read + RFO + write)
+template <bool NT>
 __attribute__((target("avx2"))) void narrow_rows4(uint32_t* dst, const int64_t* q, int64_t rows, const uint8_t sh[4]) {
   const __m256i vs = _mm256_set_epi64x(sh[3], sh[2], sh[1], sh[0]);
   const __m256i even = _mm256_set_epi32(7, 5, 3, 1, 6, 4, 2, 0);
   for (int64_t r = 0; r < rows; ++r) {
     const __m256i v = _mm256_srlv_epi64(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(q + r * 4)), vs);
-    _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + r * 4),
-                     _mm256_castsi256_si128(_mm256_permutevar8x32_epi32(v, even)));
+    const __m128i lo = _mm256_castsi256_si128(_mm256_permutevar8x32_epi32(v, even));
+    if constexpr (NT) _mm_stream_si128(reinterpret_cast<__m128i*>(dst + r * 4), lo);
+    else _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + r * 4), lo);
   }
+}
+
+// memcpy into a 16-B aligned staging section with non-temporal stores (whole 16-B chunks; the tail
+// with plain stores)
+__attribute__((target("avx2"))) void nt_copy(void* dst, const void* src, size_t bytes) {
+  uint8_t* d = static_cast<uint8_t*>(dst);
+  const uint8_t* s = static_cast<const uint8_t*>(src);
+  size_t i = 0;
+  for (; i + 16 <= bytes; i += 16)
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i), _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i)));
+  if (i < bytes) std::memcpy(d + i, s + i, bytes - i);
 }
 
 // dst[0, n) = src[0, n) and the OR of all values (its sign says whether any is negative), in one
 // pass: the aggregation's request records are validated while they are packed.
+template <bool NT>
 __attribute__((target("avx2"))) int64_t copy_or_i64(int64_t* dst, const int64_t* src, int64_t n) {
   __m256i acc = _mm256_setzero_si256();
   int64_t i = 0;
   for (; i + 4 <= n; i += 4) {
     const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
-    _mm256_storeu_si256(reinterpret_cast<__m256i*>(dst + i), v);
+    if constexpr (NT) {   // (dst 16-B aligned: two 16-B streams)
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), _mm256_castsi256_si128(v));
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 2), _mm256_extracti128_si256(v, 1));
+    } else {
+      _mm256_storeu_si256(reinterpret_cast<__m256i*>(dst + i), v);
+    }
     acc = _mm256_or_si256(acc, v);
   }
   alignas(32) int64_t lanes[4];
@@ -1276,7 +1298,16 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
       // 2. pack (and the negative-request check, on the copied values); 3. launch
       int64_t bad[PlanPool::kMax];
       std::fill(bad, bad + PlanPool::kMax, INT64_MAX);
+      // non-temporal stores for the request records of large calls (PE_AGG_NO_NT=1: plain stores, A/B)
+      static const bool nt_env = std::getenv("PE_AGG_NO_NT") == nullptr;
+      const bool nt = nt_env && n_jobs > kLatJobs;
       auto pack = [&](int64_t s0, int64_t s1, int64_t& badv) {
+        struct Fence {   // the streamed lines are globally visible before the pack returns (the DMA reads them)
+          bool on;
+          ~Fence() {
+            if (on) _mm_sfence();
+          }
+        } fence{nt};
         for (int64_t k = s0; k < s1; ++k) {
           const AggSeg& sg = all[(size_t)k];
           uint8_t* b = ctx->a_stage.p + so[k];
@@ -1293,12 +1324,16 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
           int64_t off[7];
           pe::agg_seg_layout(sg.nj, sg.ng, sg.nc, v1, off, ak, sg.narrow);
           // offsets copied as they are (the kernel rebases by h.g0 / h.c0): every section is a memcpy
-          std::memcpy(b + off[0], job_group_off + sg.j0, (size_t)(sg.nj + 1) * 4);
-          if (v1) std::memcpy(b + off[1], min_member + sg.j0, (size_t)sg.nj * 4);
+          auto copy = [nt](void* d, const void* src, size_t bytes) {
+            if (nt) nt_copy(d, src, bytes);
+            else std::memcpy(d, src, bytes);
+          };
+          copy(b + off[0], job_group_off + sg.j0, (size_t)(sg.nj + 1) * 4);
+          if (v1) copy(b + off[1], min_member + sg.j0, (size_t)sg.nj * 4);
           if (sg.ng > 0) {
-            std::memcpy(b + off[2], group_replicas + g0, (size_t)sg.ng * 4);
+            copy(b + off[2], group_replicas + g0, (size_t)sg.ng * 4);
             const int32_t c0 = h.c0;
-            std::memcpy(b + off[3], gco + g0, (size_t)(sg.ng + 1) * 4);
+            copy(b + off[3], gco + g0, (size_t)(sg.ng + 1) * 4);
             if (sg.nc > 0) {
               const int64_t* q = cont_req + (int64_t)c0 * n_keys;
               const int64_t nq = (int64_t)sg.nc * n_keys;
@@ -1307,7 +1342,8 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
                 std::memcpy(b + off[4], sg.sh, 16);
                 uint32_t* d = reinterpret_cast<uint32_t*>(b + off[4] + 16);
                 if (n_keys == 4 && ND == 4) {
-                  narrow_rows4(d, q, sg.nc, sg.sh);
+                  if (nt) narrow_rows4<true>(d, q, sg.nc, sg.sh);
+                  else narrow_rows4<false>(d, q, sg.nc, sg.sh);
                 } else {
                   for (int32_t c = 0; c < sg.nc; ++c) {
                     for (int k = 0; k < n_keys; ++k)
@@ -1317,7 +1353,8 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
                 }
                 any = 0;
               } else if (n_keys == ND) {
-                any = copy_or_i64(reinterpret_cast<int64_t*>(b + off[4]), q, nq);   // one pass
+                any = nt ? copy_or_i64<true>(reinterpret_cast<int64_t*>(b + off[4]), q, nq)   // one pass
+                         : copy_or_i64<false>(reinterpret_cast<int64_t*>(b + off[4]), q, nq);
               } else {   // a key table narrower than its kernel: rows padded with zeros (never present)
                 int64_t* d = reinterpret_cast<int64_t*>(b + off[4]);
                 int64_t acc = 0;
@@ -1327,7 +1364,7 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
                 }
                 any = acc;
               }
-              std::memcpy(b + off[5], cont_flags + (int64_t)c0 * ak.fb, (size_t)sg.nc * ak.fb);
+              copy(b + off[5], cont_flags + (int64_t)c0 * ak.fb, (size_t)sg.nc * ak.fb);
               if (any < 0 && badv == INT64_MAX)
                 for (int64_t i = 0; i < nq; ++i)
                   if (q[i] < 0) {
