@@ -36,8 +36,8 @@ def _spawn(tmp_path, world, mix, n_nodes, n_jobs, transport, env):
 
 def _env(**kv):
     env = dict(os.environ)
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PE_HOST_MERGE", "PE_NO_ZC_EXCHANGE", "PE_HX_GPU_TIMEOUT_S", "PE_MERGE_RANKED", "PE_MERGE_SORT",
-              "PE_ZC_DEV_MERGE", "PE_HX_TIMEOUT_S"):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PE_HOST_MERGE", "PE_NO_ZC_EXCHANGE", "PE_HX_GPU_TIMEOUT_S", "PE_MERGE_RANKED",
+              "PE_MERGE_SORT", "PE_ZC_DEV_MERGE", "PE_HX_TIMEOUT_S", "PE_XCHG_THREADS"):
         env.pop(k, None)
     env.update(kv)
     return env
@@ -57,6 +57,9 @@ def _env(**kv):
                                                                            (2, "gang8", 6000, 300, True, "shm"),
                                                                            (2, "gang8", 6000, 300, False, "shm-grow"),
                                                                            (3, "island8", 9000, 300, False, "shm-grow"),
+                                                                           # five ranks, the host merge on 3 threads
+                                                                           # (groups split unevenly, w mod 3)
+                                                                           (5, "mixed", 25000, 400, False, "shm-t3"),
                                                                            # eight ranks: BASELINE cfg3's split
                                                                            (8, "mixed", 40000, 600, False, "shm"),
                                                                            (8, "island8", 16000, 300, False,
@@ -72,11 +75,12 @@ def test_sharded_greedy_across_processes(tmp_path, world, mix, n_nodes, n_jobs, 
     all-gather (PE_NO_ZC_EXCHANGE=1); "-sortmerge" / "-ranked": the other merge kernel forced
     (PE_MERGE_SORT=1 at 2 ranks, PE_MERGE_RANKED=1 at 3); "shm-grow": zero-copy with lists of 8 keys
     that rescan and segment slots for the grown stride (the ranks' lists grow after the first
-    rescan).  Either way the windows are pipelined.  (3 ranks over 2 nodes: one rank's shard is
+    rescan); "shm-t3": zero-copy with the host merge shared by 3 threads (PE_XCHG_THREADS).  Either way
+    the windows are pipelined.  (3 ranks over 2 nodes: one rank's shard is
     empty -- its windows are empty lists, signalled.)"""
     base, _, variant = transport.partition("-")
     extra = {"copy": {"PE_NO_ZC_EXCHANGE": "1"}, "sortmerge": {"PE_MERGE_SORT": "1"}, "ranked": {"PE_MERGE_RANKED": "1"},
-             "devmerge": {"PE_ZC_DEV_MERGE": "1"}, "grow": {}, "": {}}[variant]
+             "devmerge": {"PE_ZC_DEV_MERGE": "1"}, "grow": {}, "t3": {"PE_XCHG_THREADS": "3"}, "": {}}[variant]
     env = _env(**({"PE_HOST_MERGE": "1"} if host_merge else {}), **extra)
     zc_expected = base == "shm" and variant != "copy" and not host_merge
     transport = "shm-grow" if variant == "grow" else base
