@@ -40,7 +40,7 @@ def test_agg_segment_sizes(eng, mode, J):
 def test_agg_segment_jobs_override(eng, monkeypatch, seg_jobs):
     """PE_AGG_SEG_JOBS (A/B knob): any segment size gives the same answers, on both call paths."""
     monkeypatch.setenv("PE_AGG_SEG_JOBS", seg_jobs)
-    for J in (1, 300, 9000):
+    for J in (1, 300, 9000, 40000):   # (40000: the chunked multi-thread path, staging sized from a bound)
         _check(eng, V1, random_csr(J, 700 + J))
 
 

@@ -1261,7 +1261,7 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
       // segment; a segment ends at 256 jobs, at a chunk or thread boundary, or where it and the next
       // job would pass AGG_SEG_BYTES -- each job's bytes are in at most two such sums.
       const int64_t raw = n_jobs * 8 + G * 8 + C * (8 * ND + ak.fb);
-      const int64_t seg_cap = n_jobs / pe::AGG_SEG_JOBS + 2 * raw / (pe::AGG_SEG_BYTES - 128) + CH * T + 2;
+      const int64_t seg_cap = n_jobs / seg_jobs + 2 * raw / (pe::AGG_SEG_BYTES - 128) + CH * T + 2;
       const int64_t seg_over = (int64_t)sizeof(pe::AggSegHdr) + 8 + 5 * 15;
       int64_t nseg = 0, total = 0;
       if (CH == 1 || one_plan) {
