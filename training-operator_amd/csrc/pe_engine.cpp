@@ -1258,8 +1258,8 @@ int agg_call(pe_ctx* ctx, int32_t mode, int64_t n_jobs, pe::AggKeys ak, int n_ke
       };
       // Pinned staging sized before the first chunk is planned (a chunked call writes chunk 0 before the
       // rest is planned): raw section bytes plus at most 8 + 5 x 15 B of padding and a header per
-      // segment; a segment ends at 256 jobs, at a chunk or thread boundary, or where it and the next
-      // job would pass AGG_SEG_BYTES -- each job's bytes are in at most two such sums.
+      // segment; a segment ends at seg_jobs jobs, at a chunk or thread boundary, or where it and the
+      // next job would pass AGG_SEG_BYTES -- each job's bytes are in at most two such sums.
       const int64_t raw = n_jobs * 8 + G * 8 + C * (8 * ND + ak.fb);
       const int64_t seg_cap = n_jobs / seg_jobs + 2 * raw / (pe::AGG_SEG_BYTES - 128) + CH * T + 2;
       const int64_t seg_over = (int64_t)sizeof(pe::AggSegHdr) + 8 + 5 * 15;
