@@ -2638,7 +2638,7 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // holds alone (its shard may be empty): ctx->walk, the segment, the communicator.
     // PE_NO_LIST_GROWTH=1 keeps topk throughout on an UNSHARDED context (A/B; read per call) -- a
     // per-process variable cannot steer sharded ranks, which must agree on the stride.
-    const bool rccl_path = ctx->comm && !(ctx->exchange && !(ctx->world == 1 && !ctx->comm));
+    const bool rccl_path = ctx->comm && !ctx->exchange;   // the windows go through ncclAllGather (= !use_exchange below)
     const bool no_growth = ctx->world == 1 && !ctx->comm && std::getenv("PE_NO_LIST_GROWTH") != nullptr;
     const int K0 = ctx->topk;
     const int Kg = std::max(K0, std::min(2 * K0, pe::WK_ROUND - 1));
