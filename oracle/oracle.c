@@ -64,16 +64,20 @@ static int mul_ovf(int64_t a, int64_t b, int64_t* r) { return __builtin_mul_over
 #define K_OVERHEAD 3
 #define ORC_MAX_KEYS 16
 
+/* (the helpers below are inlined into each entry point with its nd / fb constant, so the fixed
+ * four-key call is the tight loop of the round-5 oracle, not a generic 16-key one) */
+#define ORC_INLINE static inline __attribute__((always_inline))
+
 /* flag word of container c: u8 (fixed dims) or u32 (key table) */
-static uint32_t flag_at(const void* fl, int fb, int32_t c) {
+ORC_INLINE uint32_t flag_at(const void* fl, int fb, int32_t c) {
   return fb == 1 ? ((const uint8_t*)fl)[c] : ((const uint32_t*)fl)[c];
 }
 
 /* v1 pod vector: sum of regular containers (util.go:133-140; init containers ignored). */
-static int v1_pod(int32_t c0, int32_t c1, int nd, int ks, const int64_t* req, const void* fl, int fb,
-                  int64_t out[ORC_MAX_KEYS], uint32_t* present) {
+ORC_INLINE int v1_pod(int32_t c0, int32_t c1, int nd, int ks, const int64_t* req, const void* fl, int fb,
+                      int64_t out[ORC_MAX_KEYS], uint32_t* present) {
   int ovf = 0;
-  memset(out, 0, sizeof(int64_t) * ORC_MAX_KEYS);
+  for (int d = 0; d < nd; ++d) out[d] = 0;
   *present = 0;
   for (int32_t c = c0; c < c1; ++c) {
     const uint32_t f = flag_at(fl, fb, c);
@@ -88,10 +92,11 @@ static int v1_pod(int32_t c0, int32_t c1, int nd, int ks, const int64_t* req, co
 }
 
 /* v2 pod vector: kueue v0.6.3 limitrange.TotalRequests restated (runtime.go:134). */
-static int v2_pod(int32_t c0, int32_t c1, int nd, int ks, const int64_t* req, const void* fl, int fb,
-                  int64_t out[ORC_MAX_KEYS], uint32_t* present) {
+ORC_INLINE int v2_pod(int32_t c0, int32_t c1, int nd, int ks, const int64_t* req, const void* fl, int fb,
+                      int64_t out[ORC_MAX_KEYS], uint32_t* present) {
   int ovf = 0;
-  int64_t side[ORC_MAX_KEYS] = {0}, initmax[ORC_MAX_KEYS] = {0}, main_[ORC_MAX_KEYS] = {0}, over[ORC_MAX_KEYS] = {0};
+  int64_t side[ORC_MAX_KEYS], initmax[ORC_MAX_KEYS], main_[ORC_MAX_KEYS], over[ORC_MAX_KEYS];
+  for (int d = 0; d < nd; ++d) side[d] = initmax[d] = main_[d] = over[d] = 0;
   *present = 0;
   for (int32_t c = c0; c < c1; ++c) {
     const uint32_t f = flag_at(fl, fb, c);
@@ -120,14 +125,15 @@ static int v2_pod(int32_t c0, int32_t c1, int nd, int ks, const int64_t* req, co
 }
 
 /* nd values per container / job, flags of fb bytes with the kind at bit ks; presence out as u8 or u16 */
-static int pg_min_resources_nd(int32_t mode, int64_t n_jobs, int nd, int fb, const int32_t* job_group_off,
+ORC_INLINE int pg_min_resources_nd(int32_t mode, int64_t n_jobs, int nd, int fb, const int32_t* job_group_off,
                                const int32_t* min_member, const int32_t* group_replicas,
                                const int32_t* group_cont_off, const int64_t* cont_req, const void* cont_flags,
                                int64_t* out_res, void* out_present, int32_t* out_members, uint8_t* out_overflow) {
   if (mode != ORC_V1 && mode != ORC_V2) return -1;
   const int ks = fb == 1 ? 4 : 16;
   for (int64_t j = 0; j < n_jobs; ++j) {
-    int64_t acc[ORC_MAX_KEYS] = {0};
+    int64_t acc[ORC_MAX_KEYS];
+    for (int d = 0; d < nd; ++d) acc[d] = 0;
     uint32_t pres = 0;
     uint8_t ovf = 0;
     int32_t pod_cnt = 0;

@@ -62,9 +62,10 @@ constexpr int MG_SEL = 1024;   // merge: keys kept after the histogram cut (sort
 // SEGMENTS in one pinned, device-mapped staging buffer: a segment holds up to AGG_SEG_JOBS
 // consecutive jobs with their groups and containers, offsets rebased to the segment, every
 // section 16-B aligned, so one block copies its whole segment into LDS with one round trip of
-// coalesced 16-B zero-copy reads (no DMA, no device copy of the inputs) and runs one job per lane
-// from LDS.  Outputs go straight into a pinned output buffer in the caller's layout.  A segment
-// larger than AGG_SEG_BYTES (one job with very many groups / containers) is read in place.
+// coalesced 16-B loads and runs one job per lane from LDS -- reading the pinned buffer over PCIe for
+// calls up to 8192 jobs, a device copy (one DMA per chunk) for larger ones.  Outputs go straight into
+// a pinned output buffer in the caller's layout.  A segment larger than AGG_SEG_BYTES (one job with
+// very many groups / containers) is read in place.
 constexpr int AGG_SEG_JOBS = 256;
 constexpr int64_t AGG_SEG_BYTES = 48 * 1024;
 struct AggSegHdr {
