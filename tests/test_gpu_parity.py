@@ -679,6 +679,29 @@ def test_greedy_signalled_windows(mix, N, J, topk, wg):
     np.testing.assert_array_equal(res["1"], res[None])
 
 
+@pytest.mark.parametrize("mix,N,J,topk,wg,resort", [("mixed", 4000, 600, 64, 64, 0), ("mixed", 2000, 400, 2, 8, 0),
+                                                    ("island8", 800, 300, 4, 16, 64), ("pytorch", 3000, 500, 1, 2, 16)])
+def test_greedy_early_post(mix, N, J, topk, wg, resort):
+    """The next window's apply + walk handed to the launch helper as soon as the current window landed
+    (default) or after the next window's first group was seen (PE_EARLY_POST=0): both exact vs the
+    oracle, identical -- small K / windows drop speculations and restart often, which rewinds the two
+    update staging slots the early post rotates."""
+    inv = synth.make_inventory(N, 131 + N, 0.35)
+    batch = synth.make_jobs(J, 137 + J, mix)
+    res = {}
+    for ep in ("0", None):
+        if ep:
+            os.environ["PE_EARLY_POST"] = ep
+        try:
+            e = Engine(0, topk=topk, window_groups=wg, **({"resort_nodes": resort} if resort else {}))
+            res[ep] = check_greedy(e, inv, batch)
+            e.place_batch(batch)   # a second batch on the same context
+            e.close()
+        finally:
+            os.environ.pop("PE_EARLY_POST", None)
+    np.testing.assert_array_equal(res["0"], res[None])
+
+
 @pytest.mark.parametrize("flags,resort", [(2, 0), (0, 1), (0, 64), (1, 16), (3, 0)])
 @pytest.mark.parametrize("mix,N,J,gpu_frac,topk,wg", [("mixed", 3000, 300, 0.3, 64, 64), ("pytorch", 2500, 300, 0.2, 2, 8),
                                                        ("gang8", 700, 150, 1.0, 4, 16), ("mixed", 5000, 200, 0.5, 1, 1),

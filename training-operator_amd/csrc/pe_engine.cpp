@@ -3415,6 +3415,17 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     std::vector<std::vector<pe::Update>> hist;   // updates of the epoch's resolved windows
     size_t n_app = 0;                             // of which posted for apply
     int next_buf = 0, upd_slot = 0;
+    // Early post (signalled windows at depth 1, one rank or a non-split exchange; PE_EARLY_POST=0: off,
+    // A/B; unsignalled windows share one request buffer, which the next walk may still read): once window i
+    // landed, the helper is given apply(i) and the scan of window i + 2 at once -- queued behind the walk
+    // of window i + 1 -- instead of after the first group of window i + 1 was seen, so the device never
+    // idles while the host posts them.  The apply records then need two staging slots: apply(i) may be
+    // written while apply(i - 1) has not run yet; the slot it reuses was read by apply(i - 2), which ran
+    // before the walk of window i, all of whose groups were resolved.
+    const bool early_post = signalled && depth == 1 && !split_x &&
+                            !(std::getenv("PE_EARLY_POST") && std::atoi(std::getenv("PE_EARLY_POST")) == 0);
+    const int upd_slots = early_post ? 2 : std::max(depth, 1);
+    bool posted = false;   // the helper already has this iteration's task (early post)
     const int nbuf = std::max(depth, 1) + 1;
     auto add_flight = [&](const pe::Cursor& from) -> Flight* {   // main thread; nullptr: no window left
       Flight f;
@@ -3465,15 +3476,31 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
       }
       // the helper: previous windows' updates applied, then windows scanned up to D ahead
       std::vector<std::pair<const std::vector<pe::Update>*, int>> to_apply;
-      for (; n_app < hist.size(); ++n_app) {
-        to_apply.emplace_back(&hist[n_app], upd_slot);
-        upd_slot = (upd_slot + 1) % std::max(depth, 1);
-      }
       std::vector<Flight*> to_scan;
-      while ((int)fl.size() < depth + 1)
-        if (Flight* f = add_flight(fl.back().end)) to_scan.push_back(f);
-        else break;
-      if (split_x) {
+      auto plan_post = [&]() {
+        to_apply.clear();
+        to_scan.clear();
+        for (; n_app < hist.size(); ++n_app) {
+          to_apply.emplace_back(&hist[n_app], upd_slot);
+          upd_slot = (upd_slot + 1) % upd_slots;
+        }
+        while ((int)fl.size() < depth + 1)
+          if (Flight* f = add_flight(fl.back().end)) to_scan.push_back(f);
+          else break;
+      };
+      auto post_scan = [&]() {   // (the non-split helper task)
+        worker->post([&, to_apply, to_scan] {
+          const auto tp = std::chrono::steady_clock::now();
+          if (trace) helper_cpu = sched_getcpu();
+          for (const auto& a : to_apply) enqueue_apply(*a.first, a.second);
+          for (Flight* f : to_scan) enqueue_window(f->groups, f->buf);
+          if (trace) tr_post.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
+        });
+      };
+      if (posted) {
+        posted = false;
+      } else if (split_x) {
+        plan_post();
         // generations assigned here, in launch order: the exchange thread waits for these windows' own
         // lists (signalled with them) while the launch helper launches the walks
         // (zero-copy: the windows' slots too, taken in the same order on every rank)
@@ -3506,13 +3533,8 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
           for (const XWin& x : xs) exchange_window(x.buf, x.wg, x.gen, true, worker.get(), zc_host ? &x.hw : nullptr);
         });
       } else {
-        worker->post([&, to_apply, to_scan] {
-          const auto tp = std::chrono::steady_clock::now();
-          if (trace) helper_cpu = sched_getcpu();
-          for (const auto& a : to_apply) enqueue_apply(*a.first, a.second);
-          for (Flight* f : to_scan) enqueue_window(f->groups, f->buf);
-          if (trace) tr_post.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
-        });
+        plan_post();
+        post_scan();
       }
       // seeds: the changes of the windows resolved since cur's scan (later states overwrite)
       seed.clear();
@@ -3536,6 +3558,11 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
         hist.push_back(std::move(upd));
         upd = {};
         fl.pop_front();
+        if (early_post) {   // the next iteration's task, now
+          plan_post();
+          post_scan();
+          posted = true;
+        }
         continue;
       }
       // done, or speculation dropped: finish the device work, apply what is left, in order (one
