@@ -1427,6 +1427,17 @@ __device__ __forceinline__ void topk_append(TopkShared& s, uint64_t k, bool take
   if (take && base + rank < MG_CAP) s.keys[base + rank] = k;
 }
 
+// Histogram add, wave-wide (every lane calls it; b < 0: nothing to count): each run of consecutive
+// lanes with the same bin adds its length with one LDS atomic from its first lane.
+__device__ __forceinline__ void hist_add_runs(int* hist, int b, int lane) {
+  const int bp = __shfl_up(b, 1, 64);
+  const bool edge = lane == 0 || bp != b;
+  const uint64_t bal = __ballot(edge);
+  const uint64_t above = lane == 63 ? 0ull : bal & (~0ull << (lane + 1));   // run ends at the next edge
+  const int next = above ? __ffsll((unsigned long long)above) - 1 : 64;
+  if (edge && b >= 0) atomicAdd(&hist[b], next - lane);
+}
+
 // 256-bin histogram cut (block-wide, wave 0 scans): with s.hist filled, the first bin whose
 // inclusive count reaches `need` (255 if none) -> s.sel_bin, and the count of the bins before it
 // -> s.sel_n.  Ends with a barrier.
@@ -1522,6 +1533,60 @@ __device__ __forceinline__ void rank_place(TopkShared& s, int C, int K) {
   }
 }
 
+// Block-wide: the C <= MG_SEL unique keys of s.sel ranked, the K + 1 smallest written ascending to the
+// front of s.keys.  Wave w < ceil(C / 64) sorts s.sel[64w, 64w + 64) in registers (a bitonic network
+// over lane shuffles; NO_KEY pads the last chunk) and writes it back; then thread t < C takes the
+// t-th sorted key: its rank is its index in its own chunk plus, per other chunk, the count of keys
+// below it (a 7-read binary search over the chunk's 64 sorted keys) -- one thread per key and
+// ~7 x chunks LDS reads, against rank_place's count over every selected key.  The caller's barrier
+// after s.sel was written precedes it; ends with a barrier.  (PE_RANK_PLACE=1 at build time: rank_place.)
+__device__ __forceinline__ void sort_rank(TopkShared& s, int C, int K) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nch = (C + 63) >> 6;
+  if (wave < nch) {
+    const int i = (wave << 6) + lane;
+    uint64_t v = i < C ? s.sel[i] : NO_KEY;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const uint64_t o = __shfl_xor(v, j, 64);
+        // the lower lane of a pair keeps the smaller key in an ascending run, the larger in a descending one
+        v = (((lane & j) == 0) == ((lane & k) == 0)) ? umin64(v, o) : umax64(v, o);
+      }
+    }
+    s.sel[i] = v;
+  }
+  __syncthreads();
+  if (tid < C) {
+    const uint64_t k = s.sel[tid];
+    int rank = lane;   // keys are unique: its index in its own sorted chunk
+    for (int c = 0; c < nch; ++c) {   // (the chunks' searches interleaved step by step measured slower:
+      if (c == wave) continue;        // rank 4.2 vs 2.7 us per call, profiles/r57_topk_ab.txt)
+      const uint64_t* ch = s.sel + (c << 6);
+      int pos = ch[31] < k ? 32 : 0;
+      pos += ch[pos + 15] < k ? 16 : 0;
+      pos += ch[pos + 7] < k ? 8 : 0;
+      pos += ch[pos + 3] < k ? 4 : 0;
+      pos += ch[pos + 1] < k ? 2 : 0;
+      pos += ch[pos] < k ? 1 : 0;
+      pos += ch[pos] < k ? 1 : 0;   // (all 64 below: pos 63 -> 64)
+      rank += pos;
+    }
+    if (rank <= K) s.keys[rank] = k;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void place_ranked(TopkShared& s, int C, int K) {
+#ifdef PE_RANK_PLACE
+  rank_place(s, C, K);
+  __syncthreads();
+#else
+  sort_rank(s, C, K);
+#endif
+}
+
 #ifdef PE_WALK_PROF   // topk_sort breakdown (diagnostics build): calls, T, C, bitonic fallbacks, phase ticks
 __device__ unsigned long long topk_prof[8];
 #define TKP(i, v) (threadIdx.x == 0 ? (void)atomicAdd(&topk_prof[i], (unsigned long long)(v)) : (void)0)
@@ -1540,8 +1605,7 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K, uint64_t bound = NO_
   if (T <= 2 * (K + 1) && T <= MG_SEL) {   // few keys: rank-place them all (no histogram, no bitonic)
     for (int i = tid; i < T; i += MG_THREADS) s.sel[i] = s.keys[i];
     __syncthreads();
-    rank_place(s, T, K);
-    __syncthreads();
+    place_ranked(s, T, K);
     return s.keys;
   }
   if (K + 1 <= MG_SEL) {
@@ -1569,14 +1633,57 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K, uint64_t bound = NO_
     }
     const int bits = 64 - __clzll((long long)((kmax - kmin) | 1));
     const int sh = bits > 8 ? bits - 8 : 0;
+#ifdef PE_HIST_PLAIN   // (A/B: one LDS atomic per key)
     for (int i = tid; i < T; i += MG_THREADS) {
       const uint64_t k = s.keys[i];
       if (k < bound) atomicAdd(&s.hist[(int)((k - kmin) >> sh)], 1);
     }
+#else
+    // one LDS atomic per run of equal bins across a wave's lanes: the walk appends its keys round by
+    // round, nearly sorted, so neighbouring lanes mostly share a bin (one atomic per key serialises there)
+    for (int i0 = 0; i0 < T; i0 += MG_THREADS) {   // (block-uniform trip count: shuffles and ballots)
+      const int i = i0 + tid;
+      const uint64_t k = i < T ? s.keys[i] : NO_KEY;
+      const int b = k < bound ? (int)((k - kmin) >> sh) : -1;
+      hist_add_runs(s.hist, b, lane);
+    }
+#endif
     __syncthreads();
     hist_cut(s, K + 1);
     const int cb = s.sel_bin;
     const int before = s.sel_n;
+#ifndef PE_TOPK_TWO_LEVEL
+    // one level when it suffices: every key below the bound in bins <= cb (the (K+1)-th smallest lies
+    // in bin cb), appended wave by wave; up to MG_SEL of them are ranked directly (the second histogram,
+    // its cut and three barriers saved), more fall through to the second level below
+    __syncthreads();                     // every thread has read sel_bin / sel_n
+    if (tid == 0) s.sel_n = 0;
+    __syncthreads();
+    for (int i0 = 0; i0 < T; i0 += MG_THREADS) {   // (block-uniform trip count: the ballot is wave-wide)
+      const int i = i0 + tid;
+      const uint64_t k = i < T ? s.keys[i] : NO_KEY;
+      const bool take = i < T && k < bound && (int)((k - kmin) >> sh) <= cb;
+      const uint64_t bal = __ballot(take);
+      if (bal) {
+        const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+        int base = 0;
+        if (take && r == 0) base = atomicAdd(&s.sel_n, __popcll(bal));
+        base = __shfl(base, __ffsll((unsigned long long)bal) - 1, 64);
+        if (take && base + r < MG_SEL) s.sel[base + r] = k;
+      }
+    }
+    __syncthreads();
+    if (s.sel_n <= MG_SEL) {
+      const int C1 = s.sel_n;
+      TKT(1);
+      TKP(3, C1);
+      TKP(4, tkt1 - tkt0);
+      place_ranked(s, C1, K);
+      TKT(2);
+      TKP(5, tkt2 - tkt1);
+      return s.keys;
+    }
+#endif
     // level 2 inside bin cb: keys in [base, base + 2^sh), 256 sub-bins of 2^sh2
     const uint64_t base = kmin + ((uint64_t)cb << sh);
     const int sh2 = sh > 8 ? sh - 8 : 0;
@@ -1585,10 +1692,19 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K, uint64_t bound = NO_
       __syncthreads();                     // every thread has read sel_bin / sel_n
       for (int i = tid; i < 256; i += MG_THREADS) s.hist[i] = 0;
       __syncthreads();
+#ifdef PE_HIST_PLAIN
       for (int i = tid; i < T; i += MG_THREADS) {
         const uint64_t k = s.keys[i];
         if (k < bound && (int)((k - kmin) >> sh) == cb) atomicAdd(&s.hist[(int)((k - base) >> sh2)], 1);
       }
+#else
+      for (int i0 = 0; i0 < T; i0 += MG_THREADS) {
+        const int i = i0 + tid;
+        const uint64_t k = i < T ? s.keys[i] : NO_KEY;
+        const int b = k < bound && (int)((k - kmin) >> sh) == cb ? (int)((k - base) >> sh2) : -1;
+        hist_add_runs(s.hist, b, lane);
+      }
+#endif
       __syncthreads();
       hist_cut(s, K + 1 - before);
       cb2 = s.sel_bin;
@@ -1611,8 +1727,7 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K, uint64_t bound = NO_
     TKP(3, C);
     TKP(4, tkt1 - tkt0);
     if (C <= MG_SEL) {
-      rank_place(s, C, K);                 // into s.keys (its old contents are no longer needed)
-      __syncthreads();
+      place_ranked(s, C, K);               // into s.keys (its old contents are no longer needed)
       TKT(2);
       TKP(5, tkt2 - tkt1);
       return s.keys;
