@@ -3403,8 +3403,9 @@ int pe_place_greedy(pe_ctx* ctx, int64_t n_jobs, const int32_t* job_group_off, c
     // where the speculation started, syncs, applies everything and restarts from the cursor.
     // Staging-buffer reuse: the apply posted in iteration j is followed, in the same post, by the
     // scan of window j + D; the slot is written again in iteration j + D, when that window's first
-    // group has been seen, i.e. after every earlier launch of the stream finished.  Blob / request
-    // buffer b is reused D + 1 windows later, after the windows in between were resolved.
+    // group has been seen, i.e. after every earlier launch of the stream finished (with the early post
+    // below, two slots: see early_post).  Blob / request buffer b is reused D + 1 windows later, after
+    // the windows in between were resolved.
     struct Flight {
       std::vector<int32_t> groups;
       pe::Cursor end;

@@ -1413,6 +1413,7 @@ struct TopkShared {
   uint64_t red[2 * (MG_THREADS / 64)];
   int hist[256];
   int total, sel_n, sel_bin;
+  int sel_c;   // topk_sort's one-level gather count (zeroed with the histogram, no barrier pair of its own)
 };
 
 // Wave-aggregated append of the lanes' keys with `take` to s.keys: one LDS atomic per wave
@@ -1624,6 +1625,7 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K, uint64_t bound = NO_
       s.red[MG_THREADS / 64 + wave] = mx;
     }
     for (int i = tid; i < 256; i += MG_THREADS) s.hist[i] = 0;
+    if (tid == 0) s.sel_c = 0;
     __syncthreads();
     uint64_t kmin = NO_KEY, kmax = 0;
 #pragma unroll
@@ -1656,9 +1658,7 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K, uint64_t bound = NO_
     // one level when it suffices: every key below the bound in bins <= cb (the (K+1)-th smallest lies
     // in bin cb), appended wave by wave; up to MG_SEL of them are ranked directly (the second histogram,
     // its cut and three barriers saved), more fall through to the second level below
-    __syncthreads();                     // every thread has read sel_bin / sel_n
-    if (tid == 0) s.sel_n = 0;
-    __syncthreads();
+    // (s.sel_c was zeroed before the first histogram's barrier; hist_cut's sel_n / sel_bin are read above)
     for (int i0 = 0; i0 < T; i0 += MG_THREADS) {   // (block-uniform trip count: the ballot is wave-wide)
       const int i = i0 + tid;
       const uint64_t k = i < T ? s.keys[i] : NO_KEY;
@@ -1667,14 +1667,14 @@ __device__ uint64_t* topk_sort(TopkShared& s, int T, int K, uint64_t bound = NO_
       if (bal) {
         const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
         int base = 0;
-        if (take && r == 0) base = atomicAdd(&s.sel_n, __popcll(bal));
+        if (take && r == 0) base = atomicAdd(&s.sel_c, __popcll(bal));
         base = __shfl(base, __ffsll((unsigned long long)bal) - 1, 64);
         if (take && base + r < MG_SEL) s.sel[base + r] = k;
       }
     }
     __syncthreads();
-    if (s.sel_n <= MG_SEL) {
-      const int C1 = s.sel_n;
+    if (s.sel_c <= MG_SEL) {
+      const int C1 = s.sel_c;
       TKT(1);
       TKP(3, C1);
       TKP(4, tkt1 - tkt0);
